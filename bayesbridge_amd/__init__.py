@@ -1,0 +1,449 @@
+"""bayesbridge_amd -- MI355X-native Bayesian bridge regression (normal-mixture Gibbs sweep).
+
+Python mirror of the reference package's R front end for the stable path
+(Code/C/BridgeWrapper.R): ``bridge_reg_stb`` (bridge.reg.stb, :194-234),
+``bridge_reg`` (bridge.reg, :240-276, method="stable") and ``retstable_ld``
+(retstable.ld, :511-537).  Each call goes through the same C ABI that R's ``.C``
+would bind (``include/bayesbridge.h``), with R's marshalling emulated here:
+column-major doubles, integer scalars, caller-allocated outputs, P x M traces
+transposed to M x P on return.
+
+All compute runs in the gfx950 HIP kernels of ``BayesBridge.so``; there is no
+CPU fallback -- the functions raise if the library or a GPU is unavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _build
+
+__all__ = ["bridge_reg_stb", "bridge_reg", "retstable_ld", "set_seed", "get_rng_state",
+           "set_rng_state", "Engine", "EngineConfig", "library", "device_count",
+           "sample_lambda", "retstable_batch", "gram", "chol_solve"]
+
+_lib: Optional[ctypes.CDLL] = None
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+class bb_config(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("p", ctypes.c_int), ("p_local", ctypes.c_int),
+                ("j0", ctypes.c_int), ("rank", ctypes.c_int), ("world", ctypes.c_int),
+                ("sig2_shape", ctypes.c_double), ("sig2_scale", ctypes.c_double),
+                ("nu_shape", ctypes.c_double), ("nu_rate", ctypes.c_double),
+                ("alpha_a", ctypes.c_double), ("alpha_b", ctypes.c_double),
+                ("true_sig2", ctypes.c_double), ("true_tau", ctypes.c_double),
+                ("true_alpha", ctypes.c_double), ("ortho", ctypes.c_int),
+                ("method", ctypes.c_int), ("trace_capacity", ctypes.c_int),
+                ("seed", ctypes.c_uint64), ("stream", ctypes.c_uint64), ("device", ctypes.c_int)]
+
+
+EXPORTED_SYMBOLS = [
+    "bridge_reg_stable", "retstable_LD", "bb_version", "bb_last_error", "bb_device_count",
+    "bb_set_seed", "bb_get_rng_state", "bb_set_rng_state", "bb_use_r_rng", "bb_set_device",
+    "bb_set_verbose", "bb_config_default", "bb_engine_create", "bb_engine_destroy",
+    "bb_comm_id_size", "bb_comm_unique_id", "bb_engine_comm_init", "bb_engine_init_state",
+    "bb_engine_run", "bb_engine_sync", "bb_engine_get_trace", "bb_engine_get_state",
+    "bb_engine_set_state", "bb_engine_method", "bb_engine_enable_timing",
+    "bb_engine_kernel_times", "bb_engine_reset_timing", "bb_engine_error_flags",
+    "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
+]
+
+
+def library(build: bool = True) -> ctypes.CDLL:
+    """Load BayesBridge.so (building it in-tree first if stale and hipcc is present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.SO_PATH
+    if build:
+        try:
+            path = _build.build()
+        except Exception:
+            if not os.path.exists(_build.SO_PATH):
+                raise
+    if not os.path.exists(path):
+        raise RuntimeError(f"BayesBridge.so not found at {path}; run bayesbridge_amd._build")
+    L = ctypes.CDLL(path)
+    c = ctypes
+    L.bb_version.restype = c.c_char_p
+    L.bb_last_error.restype = c.c_char_p
+    L.bb_device_count.restype = c.c_int
+    L.bb_set_seed.argtypes = [c.c_uint64]
+    L.bb_get_rng_state.argtypes = [c.POINTER(c.c_uint64), c.POINTER(c.c_uint64)]
+    L.bb_set_rng_state.argtypes = [c.c_uint64, c.c_uint64]
+    L.bb_use_r_rng.argtypes = [c.c_int]
+    L.bb_set_device.argtypes = [c.c_int]
+    L.bb_set_verbose.argtypes = [c.c_int]
+    L.bb_config_default.argtypes = [c.POINTER(bb_config)]
+    L.bb_engine_create.argtypes = [c.POINTER(bb_config), _dp, _dp, c.POINTER(c.c_void_p)]
+    L.bb_engine_destroy.argtypes = [c.c_void_p]
+    L.bb_comm_id_size.restype = c.c_int
+    L.bb_comm_unique_id.argtypes = [c.c_void_p]
+    L.bb_engine_comm_init.argtypes = [c.c_void_p, c.c_void_p]
+    L.bb_engine_init_state.argtypes = [c.c_void_p]
+    L.bb_engine_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
+    L.bb_engine_sync.argtypes = [c.c_void_p]
+    L.bb_engine_get_trace.argtypes = [c.c_void_p, c.c_int, c.c_int, _dp, _dp, _dp, _dp, _dp]
+    L.bb_engine_get_state.argtypes = [c.c_void_p, _dp, _dp, _dp, _dp, _dp]
+    L.bb_engine_set_state.argtypes = [c.c_void_p, _dp, c.c_double, c.c_double, c.c_double]
+    L.bb_engine_method.argtypes = [c.c_void_p]
+    L.bb_engine_enable_timing.argtypes = [c.c_void_p, c.c_int]
+    L.bb_engine_reset_timing.argtypes = [c.c_void_p]
+    L.bb_engine_kernel_times.argtypes = [c.c_void_p, _dp, _dp, _ip]
+    L.bb_engine_error_flags.argtypes = [c.c_void_p, c.POINTER(c.c_uint32)]
+    L.bb_retstable_batch.argtypes = [_dp, _dp, _dp, _dp, c.c_int, c.c_uint64, c.c_uint64,
+                                     c.c_uint64, c.c_int]
+    L.bb_sample_lambda.argtypes = [_dp, _dp, c.c_int, c.c_double, c.c_double, c.c_uint64,
+                                   c.c_uint64, c.c_uint64, c.c_uint64, c.c_int]
+    L.bb_gram.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
+    L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    return int(library().bb_device_count())
+
+
+def _require_gpu():
+    if device_count() < 1:
+        raise RuntimeError("bayesbridge_amd: no HIP device visible (the sampler has no CPU path)")
+
+
+def _err() -> str:
+    return library().bb_last_error().decode()
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {_err()}")
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def set_seed(seed: int) -> None:
+    """Seed the Philox key for subsequent calls (stream counter reset to 0)."""
+    library().bb_set_seed(int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+
+def get_rng_state():
+    s, t = ctypes.c_uint64(), ctypes.c_uint64()
+    library().bb_get_rng_state(ctypes.byref(s), ctypes.byref(t))
+    return int(s.value), int(t.value)
+
+
+def set_rng_state(seed: int, stream: int) -> None:
+    library().bb_set_rng_state(int(seed), int(stream))
+
+
+def set_verbose(v: int) -> None:
+    library().bb_set_verbose(int(v))
+
+
+# ---------------------------------------------------------------------------
+# R front-end mirror (Code/C/BridgeWrapper.R)
+# ---------------------------------------------------------------------------
+def _is_above(param, val, name):
+    """BridgeWrapper.R:31-47 (is.above): TRUE iff param >= val and numeric."""
+    above = True
+    if not np.issubdtype(np.asarray(param).dtype, np.number):
+        print(f"Error: {name} is not numeric.")
+        return False
+    if np.any(np.asarray(param) < val):
+        print(f"Error: {name}<{val}")
+        above = False
+    return above
+
+
+def check_parameters(N, R, M, sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a, alpha_b):
+    """BridgeWrapper.R:50-69 (check.parameters)."""
+    ok = True
+    if N != R:
+        print("Error: y and X do not conform.")
+        ok = False
+    checks = [_is_above(M, 1, "niter"), _is_above(sig2_shape, 0, "sig2.shape"),
+              _is_above(sig2_scale, 0, "sig2.scale"), _is_above(nu_shape, 0, "nu.shape"),
+              _is_above(nu_rate, 0, "nu.rate"), _is_above(alpha_a, -1, "alpha.a"),
+              _is_above(alpha_b, -1, "alpha.b")]
+    return ok and all(checks)
+
+
+def bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,
+                   nu_rate=2.0, alpha_a=1.0, alpha_b=1.0, sig2_true=0.0, tau_true=0.0,
+                   burn=500, ortho=False, colnames=None):
+    """bridge.reg.stb (BridgeWrapper.R:194-234) through ``.C("bridge_reg_stable", ...)``.
+
+    Returns a dict: beta (M x P), lambda (M x P), sig2, tau, alpha (M), runtime.
+    ``alpha`` is alpha.true (> 0 fixes alpha; <= 0 samples it by MH).
+    """
+    L = library()
+    _require_gpu()
+    y = np.asarray(y, dtype=np.float64).ravel()
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    N = y.shape[0]
+    R, P = X.shape
+    M = int(nsamp)
+    if not check_parameters(N, R, M, sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
+                            alpha_b):
+        # the R wrapper halts here (`break` outside a loop, BridgeWrapper.R:212)
+        raise ValueError("bridge_reg_stb: invalid parameters")
+    beta = np.zeros((P, M), order="F")
+    lam = np.zeros((P, M), order="F")
+    sig2 = np.zeros(M)
+    tau = np.zeros(M)
+    alph = np.zeros(M)
+    Xf = np.asfortranarray(X)
+    d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
+    i = lambda v: ctypes.byref(ctypes.c_int(int(v)))  # noqa: E731
+    rt = ctypes.c_double(0.0)
+    L.bridge_reg_stable(_p(beta), _p(lam), _p(sig2), _p(tau), _p(alph), _p(y), _p(Xf),
+                        d(sig2_shape), d(sig2_scale), d(nu_shape), d(nu_rate), d(alpha_a),
+                        d(alpha_b), d(sig2_true), d(tau_true), d(alpha), i(P), i(N), i(M),
+                        i(burn), ctypes.byref(rt), i(1 if ortho else 0))
+    out = {"beta": beta.T.copy(), "lambda": lam.T.copy(), "sig2": sig2, "tau": tau,
+           "alpha": alph, "runtime": rt.value}
+    if colnames is not None:
+        out["colnames"] = list(colnames)
+    return out
+
+
+def bridge_reg(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,
+               nu_rate=2.0, alpha_a=1.0, alpha_b=1.0, sig2_true=0.0, tau_true=0.0, burn=500,
+               method="triangle", ortho=False):
+    """bridge.reg (BridgeWrapper.R:240-276).
+
+    Like the reference, the "stable" branch IGNORES the caller's hyper-parameters and
+    calls bridge.reg.stb with alpha=0.5, nu.shape = nu.rate = 0.5, burn=500.  The
+    triangle method is outside this build's scope.
+    """
+    if method == "stable":
+        return bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0,
+                              nu_shape=0.5, nu_rate=0.5, alpha_a=1.0, alpha_b=1.0,
+                              sig2_true=0.0, tau_true=0.0, burn=500, ortho=ortho)
+    if method == "triangle":
+        raise NotImplementedError("bridge.reg(method='triangle') is not part of this build")
+    print('Unrecognized method.  Use "triangles" or "stable".')
+    return None
+
+
+def retstable_ld(num=1, alpha=1.0, V0=1.0, h=1.0):
+    """retstable.ld (BridgeWrapper.R:511-537) through ``.C("retstable_LD", ...)``.
+
+    Draws from the exponentially tilted positive stable law with Laplace transform
+    exp(-V0((h+t)^alpha - h^alpha)).  Invalid parameters print and return NaN, as
+    the R function prints and returns NA.
+    """
+    if not np.all(np.asarray(V0) > 0):
+        print("V0 must be > 0.")
+        return np.nan
+    if not np.all(np.asarray(h) >= 0):
+        print("h must be >= 0")
+        return np.nan
+    a = np.asarray(alpha)
+    if not (np.all(a > 0) and np.all(a <= 1)):
+        print("alpha must be in (0,1].")
+        return np.nan
+    L = library()
+    _require_gpu()
+    num = int(num)
+    # R's array(v, num) recycles
+    alpha_a = np.resize(np.asarray(alpha, dtype=np.float64), num)
+    h_a = np.resize(np.asarray(h, dtype=np.float64), num)
+    V0_a = np.resize(np.asarray(V0, dtype=np.float64), num)
+    x = np.zeros(num)
+    L.retstable_LD(_p(x), _p(alpha_a), _p(V0_a), _p(h_a), ctypes.byref(ctypes.c_int(num)))
+    return x
+
+
+# ---------------------------------------------------------------------------
+# Kernel-level helpers (tests / microbenchmarks)
+# ---------------------------------------------------------------------------
+def retstable_batch(alpha, V0, h, seed, stream=0, t=0, group=0):
+    L = library()
+    _require_gpu()
+    alpha = np.ascontiguousarray(alpha, dtype=np.float64)
+    V0 = np.ascontiguousarray(V0, dtype=np.float64)
+    h = np.ascontiguousarray(h, dtype=np.float64)
+    x = np.zeros(h.shape[0])
+    _check(L.bb_retstable_batch(_p(x), _p(alpha), _p(V0), _p(h), h.shape[0], seed, stream, t,
+                                group), "bb_retstable_batch")
+    return x
+
+
+def sample_lambda(beta, alpha, tau, seed, stream, t, j0=0, group=0):
+    L = library()
+    _require_gpu()
+    beta = np.ascontiguousarray(beta, dtype=np.float64)
+    lam = np.zeros_like(beta)
+    _check(L.bb_sample_lambda(_p(lam), _p(beta), beta.shape[0], alpha, tau, seed, stream, t, j0,
+                              group), "bb_sample_lambda")
+    return lam
+
+
+def gram(Y, w):
+    """C = Y diag(w) Y' on the device (fp64 MFMA)."""
+    L = library()
+    _require_gpu()
+    Y = np.asfortranarray(Y, dtype=np.float64)
+    w = np.ascontiguousarray(w, dtype=np.float64)
+    n, k = Y.shape
+    C = np.zeros((n, n), order="F")
+    _check(L.bb_gram(_p(C), _p(Y), _p(w), n, k), "bb_gram")
+    return C
+
+
+def chol_solve(A, b):
+    L = library()
+    _require_gpu()
+    A = np.asfortranarray(A, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    nrhs = 1 if b.ndim == 1 else b.shape[1]
+    bf = np.asfortranarray(b.reshape(A.shape[0], nrhs))
+    x = np.zeros_like(bf, order="F")
+    _check(L.bb_chol_solve(_p(x), _p(A), _p(bf), A.shape[0], nrhs), "bb_chol_solve")
+    return x.ravel() if b.ndim == 1 else x
+
+
+# ---------------------------------------------------------------------------
+# Engine (benchmarks, multi-GPU, teacher-forced tests)
+# ---------------------------------------------------------------------------
+@dataclass
+class EngineConfig:
+    n: int
+    p: int
+    p_local: int = 0
+    j0: int = 0
+    rank: int = 0
+    world: int = 1
+    sig2_shape: float = 0.0
+    sig2_scale: float = 0.0
+    nu_shape: float = 2.0
+    nu_rate: float = 2.0
+    alpha_a: float = 1.0
+    alpha_b: float = 1.0
+    true_sig2: float = 0.0
+    true_tau: float = 0.0
+    true_alpha: float = 0.5
+    ortho: bool = False
+    method: int = 0
+    trace_capacity: int = 1
+    seed: int = 0xB4E5B41D6E
+    stream: int = 0
+    device: int = 0
+
+    def to_c(self) -> bb_config:
+        c = bb_config()
+        library().bb_config_default(ctypes.byref(c))
+        for name, _ in bb_config._fields_:
+            v = getattr(self, name)
+            setattr(c, name, int(v) if isinstance(v, bool) else v)
+        if c.p_local <= 0:
+            c.p_local = c.p
+        return c
+
+
+class Engine:
+    """One Gibbs chain (or one column shard of it) resident on one GPU."""
+
+    def __init__(self, cfg: EngineConfig, X_local, y):
+        L = library()
+        _require_gpu()
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        X_local = np.asfortranarray(X_local, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        assert X_local.shape == (cfg.n, self._c.p_local), X_local.shape
+        self.p_local = self._c.p_local
+        h = ctypes.c_void_p()
+        _check(L.bb_engine_create(ctypes.byref(self._c), _p(X_local), _p(y), ctypes.byref(h)),
+               "bb_engine_create")
+        self._h = h
+
+    def comm_init(self, id_bytes: bytes):
+        _check(library().bb_engine_comm_init(self._h, ctypes.c_char_p(id_bytes)),
+               "bb_engine_comm_init")
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        L = library()
+        buf = ctypes.create_string_buffer(L.bb_comm_id_size())
+        _check(L.bb_comm_unique_id(buf), "bb_comm_unique_id")
+        return buf.raw
+
+    def init_state(self):
+        _check(library().bb_engine_init_state(self._h), "bb_engine_init_state")
+
+    def run(self, t0: int, count: int, first_slot: int = -1, slot_step: int = 1,
+            mcmc_phase: int = 1):
+        _check(library().bb_engine_run(self._h, int(t0), int(count), int(first_slot),
+                                       int(slot_step), int(mcmc_phase)), "bb_engine_run")
+
+    def sync(self):
+        _check(library().bb_engine_sync(self._h), "bb_engine_sync")
+
+    def method(self) -> int:
+        return int(library().bb_engine_method(self._h))
+
+    def trace(self, slot0: int, count: int):
+        pl = self.p_local
+        beta = np.zeros((pl, count), order="F")
+        lam = np.zeros((pl, count), order="F")
+        sig2, tau, alpha = np.zeros(count), np.zeros(count), np.zeros(count)
+        _check(library().bb_engine_get_trace(self._h, slot0, count, _p(beta), _p(lam), _p(sig2),
+                                             _p(tau), _p(alpha)), "bb_engine_get_trace")
+        return dict(beta=beta, **{"lambda": lam}, sig2=sig2, tau=tau, alpha=alpha)
+
+    def state(self):
+        pl = self.p_local
+        beta, lam = np.zeros(pl), np.zeros(pl)
+        tau, sig2, alpha = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        _check(library().bb_engine_get_state(self._h, _p(beta), _p(lam), ctypes.byref(tau),
+                                             ctypes.byref(sig2), ctypes.byref(alpha)),
+               "bb_engine_get_state")
+        return dict(beta=beta, **{"lambda": lam}, tau=tau.value, sig2=sig2.value,
+                    alpha=alpha.value)
+
+    def set_state(self, beta, tau, sig2, alpha):
+        beta = np.ascontiguousarray(beta, dtype=np.float64)
+        _check(library().bb_engine_set_state(self._h, _p(beta), tau, sig2, alpha),
+               "bb_engine_set_state")
+
+    def enable_timing(self, on: bool = True):
+        library().bb_engine_enable_timing(self._h, 1 if on else 0)
+
+    def reset_timing(self):
+        library().bb_engine_reset_timing(self._h)
+
+    def kernel_times(self):
+        g, s, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _check(library().bb_engine_kernel_times(self._h, ctypes.byref(g), ctypes.byref(s),
+                                                ctypes.byref(n)), "bb_engine_kernel_times")
+        return g.value, s.value, n.value
+
+    def error_flags(self) -> int:
+        f = ctypes.c_uint32()
+        _check(library().bb_engine_error_flags(self._h, ctypes.byref(f)), "bb_engine_error_flags")
+        return int(f.value)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            library().bb_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

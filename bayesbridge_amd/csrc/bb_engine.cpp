@@ -1,0 +1,882 @@
+// bb_engine.cpp -- host side of the MI355X BayesBridge drop-in: the Gibbs driver
+// (restating Code/C/BridgeWrapper.cpp:207-313 and :434-537) over the HIP kernels of
+// bb_kernels.hip, RCCL for column-sharded multi-GPU runs, and the extern "C" entry
+// points declared in include/bayesbridge.h.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/bayesbridge.h"
+#include "bb_kernels.h"
+
+using namespace bb;
+
+namespace {
+
+thread_local std::string g_last_error;
+std::mutex g_mu;
+uint64_t g_seed = 0xB4E5B41D6EULL;
+uint64_t g_stream = 0;
+int g_device = 0;
+int g_verbose = 1;
+int g_use_r_rng = 1;
+
+void set_error(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPCHECK(x)                                                                       \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            char b_[512];                                                                 \
+            snprintf(b_, sizeof(b_), "HIP error %s at %s:%d: %s", hipGetErrorName(e_),    \
+                     __FILE__, __LINE__, #x);                                             \
+            throw HipError(b_);                                                           \
+        }                                                                                 \
+    } while (0)
+
+#define NCCLCHECK(x)                                                                      \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess) {                                                          \
+            char b_[512];                                                                 \
+            snprintf(b_, sizeof(b_), "RCCL error %s at %s:%d", ncclGetErrorString(r_),    \
+                     __FILE__, __LINE__);                                                 \
+            throw HipError(b_);                                                           \
+        }                                                                                 \
+    } while (0)
+
+inline int round_up(int x, int m) { return ((x + m - 1) / m) * m; }
+
+template <typename T>
+T *dalloc(size_t count, std::vector<void *> &owned) {
+    void *p = nullptr;
+    if (count == 0) count = 1;
+    HIPCHECK(hipMalloc(&p, count * sizeof(T)));
+    HIPCHECK(hipMemset(p, 0, count * sizeof(T)));
+    owned.push_back(p);
+    return (T *)p;
+}
+
+// R's RNG, resolved at run time when this library is loaded inside R.
+struct RRng {
+    void (*get)(void) = nullptr;
+    void (*put)(void) = nullptr;
+    double (*unif)(void) = nullptr;
+    bool tried = false;
+    bool ok() {
+        if (!tried) {
+            tried = true;
+            get = (void (*)(void))dlsym(RTLD_DEFAULT, "GetRNGstate");
+            put = (void (*)(void))dlsym(RTLD_DEFAULT, "PutRNGstate");
+            unif = (double (*)(void))dlsym(RTLD_DEFAULT, "unif_rand");
+        }
+        return get && put && unif;
+    }
+} g_rrng;
+
+// Key for one .C call: from R's RNG if present, else (seed, stream++).
+void next_call_key(uint64_t *k0, uint64_t *k1) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_use_r_rng && g_rrng.ok()) {
+        g_rrng.get();
+        uint64_t a = (uint64_t)(g_rrng.unif() * 4294967296.0);
+        uint64_t b = (uint64_t)(g_rrng.unif() * 4294967296.0);
+        uint64_t c = (uint64_t)(g_rrng.unif() * 4294967296.0);
+        g_rrng.put();
+        *k0 = (a << 32) ^ b;
+        *k1 = c;
+        return;
+    }
+    *k0 = g_seed;
+    *k1 = g_stream++;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Engine
+// ---------------------------------------------------------------------------
+struct bb_engine {
+    bb_config cfg{};
+    int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
+    int method = 0;  // 1 chol, 2 woodbury, 3 ortho
+    int group = 1;
+    Hyper hy{};
+    hipStream_t stream = nullptr;
+    std::vector<void *> owned;
+
+    double *X = nullptr, *y = nullptr;
+    double *beta = nullptr, *lam = nullptr, *D = nullptr, *u = nullptr;
+    DevScalars *sc = nullptr;
+    uint32_t *err = nullptr;
+    double *xb_part = nullptr, *red1 = nullptr;
+    int nparts = 0, nbS = 0;
+    // woodbury
+    double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *PT = nullptr,
+           *w = nullptr;
+    int S = 1;
+    size_t slab_stride = 0;
+    // chol / ortho
+    double *G = nullptr, *cvec = nullptr, *A = nullptr, *Y2 = nullptr, *W2 = nullptr,
+           *gdiag = nullptr;
+    // traces
+    double *tr_beta = nullptr, *tr_lam = nullptr, *tr_sig2 = nullptr, *tr_tau = nullptr,
+           *tr_alpha = nullptr;
+    int cap = 1;
+    // communicator
+    ncclComm_t comm = nullptr;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, int>> gram_pairs, sweep_pairs;
+    size_t ev_next = 0;
+
+    ~bb_engine() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (comm) ncclCommDestroy(comm);
+        for (auto e : ev_pool) (void)hipEventDestroy(e);
+        for (void *q : owned) (void)hipFree(q);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int ev() {
+        if (ev_next == ev_pool.size()) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreate(&e));
+            ev_pool.push_back(e);
+        }
+        return (int)ev_next++;
+    }
+
+    void allreduce(double *buf, size_t count) {
+        if (cfg.world <= 1) return;
+        if (!comm) throw HipError("world > 1 but no communicator (call bb_engine_comm_init)");
+        NCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, stream));
+    }
+
+    double *slot_ptr(double *base, int slot, int stride) {
+        if (slot < 0 || base == nullptr) return nullptr;
+        return base + (size_t)(slot % cap) * stride;
+    }
+
+    void pre_and_scalars(uint64_t t, int slot, int tau_only) {
+        launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
+        allreduce(red1, (size_t)nbS + n_pad);
+        launch_scalars(stream, red1, nbS, y, n, p, sc, hy, cfg.seed, cfg.stream, t,
+                       slot_ptr(tr_tau, slot, 1), slot_ptr(tr_sig2, slot, 1),
+                       slot_ptr(tr_alpha, slot, 1), tau_only, err);
+    }
+
+    void sweep(uint64_t t, int slot, int mcmc_phase) {
+        int e_sw0 = -1;
+        if (timing) {
+            e_sw0 = ev();
+            HIPCHECK(hipEventRecord(ev_pool[e_sw0], stream));
+        }
+        pre_and_scalars(t, slot, 0);
+        double *trl = slot_ptr(tr_lam, slot, p_loc);
+        double *trb = slot_ptr(tr_beta, slot, p_loc);
+        if (method == 2) {
+            launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
+                          t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            int eg0 = -1, eg1 = -1;
+            if (timing) {
+                eg0 = ev();
+                HIPCHECK(hipEventRecord(ev_pool[eg0], stream));
+            }
+            launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
+            if (timing) {
+                eg1 = ev();
+                HIPCHECK(hipEventRecord(ev_pool[eg1], stream));
+                gram_pairs.push_back({eg0, eg1});
+            }
+            launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
+            launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad), red2);
+            allreduce(red2, (size_t)n_pad * n_pad + n_pad);
+            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, PT);
+            chol_bsolve(stream, M, n_pad, n_pad, M + (size_t)n_pad * n_pad, w, 1);
+            launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
+        } else {
+            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
+                          group, lam, nullptr, nullptr, trl, err);
+            if (method == 1) {
+                launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
+                chol_factor(stream, A, p_pad, p_pad, 1, err, PT);
+                launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
+                chol_bsolve(stream, A, p_pad, p_pad, Y2, W2, 2);
+                launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
+            } else {
+                launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta,
+                                  trb);
+            }
+        }
+        launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
+        if (!hy.know_alpha) {
+            // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
+            // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
+            const double pr_a = (method != 3 && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
+            launch_alpha_mh(stream, beta, p, sc, pr_a, hy.alpha_b, cfg.seed, cfg.stream, t,
+                            slot_ptr(tr_alpha, slot, 1));
+        }
+        if (timing) {
+            int e_sw1 = ev();
+            HIPCHECK(hipEventRecord(ev_pool[e_sw1], stream));
+            sweep_pairs.push_back({e_sw0, e_sw1});
+        }
+    }
+
+    uint32_t read_err() {
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpyAsync(&f, err, sizeof(f), hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        return f;
+    }
+    void clear_err() { HIPCHECK(hipMemsetAsync(err, 0, sizeof(uint32_t), stream)); }
+};
+
+namespace {
+
+void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
+    const bb_config &c = e->cfg;
+    e->n = c.n;
+    e->p = c.p;
+    e->p_loc = c.p_local;
+    e->n_pad = round_up(c.n, kGramTile);
+    e->p_pad = round_up(c.p_local, 256);
+    e->cap = c.trace_capacity < 1 ? 1 : c.trace_capacity;
+    e->hy = Hyper{c.sig2_shape, c.sig2_scale, c.nu_shape, c.nu_rate, c.alpha_a, c.alpha_b,
+                  c.true_tau > 0, c.true_sig2 > 0, c.true_alpha > 0};
+    if (c.ortho) e->method = 3;
+    else if (c.method == 1 || (c.method == 0 && c.p <= c.n)) e->method = 1;
+    else e->method = 2;
+    if (c.world > 1 && e->method != 2)
+        throw HipError("column sharding (world > 1) is implemented for the Woodbury path only");
+    if (c.world > 1 && !e->hy.know_alpha)
+        throw HipError("unknown alpha with world > 1 is not supported");
+    if (e->method == 1 && c.p > 16384) throw HipError("p x p Cholesky path limited to p <= 16384");
+    if (e->method == 2 && e->n_pad > 8192)
+        throw HipError("Woodbury path limited to n <= 8192 in this build");
+
+    HIPCHECK(hipSetDevice(c.device));
+    HIPCHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    auto &o = e->owned;
+    const int n_pad = e->n_pad, p_pad = e->p_pad;
+    e->X = dalloc<double>((size_t)n_pad * p_pad, o);
+    HIPCHECK(hipMemcpy2D(e->X, (size_t)n_pad * sizeof(double), Xh, (size_t)c.n * sizeof(double),
+                         (size_t)c.n * sizeof(double), (size_t)c.p_local, hipMemcpyHostToDevice));
+    e->y = dalloc<double>(n_pad, o);
+    HIPCHECK(hipMemcpy(e->y, yh, (size_t)c.n * sizeof(double), hipMemcpyHostToDevice));
+    e->beta = dalloc<double>(p_pad, o);
+    e->lam = dalloc<double>(p_pad, o);
+    e->D = dalloc<double>(p_pad, o);
+    e->u = dalloc<double>(p_pad, o);
+    e->sc = dalloc<DevScalars>(1, o);
+    e->err = dalloc<uint32_t>(4, o);
+    e->nparts = xv_chunks(p_pad);
+    e->xb_part = dalloc<double>((size_t)e->nparts * n_pad, o);
+    e->nbS = pre_blocks_s(c.p_local);
+    e->red1 = dalloc<double>((size_t)e->nbS + n_pad, o);
+    e->group = stable_group_for(c.p_local);
+    e->tr_beta = dalloc<double>((size_t)c.p_local * e->cap, o);
+    e->tr_lam = dalloc<double>((size_t)c.p_local * e->cap, o);
+    e->tr_sig2 = dalloc<double>(e->cap, o);
+    e->tr_tau = dalloc<double>(e->cap, o);
+    e->tr_alpha = dalloc<double>(e->cap, o);
+
+    if (e->method == 2) {
+        e->S = gram_splits_for(n_pad, p_pad);
+        e->slab_stride = (size_t)n_pad * n_pad;
+        e->slabs = dalloc<double>(e->slab_stride * e->S, o);
+        e->xu_part = dalloc<double>((size_t)xv_chunks(p_pad) * n_pad, o);
+        e->red2 = dalloc<double>((size_t)n_pad * n_pad + n_pad, o);
+        e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
+        e->w = dalloc<double>(n_pad, o);
+    }
+    e->PT = dalloc<double>((size_t)kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
+    // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
+    const bool small = c.p <= c.n && c.world == 1;
+    if (e->method != 2 || small) {
+        e->cvec = dalloc<double>(p_pad, o);
+        launch_coldot(e->stream, e->X, n_pad, n_pad, e->y, c.p_local, e->cvec);
+        e->gdiag = dalloc<double>(p_pad, o);
+        if (small) {
+            // G = X'X: transpose X (n_pad x p_pad) into Xt (p_pad x n_pad), Gram over rows.
+            double *Xt = nullptr;
+            HIPCHECK(hipMalloc(&Xt, (size_t)p_pad * n_pad * sizeof(double)));
+            launch_transpose(e->stream, e->X, n_pad, n_pad, p_pad, Xt, p_pad);
+            double *ones = nullptr;
+            HIPCHECK(hipMalloc(&ones, (size_t)n_pad * sizeof(double)));
+            std::vector<double> h1(n_pad, 1.0);
+            HIPCHECK(hipMemcpyAsync(ones, h1.data(), n_pad * sizeof(double),
+                                    hipMemcpyHostToDevice, e->stream));
+            const int Sg = gram_splits_for(p_pad, n_pad);
+            double *sl = nullptr;
+            HIPCHECK(hipMalloc(&sl, (size_t)Sg * p_pad * p_pad * sizeof(double)));
+            launch_gram(e->stream, Xt, p_pad, ones, p_pad, n_pad, Sg, sl, p_pad,
+                        (size_t)p_pad * p_pad);
+            double *red = nullptr;
+            HIPCHECK(hipMalloc(&red, ((size_t)p_pad * p_pad + p_pad) * sizeof(double)));
+            launch_slab_sum(e->stream, sl, Sg, (size_t)p_pad * p_pad, p_pad, nullptr, 0, red);
+            e->G = dalloc<double>((size_t)p_pad * p_pad, o);
+            HIPCHECK(hipMemcpyAsync(e->G, red, (size_t)p_pad * p_pad * sizeof(double),
+                                    hipMemcpyDeviceToDevice, e->stream));
+            HIPCHECK(hipStreamSynchronize(e->stream));
+            (void)hipFree(Xt);
+            (void)hipFree(ones);
+            (void)hipFree(sl);
+            (void)hipFree(red);
+            launch_gdiag(e->stream, e->G, p_pad, c.p_local, e->gdiag);
+            e->A = dalloc<double>((size_t)p_pad * (p_pad + kNB), o);
+            e->Y2 = dalloc<double>((size_t)2 * p_pad, o);
+            e->W2 = dalloc<double>((size_t)2 * p_pad, o);
+        } else {
+            launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->gdiag);
+        }
+    }
+    HIPCHECK(hipStreamSynchronize(e->stream));
+}
+
+void engine_init_state(bb_engine *e) {
+    const bb_config &c = e->cfg;
+    // least squares start (BridgeWrapper.cpp:242-244, BridgeRegression.cpp:79-91)
+    bool ls_ok = false;
+    if (e->G != nullptr) {
+        e->clear_err();
+        launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, e->p_pad, e->A,
+                      e->p_pad, e->p_pad);
+        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT);
+        HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
+                                e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
+        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Y2, e->W2, 1);
+        uint32_t f = e->read_err();
+        ls_ok = (f & 8u) == 0;
+        if (ls_ok) {
+            HIPCHECK(hipMemcpyAsync(e->beta, e->W2, (size_t)e->p * sizeof(double),
+                                    hipMemcpyDeviceToDevice, e->stream));
+        }
+        e->clear_err();
+    }
+    if (!ls_ok) {
+        HIPCHECK(hipMemsetAsync(e->beta, 0, (size_t)e->p_pad * sizeof(double), e->stream));
+        if (g_verbose && c.rank == 0) {
+            printf("Warning: cannot calculate least squares estimate; X'X is singular.\n");
+            printf("Warning: setting least squares estimate to 0.0.\n");
+        }
+    }
+    DevScalars s{};
+    s.alpha = c.true_alpha > 0 ? c.true_alpha : 0.5;
+    s.sig2 = c.true_sig2 > 0 ? c.true_sig2 : 0.0;
+    s.tau = c.true_tau > 0 ? c.true_tau : 0.0;
+    HIPCHECK(hipMemcpyAsync(e->sc, &s, sizeof(s), hipMemcpyHostToDevice, e->stream));
+    // trace slot 0 holds the starting values (as the reference's slot 0 before burn-in)
+    HIPCHECK(hipMemcpyAsync(e->tr_beta, e->beta, (size_t)e->p_loc * sizeof(double),
+                            hipMemcpyDeviceToDevice, e->stream));
+    launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
+    if (e->method != 3 && !e->hy.know_tau) e->pre_and_scalars(0, 0, 1);  // :262
+    else launch_record_scalars(e->stream, e->sc, e->tr_tau, e->tr_sig2, e->tr_alpha);
+    HIPCHECK(hipStreamSynchronize(e->stream));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *bb_version(void) { return "bayesbridge_amd 0.1 (gfx950)"; }
+const char *bb_last_error(void) { return g_last_error.c_str(); }
+
+int bb_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void bb_set_seed(uint64_t seed) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_seed = seed;
+    g_stream = 0;
+}
+void bb_get_rng_state(uint64_t *seed, uint64_t *stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (seed) *seed = g_seed;
+    if (stream) *stream = g_stream;
+}
+void bb_set_rng_state(uint64_t seed, uint64_t stream) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_seed = seed;
+    g_stream = stream;
+}
+void bb_use_r_rng(int enable) { g_use_r_rng = enable; }
+int bb_set_device(int device) {
+    if (device < 0 || device >= bb_device_count()) {
+        set_error("invalid device %d", device);
+        return -1;
+    }
+    g_device = device;
+    return 0;
+}
+void bb_set_verbose(int verbose) { g_verbose = verbose; }
+
+void bb_config_default(bb_config *c) {
+    memset(c, 0, sizeof(*c));
+    c->world = 1;
+    c->sig2_shape = 0.0;
+    c->sig2_scale = 0.0;
+    c->nu_shape = 2.0;
+    c->nu_rate = 2.0;
+    c->alpha_a = 1.0;
+    c->alpha_b = 1.0;
+    c->true_alpha = 0.5;
+    c->trace_capacity = 1;
+    c->seed = 0xB4E5B41D6EULL;
+}
+
+int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
+                     bb_engine **out) {
+    *out = nullptr;
+    bb_engine *e = new bb_engine();
+    try {
+        e->cfg = *cfg;
+        if (e->cfg.p_local <= 0) e->cfg.p_local = e->cfg.p;
+        if (e->cfg.world < 1) e->cfg.world = 1;
+        if (cfg->n <= 0 || cfg->p <= 0) throw HipError("n and p must be positive");
+        engine_setup(e, X_local, y);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        delete e;
+        return -1;
+    }
+    *out = e;
+    return 0;
+}
+
+void bb_engine_destroy(bb_engine *e) { delete e; }
+
+int bb_comm_id_size(void) { return (int)sizeof(ncclUniqueId); }
+int bb_comm_unique_id(void *id_bytes) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+        set_error("ncclGetUniqueId failed");
+        return -1;
+    }
+    memcpy(id_bytes, &id, sizeof(id));
+    return 0;
+}
+int bb_engine_comm_init(bb_engine *e, const void *id_bytes) {
+    try {
+        HIPCHECK(hipSetDevice(e->cfg.device));
+        ncclUniqueId id;
+        memcpy(&id, id_bytes, sizeof(id));
+        NCCLCHECK(ncclCommInitRank(&e->comm, e->cfg.world, id, e->cfg.rank));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_init_state(bb_engine *e) {
+    try {
+        HIPCHECK(hipSetDevice(e->cfg.device));
+        engine_init_state(e);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_run(bb_engine *e, uint64_t t0, int count, int first_slot, int slot_step,
+                  int mcmc_phase) {
+    try {
+        HIPCHECK(hipSetDevice(e->cfg.device));
+        for (int k = 0; k < count; ++k) {
+            const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
+            e->sweep(t0 + (uint64_t)k, slot, mcmc_phase);
+        }
+        HIPCHECK(hipGetLastError());
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_sync(bb_engine *e) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_get_trace(bb_engine *e, int slot0, int count, double *beta, double *lambda,
+                        double *sig2, double *tau, double *alpha) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        for (int k = 0; k < count; ++k) {
+            const int s = (slot0 + k) % e->cap;
+            const size_t pl = (size_t)e->p_loc;
+            if (beta)
+                HIPCHECK(hipMemcpy(beta + k * pl, e->tr_beta + s * pl, pl * sizeof(double),
+                                   hipMemcpyDeviceToHost));
+            if (lambda)
+                HIPCHECK(hipMemcpy(lambda + k * pl, e->tr_lam + s * pl, pl * sizeof(double),
+                                   hipMemcpyDeviceToHost));
+            if (sig2)
+                HIPCHECK(hipMemcpy(sig2 + k, e->tr_sig2 + s, sizeof(double), hipMemcpyDeviceToHost));
+            if (tau)
+                HIPCHECK(hipMemcpy(tau + k, e->tr_tau + s, sizeof(double), hipMemcpyDeviceToHost));
+            if (alpha)
+                HIPCHECK(
+                    hipMemcpy(alpha + k, e->tr_alpha + s, sizeof(double), hipMemcpyDeviceToHost));
+        }
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_get_state(bb_engine *e, double *beta, double *lambda, double *tau, double *sig2,
+                        double *alpha) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        if (beta)
+            HIPCHECK(hipMemcpy(beta, e->beta, (size_t)e->p_loc * sizeof(double),
+                               hipMemcpyDeviceToHost));
+        if (lambda)
+            HIPCHECK(hipMemcpy(lambda, e->lam, (size_t)e->p_loc * sizeof(double),
+                               hipMemcpyDeviceToHost));
+        DevScalars s;
+        HIPCHECK(hipMemcpy(&s, e->sc, sizeof(s), hipMemcpyDeviceToHost));
+        if (tau) *tau = s.tau;
+        if (sig2) *sig2 = s.sig2;
+        if (alpha) *alpha = s.alpha;
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig2,
+                        double alpha) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        HIPCHECK(hipMemcpy(e->beta, beta, (size_t)e->p_loc * sizeof(double),
+                           hipMemcpyHostToDevice));
+        DevScalars s;
+        HIPCHECK(hipMemcpy(&s, e->sc, sizeof(s), hipMemcpyDeviceToHost));
+        s.tau = tau;
+        s.sig2 = sig2;
+        s.alpha = alpha;
+        HIPCHECK(hipMemcpy(e->sc, &s, sizeof(s), hipMemcpyHostToDevice));
+        launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
+        HIPCHECK(hipStreamSynchronize(e->stream));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_method(const bb_engine *e) { return e->method; }
+
+int bb_engine_enable_timing(bb_engine *e, int enable) {
+    e->timing = enable != 0;
+    return 0;
+}
+
+int bb_engine_reset_timing(bb_engine *e) {
+    (void)hipStreamSynchronize(e->stream);
+    e->gram_pairs.clear();
+    e->sweep_pairs.clear();
+    e->ev_next = 0;
+    return 0;
+}
+
+int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
+                           int *samples) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        double g = 0, s = 0;
+        for (auto &pr : e->gram_pairs) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, e->ev_pool[pr.first], e->ev_pool[pr.second]));
+            g += ms;
+        }
+        for (auto &pr : e->sweep_pairs) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, e->ev_pool[pr.first], e->ev_pool[pr.second]));
+            s += ms;
+        }
+        if (gram_ms_avg) *gram_ms_avg = e->gram_pairs.empty() ? 0.0 : g / e->gram_pairs.size();
+        if (sweep_ms_avg)
+            *sweep_ms_avg = e->sweep_pairs.empty() ? 0.0 : s / e->sweep_pairs.size();
+        if (samples) *samples = (int)e->sweep_pairs.size();
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_error_flags(bb_engine *e, uint32_t *flags) {
+    try {
+        *flags = e->read_err();
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// kernel-level entry points
+// ---------------------------------------------------------------------------
+int bb_retstable_batch(double *x, const double *alpha, const double *V0, const double *h, int num,
+                       uint64_t seed, uint64_t stream, uint64_t t, int group) {
+    if (num <= 0) return 0;
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        double *da = dalloc<double>(num, owned), *dv = dalloc<double>(num, owned),
+               *dh = dalloc<double>(num, owned), *dx = dalloc<double>(num, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        HIPCHECK(hipMemcpy(da, alpha, num * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dv, V0, num * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dh, h, num * sizeof(double), hipMemcpyHostToDevice));
+        if (group <= 0) group = stable_group_for(num);
+        launch_retstable_batch(0, dx, da, dv, dh, num, seed, stream, t, group, de);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(x, dx, num * sizeof(double), hipMemcpyDeviceToHost));
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+        if (f & 4u) {
+            fprintf(stderr, "Problem with parameter.\n");  // retstable.cpp:112-115
+        }
+        rc = (int)(f & ~4u) ? -2 : 0;
+        if (rc) set_error("retstable: rejection cap reached (flags %u)", f);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, double tau,
+                     uint64_t seed, uint64_t stream, uint64_t t, uint64_t j0, int group) {
+    if (p <= 0) return 0;
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        double *db = dalloc<double>(p, owned), *dl = dalloc<double>(p, owned);
+        DevScalars *dsc = dalloc<DevScalars>(1, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        DevScalars s{};
+        s.tau = tau;
+        s.alpha = alpha;
+        HIPCHECK(hipMemcpy(dsc, &s, sizeof(s), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(db, beta, p * sizeof(double), hipMemcpyHostToDevice));
+        if (group <= 0) group = stable_group_for(p);
+        launch_lambda(0, db, p, p, j0, dsc, seed, stream, t, LAMBDA_ONLY, group, dl, nullptr,
+                      nullptr, nullptr, de);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(lambda, dl, p * sizeof(double), hipMemcpyDeviceToHost));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_gram(double *C, const double *Yh, const double *wh, int n, int k) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile);
+        const int k_pad = round_up(k, 256);
+        double *dY = dalloc<double>((size_t)n_pad * k_pad, owned);
+        double *dw = dalloc<double>(k_pad, owned);
+        HIPCHECK(hipMemcpy2D(dY, (size_t)n_pad * sizeof(double), Yh, (size_t)n * sizeof(double),
+                             (size_t)n * sizeof(double), (size_t)k, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dw, wh, (size_t)k * sizeof(double), hipMemcpyHostToDevice));
+        const int S = gram_splits_for(n_pad, k_pad);
+        const size_t stride = (size_t)n_pad * n_pad;
+        double *sl = dalloc<double>(stride * S, owned);
+        double *red = dalloc<double>(stride + n_pad, owned);
+        launch_gram(0, dY, n_pad, dw, n_pad, k_pad, S, sl, n_pad, stride);
+        launch_slab_sum(0, sl, S, stride, n_pad, nullptr, 0, red);
+        HIPCHECK(hipGetLastError());
+        std::vector<double> h(stride);
+        HIPCHECK(hipMemcpy(h.data(), red, stride * sizeof(double), hipMemcpyDeviceToHost));
+        for (int c = 0; c < n; ++c)
+            for (int r = 0; r < n; ++r)
+                C[(size_t)r + (size_t)c * n] =
+                    r <= c ? h[(size_t)r + (size_t)c * n_pad] : h[(size_t)c + (size_t)r * n_pad];
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        if (nrhs < 1 || nrhs > 2) throw HipError("nrhs must be 1 or 2");
+        HIPCHECK(hipSetDevice(g_device));
+        const int m_pad = round_up(m, kNB);
+        double *dA = dalloc<double>((size_t)m_pad * (m_pad + kNB), owned);
+        // identity padding, then the user block and the RHS (forward-solved in place)
+        std::vector<double> h((size_t)m_pad * (m_pad + kNB), 0.0);
+        for (int c = 0; c < m_pad; ++c)
+            for (int r = 0; r <= c; ++r)
+                h[(size_t)r + (size_t)c * m_pad] =
+                    (r < m && c < m) ? Ah[(size_t)r + (size_t)c * m] : (r == c ? 1.0 : 0.0);
+        for (int q = 0; q < nrhs; ++q)
+            for (int r = 0; r < m; ++r) h[(size_t)r + (size_t)(m_pad + q) * m_pad] = bh[r + (size_t)q * m];
+        HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        double *PT = dalloc<double>((size_t)kNB * (m_pad + kNB), owned);
+        double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        chol_factor(0, dA, m_pad, m_pad, 1, de, PT);
+        chol_bsolve(0, dA, m_pad, m_pad, dA + (size_t)m_pad * m_pad, W, nrhs);
+        HIPCHECK(hipGetLastError());
+        std::vector<double> hw((size_t)m_pad * nrhs);
+        HIPCHECK(hipMemcpy(hw.data(), W, hw.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int q = 0; q < nrhs; ++q)
+            for (int r = 0; r < m; ++r) x[r + (size_t)q * m] = hw[r + (size_t)q * m_pad];
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+        if (f & 8u) {
+            set_error("matrix is not positive definite");
+            rc = -3;
+        }
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Reference .C entry points
+// ---------------------------------------------------------------------------
+void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num) {
+    uint64_t k0, k1;
+    next_call_key(&k0, &k1);
+    int rc = bb_retstable_batch(x, alpha, V0, h, *num, k0, k1, 0, 0);
+    if (rc != 0) fprintf(stderr, "Error: retstable_LD: %s\n", g_last_error.c_str());
+}
+
+void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,
+                       double *alphap, const double *yp, const double *Xp,
+                       const double *sig2_shape, const double *sig2_scale,
+                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                       const double *alpha_b, const double *true_sig2, const double *true_tau,
+                       const double *true_alpha, const int *P, const int *N, const int *M,
+                       const int *burn, double *runtime, const int *ortho) {
+    const int p = *P, n = *N, m = *M, b = *burn;
+    bb_config c;
+    bb_config_default(&c);
+    c.n = n;
+    c.p = p;
+    c.p_local = p;
+    c.sig2_shape = *sig2_shape;
+    c.sig2_scale = *sig2_scale;
+    c.nu_shape = *nu_shape;
+    c.nu_rate = *nu_rate;
+    c.alpha_a = *alpha_a;
+    c.alpha_b = *alpha_b;
+    c.true_sig2 = *true_sig2;
+    c.true_tau = *true_tau;
+    c.true_alpha = *true_alpha;
+    c.ortho = *ortho != 0;
+    c.trace_capacity = m < 1 ? 1 : m;
+    c.device = g_device;
+    next_call_key(&c.seed, &c.stream);
+    const bool know_sig2 = c.true_sig2 > 0, know_tau = c.true_tau > 0, know_alpha = c.true_alpha > 0;
+    if (g_verbose) {  // BridgeWrapper.cpp:235-240
+        printf("Bridge Regression (mix. of normals):");
+        if (know_alpha) printf(" known alpha=%g", c.true_alpha);
+        if (know_sig2) printf(", sig2=%g", c.true_sig2);
+        if (know_tau) printf(", tau=%g", c.true_tau);
+        if (c.ortho) printf("\nAssuming orthogonal design matrix!");
+        printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
+    }
+    bb_engine *e = nullptr;
+    if (bb_engine_create(&c, Xp, yp, &e) != 0) {
+        printf("Error: %s\n", g_last_error.c_str());
+        printf("Aborting Gibbs sampler.\n");
+        *runtime = 0.0;
+        return;
+    }
+    double rt = 0.0;
+    bool ok = bb_engine_init_state(e) == 0;
+    if (ok) {
+        auto t0 = std::chrono::steady_clock::now();
+        ok = bb_engine_run(e, 1, b + 1, 0, 0, 0) == 0 && bb_engine_sync(e) == 0;
+        auto t1 = std::chrono::steady_clock::now();
+        if (g_verbose && ok) {
+            double bt = std::chrono::duration<double>(t1 - t0).count();
+            printf("Burn-in complete: %g sec. for %i iterations.\n", bt, b);
+            if (b > 0) printf("Expect approx. %g sec. for %i samples.\n", bt * m / b, m);
+        }
+        auto t2 = std::chrono::steady_clock::now();
+        if (ok && m > 1) ok = bb_engine_run(e, (uint64_t)b + 2, m - 1, 1, 1, 1) == 0;
+        ok = (bb_engine_sync(e) == 0) && ok;
+        auto t3 = std::chrono::steady_clock::now();
+        rt = std::chrono::duration<double>(t3 - t2).count();
+        uint32_t f = 0;
+        if (ok && bb_engine_error_flags(e, &f) == 0 && (f & ~4u)) {
+            printf("Error: numerical failure in the device sampler (flags %u)\n", f);
+            printf("Aborting Gibbs sampler.\n");
+        }
+    }
+    if (!ok) {
+        printf("Error: %s\n", g_last_error.c_str());
+        printf("Aborting Gibbs sampler.\n");
+    }
+    bb_engine_get_trace(e, 0, m, betap, lambdap, sig2p, taup, alphap);
+    if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
+    *runtime = rt;
+    bb_engine_destroy(e);
+}
+
+}  // extern "C"

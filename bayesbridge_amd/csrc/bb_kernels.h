@@ -1,0 +1,129 @@
+// bb_kernels.h -- host-side launch wrappers for the gfx950 kernels of the stable sweep.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bb {
+
+struct Key;
+
+// Chain scalars kept on the device (read by kernels, written by the scalar draws).
+struct DevScalars {
+    double tau, sig2, alpha;
+    double s_abs_pow;  // last sum |beta|^alpha (diagnostic)
+    double rss;        // last residual sum of squares (diagnostic)
+    double pad[3];
+};
+
+// Hyper-parameters of bridge.reg.stb (BridgeWrapper.R:194-201).
+struct Hyper {
+    double sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a, alpha_b;
+    int know_tau, know_sig2, know_alpha;
+};
+
+constexpr int kGramTile = 128;  // Gram output tile (rows of X per tile)
+constexpr int kGramBK = 16;     // Gram K step
+constexpr int kNB = 64;         // Cholesky block
+constexpr int kXvCols = 256;    // columns per block of the X.v partial-sum kernel
+constexpr int kXvRows = 512;    // rows per block of the X.v partial-sum kernel
+
+enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
+
+// Number of lanes cooperating on one tilted-stable draw for a problem of `count` draws.
+int stable_group_for(long count);
+
+void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const double *V0,
+                            const double *h, int num, uint64_t k0, uint64_t k1, uint64_t t,
+                            int group, uint32_t *err);
+
+void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                   const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int mode,
+                   int group, double *lam, double *D, double *u, double *lam_trace,
+                   uint32_t *err);
+
+// slabs[s] (ld = ldo) gets the upper triangle (column-major) of Y diag(w) Y' over
+// K-range s; Y is n_pad x K column-major with ld = ldy (n_pad multiple of 128).
+int gram_splits_for(int n_pad, int K);
+void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n_pad, int K,
+                 int S, double *slabs, int ldo, size_t slab_stride);
+
+// part[cb * n_pad + r] = sum over columns j of chunk cb of X[r, j] * v[j].
+int xv_chunks(int ncols);
+void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
+               double *part);
+
+// red1 = [S_alpha partials (nbS) | sum_q part[q] (n_pad)].
+int pre_blocks_s(int p_loc);
+void launch_pre(hipStream_t s, const double *part, int nparts, int n_pad, const double *beta,
+                int p_loc, const DevScalars *sc, double *red1, int nbS);
+
+// tau / sig2 draws from red1 (tau_only: initial draw at t = 0).
+void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y, int n,
+                    int p, DevScalars *sc, Hyper hy, uint64_t k0, uint64_t k1, uint64_t t,
+                    double *tau_tr, double *sig2_tr, double *alpha_tr, int tau_only,
+                    uint32_t *err);
+
+// red2 = [sum_s slabs (upper, n_pad^2) | sum_q xu_part (n_pad)].
+void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
+                     const double *xu_part, int nxu, double *red2);
+
+// M (upper, ld = ldm) = I + red2 / sig2; column rhs_col = y/sig - (xu/sig + delta).
+void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,
+                   const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *M,
+                   int ldm, int rhs_col);
+
+// A (upper) = G + diag(lambda sig2 / tau^2) (or G alone if lam == nullptr); column
+// rhs_col = c.  Padding: identity.
+void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
+                   const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
+                   int rhs_col);
+
+// In-place upper Cholesky A = U'U of the leading m_pad x m_pad block with the
+// forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
+// PT: scratch of kNB x (m_pad + nrhs_blocks * kNB) doubles.
+void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
+                 double *PT);
+
+// Backward solve U W = Y (Y, W: m_pad x nrhs, ld = m_pad); Y is overwritten.
+void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, double *Y, double *W,
+                 int nrhs);
+
+// beta_j = u_j + D_j (X_j . w) / sig (Woodbury update); writes beta and trace.
+void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,
+                          const double *u, const double *D, const DevScalars *sc, int p_loc,
+                          double *beta, double *beta_trace);
+
+// Build the 2-RHS backward-solve input [U'^-1 c | z] (chol path).
+void launch_chol_rhs(hipStream_t s, const double *A, int lda, int rhs_col, int p, int p_pad,
+                     uint64_t k0, uint64_t k1, uint64_t t, double *Y2);
+
+// beta = m + sqrt(sig2) x (chol path) from W2 = [m | x].
+void launch_beta_chol(hipStream_t s, const double *W2, int p_pad, const DevScalars *sc, int p,
+                      double *beta, double *beta_trace);
+
+// Orthogonal design: beta_i ~ N(c_i/u_i, sig2/u_i), u_i = G_ii + lambda_i sig2/tau^2.
+void launch_beta_ortho(hipStream_t s, const double *gdiag, const double *c, const double *lam,
+                       const DevScalars *sc, int p, uint64_t k0, uint64_t k1, uint64_t t,
+                       double *beta, double *beta_trace);
+
+// alpha | beta, tau random-walk MH (world == 1).
+void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, double pr_a,
+                     double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr);
+
+// Copy the scalars into trace slots (known parameters / alpha when known).
+void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
+                           double *sig2_tr, double *alpha_tr);
+
+// Element-wise helpers.
+void launch_copy_cols(hipStream_t s, const double *src, int lds, double *dst, int ldd, int rows,
+                      int cols);
+void launch_gdiag(hipStream_t s, const double *G, int ldg, int p, double *d);
+void launch_sum_into(hipStream_t s, const double *a, double *b, size_t n);
+void launch_transpose(hipStream_t s, const double *src, int lds, int rows, int cols, double *dst,
+                      int ldd);
+void launch_coldot(hipStream_t s, const double *X, int ldx, int n_pad, const double *v, int ncols,
+                   double *out);
+void launch_colnorm2(hipStream_t s, const double *X, int ldx, int n_pad, int ncols, double *out);
+
+}  // namespace bb

@@ -1,0 +1,956 @@
+// bb_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the BayesBridge stable Gibbs sweep.
+//
+// Reference call sites replaced (Code/C/...):
+//   retstable.cpp:94-271 / BridgeRegression.cpp:506-510   -> k_retstable_batch, k_lambda
+//   BridgeRegression.cpp:436-465 (sig2, tau)               -> k_pre, k_scalars
+//   BridgeRegression.cpp:552-575 (beta, p x p Cholesky)    -> k_form_a, chol_*, k_chol_rhs,
+//                                                             k_beta_chol
+//   beta | rest for p > n (Woodbury form of the same law)  -> k_gram, k_xv, k_slab_sum,
+//                                                             k_form_m, chol_*, k_beta_wb
+//   BridgeRegression.cpp:514-521 (ortho)                   -> k_beta_ortho
+//   BridgeRegression.cpp:469-503 (alpha MH)                -> k_alpha_mh
+//   BridgeRegression.cpp:24-25 (X'X, X'y setup)            -> k_transpose + k_gram, k_coldot
+//
+// Layout: X is column-major n_pad x p_pad (n_pad multiple of 128, zero padded rows and
+// columns).  Symmetric matrices keep their UPPER triangle in column-major storage, the
+// reference's chol(U, VInv, 'U') convention (A = U'U).
+#include <hip/hip_runtime.h>
+
+#include "bb_kernels.h"
+#include "bb_sampler.h"
+
+namespace bb {
+
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// reductions (deterministic: fixed tree per launch geometry)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;  // lane 0
+}
+
+__device__ __forceinline__ double wave_allsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double *sh) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < NT / 64; ++i) r += sh[i];
+    }
+    __syncthreads();
+    return r;  // thread 0
+}
+
+// ---------------------------------------------------------------------------
+// tilted stable draws
+// ---------------------------------------------------------------------------
+int stable_group_for(long count) {
+    long target = 131072;  // lanes worth of attempts in flight (256 CUs x 4 SIMD x 2 x 64)
+    long g = 1;
+    while (g < 64 && count * g * 2 <= target) g *= 2;
+    return (int)g;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_retstable_batch(double *x, const double *alpha,
+                                                         const double *V0, const double *h,
+                                                         int num, Key key, uint64_t t,
+                                                         uint32_t *err) {
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const long i = gid / G;
+    const bool active = i < num;
+    const double hh = active ? h[i] : 0.0;
+    const double aa = active ? alpha[i] : 0.5;
+    const double vv = active ? V0[i] : 1.0;
+    double r = stable_group_draw<G>(active, hh, aa, vv, key, t, (uint64_t)i, err);
+    if (active && (threadIdx.x & (G - 1)) == 0) x[i] = r;
+}
+
+void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const double *V0,
+                            const double *h, int num, uint64_t k0, uint64_t k1, uint64_t t,
+                            int group, uint32_t *err) {
+    if (num <= 0) return;
+    Key key{k0, k1};
+    long threads = (long)num * group;
+    int blocks = (int)((threads + 255) / 256);
+    switch (group) {
+#define BB_CASE(G)                                                                           \
+    case G:                                                                                  \
+        k_retstable_batch<G><<<blocks, 256, 0, s>>>(x, alpha, V0, h, num, key, t, err);     \
+        break;
+        BB_CASE(1) BB_CASE(2) BB_CASE(4) BB_CASE(8) BB_CASE(16) BB_CASE(32) BB_CASE(64)
+#undef BB_CASE
+        default:
+            k_retstable_batch<1><<<(num + 255) / 256, 256, 0, s>>>(x, alpha, V0, h, num, key, t,
+                                                                   err);
+    }
+}
+
+// lambda_j = 2 retstable(beta_j^2 / tau^2, alpha / 2, 1)   (BridgeRegression.cpp:506-510);
+// Woodbury mode also forms D_j = tau^2 / lambda_j and u_j = sqrt(D_j) z_j.
+template <int G>
+__global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, int p_pad,
+                                                uint64_t j0, const DevScalars *sc, Key key,
+                                                uint64_t t, int mode, double *lam, double *D,
+                                                double *u, double *lam_trace, uint32_t *err) {
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const long i = gid / G;
+    const bool active = i < p_loc;
+    const double tau = sc->tau;
+    const double alpha = sc->alpha;
+    const double b = active ? beta[i] : 0.0;
+    const double h = b * b / (tau * tau);
+    double x = stable_group_draw<G>(active, h, 0.5 * alpha, 1.0, key, t, j0 + (uint64_t)i, err);
+    if ((threadIdx.x & (G - 1)) == 0 && i < p_pad) {
+        if (active) {
+            const double l = 2 * x;
+            lam[i] = l;
+            if (lam_trace) lam_trace[i] = l;
+            if (mode == LAMBDA_WOODBURY) {
+                const double d = (tau * tau) / l;
+                D[i] = d;
+                u[i] = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
+            }
+        } else {
+            lam[i] = 1.0;
+            if (mode == LAMBDA_WOODBURY) {
+                D[i] = 0.0;
+                u[i] = 0.0;
+            }
+        }
+    }
+}
+
+void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                   const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int mode,
+                   int group, double *lam, double *D, double *u, double *lam_trace,
+                   uint32_t *err) {
+    Key key{k0, k1};
+    long threads = (long)p_pad * group;
+    int blocks = (int)((threads + 255) / 256);
+    switch (group) {
+#define BB_CASE(G)                                                                            \
+    case G:                                                                                   \
+        k_lambda<G><<<blocks, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,  \
+                                           u, lam_trace, err);                                \
+        break;
+        BB_CASE(1) BB_CASE(2) BB_CASE(4) BB_CASE(8) BB_CASE(16) BB_CASE(32) BB_CASE(64)
+#undef BB_CASE
+        default:
+            k_lambda<1><<<(p_pad + 255) / 256, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
+                                                            mode, lam, D, u, lam_trace, err);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Gram: slabs[s] = Y[:, Ks] diag(w[Ks]) Y[:, Ks]'  with v_mfma_f64_16x16x4_f64.
+// Block = one 128x128 lower tile (I >= J) x one K split; 4 waves in 2x2, each wave
+// 64x64 = 4x4 MFMA tiles.  Y tiles staged through LDS as [k][row] (row contiguous,
+// ld 144 so that the two 16-lane halves of a ds_read_b64 group hit disjoint banks);
+// w is applied while staging the B operand.  Output tile D[i][j] is stored transposed
+// at (J*128+j, I*128+i) -> upper triangle of a column-major matrix, coalesced.
+// Split s = blockIdx % S so that all blocks of one split share an XCD (and its L2).
+// ---------------------------------------------------------------------------
+constexpr int kGLD = 144;
+
+__global__ __launch_bounds__(256, 2) void k_gram(const double *__restrict__ Y, int ldy,
+                                                 const double *__restrict__ w, int K, int S,
+                                                 double *__restrict__ out, int ldo,
+                                                 size_t slab_stride) {
+    __shared__ double As[kGramBK * kGLD];
+    __shared__ double Bs[kGramBK * kGLD];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int s = blockIdx.x % S;
+    const int tile = blockIdx.x / S;
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int J = tile - I * (I + 1) / 2;
+    const int kchunk = K / S;
+    const int kb = s * kchunk, ke = kb + kchunk;
+    const double *Ya = Y + (size_t)I * kGramTile;
+    const double *Yb = Y + (size_t)J * kGramTile;
+    const int lr = (tid & 63) * 2;
+    const int lk = tid >> 6;
+    double2 ra[4], rb[4];
+    double wk[4];
+    v4d acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = (v4d){0.0, 0.0, 0.0, 0.0};
+    const int wr = wid >> 1, wc = wid & 1;
+
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + lk + 4 * q;
+            ra[q] = *(const double2 *)(Ya + lr + (size_t)k * ldy);
+            rb[q] = *(const double2 *)(Yb + lr + (size_t)k * ldy);
+            wk[q] = w[k];
+        }
+    };
+    auto sstore = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int kk = lk + 4 * q;
+            *(double2 *)(As + kk * kGLD + lr) = ra[q];
+            double2 b = rb[q];
+            b.x *= wk[q];
+            b.y *= wk[q];
+            *(double2 *)(Bs + kk * kGLD + lr) = b;
+        }
+    };
+
+    if (kb < ke) {
+        gload(kb);
+        sstore();
+        __syncthreads();
+        for (int k0 = kb; k0 < ke; k0 += kGramBK) {
+            const bool more = (k0 + kGramBK) < ke;
+            if (more) gload(k0 + kGramBK);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const int krow = kk * 4 + (lane >> 4);
+                double a[4], b[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) a[m] = As[krow * kGLD + wr * 64 + m * 16 + (lane & 15)];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) b[m] = Bs[krow * kGLD + wc * 64 + m * 16 + (lane & 15)];
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                    for (int nj = 0; nj < 4; ++nj)
+                        acc[mi][nj] =
+                            __builtin_amdgcn_mfma_f64_16x16x4f64(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
+            }
+            __syncthreads();
+            if (more) {
+                sstore();
+                __syncthreads();
+            }
+        }
+    }
+    double *o = out + (size_t)s * slab_stride;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = wr * 64 + mi * 16 + (lane >> 4) + 4 * r;
+                const int j = wc * 64 + nj * 16 + (lane & 15);
+                o[(size_t)(J * kGramTile + j) + (size_t)(I * kGramTile + i) * ldo] = acc[mi][nj][r];
+            }
+}
+
+int gram_splits_for(int n_pad, int K) {
+    const int nt = n_pad / kGramTile;
+    const int tiles = nt * (nt + 1) / 2;
+    int S = 1;
+    // aim for >= 4 blocks per CU, keep >= 8 K-steps per split, K % (16 S) == 0
+    while (S < 64 && tiles * S < 1024 && (K % (kGramBK * S * 2)) == 0 &&
+           K / (S * 2) >= 8 * kGramBK)
+        S *= 2;
+    return S;
+}
+
+void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n_pad, int K,
+                 int S, double *slabs, int ldo, size_t slab_stride) {
+    const int nt = n_pad / kGramTile;
+    const int tiles = nt * (nt + 1) / 2;
+    k_gram<<<tiles * S, 256, 0, s>>>(Y, ldy, w, K, S, slabs, ldo, slab_stride);
+}
+
+// ---------------------------------------------------------------------------
+// X.v partial sums: part[cb][r] = sum_{j in chunk cb} X[r, j] v[j] (column order).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_xv(const double *__restrict__ X, int ldx,
+                                            const double *__restrict__ v, int ncols, int n_pad,
+                                            double *__restrict__ part) {
+    __shared__ double vs[kXvCols];
+    const int cb = blockIdx.x, rb = blockIdx.y;
+    const int c0 = cb * kXvCols;
+    const int nc = min(kXvCols, ncols - c0);
+    for (int i = threadIdx.x; i < kXvCols; i += 256) vs[i] = (i < nc) ? v[c0 + i] : 0.0;
+    __syncthreads();
+    const int r = rb * kXvRows + 2 * threadIdx.x;
+    if (r >= n_pad) return;
+    const double *xp = X + (size_t)c0 * ldx + r;
+    double ax = 0.0, ay = 0.0;
+    int j = 0;
+    for (; j + 4 <= nc; j += 4) {
+        double2 x0 = *(const double2 *)(xp + (size_t)(j + 0) * ldx);
+        double2 x1 = *(const double2 *)(xp + (size_t)(j + 1) * ldx);
+        double2 x2 = *(const double2 *)(xp + (size_t)(j + 2) * ldx);
+        double2 x3 = *(const double2 *)(xp + (size_t)(j + 3) * ldx);
+        ax += x0.x * vs[j];
+        ay += x0.y * vs[j];
+        ax += x1.x * vs[j + 1];
+        ay += x1.y * vs[j + 1];
+        ax += x2.x * vs[j + 2];
+        ay += x2.y * vs[j + 2];
+        ax += x3.x * vs[j + 3];
+        ay += x3.y * vs[j + 3];
+    }
+    for (; j < nc; ++j) {
+        double2 x0 = *(const double2 *)(xp + (size_t)j * ldx);
+        ax += x0.x * vs[j];
+        ay += x0.y * vs[j];
+    }
+    *(double2 *)(part + (size_t)cb * n_pad + r) = make_double2(ax, ay);
+}
+
+int xv_chunks(int ncols) { return (ncols + kXvCols - 1) / kXvCols; }
+
+void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
+               double *part) {
+    dim3 grid(xv_chunks(ncols), (n_pad + kXvRows - 1) / kXvRows);
+    k_xv<<<grid, 256, 0, s>>>(X, ldx, v, ncols, n_pad, part);
+}
+
+// ---------------------------------------------------------------------------
+// pre-scalar reductions: S_alpha partials and X beta (sum of X.v partials).
+// ---------------------------------------------------------------------------
+int pre_blocks_s(int p_loc) {
+    int b = (p_loc + 2047) / 2048;
+    return b < 1 ? 1 : (b > 128 ? 128 : b);
+}
+
+__global__ __launch_bounds__(256) void k_pre(const double *part, int nparts, int n_pad,
+                                             const double *beta, int p_loc,
+                                             const DevScalars *sc, double *red1, int nbS) {
+    __shared__ double sh[4];
+    if ((int)blockIdx.x < nbS) {
+        const double alpha = sc->alpha;
+        const int per = (p_loc + nbS - 1) / nbS;
+        const int j0 = blockIdx.x * per, j1 = min(p_loc, j0 + per);
+        double v = 0.0;
+        for (int j = j0 + threadIdx.x; j < j1; j += 256) v += exp(alpha * log(fabs(beta[j])));
+        v = block_sum<256>(v, sh);
+        if (threadIdx.x == 0) red1[blockIdx.x] = v;
+    } else {
+        const int r = (blockIdx.x - nbS) * 256 + threadIdx.x;
+        if (r < n_pad) {
+            double v = 0.0;
+            for (int q = 0; q < nparts; ++q) v += part[(size_t)q * n_pad + r];
+            red1[nbS + r] = v;
+        }
+    }
+}
+
+void launch_pre(hipStream_t s, const double *part, int nparts, int n_pad, const double *beta,
+                int p_loc, const DevScalars *sc, double *red1, int nbS) {
+    k_pre<<<nbS + (n_pad + 255) / 256, 256, 0, s>>>(part, nparts, n_pad, beta, p_loc, sc, red1,
+                                                     nbS);
+}
+
+// tau | beta (BridgeRegression.cpp:453-465) and sig2 | beta (:436-450).
+__global__ __launch_bounds__(256) void k_scalars(const double *red1, int nbS, const double *y,
+                                                 int n, int p, DevScalars *sc, Hyper hy,
+                                                 Key key, uint64_t t, double *tau_tr,
+                                                 double *sig2_tr, double *alpha_tr, int tau_only,
+                                                 uint32_t *err) {
+    __shared__ double sh[4];
+    const double *xb = red1 + nbS;
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double r = y[i] - xb[i];
+        v += r * r;
+    }
+    const double rss = block_sum<256>(v, sh);
+    if (threadIdx.x == 0) {
+        double S = 0.0;
+        for (int q = 0; q < nbS; ++q) S += red1[q];
+        const double alpha = sc->alpha;
+        if (!hy.know_tau) {
+            const double shape = hy.nu_shape + ((double)p) / alpha;
+            const double rate = hy.nu_rate + S;
+            const double nu = gamma1(shape, key, t, KIND_TAU, err) / rate;
+            sc->tau = exp(-1.0 * log(nu) / alpha);
+        }
+        if (!tau_only && !hy.know_sig2) {
+            const double shape = hy.sig2_shape + 0.5 * (double)n;
+            const double scale = hy.sig2_scale + 0.5 * rss;
+            sc->sig2 = scale / gamma1(shape, key, t, KIND_SIG2, err);
+        }
+        sc->s_abs_pow = S;
+        sc->rss = rss;
+        if (tau_tr) *tau_tr = sc->tau;
+        if (sig2_tr) *sig2_tr = sc->sig2;
+        if (alpha_tr) *alpha_tr = sc->alpha;
+    }
+}
+
+void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y, int n,
+                    int p, DevScalars *sc, Hyper hy, uint64_t k0, uint64_t k1, uint64_t t,
+                    double *tau_tr, double *sig2_tr, double *alpha_tr, int tau_only,
+                    uint32_t *err) {
+    k_scalars<<<1, 256, 0, s>>>(red1, nbS, y, n, p, sc, hy, Key{k0, k1}, t, tau_tr, sig2_tr,
+                                alpha_tr, tau_only, err);
+}
+
+// ---------------------------------------------------------------------------
+// Woodbury system assembly.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_slab_sum(const double *slabs, int S, size_t stride,
+                                                  int n_pad, const double *xu_part, int nxu,
+                                                  double *red2) {
+    const size_t nn = (size_t)n_pad * n_pad;
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx < nn) {
+        const int r = (int)(idx % n_pad), c = (int)(idx / n_pad);
+        double v = 0.0;
+        if (r <= c)
+            for (int q = 0; q < S; ++q) v += slabs[(size_t)q * stride + idx];
+        red2[idx] = v;
+    } else if (idx < nn + (size_t)n_pad) {
+        const int r = (int)(idx - nn);
+        double v = 0.0;
+        for (int q = 0; q < nxu; ++q) v += xu_part[(size_t)q * n_pad + r];
+        red2[idx] = v;
+    }
+}
+
+void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
+                     const double *xu_part, int nxu, double *red2) {
+    const size_t tot = (size_t)n_pad * n_pad + n_pad;
+    k_slab_sum<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(slabs, S, slab_stride, n_pad,
+                                                             xu_part, nxu, red2);
+}
+
+__global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n_pad,
+                                                const double *y, const DevScalars *sc, Key key,
+                                                uint64_t t, double *M, int ldm, int rhs_col) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t tot = (size_t)n_pad * (n_pad + kNB);
+    if (idx >= tot) return;
+    const int r = (int)(idx % n_pad), c = (int)(idx / n_pad);
+    const double sig2 = sc->sig2;
+    double *dst = M + (size_t)r + (size_t)c * ldm;
+    if (c < n_pad) {
+        if (r <= c) *dst = red2[idx] / sig2 + (r == c ? 1.0 : 0.0);
+    } else if (c == rhs_col) {
+        double v = 0.0;
+        if (r < n) {
+            const double sig = sqrt(sig2);
+            const double delta = normal_at(key, t, KIND_DELTA, (uint64_t)r);
+            const double xu = red2[(size_t)n_pad * n_pad + r];
+            v = y[r] / sig - (xu / sig + delta);
+        }
+        *dst = v;
+    } else {
+        *dst = 0.0;
+    }
+}
+
+void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,
+                   const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *M,
+                   int ldm, int rhs_col) {
+    const size_t tot = (size_t)n_pad * (n_pad + kNB);
+    k_form_m<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(red2, n, n_pad, y, sc, Key{k0, k1}, t,
+                                                           M, ldm, rhs_col);
+}
+
+__global__ __launch_bounds__(256) void k_form_a(const double *G, int ldg, const double *lam,
+                                                const DevScalars *sc, const double *cvec, int p,
+                                                int p_pad, double *A, int lda, int rhs_col) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t tot = (size_t)p_pad * (p_pad + kNB);
+    if (idx >= tot) return;
+    const int r = (int)(idx % p_pad), c = (int)(idx / p_pad);
+    double *dst = A + (size_t)r + (size_t)c * lda;
+    if (c < p_pad) {
+        if (r <= c) {
+            double v = G[(size_t)r + (size_t)c * ldg];
+            if (r == c) {
+                if (r < p) {
+                    if (lam) {
+                        const double tau = sc->tau;
+                        v += lam[r] * sc->sig2 / (tau * tau);
+                    }
+                } else {
+                    v = 1.0;
+                }
+            }
+            *dst = v;
+        }
+    } else if (c == rhs_col) {
+        *dst = (r < p) ? cvec[r] : 0.0;
+    } else {
+        *dst = 0.0;
+    }
+}
+
+void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
+                   const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
+                   int rhs_col) {
+    const size_t tot = (size_t)p_pad * (p_pad + kNB);
+    k_form_a<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(G, ldg, lam, sc, c, p, p_pad, A, lda,
+                                                           rhs_col);
+}
+
+// ---------------------------------------------------------------------------
+// Blocked right-looking Cholesky A = U'U (upper, column-major, NB = 64) with the
+// forward solve folded into trailing right-hand-side column blocks.
+//
+// k_chol_panel (step k): workgroup q factors the augmented block [A_kk | A_kj],
+// j = k + q, in registers (thread = one row x 8 or 16 columns; row c of the block is
+// broadcast through LDS each step, one barrier per pivot).  q == 0 writes U_kk;
+// q > 0 writes U_kj = U_kk^-T A_kj and a row-major copy PT[s][j*64 + x] used by the
+// trailing update so that its MFMA operands are lane-contiguous.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void k_chol_panel(double *A, int lda, int k, double *PT,
+                                                    int ldpt, uint32_t *err) {
+    __shared__ double buf[2][128];
+    __shared__ double dsq[64];
+    const int j = k + blockIdx.x;
+    const bool aug = (j != k);
+    const int ncol = aug ? 128 : 64;
+    const int nm = ncol / 8;
+    const int tid = threadIdx.x;
+    const int r = tid & 63;
+    const int cg = tid >> 6;  // 0..7
+    const int kb = k * kNB, jb = j * kNB;
+    double a[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int cc = cg + 8 * m;
+        double v = 0.0;
+        if (m < nm) {
+            const double *colp = (cc < 64) ? A + (size_t)(kb + cc) * lda + kb
+                                           : A + (size_t)(jb + cc - 64) * lda + kb;
+            v = colp[r];
+        }
+        a[m] = v;
+    }
+    if (r == 0) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            if (m < nm) buf[0][cg + 8 * m] = a[m];
+    }
+    __syncthreads();
+    for (int c = 0; c < 64; ++c) {
+        const double *bc = buf[c & 1];
+        const double piv = bc[c];
+        if (tid == 0) {
+            dsq[c] = sqrt(piv);
+            if (!(piv > 0.0) && err) atomicOr(err, 8u);
+        }
+        if (r > c) {
+            const double l = bc[r] / piv;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int cc = cg + 8 * m;
+                if (m < nm && cc >= r) a[m] -= l * bc[cc];
+            }
+        }
+        if (r == c + 1) {
+            double *bn = buf[(c + 1) & 1];
+#pragma unroll
+            for (int m = 0; m < 16; ++m)
+                if (m < nm) bn[cg + 8 * m] = a[m];
+        }
+        __syncthreads();
+    }
+    const double d = dsq[r];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int cc = cg + 8 * m;
+        if (m >= nm) continue;
+        if (!aug) {
+            if (r < cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = a[m] / d;
+            else if (r == cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = d;
+        } else if (cc >= 64) {
+            const double v = a[m] / d;
+            A[(size_t)(kb + r) + (size_t)(jb + cc - 64) * lda] = v;
+            PT[(size_t)r * ldpt + jb + cc - 64] = v;
+        }
+    }
+}
+
+// Trailing update A_ij -= U_ki' U_kj for k < i <= j (i < nblk), j < ncb.
+// D[x][y] = sum_s U_kj[s][x] U_ki[s][y] via v_mfma_f64_16x16x4_f64 with operands read
+// lane-contiguously from PT; A_ij[y][x] -= D[x][y] (coalesced along y).
+__global__ __launch_bounds__(256) void k_chol_update(double *A, int lda, int k, int nblk,
+                                                     int ncb, const double *__restrict__ PT,
+                                                     int ldpt) {
+    const int a = nblk - k - 1;
+    const int tri = a * (a + 1) / 2;
+    const int t = blockIdx.x;
+    int i, j;
+    if (t < tri) {
+        int jj = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
+        while (jj * (jj + 1) / 2 > t) --jj;
+        j = k + 1 + jj;
+        i = k + 1 + (t - jj * (jj + 1) / 2);
+    } else {
+        const int t2 = t - tri;
+        j = nblk + t2 / a;
+        i = k + 1 + t2 % a;
+    }
+    (void)ncb;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wx = (wid >> 1) * 32, wy = (wid & 1) * 32;
+    const int ib = i * kNB, jb = j * kNB;
+    v4d acc[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[p][q] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int kk = 0; kk < kNB / 4; ++kk) {
+        const int srow = kk * 4 + (lane >> 4);
+        const double *pr = PT + (size_t)srow * ldpt;
+        double av[2], bv[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) av[m] = pr[jb + wx + m * 16 + (lane & 15)];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) bv[m] = pr[ib + wy + m * 16 + (lane & 15)];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int x = wx + p * 16 + (lane >> 4) + 4 * rr;  // column within block j
+                const int y = wy + q * 16 + (lane & 15);           // row within block i
+                double *dst = A + (size_t)(ib + y) + (size_t)(jb + x) * lda;
+                *dst -= acc[p][q][rr];
+            }
+}
+
+// Backward solve step k: every workgroup solves U_kk w_k = y_k in LDS (redundantly);
+// workgroup 0 stores w_k; workgroup i < k applies y_i -= U_ik w_k.
+__global__ __launch_bounds__(256) void k_bsolve_step(const double *A, int lda, int k,
+                                                     int m_pad, double *Y, double *W,
+                                                     int nrhs) {
+    __shared__ double U[64][65];
+    __shared__ double yv[2][64];
+    __shared__ double wv[2][64];
+    const int tid = threadIdx.x, r = tid & 63, q = tid >> 6;
+    const int kb = k * kNB;
+    for (int c = q; c < 64; c += 4) U[r][c] = A[(size_t)(kb + r) + (size_t)(kb + c) * lda];
+    if (q < nrhs) yv[q][r] = Y[(size_t)q * m_pad + kb + r];
+    __syncthreads();
+    for (int c = 63; c >= 0; --c) {
+        if (q < nrhs) {
+            const double wc = yv[q][c] / U[c][c];
+            if (r < c) yv[q][r] -= U[r][c] * wc;
+            if (r == c) wv[q][c] = wc;
+        }
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && q < nrhs) W[(size_t)q * m_pad + kb + r] = wv[q][r];
+    if (k > 0 && q < nrhs) {
+        const int ib = blockIdx.x * kNB;
+        double acc = 0.0;
+        for (int c = 0; c < 64; ++c) acc += A[(size_t)(ib + r) + (size_t)(kb + c) * lda] * wv[q][c];
+        Y[(size_t)q * m_pad + ib + r] -= acc;
+    }
+}
+
+void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, double *Y, double *W,
+                 int nrhs) {
+    const int nblk = m_pad / kNB;
+    for (int k = nblk - 1; k >= 0; --k)
+        k_bsolve_step<<<k > 0 ? k : 1, 256, 0, s>>>(A, lda, k, m_pad, Y, W, nrhs);
+}
+
+void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks,
+                    uint32_t *err, double *PT) {
+    const int nblk = m_pad / kNB;
+    const int ncb = nblk + nrhs_blocks;
+    const int ldpt = ncb * kNB;
+    for (int k = 0; k < nblk; ++k) {
+        k_chol_panel<<<ncb - k, 512, 0, s>>>(A, lda, k, PT, ldpt, err);
+        const int a = nblk - k - 1;
+        const int tiles = a * (a + 1) / 2 + a * nrhs_blocks;
+        if (tiles > 0) k_chol_update<<<tiles, 256, 0, s>>>(A, lda, k, nblk, ncb, PT, ldpt);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// beta updates
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_beta_wb(const double *__restrict__ X, int ldx,
+                                                 int n_pad, const double *__restrict__ w,
+                                                 const double *u, const double *D,
+                                                 const DevScalars *sc, int p_loc, double *beta,
+                                                 double *trace) {
+    extern __shared__ double ws[];
+    for (int i = threadIdx.x; i < n_pad; i += 256) ws[i] = w[i];
+    __syncthreads();
+    const double sig = sqrt(sc->sig2);
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nw = gridDim.x * 4;
+    for (int j = wave; j < p_loc; j += nw) {
+        const double *col = X + (size_t)j * ldx;
+        double s = 0.0;
+        for (int r = 2 * lane; r < n_pad; r += 128) {
+            const double2 x = *(const double2 *)(col + r);
+            s += x.x * ws[r];
+            s += x.y * ws[r + 1];
+        }
+        s = wave_allsum(s);
+        if (lane == 0) {
+            const double b = u[j] + D[j] * s / sig;
+            beta[j] = b;
+            if (trace) trace[j] = b;
+        }
+    }
+}
+
+void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,
+                          const double *u, const double *D, const DevScalars *sc, int p_loc,
+                          double *beta, double *beta_trace) {
+    int blocks = (p_loc + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    k_beta_wb<<<blocks, 256, n_pad * sizeof(double), s>>>(X, ldx, n_pad, w, u, D, sc, p_loc,
+                                                          beta, beta_trace);
+}
+
+__global__ __launch_bounds__(256) void k_chol_rhs(const double *A, int lda, int rhs_col, int p,
+                                                  int p_pad, Key key, uint64_t t, double *Y2) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= p_pad) return;
+    Y2[r] = A[(size_t)r + (size_t)rhs_col * lda];
+    Y2[(size_t)p_pad + r] = (r < p) ? normal_at(key, t, KIND_BETA_Z, (uint64_t)r) : 0.0;
+}
+
+void launch_chol_rhs(hipStream_t s, const double *A, int lda, int rhs_col, int p, int p_pad,
+                     uint64_t k0, uint64_t k1, uint64_t t, double *Y2) {
+    k_chol_rhs<<<(p_pad + 255) / 256, 256, 0, s>>>(A, lda, rhs_col, p, p_pad, Key{k0, k1}, t, Y2);
+}
+
+__global__ __launch_bounds__(256) void k_beta_chol(const double *W2, int p_pad,
+                                                   const DevScalars *sc, int p, double *beta,
+                                                   double *trace) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= p) return;
+    const double sig = sqrt(sc->sig2);
+    const double b = W2[r] + sig * W2[(size_t)p_pad + r];
+    beta[r] = b;
+    if (trace) trace[r] = b;
+}
+
+void launch_beta_chol(hipStream_t s, const double *W2, int p_pad, const DevScalars *sc, int p,
+                      double *beta, double *beta_trace) {
+    k_beta_chol<<<(p + 255) / 256, 256, 0, s>>>(W2, p_pad, sc, p, beta, beta_trace);
+}
+
+__global__ __launch_bounds__(256) void k_beta_ortho(const double *gdiag, const double *cvec,
+                                                    const double *lam, const DevScalars *sc,
+                                                    int p, Key key, uint64_t t, double *beta,
+                                                    double *trace) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p) return;
+    const double sig2 = sc->sig2, tau = sc->tau;
+    const double uu = gdiag[i] + lam[i] * sig2 / (tau * tau);
+    const double sd = sqrt(sig2 / uu);
+    const double m = cvec[i] / uu;
+    const double b = m + sd * normal_at(key, t, KIND_BETA_Z, (uint64_t)i);
+    beta[i] = b;
+    if (trace) trace[i] = b;
+}
+
+void launch_beta_ortho(hipStream_t s, const double *gdiag, const double *c, const double *lam,
+                       const DevScalars *sc, int p, uint64_t k0, uint64_t k1, uint64_t t,
+                       double *beta, double *beta_trace) {
+    k_beta_ortho<<<(p + 255) / 256, 256, 0, s>>>(gdiag, c, lam, sc, p, Key{k0, k1}, t, beta,
+                                                 beta_trace);
+}
+
+// alpha | beta, tau: BridgeRegression.cpp:469-503 (single workgroup).
+__global__ __launch_bounds__(1024) void k_alpha_mh(const double *beta, int p, DevScalars *sc,
+                                                   double pr_a, double pr_b, Key key,
+                                                   uint64_t t, double *alpha_tr) {
+    __shared__ double sh[16];
+    const double tau = sc->tau;
+    const double a_old = sc->alpha;
+    const double ep = 0.1;
+    U4 u = uniforms(key, t, KIND_ALPHA, 0, 0, 0);
+    const double l_new = fmax(0.0, a_old - ep);
+    const double r_new = fmin(1.0, a_old + ep);
+    const double d_new = r_new - l_new;
+    const double a_new = l_new + d_new * u.r[0];
+    double sn = 0.0, so = 0.0;
+    for (int i = threadIdx.x; i < p; i += 1024) {
+        const double si = log(fabs(beta[i] / tau));
+        sn += exp(a_new * si);
+        so += exp(a_old * si);
+    }
+    const double Sn = block_sum<1024>(sn, sh);
+    const double So = block_sum<1024>(so, sh);
+    if (threadIdx.x == 0) {
+        const double pp = (double)p;
+        const double llh_new = pp * log(a_new) - pp * lgamma(1.0 / a_new) - Sn;
+        const double llh_old = pp * log(a_old) - pp * lgamma(1.0 / a_old) - So;
+        const double lbc = lgamma(pr_a) + lgamma(pr_b) - lgamma(pr_a + pr_b);
+        const double ldb_new = (pr_a - 1.0) * log(a_new) + (pr_b - 1.0) * log(1.0 - a_new) - lbc;
+        const double ldb_old = (pr_a - 1.0) * log(a_old) + (pr_b - 1.0) * log(1.0 - a_old) - lbc;
+        const double l_old = fmax(0.0, a_new - ep);
+        const double r_old = fmin(1.0, a_new + ep);
+        const double d_old = r_old - l_old;
+        const double log_accept = llh_new - llh_old + ldb_new - ldb_old + log(d_old) - log(d_new);
+        double an = a_new;
+        if (u.r[1] > exp(log_accept)) an = a_old;
+        sc->alpha = an;
+        if (alpha_tr) *alpha_tr = an;
+    }
+}
+
+void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, double pr_a,
+                     double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr) {
+    k_alpha_mh<<<1, 1024, 0, s>>>(beta, p, sc, pr_a, pr_b, Key{k0, k1}, t, alpha_tr);
+}
+
+__global__ void k_record_scalars(const DevScalars *sc, double *tau_tr, double *sig2_tr,
+                                 double *alpha_tr) {
+    if (threadIdx.x == 0) {
+        if (tau_tr) *tau_tr = sc->tau;
+        if (sig2_tr) *sig2_tr = sc->sig2;
+        if (alpha_tr) *alpha_tr = sc->alpha;
+    }
+}
+
+void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
+                           double *sig2_tr, double *alpha_tr) {
+    k_record_scalars<<<1, 64, 0, s>>>(sc, tau_tr, sig2_tr, alpha_tr);
+}
+
+// ---------------------------------------------------------------------------
+// setup helpers
+// ---------------------------------------------------------------------------
+__global__ void k_copy_cols(const double *src, int lds, double *dst, int ldd, int rows,
+                            int cols) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)rows * cols) return;
+    const int r = (int)(idx % rows), c = (int)(idx / rows);
+    dst[(size_t)r + (size_t)c * ldd] = src[(size_t)r + (size_t)c * lds];
+}
+
+void launch_copy_cols(hipStream_t s, const double *src, int lds, double *dst, int ldd, int rows,
+                      int cols) {
+    const size_t tot = (size_t)rows * cols;
+    if (tot == 0) return;
+    k_copy_cols<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(src, lds, dst, ldd, rows, cols);
+}
+
+__global__ void k_gdiag(const double *G, int ldg, int p, double *d) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < p) d[i] = G[(size_t)i + (size_t)i * ldg];
+}
+
+void launch_gdiag(hipStream_t s, const double *G, int ldg, int p, double *d) {
+    k_gdiag<<<(p + 255) / 256, 256, 0, s>>>(G, ldg, p, d);
+}
+
+__global__ void k_sum_into(const double *a, double *b, size_t n) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) b[i] += a[i];
+}
+
+void launch_sum_into(hipStream_t s, const double *a, double *b, size_t n) {
+    if (n == 0) return;
+    k_sum_into<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(a, b, n);
+}
+
+// 32x32 LDS-tiled transpose: dst (cols x rows, ldd) = src' (rows x cols, lds).
+__global__ __launch_bounds__(256) void k_transpose(const double *src, int lds, int rows,
+                                                   int cols, double *dst, int ldd) {
+    __shared__ double tile[32][33];
+    const int bx = blockIdx.x * 32, by = blockIdx.y * 32;  // bx: rows of src, by: cols of src
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // ty 0..7
+    for (int k = ty; k < 32; k += 8) {
+        const int r = bx + tx, c = by + k;
+        tile[k][tx] = (r < rows && c < cols) ? src[(size_t)r + (size_t)c * lds] : 0.0;
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {
+        const int c = by + tx, r = bx + k;  // dst row = c, dst col = r
+        if (c < cols && r < rows) dst[(size_t)c + (size_t)r * ldd] = tile[tx][k];
+    }
+}
+
+void launch_transpose(hipStream_t s, const double *src, int lds, int rows, int cols, double *dst,
+                      int ldd) {
+    dim3 grid((rows + 31) / 32, (cols + 31) / 32);
+    k_transpose<<<grid, 256, 0, s>>>(src, lds, rows, cols, dst, ldd);
+}
+
+// c_j = X_j . v for j < ncols (wave per column).
+__global__ __launch_bounds__(256) void k_coldot(const double *__restrict__ X, int ldx,
+                                                int n_pad, const double *__restrict__ v,
+                                                int ncols, double *out) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nw = gridDim.x * 4;
+    for (int j = wave; j < ncols; j += nw) {
+        const double *col = X + (size_t)j * ldx;
+        double s = 0.0;
+        for (int r = 2 * lane; r < n_pad; r += 128) {
+            const double2 x = *(const double2 *)(col + r);
+            s += x.x * v[r];
+            s += x.y * v[r + 1];
+        }
+        s = wave_allsum(s);
+        if (lane == 0) out[j] = s;
+    }
+}
+
+void launch_coldot(hipStream_t s, const double *X, int ldx, int n_pad, const double *v, int ncols,
+                   double *out) {
+    int blocks = (ncols + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    k_coldot<<<blocks, 256, 0, s>>>(X, ldx, n_pad, v, ncols, out);
+}
+
+// d_j = sum_r X[r, j]^2 (diagonal of X'X).
+__global__ __launch_bounds__(256) void k_colnorm2(const double *__restrict__ X, int ldx,
+                                                  int n_pad, int ncols, double *out) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nw = gridDim.x * 4;
+    for (int j = wave; j < ncols; j += nw) {
+        const double *col = X + (size_t)j * ldx;
+        double s = 0.0;
+        for (int r = 2 * lane; r < n_pad; r += 128) {
+            const double2 x = *(const double2 *)(col + r);
+            s += x.x * x.x;
+            s += x.y * x.y;
+        }
+        s = wave_allsum(s);
+        if (lane == 0) out[j] = s;
+    }
+}
+
+void launch_colnorm2(hipStream_t s, const double *X, int ldx, int n_pad, int ncols, double *out) {
+    int blocks = (ncols + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    k_colnorm2<<<blocks, 256, 0, s>>>(X, ldx, n_pad, ncols, out);
+}
+
+}  // namespace bb

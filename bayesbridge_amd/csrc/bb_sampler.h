@@ -1,0 +1,281 @@
+// bb_sampler.h -- device-side variate generation for the stable Gibbs sweep (gfx950).
+//
+// Philox4x64-10 counter RNG held in registers, Box-Muller normals, Marsaglia-Tsang
+// gamma, and the two attempt bodies of Devroye's (2009) double-rejection sampler for
+// the exponentially tilted positive stable law, restating Code/C/retstable.cpp:94-271.
+//
+// Counter layout (DESIGN.md "RNG counter layout"): key = (seed, stream),
+// ctr = (t, kind << 56 | j, a, b).  A variate depends only on its counter, so any
+// lane may evaluate any attempt: the group sampler below evaluates G consecutive
+// outer attempts of one coefficient in G lanes and keeps the first accepted one,
+// which reproduces the sequential rejection loop exactly.
+//
+// All arithmetic is IEEE fp64; the library is compiled with -ffp-contract=off so
+// that expression trees round like the CPU checker's.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bb {
+
+enum Kind : unsigned {
+    KIND_LAMBDA_INNER = 1,
+    KIND_LAMBDA_OUTER = 2,
+    KIND_TAU = 3,
+    KIND_SIG2 = 4,
+    KIND_BETA_Z = 5,
+    KIND_DELTA = 6,
+    KIND_ALPHA = 7,
+};
+
+struct Key {
+    uint64_t k0, k1;
+};
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kSqrtPi = 1.772453850905516027298167483341;  // retstable.cpp:14-16
+constexpr double kSqrt2 = 1.41421356237309504880;
+constexpr double kPi2 = 1.57079632679489661923;
+
+struct U4 {
+    double r[4];
+};
+
+__device__ __forceinline__ void philox4x64(uint64_t c0, uint64_t c1, uint64_t c2, uint64_t c3,
+                                           uint64_t k0, uint64_t k1, uint64_t out[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B97F4A7C15ULL;
+            k1 += 0xBB67AE8584CAA73BULL;
+        }
+        const uint64_t a0 = 0xD2E7470EE14C6C93ULL, a1 = 0xCA5A826395121157ULL;
+        uint64_t hi0 = __umul64hi(a0, c0), lo0 = a0 * c0;
+        uint64_t hi1 = __umul64hi(a1, c2), lo1 = a1 * c2;
+        uint64_t n0 = hi1 ^ c1 ^ k0;
+        uint64_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+// Four open-interval (0,1) uniforms with 53-bit resolution from one Philox block.
+__device__ __forceinline__ U4 uniforms(Key key, uint64_t t, unsigned kind, uint64_t j, uint64_t a,
+                                       uint64_t b) {
+    uint64_t o[4];
+    philox4x64(t, ((uint64_t)kind << 56) | j, a, b, key.k0, key.k1, o);
+    U4 u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u.r[i] = ((double)(o[i] >> 11) + 0.5) * 0x1.0p-53;
+    return u;
+}
+
+__device__ __forceinline__ double bm_normal(double r0, double r1) {
+    return sqrt(-2.0 * log(r0)) * cos(2.0 * kPi * r1);
+}
+
+// Standard normal variate with index j of stream `kind` at sweep t.
+__device__ __forceinline__ double normal_at(Key key, uint64_t t, unsigned kind, uint64_t j) {
+    U4 u = uniforms(key, t, kind, j, 0, 0);
+    return bm_normal(u.r[0], u.r[1]);
+}
+
+// Ga(shape, rate 1): Marsaglia & Tsang (2000), one Philox block per attempt,
+// boost u^(1/a) for shape < 1.  Stream (t, kind, j=0, attempt, 0).
+__device__ inline double gamma1(double shape, Key key, uint64_t t, unsigned kind,
+                                uint32_t *err) {
+    double a = shape, boost = 1.0;
+    if (a < 1.0) {
+        U4 u = uniforms(key, t, kind, 0, 0, 1);
+        boost = pow(u.r[0], 1.0 / a);
+        a += 1.0;
+    }
+    double d = a - 1.0 / 3.0;
+    double cc = 1.0 / sqrt(9.0 * d);
+    for (uint64_t k = 0; k < (1ull << 24); ++k) {
+        U4 u = uniforms(key, t, kind, 0, k, 0);
+        double x = bm_normal(u.r[0], u.r[1]);
+        double v = 1.0 + cc * x;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        double uu = u.r[2];
+        double x2 = x * x;
+        if (uu < 1.0 - 0.0331 * x2 * x2) return d * v * boost;
+        if (log(uu) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v * boost;
+    }
+    if (err) atomicOr(err, 1u);
+    return __builtin_nan("");
+}
+
+// ---------------------------------------------------------------------------
+// Tilted positive stable law, Code/C/retstable.cpp.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double sinc_mm(double x) {  // retstable.cpp:18-29
+    double ax = fabs(x);
+    if (ax < 0.006) {
+        if (x == 0.) return 1;
+        double x2 = x * x;
+        if (ax < 2e-4) return 1. - x2 / 6.;
+        return 1. - x2 / 6. * (1 - x2 / 20.);
+    }
+    return sin(x) / x;
+}
+
+__device__ __forceinline__ double zolotarev_A(double x, double alpha) {  // :40-47
+    double ia = 1. - alpha;
+    return pow(ia * sinc_mm(ia * x), ia) * pow(alpha * sinc_mm(alpha * x), alpha) / sinc_mm(x);
+}
+
+__device__ __forceinline__ double b_over_b0(double x, double alpha) {  // :73-77
+    double ia = 1. - alpha;
+    double den = pow(sinc_mm(alpha * x), alpha) * pow(sinc_mm(ia * x), ia);
+    return sinc_mm(x) / den;
+}
+
+// Per-coefficient constants (retstable.cpp:121-147).
+struct StableParams {
+    double h, alpha, V0, b, lambda_alpha, gamma, sgamma, xi, psi, w1, w2, w3, c1;
+};
+
+__device__ __forceinline__ StableParams stable_params(double h, double alpha, double V0) {
+    StableParams s;
+    s.h = h;
+    s.alpha = alpha;
+    s.V0 = V0;
+    s.c1 = sqrt(kPi2);
+    const double c2 = 2. + s.c1;
+    s.b = (1. - alpha) / alpha;
+    s.lambda_alpha = pow(h, alpha) * V0;
+    s.gamma = s.lambda_alpha * alpha * (1. - alpha);
+    s.sgamma = sqrt(s.gamma);
+    double c3 = c2 * s.sgamma;
+    s.xi = (1. + kSqrt2 * c3) / kPi;
+    s.psi = c3 * exp(-s.gamma * kPi * kPi / 8.) / kSqrtPi;
+    s.w1 = s.c1 * s.xi / s.sgamma;
+    s.w2 = 2. * kSqrtPi * s.psi;
+    s.w3 = s.xi * kPi;
+    return s;
+}
+
+// One outer attempt o of coefficient j (retstable.cpp:155-256): runs the inner
+// loop (:162-207) on blocks (t, INNER|j, o, i), then the outer test on block
+// (t, OUTER|j, o, 0).  Returns true and sets X if accepted.
+__device__ inline bool stable_outer_attempt(const StableParams &s, Key key, uint64_t t,
+                                            uint64_t j, uint64_t o, double &X,
+                                            uint32_t *err) {
+    const double alpha = s.alpha, gamma = s.gamma, sgamma = s.sgamma;
+    double U = 0, z = 0, Z = 0;
+    bool inner_ok = false;
+    for (uint64_t i = 0; i < (1ull << 20); ++i) {
+        U4 r = uniforms(key, t, KIND_LAMBDA_INNER, j, o, i);
+        double V = r.r[0];
+        if (gamma >= 1) {
+            if (V < s.w1 / (s.w1 + s.w2)) U = fabs(bm_normal(r.r[2], r.r[3])) / sgamma;
+            else {
+                double W_ = r.r[2];
+                U = kPi * (1. - W_ * W_);
+            }
+        } else {
+            double W_ = r.r[2];
+            if (V < s.w3 / (s.w2 + s.w3)) U = kPi * W_;
+            else U = kPi * (1. - W_ * W_);
+        }
+        double W = r.r[1];
+        double zeta = sqrt(b_over_b0(U, alpha));
+        z = 1 / (1 - pow(1 + alpha * zeta / sgamma, -1 / alpha));
+        double rho = kPi * exp(-s.lambda_alpha * (1. - 1. / (zeta * zeta))) /
+                     ((1. + s.c1) * sgamma / zeta + z);
+        double d = 0.;
+        if (U >= 0 && gamma >= 1) d += s.xi * exp(-gamma * U * U / 2.);
+        if (U > 0 && U < kPi) d += s.psi / sqrt(kPi - U);
+        if (U >= 0 && U <= kPi && gamma < 1) d += s.xi;
+        rho *= d;
+        Z = W * rho;
+        if (U < kPi && Z <= 1.) {
+            inner_ok = true;
+            break;
+        }
+    }
+    if (!inner_ok) {
+        if (err) atomicOr(err, 2u);
+        X = __builtin_nan("");
+        return true;  // give up on this coefficient (flagged)
+    }
+    double a = pow(zolotarev_A(U, alpha), 1. / (1. - alpha));  // :212-218
+    double m = pow(s.b / a, alpha) * s.lambda_alpha;
+    double delta = sqrt(m * alpha / a);
+    double a1 = delta * s.c1;
+    double a2 = delta;
+    double a3 = z / a;
+    double ssum = a1 + a2 + a3;
+
+    U4 r = uniforms(key, t, KIND_LAMBDA_OUTER, j, o, 0);
+    double V_ = r.r[0], N_ = 0., E_ = 0.;  // :224-238
+    double Xc;
+    if (V_ < a1 / ssum) {
+        N_ = bm_normal(r.r[1], r.r[2]);
+        Xc = m - delta * fabs(N_);
+    } else {
+        if (V_ < (a1 + a2) / ssum) Xc = m + delta * r.r[1];
+        else {
+            E_ = -log(r.r[1]);
+            Xc = m + delta + E_ * a3;
+        }
+    }
+    double E = -log(Z);
+    double c = a * (Xc - m);  // :247-251
+    c += (m != 0) ? s.h * (pow(Xc, -1. * s.b) - pow(m, -1. * s.b)) : 0.0;
+    if (Xc < m) c -= N_ * N_ / 2.;
+    else if (Xc > m + delta) c -= E_;
+    X = Xc;
+    return (Xc >= 0 && c <= E);
+}
+
+__device__ __forceinline__ double stable_finish(const StableParams &s, double X) {
+    return exp(1 / s.alpha * log(s.V0) - s.b * log(X));  // :270
+}
+
+// Group sampler: the G lanes [gbase, gbase+G) of a wave cooperate on one
+// coefficient.  Every lane of the wave must call this (ballot/shuffle inside);
+// `active` marks lanes whose group has a coefficient.  Returns the draw in every
+// lane of the group.
+template <int G>
+__device__ inline double stable_group_draw(bool active, double h, double alpha, double V0,
+                                           Key key, uint64_t t, uint64_t j, uint32_t *err) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    if (active && alpha == 1.) active = false;  // :104-110 returns V0, no RNG used
+    double result = V0;
+    bool done = !active;
+    StableParams s;
+    if (active) {
+        if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) atomicOr(err, 4u);  // :112-115
+        s = stable_params(h, alpha, V0);
+    }
+    uint64_t base = 0;
+    for (int round = 0; round < (1 << 20); ++round) {
+        bool acc = false;
+        double X = 0.0;
+        if (!done) acc = stable_outer_attempt(s, key, t, j, base + (uint64_t)g, X, err);
+        uint64_t m = (__ballot(acc) >> gbase) & gmask;
+        int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
+        double Xw = __shfl(X, gbase + win, 64);
+        if (!done && m) {
+            result = stable_finish(s, Xw);
+            done = true;
+        }
+        base += G;
+        if (__all(done)) break;
+    }
+    return result;
+}
+
+}  // namespace bb

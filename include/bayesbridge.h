@@ -1,0 +1,194 @@
+/*
+ * bayesbridge.h -- C ABI of the MI355X-native BayesBridge drop-in (BayesBridge.so).
+ *
+ * Part 1: the reference's own .C() entry points for the normal-mixture
+ * ("stable") path, with identical names, argument order and meaning, so that
+ * the reference R front end (`.C("bridge_reg_stable", ..., PACKAGE="BayesBridge")`,
+ * Code/C/BridgeWrapper.R:220-228 and :534) binds them unchanged.
+ *
+ * Part 2: bb_* extensions (seeding, device engine for benchmarks / multi-GPU,
+ * diagnostics).  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * Error behaviour follows the reference: the .C entry points never throw or
+ * return a status; problems are printed and partial traces are returned
+ * (Code/C/BridgeWrapper.cpp:300-304).  bb_* functions return 0 on success and
+ * a negative code on failure (message via bb_last_error()).
+ */
+#ifndef BAYESBRIDGE_AMD_H
+#define BAYESBRIDGE_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Part 1: reference .C entry points                                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Gibbs sampler for Bayesian bridge regression, normal-mixture ("stable")
+ * representation.  Replaces Code/C/BridgeWrapper.h:205-226 (declaration) /
+ * Code/C/BridgeWrapper.cpp:659-732 (implementation), which drives
+ * bridge_regression_stable (:207-313) or bridge_regression_stable_ortho (:434-537).
+ *
+ * Outputs (caller-allocated, column-major as R passes them):
+ *   betap, lambdap : P x M  (sample i at offset i*P)
+ *   sig2p, taup, alphap : M
+ *   runtime : post-burn-in wall seconds (the reference reports post-burn CPU
+ *             seconds from clock())
+ * Inputs: yp (N), Xp (N x P column-major), hyper-parameters as in
+ * bridge.reg.stb (BridgeWrapper.R:194-234); true_* > 0 fixes that parameter.
+ * `ortho` is declared `const bool*` in the reference but R passes
+ * as.integer(ortho) (4 bytes); this implementation reads it as an int.
+ */
+void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,
+                       double *alphap, const double *yp, const double *Xp,
+                       const double *sig2_shape, const double *sig2_scale,
+                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                       const double *alpha_b, const double *true_sig2, const double *true_tau,
+                       const double *true_alpha, const int *P, const int *N, const int *M,
+                       const int *burn, double *runtime, const int *ortho);
+
+/*
+ * Batch exponentially tilted positive alpha-stable draws (Devroye 2009 double
+ * rejection): x[i] has Laplace transform exp(-V0[i]((h[i]+t)^alpha[i] - h[i]^alpha[i])).
+ * Replaces Code/C/BridgeWrapper.h:244 / BridgeWrapper.cpp:965-984, which loops
+ * retstable_LD(h, alpha, RNG&, V0) of Code/C/retstable.cpp:94-271.
+ */
+void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num);
+
+/* ------------------------------------------------------------------------ */
+/* Part 2: extensions                                                        */
+/* ------------------------------------------------------------------------ */
+
+/* Library / device information. */
+const char *bb_version(void);
+const char *bb_last_error(void);
+int bb_device_count(void);
+
+/*
+ * RNG seeding.  Every variate is Philox4x64-10 of a counter; the key
+ * is (seed, stream).  bb_set_seed sets the seed and resets the stream to 0; each
+ * .C call consumes one stream value.  When the library runs inside R (the
+ * symbols GetRNGstate / unif_rand / PutRNGstate resolve), the seed is instead
+ * drawn from R's RNG on every .C call, so set.seed() reproduces results.
+ */
+void bb_set_seed(uint64_t seed);
+void bb_get_rng_state(uint64_t *seed, uint64_t *stream);
+void bb_set_rng_state(uint64_t seed, uint64_t stream);
+void bb_use_r_rng(int enable); /* default 1: use R's RNG when present */
+
+/* Select the device used by the .C entry points (default 0). */
+int bb_set_device(int device);
+
+/* Verbosity of the reference-style progress messages (0 silences them). */
+void bb_set_verbose(int verbose);
+
+/*
+ * Device engine: one Gibbs chain on one GPU, holding a column shard
+ * [j0, j0 + p_local) of an N x P problem.  Used by bench.py, the multi-GPU path
+ * and the tests.  Sweeps are enqueued asynchronously on the engine's stream.
+ */
+typedef struct bb_engine bb_engine;
+
+typedef struct bb_config {
+    int n;              /* rows */
+    int p;              /* global number of columns */
+    int p_local;        /* columns held by this engine (== p unless sharded) */
+    int j0;             /* global index of this engine's first column */
+    int rank, world;    /* shard id and count (world > 1 requires a communicator) */
+    double sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a, alpha_b;
+    double true_sig2, true_tau, true_alpha;
+    int ortho;          /* orthogonal-design variant (sample_beta_stable_ortho) */
+    int method;         /* 0 auto (chol if p <= n else woodbury), 1 chol, 2 woodbury */
+    int trace_capacity; /* number of trace slots kept on device (>= 1) */
+    uint64_t seed, stream;
+    int device;
+} bb_config;
+
+void bb_config_default(bb_config *cfg);
+
+/* Create: X_local is N x p_local column-major (host), y is N (host). */
+int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
+                     bb_engine **out);
+void bb_engine_destroy(bb_engine *e);
+
+/*
+ * RCCL communicator for world > 1: rank 0 calls bb_comm_unique_id, the bytes are
+ * broadcast out of band (torch.distributed store), every rank calls
+ * bb_engine_comm_init.  id_bytes is bb_comm_id_size() bytes.
+ */
+int bb_comm_id_size(void);
+int bb_comm_unique_id(void *id_bytes);
+int bb_engine_comm_init(bb_engine *e, const void *id_bytes);
+
+/*
+ * Initialise the chain state as the reference does (BridgeWrapper.cpp:242-262):
+ * beta = least squares (0 when X'X is singular or p > n), alpha = 0.5 (or
+ * true_alpha), then the pre-burn tau draw (non-ortho only).
+ */
+int bb_engine_init_state(bb_engine *e);
+
+/*
+ * Enqueue `count` sweeps starting at global sweep index t0 (t = 1 + i for burn-in
+ * sweep i, t = burn + 1 + i for MCMC sweep i; BridgeWrapper.cpp:266,287).  Sweep k
+ * records its state in trace slot first_slot + k * slot_step (mod trace_capacity);
+ * first_slot < 0 records nothing.  Burn-in uses slot_step 0 (everything in slot 0,
+ * as the reference does).  mcmc_phase selects the (alpha_b, alpha_b) prior pair of
+ * the reference's MCMC loop (BridgeWrapper.cpp:294) over (alpha_a, alpha_b) (:272).
+ */
+int bb_engine_run(bb_engine *e, uint64_t t0, int count, int first_slot, int slot_step,
+                  int mcmc_phase);
+int bb_engine_sync(bb_engine *e);
+
+/* Copy trace slots [slot0, slot0 + count) to host buffers (any may be NULL).
+ * beta/lambda are p_local x count. */
+int bb_engine_get_trace(bb_engine *e, int slot0, int count, double *beta, double *lambda,
+                        double *sig2, double *tau, double *alpha);
+
+/* Current chain state (beta, lambda: p_local; scalars). */
+int bb_engine_get_state(bb_engine *e, double *beta, double *lambda, double *tau,
+                        double *sig2, double *alpha);
+/* Overwrite the current chain state (teacher forcing in tests). */
+int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig2,
+                        double alpha);
+
+/* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho. */
+int bb_engine_method(const bb_engine *e);
+
+/* Per-kernel timing: milliseconds of the last sweep's Gram kernel and of the
+ * whole last sweep, measured with HIP events on the engine's stream. */
+int bb_engine_enable_timing(bb_engine *e, int enable);
+int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
+                           int *samples);
+int bb_engine_reset_timing(bb_engine *e);
+
+/* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
+int bb_engine_error_flags(bb_engine *e, uint32_t *flags);
+
+/* ---- kernel-level entry points (tests / microbenchmarks) ---- */
+
+/* Tilted-stable batch with explicit key and counter base t (host buffers). */
+int bb_retstable_batch(double *x, const double *alpha, const double *V0, const double *h,
+                       int num, uint64_t seed, uint64_t stream, uint64_t t, int group);
+
+/* lambda_j = 2 * retstable(beta_j^2/tau^2, alpha/2, 1) for global j = j0 + i. */
+int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, double tau,
+                     uint64_t seed, uint64_t stream, uint64_t t, uint64_t j0, int group);
+
+/* Gram C = Y diag(w) Y' (Y: n x k column-major) via the fp64 MFMA kernel;
+ * C is n x n column-major, full symmetric result. */
+int bb_gram(double *C, const double *Y, const double *w, int n, int k);
+
+/* SPD solve via the blocked device Cholesky: A (m x m, column-major, only the
+ * upper triangle read) -> x = A^-1 b for nrhs right-hand sides (m x nrhs). */
+int bb_chol_solve(double *x, const double *A, const double *b, int m, int nrhs);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BAYESBRIDGE_AMD_H */

@@ -1,0 +1,158 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for the BayesBridge stable Gibbs sweep.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg import this package, and only as the checker.  The product
+(``bayesbridge_amd`` / ``BayesBridge.so``) never imports, links or calls it.
+
+PARITY UNPINNED against reference outputs (no reference fixtures exist and the
+reference cannot be built or run here -- see ``bb_oracle.c`` header and
+DESIGN.md); pinned instead by Philox KATs, numpy's Philox, analytic moments of
+the tilted stable law and exact-posterior quadrature (tests/test_oracle_cpu.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libbboracle.so")
+_lib = None
+
+KIND_LAMBDA_INNER = 1
+KIND_LAMBDA_OUTER = 2
+KIND_TAU = 3
+KIND_SIG2 = 4
+KIND_BETA_Z = 5
+KIND_DELTA = 6
+KIND_ALPHA = 7
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_dp = ctypes.POINTER(ctypes.c_double)
+_lp = ctypes.POINTER(ctypes.c_long)
+
+
+def build() -> str:
+    src = os.path.join(_HERE, "bb_oracle.c")
+    if (not os.path.exists(_LIB_PATH)) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.bbo_philox4x64.argtypes = [_u64p, _u64p, _u64p]
+        L.bbo_uniforms.argtypes = [_u64p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_uint64,
+                                   ctypes.c_uint64, ctypes.c_uint64, _dp]
+        L.bbo_normals.argtypes = [_dp, ctypes.c_long, _u64p, ctypes.c_uint64, ctypes.c_uint,
+                                  ctypes.c_uint64]
+        L.bbo_retstable.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double, _u64p,
+                                    ctypes.c_uint64, ctypes.c_uint64, _lp, _lp]
+        L.bbo_retstable.restype = ctypes.c_double
+        L.bbo_retstable_batch.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_long, _u64p,
+                                          ctypes.c_uint64]
+        L.bbo_sample_lambda.argtypes = [_dp, _dp, ctypes.c_long, ctypes.c_double,
+                                        ctypes.c_double, _u64p, ctypes.c_uint64,
+                                        ctypes.c_uint64, _lp]
+        L.bbo_gamma1.argtypes = [ctypes.c_double, _u64p, ctypes.c_uint64, ctypes.c_uint]
+        L.bbo_gamma1.restype = ctypes.c_double
+        L.bbo_tau_from_sum.argtypes = [ctypes.c_double, ctypes.c_long, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, _u64p, ctypes.c_uint64]
+        L.bbo_tau_from_sum.restype = ctypes.c_double
+        L.bbo_sum_abs_pow.argtypes = [_dp, ctypes.c_long, ctypes.c_double]
+        L.bbo_sum_abs_pow.restype = ctypes.c_double
+        L.bbo_sig2_from_rss.argtypes = [ctypes.c_double, ctypes.c_long, ctypes.c_double,
+                                        ctypes.c_double, _u64p, ctypes.c_uint64]
+        L.bbo_sig2_from_rss.restype = ctypes.c_double
+        L.bbo_alpha_mh.argtypes = [ctypes.c_double, _dp, ctypes.c_long, ctypes.c_double,
+                                   ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp,
+                                   _u64p, ctypes.c_uint64]
+        L.bbo_alpha_mh.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _key(seed: int, stream: int):
+    return (ctypes.c_uint64 * 2)(seed & 0xFFFFFFFFFFFFFFFF, stream & 0xFFFFFFFFFFFFFFFF)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def philox4x64(ctr, key):
+    c = (ctypes.c_uint64 * 4)(*[int(x) for x in ctr])
+    k = (ctypes.c_uint64 * 2)(*[int(x) for x in key])
+    o = (ctypes.c_uint64 * 4)()
+    lib().bbo_philox4x64(c, k, o)
+    return [int(x) for x in o]
+
+
+def uniforms(seed, stream, t, kind, j, a=0, b=0):
+    out = (ctypes.c_double * 4)()
+    lib().bbo_uniforms(_key(seed, stream), t, kind, j, a, b, out)
+    return np.array(out[:])
+
+
+def normals(count, seed, stream, t, kind, j0=0):
+    out = np.empty(count, dtype=np.float64)
+    lib().bbo_normals(_ptr(out), count, _key(seed, stream), t, kind, j0)
+    return out
+
+
+def retstable(h, alpha, V0=1.0, seed=0, stream=0, t=0, j=0, counts=False):
+    no, ni = ctypes.c_long(0), ctypes.c_long(0)
+    x = lib().bbo_retstable(float(h), float(alpha), float(V0), _key(seed, stream), t, j,
+                            ctypes.byref(no), ctypes.byref(ni))
+    if counts:
+        return x, no.value, ni.value
+    return x
+
+
+def retstable_batch(alpha, V0, h, seed=0, stream=0, t=0):
+    """Mirror of ``.C("retstable_LD", x, alpha, V0, h, num)`` (BridgeWrapper.cpp:965-984)."""
+    alpha = np.ascontiguousarray(alpha, dtype=np.float64)
+    V0 = np.ascontiguousarray(V0, dtype=np.float64)
+    h = np.ascontiguousarray(h, dtype=np.float64)
+    x = np.zeros(h.shape[0], dtype=np.float64)
+    lib().bbo_retstable_batch(_ptr(x), _ptr(alpha), _ptr(V0), _ptr(h), h.shape[0],
+                              _key(seed, stream), t)
+    return x
+
+
+def sample_lambda(beta, alpha, tau, seed, stream, t, j0=0):
+    beta = np.ascontiguousarray(beta, dtype=np.float64)
+    lam = np.empty_like(beta)
+    att = ctypes.c_long(0)
+    lib().bbo_sample_lambda(_ptr(lam), _ptr(beta), beta.shape[0], alpha, tau,
+                            _key(seed, stream), t, j0, ctypes.byref(att))
+    return lam
+
+
+def gamma1(shape, seed, stream, t, kind):
+    return lib().bbo_gamma1(shape, _key(seed, stream), t, kind)
+
+
+def sum_abs_pow(beta, alpha):
+    beta = np.ascontiguousarray(beta, dtype=np.float64)
+    return lib().bbo_sum_abs_pow(_ptr(beta), beta.shape[0], alpha)
+
+
+def tau_from_sum(s, p, alpha, nu_shape, nu_rate, seed, stream, t):
+    return lib().bbo_tau_from_sum(s, p, alpha, nu_shape, nu_rate, _key(seed, stream), t)
+
+
+def sig2_from_rss(rss, n, sig2_shape, sig2_scale, seed, stream, t):
+    return lib().bbo_sig2_from_rss(rss, n, sig2_shape, sig2_scale, _key(seed, stream), t)
+
+
+def alpha_mh(a_old, beta, tau, pr_a, pr_b, seed, stream, t, ep=0.1):
+    beta = np.ascontiguousarray(beta, dtype=np.float64)
+    s = np.empty_like(beta)
+    return lib().bbo_alpha_mh(a_old, _ptr(beta), beta.shape[0], tau, pr_a, pr_b, ep, _ptr(s),
+                              _key(seed, stream), t)

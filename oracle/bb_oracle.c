@@ -1,0 +1,348 @@
+/*
+ * bb_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference BayesBridge normal-mixture ("stable") Gibbs
+ * sweep, used exclusively as the checker by tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg.  Nothing in the product (bayesbridge_amd/,
+ * BayesBridge.so) links, loads or calls this file.
+ *
+ * PARITY UNPINNED against the reference's own outputs: the reference ships no
+ * golden vectors / fixtures for this path, R is not installed,
+ * and the reference C++ cannot be built here (Code/C/retstable.h:7 includes the
+ * un-vendored RNG.hpp; BridgeRegression.h:67-68 includes the un-vendored
+ * Matrix.h / RNG.hpp).  This restatement is pinned instead by
+ *   - Philox4x64-10 known-answer vectors (Random123 KAT) and numpy's
+ *     independent Philox implementation (tests/test_oracle_cpu.py),
+ *   - analytic properties of the exponentially tilted stable law
+ *     (E[S] = a h^(a-1), Laplace transform exp(-((h+t)^a - h^a))),
+ *   - closed-form Gaussian conditional moments of beta | rest, and
+ *   - 1-D quadrature of the exact bridge posterior (known sig2, tau).
+ *
+ * The reference draws its variates from R's RNG (absent).  Here every variate
+ * is a pure function of a Philox counter (DESIGN.md "RNG counter layout"), the
+ * same layout the HIP kernels use, so the GPU path and this oracle consume
+ * identical uniforms on fixed seeds.
+ *
+ * Reference citations are relative to /root/reference/.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+#define BBO_SQRT_PI 1.772453850905516027298167483341 /* retstable.cpp:14-16 */
+#define BBO_SQRT2 1.41421356237309504880
+#define BBO_PI_2 1.57079632679489661923
+
+/* ----------------------------------------------------------------------- */
+/* Philox4x64-10 (Salmon et al. 2011).  Independent of the product's copy. */
+/* ----------------------------------------------------------------------- */
+static inline void mulhilo64(uint64_t a, uint64_t b, uint64_t *hi, uint64_t *lo)
+{
+    __uint128_t p = (__uint128_t)a * (__uint128_t)b;
+    *hi = (uint64_t)(p >> 64);
+    *lo = (uint64_t)p;
+}
+
+void bbo_philox4x64(const uint64_t ctr_in[4], const uint64_t key_in[2], uint64_t out[4])
+{
+    uint64_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint64_t k0 = key_in[0], k1 = key_in[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) {
+            k0 += 0x9E3779B97F4A7C15ULL;
+            k1 += 0xBB67AE8584CAA73BULL;
+        }
+        uint64_t hi0, lo0, hi1, lo1;
+        mulhilo64(0xD2E7470EE14C6C93ULL, c0, &hi0, &lo0);
+        mulhilo64(0xCA5A826395121157ULL, c2, &hi1, &lo1);
+        uint64_t n0 = hi1 ^ c1 ^ k0;
+        uint64_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Counter layout: ctr = {t, (kind << 56) | j, a, b}; key = {seed, stream}. */
+enum {
+    BBO_KIND_LAMBDA_INNER = 1,
+    BBO_KIND_LAMBDA_OUTER = 2,
+    BBO_KIND_TAU = 3,
+    BBO_KIND_SIG2 = 4,
+    BBO_KIND_BETA_Z = 5,
+    BBO_KIND_DELTA = 6,
+    BBO_KIND_ALPHA = 7,
+};
+
+static inline void draw4(const uint64_t key[2], uint64_t t, unsigned kind, uint64_t j,
+                         uint64_t a, uint64_t b, double u[4])
+{
+    uint64_t ctr[4] = {t, ((uint64_t)kind << 56) | j, a, b}, o[4];
+    bbo_philox4x64(ctr, key, o);
+    for (int i = 0; i < 4; ++i)
+        u[i] = ((double)(o[i] >> 11) + 0.5) * 0x1.0p-53; /* open (0,1) */
+}
+
+static inline double bm_normal(double r0, double r1)
+{
+    return sqrt(-2.0 * log(r0)) * cos(2.0 * M_PI * r1);
+}
+
+void bbo_uniforms(const uint64_t key[2], uint64_t t, unsigned kind, uint64_t j,
+                  uint64_t a, uint64_t b, double out[4])
+{
+    draw4(key, t, kind, j, a, b, out);
+}
+
+/* z_j ~ N(0,1) for j in [j0, j0+count): one Philox block per normal. */
+void bbo_normals(double *out, long count, const uint64_t key[2], uint64_t t,
+                 unsigned kind, uint64_t j0)
+{
+    for (long i = 0; i < count; ++i) {
+        double u[4];
+        draw4(key, t, kind, j0 + (uint64_t)i, 0, 0, u);
+        out[i] = bm_normal(u[0], u[1]);
+    }
+}
+
+/* ----------------------------------------------------------------------- */
+/* Exponentially tilted positive stable sampler: Code/C/retstable.cpp.      */
+/* ----------------------------------------------------------------------- */
+static double sinc_MM(double x) /* retstable.cpp:18-29 */
+{
+    double ax = fabs(x);
+    if (ax < 0.006) {
+        if (x == 0.) return 1;
+        double x2 = x * x;
+        if (ax < 2e-4) return 1. - x2 / 6.;
+        return 1. - x2 / 6. * (1 - x2 / 20.);
+    }
+    return sin(x) / x;
+}
+
+static double A_(double x, double alpha) /* retstable.cpp:40-47 (_A_3) */
+{
+    double Ia = 1. - alpha;
+    return pow(Ia * sinc_MM(Ia * x), Ia) * pow(alpha * sinc_MM(alpha * x), alpha) / sinc_MM(x);
+}
+
+static double BdB0(double x, double alpha) /* retstable.cpp:73-77 */
+{
+    double Ia = 1. - alpha;
+    double den = pow(sinc_MM(alpha * x), alpha) * pow(sinc_MM(Ia * x), Ia);
+    return sinc_MM(x) / den;
+}
+
+/*
+ * retstable.cpp:94-271.  Outer attempt o uses block (t, OUTER|j, o, 0); inner
+ * attempt i of outer attempt o uses block (t, INNER|j, o, i).  Slots: inner
+ * r0=V, r1=W, r2=W_ (or Box-Muller u1), r3=Box-Muller u2; outer r0=V_,
+ * r1=unif / exp / Box-Muller u1, r2=Box-Muller u2.
+ * *n_outer / *n_inner (may be NULL) return the attempts consumed.
+ */
+double bbo_retstable(double h, double alpha, double V0, const uint64_t key[2],
+                     uint64_t t, uint64_t j, long *n_outer, long *n_inner)
+{
+    if (n_outer) *n_outer = 0;
+    if (n_inner) *n_inner = 0;
+    if (alpha == 1.) return V0; /* :104-110 */
+    if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) { /* :112-115 (print only) */
+        fprintf(stderr, "Problem with parameter.\n");
+        fprintf(stderr, "V0: %g; h: %g; alpha: %g\n", V0, h, alpha);
+    }
+    const double c1 = sqrt(BBO_PI_2); /* :121-123 */
+    const double c2 = 2. + c1;
+    double b = (1. - alpha) / alpha;
+
+    double lambda_alpha = pow(h, alpha) * V0; /* :131 */
+    double gamma = lambda_alpha * alpha * (1. - alpha); /* :140-147 */
+    double sgamma = sqrt(gamma);
+    double c3 = c2 * sgamma;
+    double xi = (1. + BBO_SQRT2 * c3) / M_PI;
+    double psi = c3 * exp(-gamma * M_PI * M_PI / 8.) / BBO_SQRT_PI;
+    double w1 = c1 * xi / sgamma;
+    double w2 = 2. * BBO_SQRT_PI * psi;
+    double w3 = xi * M_PI;
+    double X = 0, c = 0, E = 0;
+    long ninner = 0;
+
+    for (uint64_t o = 0;; ++o) { /* outer loop :155-256 */
+        double U = 0, z = 0, Z = 0;
+        for (uint64_t i = 0;; ++i) { /* inner loop :162-207 */
+            double r[4];
+            draw4(key, t, BBO_KIND_LAMBDA_INNER, j, o, i, r);
+            ++ninner;
+            double V = r[0];
+            if (gamma >= 1) {
+                if (V < w1 / (w1 + w2)) U = fabs(bm_normal(r[2], r[3])) / sgamma;
+                else {
+                    double W_ = r[2];
+                    U = M_PI * (1. - W_ * W_);
+                }
+            } else {
+                double W_ = r[2];
+                if (V < w3 / (w2 + w3)) U = M_PI * W_;
+                else U = M_PI * (1. - W_ * W_);
+            }
+            double W = r[1];
+            double zeta = sqrt(BdB0(U, alpha));
+            z = 1 / (1 - pow(1 + alpha * zeta / sgamma, -1 / alpha));
+            double rho = M_PI * exp(-lambda_alpha * (1. - 1. / (zeta * zeta))) /
+                         ((1. + c1) * sgamma / zeta + z);
+            double d = 0.;
+            if (U >= 0 && gamma >= 1) d += xi * exp(-gamma * U * U / 2.);
+            if (U > 0 && U < M_PI) d += psi / sqrt(M_PI - U);
+            if (U >= 0 && U <= M_PI && gamma < 1) d += xi;
+            rho *= d;
+            Z = W * rho;
+            if (U < M_PI && Z <= 1.) break;
+        }
+        double a = pow(A_(U, alpha), 1. / (1. - alpha)); /* :212-218 */
+        double m = pow(b / a, alpha) * lambda_alpha;
+        double delta = sqrt(m * alpha / a);
+        double a1 = delta * c1;
+        double a2 = delta;
+        double a3 = z / a;
+        double s = a1 + a2 + a3;
+
+        double r[4];
+        draw4(key, t, BBO_KIND_LAMBDA_OUTER, j, o, 0, r);
+        double V_ = r[0], N_ = 0., E_ = 0.; /* :224-238 */
+        if (V_ < a1 / s) {
+            N_ = bm_normal(r[1], r[2]);
+            X = m - delta * fabs(N_);
+        } else {
+            if (V_ < (a1 + a2) / s) X = m + delta * r[1];
+            else {
+                E_ = -log(r[1]);
+                X = m + delta + E_ * a3;
+            }
+        }
+        E = -log(Z); /* :239 */
+        c = a * (X - m); /* :247-251 (incl. the "MYMY" h=0 guard) */
+        c += (m != 0) ? h * (pow(X, -1. * b) - pow(m, -1. * b)) : 0.0;
+        if (X < m) c -= N_ * N_ / 2.;
+        else if (X > m + delta) c -= E_;
+        if (X >= 0 && c <= E) { /* :256 */
+            if (n_outer) *n_outer = (long)o + 1;
+            if (n_inner) *n_inner = ninner;
+            break;
+        }
+    }
+    return exp(1 / alpha * log(V0) - b * log(X)); /* :270 */
+}
+
+/* BridgeWrapper.cpp:965-984 (batch .C entry), counters (t, j = i). */
+void bbo_retstable_batch(double *x, const double *alpha, const double *V0, const double *h,
+                         long num, const uint64_t key[2], uint64_t t)
+{
+    for (long i = 0; i < num; ++i)
+        x[i] = bbo_retstable(h[i], alpha[i], V0[i], key, t, (uint64_t)i, NULL, NULL);
+}
+
+/* BridgeRegression.cpp:506-510; j0 = global index of beta[0] (column shards). */
+void bbo_sample_lambda(double *lambda, const double *beta, long p, double alpha, double tau,
+                       const uint64_t key[2], uint64_t t, uint64_t j0, long *attempts)
+{
+    long tot = 0;
+    for (long j = 0; j < p; ++j) {
+        long no = 0;
+        lambda[j] = 2 * bbo_retstable(beta[j] * beta[j] / (tau * tau), 0.5 * alpha, 1.0, key, t,
+                                      j0 + (uint64_t)j, &no, NULL);
+        tot += no;
+    }
+    if (attempts) *attempts = tot;
+}
+
+/* ----------------------------------------------------------------------- */
+/* Gamma / inverse gamma: the RNG contract gamma_rate / igamma.  */
+/* Marsaglia-Tsang with one Philox block per attempt.                       */
+/* ----------------------------------------------------------------------- */
+double bbo_gamma1(double shape, const uint64_t key[2], uint64_t t, unsigned kind)
+{
+    double a = shape, boost = 1.0;
+    if (a < 1.0) {
+        double u[4];
+        draw4(key, t, kind, 0, 0, 1, u);
+        boost = pow(u[0], 1.0 / a);
+        a += 1.0;
+    }
+    double d = a - 1.0 / 3.0;
+    double cc = 1.0 / sqrt(9.0 * d);
+    for (uint64_t k = 0;; ++k) {
+        double u[4];
+        draw4(key, t, kind, 0, k, 0, u);
+        double x = bm_normal(u[0], u[1]);
+        double v = 1.0 + cc * x;
+        if (v <= 0.0) continue;
+        v = v * v * v;
+        double uu = u[2];
+        double x2 = x * x;
+        if (uu < 1.0 - 0.0331 * x2 * x2) return d * v * boost;
+        if (log(uu) < 0.5 * x2 + d * (1.0 - v + log(v))) return d * v * boost;
+    }
+}
+
+/* BridgeRegression.cpp:453-465: nu ~ Ga(nu_shape + p/alpha, rate = nu_rate + sum|b|^a). */
+double bbo_tau_from_sum(double sum_abs_pow, long p, double alpha, double nu_shape, double nu_rate,
+                        const uint64_t key[2], uint64_t t)
+{
+    double shape = nu_shape + ((double)p) / alpha;
+    double rate = nu_rate + sum_abs_pow;
+    double nu = bbo_gamma1(shape, key, t, BBO_KIND_TAU) / rate;
+    return exp(-1.0 * log(nu) / alpha);
+}
+
+double bbo_sum_abs_pow(const double *beta, long p, double alpha)
+{
+    double rate = 0.0;
+    for (long j = 0; j < p; ++j) rate += exp(alpha * log(fabs(beta[j])));
+    return rate;
+}
+
+/* BridgeRegression.cpp:436-450: sig2 ~ IG(a + n/2, scale = b + rss/2). */
+double bbo_sig2_from_rss(double rss, long n, double sig2_shape, double sig2_scale,
+                         const uint64_t key[2], uint64_t t)
+{
+    double shape = sig2_shape + 0.5 * (double)n;
+    double scale = sig2_scale + 0.5 * rss;
+    return scale / bbo_gamma1(shape, key, t, BBO_KIND_SIG2);
+}
+
+/* BridgeRegression.cpp:469-476 */
+static double llh_alpha_marg(double alpha, const double *s, long p)
+{
+    double pp = (double)p;
+    double llh = pp * log(alpha) - pp * lgamma(1.0 / alpha);
+    for (long i = 0; i < p; ++i) llh -= exp(alpha * s[i]);
+    return llh;
+}
+
+static double log_dbeta(double x, double a, double b)
+{
+    return (a - 1.0) * log(x) + (b - 1.0) * log(1.0 - x) - (lgamma(a) + lgamma(b) - lgamma(a + b));
+}
+
+/* BridgeRegression.cpp:478-503 (random-walk MH on alpha, window ep).  s is scratch (p). */
+double bbo_alpha_mh(double a_old, const double *beta, long p, double tau, double pr_a,
+                    double pr_b, double ep, double *s, const uint64_t key[2], uint64_t t)
+{
+    for (long i = 0; i < p; ++i) s[i] = log(fabs(beta[i] / tau));
+    double u[4];
+    draw4(key, t, BBO_KIND_ALPHA, 0, 0, 0, u);
+    double l_new = fmax(0.0, a_old - ep);
+    double r_new = fmin(1.0, a_old + ep);
+    double d_new = r_new - l_new;
+    double a_new = l_new + d_new * u[0]; /* r.flat(l_new, r_new) */
+    double l_old = fmax(0.0, a_new - ep);
+    double r_old = fmin(1.0, a_new + ep);
+    double d_old = r_old - l_old;
+    double log_accept = llh_alpha_marg(a_new, s, p) - llh_alpha_marg(a_old, s, p) +
+                        log_dbeta(a_new, pr_a, pr_b) - log_dbeta(a_old, pr_a, pr_b) +
+                        log(d_old) - log(d_new);
+    if (u[1] > exp(log_accept)) return a_old;
+    return a_new;
+}

@@ -1,0 +1,223 @@
+"""TEST INFRASTRUCTURE ONLY -- numpy restatement of the reference stable Gibbs driver.
+
+Restates ``bridge_regression_stable`` (Code/C/BridgeWrapper.cpp:207-313), its
+orthogonal-design twin (:434-537) and the conditional samplers of
+Code/C/BridgeRegression.cpp (:436-465 tau/sig2, :469-503 alpha, :506-510 lambda,
+:514-521 beta ortho, :552-575 beta).  Scalar draws and the tilted-stable
+sampler come from the C oracle (``oracle/bb_oracle.c``); dense linear algebra
+from numpy/scipy LAPACK.
+
+Used only as the checker (tests, smoke) and as bench.py's ``cpu_baseline``.
+PARITY UNPINNED against reference outputs -- see oracle/__init__.py.
+
+RNG counter layout (shared with the HIP path):
+    key = (seed, stream); ctr = (t, kind << 56 | j, a, b)
+    t = 0 is the pre-burn tau draw (BridgeWrapper.cpp:262), burn-in sweep i
+    (0..burn) is t = 1 + i, MCMC sweep i (1..M-1) is t = burn + 1 + i.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import scipy.linalg as sla
+
+from . import (KIND_BETA_Z, KIND_DELTA, alpha_mh, normals, sample_lambda, sig2_from_rss,
+               sum_abs_pow, tau_from_sum)
+
+
+def least_squares(G, c, n):
+    """BridgeRegression.cpp:79-91: symsolve(XX, Xy); singular X'X -> 0 with a warning.
+
+    p > n is singular by construction and returns 0 without factorising.
+    """
+    p = G.shape[0]
+    if p > n:
+        return np.zeros(p), False
+    try:
+        L = np.linalg.cholesky(G)
+    except np.linalg.LinAlgError:
+        return np.zeros(p), False
+    y = sla.solve_triangular(L, c, lower=True)
+    return sla.solve_triangular(L.T, y, lower=False), True
+
+
+def beta_step_chol(G, c, lam, sig2, tau, z):
+    """BridgeRegression.cpp:552-575 (reference-literal p x p Cholesky)."""
+    A = G.copy()
+    A[np.diag_indices_from(A)] += lam * sig2 / (tau * tau)
+    U = sla.cholesky(A, lower=False)  # A = U'U  (chol(U, VInv, 'U'))
+    b = sla.solve_triangular(U, c, trans="T", lower=False)
+    b = sla.solve_triangular(U, b, lower=False)
+    x = sla.solve_triangular(U, z, lower=False)
+    return b + np.sqrt(sig2) * x
+
+
+def beta_step_woodbury(X, y, lam, sig2, tau, z, delta):
+    """Exact draw of the same conditional for p > n (Bhattacharya et al. 2016).
+
+    Delta = tau^2/lambda, u = sqrt(Delta) z, v = X u / sig + delta,
+    M = I + X diag(Delta) X' / sig2, w = M^-1 (y/sig - v), beta = u + Delta X'w / sig.
+    """
+    sig = np.sqrt(sig2)
+    D = (tau * tau) / lam
+    u = np.sqrt(D) * z
+    v = (X @ u) / sig + delta
+    M = (X * D) @ X.T / sig2
+    M[np.diag_indices_from(M)] += 1.0
+    Lm = np.linalg.cholesky(M)
+    w = sla.solve_triangular(Lm, y / sig - v, lower=True)
+    w = sla.solve_triangular(Lm.T, w, lower=False)
+    return u + D * (X.T @ w) / sig
+
+
+def beta_step_ortho(Gdiag, c, lam, sig2, tau, z):
+    """BridgeRegression.cpp:514-521."""
+    u = Gdiag + lam * sig2 / (tau * tau)
+    s = np.sqrt(sig2 / u)
+    m = c / u
+    return m + s * z
+
+
+def bridge_regression_stable(y, X, nsamp, burn=500, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0,
+                             nu_shape=2.0, nu_rate=2.0, alpha_a=1.0, alpha_b=1.0,
+                             true_sig2=0.0, true_tau=0.0, true_alpha=None, ortho=False,
+                             seed=0, stream=0, method="auto", record_state=False):
+    """Restatement of bridge_reg_stable / bridge_regression_stable[_ortho].
+
+    ``alpha`` plays the role of bridge.reg.stb's ``alpha`` (= true_alpha).  Returns a
+    dict with traces beta (P x M), lambda (P x M), sig2, tau, alpha (M), runtime.
+    ``method``: "chol" (reference-literal), "woodbury" (p > n draw), "auto" (chol if
+    p <= n else woodbury -- the HIP path's choice).
+    """
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, p = X.shape
+    M = int(nsamp)
+    if true_alpha is None:
+        true_alpha = alpha
+    know_sig2 = true_sig2 > 0
+    know_tau = true_tau > 0
+    know_alpha = true_alpha > 0
+    if method == "auto":
+        method = "chol" if p <= n else "woodbury"
+    if ortho:
+        method = "ortho"
+
+    need_G = method in ("chol", "ortho") or p <= n
+    G = X.T @ X if need_G else None
+    c = X.T @ y
+    if G is not None:
+        b0, _ = least_squares(G, c, n)
+    else:
+        b0 = np.zeros(p)
+
+    beta = np.zeros((p, M))
+    lam = np.ones((p, M))
+    sig2 = np.zeros(M)
+    tau = np.zeros(M)
+    alph = np.zeros(M)
+    beta[:, 0] = b0
+    alph[0] = 0.5
+    if know_sig2:
+        sig2[:] = true_sig2
+    if know_tau:
+        tau[:] = true_tau
+    if know_alpha:
+        alph[:] = true_alpha
+
+    def draw_tau(b, a, t):
+        return tau_from_sum(sum_abs_pow(b, a), p, a, nu_shape, nu_rate, seed, stream, t)
+
+    def draw_sig2(b, t):
+        r = y - X @ b
+        return sig2_from_rss(float(r @ r), n, sig2_shape, sig2_scale, seed, stream, t)
+
+    def draw_beta(lmb, s2, tu, t):
+        z = normals(p, seed, stream, t, KIND_BETA_Z)
+        if method == "chol":
+            return beta_step_chol(G, c, lmb, s2, tu, z)
+        if method == "ortho":
+            return beta_step_ortho(np.diag(G).copy(), c, lmb, s2, tu, z)
+        d = normals(n, seed, stream, t, KIND_DELTA)
+        return beta_step_woodbury(X, y, lmb, s2, tu, z, d)
+
+    states = []
+    if not know_tau and not ortho:  # BridgeWrapper.cpp:262 (the non-ortho driver only)
+        tau[0] = draw_tau(beta[:, 0], alph[0], 0)
+    # Burn-in (:266-276 / ortho :493-503), all in slot 0.
+    for i in range(burn + 1):
+        t = 1 + i
+        if not know_tau:
+            tau[0] = draw_tau(beta[:, 0], alph[0], t)
+        if not know_sig2:
+            sig2[0] = draw_sig2(beta[:, 0], t)
+        lam[:, 0] = sample_lambda(beta[:, 0], alph[0], tau[0], seed, stream, t)
+        beta[:, 0] = draw_beta(lam[:, 0], sig2[0], tau[0], t)
+        if not know_alpha:
+            alph[0] = alpha_mh(alph[0], beta[:, 0], tau[0], alpha_a, alpha_b, seed, stream, t)
+        if record_state:
+            states.append((t, tau[0], sig2[0], lam[:, 0].copy(), beta[:, 0].copy(), alph[0]))
+    t0 = time.perf_counter()
+    # MCMC (:287-298 / ortho :513-523).  Quirk kept: non-ortho passes (alpha_b, alpha_b).
+    pa = alpha_a if ortho else alpha_b
+    for i in range(1, M):
+        t = burn + 1 + i
+        if not know_tau:
+            tau[i] = draw_tau(beta[:, i - 1], alph[i - 1], t)
+        if not know_sig2:
+            sig2[i] = draw_sig2(beta[:, i - 1], t)
+        lam[:, i] = sample_lambda(beta[:, i - 1], alph[i - 1], tau[i], seed, stream, t)
+        beta[:, i] = draw_beta(lam[:, i], sig2[i], tau[i], t)
+        if not know_alpha:
+            alph[i] = alpha_mh(alph[i - 1], beta[:, i], tau[i], pa, alpha_b, seed, stream, t)
+        if record_state:
+            states.append((t, tau[i], sig2[i], lam[:, i].copy(), beta[:, i].copy(), alph[i]))
+    runtime = time.perf_counter() - t0
+    out = dict(beta=beta, **{"lambda": lam}, sig2=sig2, tau=tau, alpha=alph, runtime=runtime,
+               method=method)
+    if record_state:
+        out["states"] = states
+    return out
+
+
+def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stream,
+                           allreduce, hyper, know_tau=False, know_sig2=False):
+    """One Gibbs sweep (tau, sig2, lambda, beta) on a column shard of X.
+
+    The multi-GPU decomposition of SURVEY.md 8(e) restated on the CPU:
+    ``allreduce`` sums a float64 vector over ranks.  Shard k holds columns
+    [j0, j0 + p_k); variates are indexed by the GLOBAL column j so the result is
+    independent of the shard count (up to Gram summation order).
+    Returns (beta_k_new, lambda_k, tau, sig2).
+    """
+    n = Xk.shape[0]
+    # 1. partial sum |b|^a and X_k b_k  -> one all-reduce
+    buf = np.concatenate([[sum_abs_pow(beta_k, alpha)], Xk @ beta_k])
+    buf = allreduce(buf)
+    S, Xb = buf[0], buf[1:]
+    if not know_tau:
+        tau = tau_from_sum(S, p, alpha, hyper["nu_shape"], hyper["nu_rate"], seed, stream, t)
+    if not know_sig2:
+        r = y - Xb
+        sig2 = sig2_from_rss(float(r @ r), n, hyper["sig2_shape"], hyper["sig2_scale"], seed,
+                             stream, t)
+    # 2. local latent draws and the partial Gram / X u  -> one all-reduce
+    lam = sample_lambda(beta_k, alpha, tau, seed, stream, t, j0=j0)
+    z = normals(beta_k.shape[0], seed, stream, t, KIND_BETA_Z, j0=j0)
+    D = (tau * tau) / lam
+    u = np.sqrt(D) * z
+    Gk = (Xk * D) @ Xk.T
+    buf = allreduce(np.concatenate([Gk.ravel(), Xk @ u]))
+    G = buf[: n * n].reshape(n, n)
+    Xu = buf[n * n:]
+    # 3. replicated n x n solve, then the local beta update
+    sig = np.sqrt(sig2)
+    delta = normals(n, seed, stream, t, KIND_DELTA)
+    v = Xu / sig + delta
+    Mm = G / sig2
+    Mm[np.diag_indices_from(Mm)] += 1.0
+    Lm = np.linalg.cholesky(Mm)
+    w = sla.solve_triangular(Lm, y / sig - v, lower=True)
+    w = sla.solve_triangular(Lm.T, w, lower=False)
+    return u + D * (Xk.T @ w) / sig, lam, tau, sig2

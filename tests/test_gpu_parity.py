@@ -1,0 +1,257 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on the
+same Philox counters.
+
+Tolerances (north star: posterior-mean beta within 1e-8 relative L2 of the CPU path):
+  * per-draw tilted-stable / lambda values: relative 1e-11 (libm vs ocml last-ulp
+    differences in pow/exp/log/sin), with accept/reject decision flips counted;
+  * Gram / Cholesky kernels: relative 1e-11 of the problem scale;
+  * whole chains: posterior mean relative L2 <= 1e-8, every trace <= 1e-6 elementwise.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import gibbs
+from tests.conftest import synthetic_problem
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xB4E5B41D6E
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def flips(a, b, tol=1e-6):
+    a, b = np.asarray(a), np.asarray(b)
+    return int(np.sum(np.abs(a - b) > tol * np.maximum(np.abs(b), 1e-300)))
+
+
+GRID_A = [0.05, 0.15, 0.25, 0.45, 0.75, 1.0]
+GRID_H = [0.0, 1e-4, 1e-2, 1.0, 1e2, 1e4, 1e6]
+
+
+def grid_inputs(reps=120):
+    a, h, v = [], [], []
+    for aa in GRID_A:
+        for hh in GRID_H:
+            for V0 in (1.0, 2.5):
+                a += [aa] * reps
+                h += [hh] * reps
+                v += [V0] * reps
+    return np.array(a), np.array(v), np.array(h)
+
+
+def test_retstable_batch_matches_oracle(gpu_lib):
+    bb = gpu_lib
+    a, v, h = grid_inputs()
+    g = bb.retstable_batch(a, v, h, seed=SEED, stream=3, t=17)
+    o = oracle.retstable_batch(a, v, h, seed=SEED, stream=3, t=17)
+    assert np.all(np.isfinite(g)) and np.all(g > 0)
+    nf = flips(g, o)
+    assert nf == 0, f"{nf} decision flips out of {len(g)}"
+    assert np.max(np.abs(g - o) / np.abs(o)) < 1e-11
+
+
+@pytest.mark.parametrize("group", [1, 2, 8, 64])
+def test_retstable_group_invariance(gpu_lib, group):
+    """G lanes per coefficient evaluate attempts speculatively; the first accepted attempt
+    in counter order wins, so every G gives the sequential result bit for bit."""
+    bb = gpu_lib
+    a, v, h = grid_inputs(reps=20)
+    ref = bb.retstable_batch(a, v, h, seed=SEED, stream=4, t=0, group=1)
+    got = bb.retstable_batch(a, v, h, seed=SEED, stream=4, t=0, group=group)
+    assert np.array_equal(ref, got)
+
+
+def test_retstable_c_entry_point(gpu_lib):
+    bb = gpu_lib
+    bb.set_seed(77)
+    x = bb.retstable_ld(5000, alpha=0.25, V0=1.0, h=1.0)
+    o = oracle.retstable_batch(np.full(5000, 0.25), np.ones(5000), np.ones(5000), seed=77,
+                               stream=0, t=0)
+    assert rel_err(x, o) < 1e-12
+    assert bb.get_rng_state() == (77, 1)
+    assert np.isnan(bb.retstable_ld(3, alpha=1.5))
+    assert np.isnan(bb.retstable_ld(3, h=-1.0))
+
+
+def test_sample_lambda_matches_oracle(gpu_lib):
+    bb = gpu_lib
+    rng = np.random.default_rng(0)
+    beta = rng.standard_normal(3000) * rng.choice([1e-4, 1e-1, 1, 10], size=3000)
+    for alpha, tau, j0 in ((0.5, 0.7, 0), (0.3, 2.0, 12345)):
+        g = bb.sample_lambda(beta, alpha, tau, SEED, 1, 9, j0=j0)
+        o = oracle.sample_lambda(beta, alpha, tau, SEED, 1, 9, j0=j0)
+        assert flips(g, o) == 0
+        assert np.max(np.abs(g - o) / o) < 1e-11
+
+
+@pytest.mark.parametrize("n,k", [(100, 50), (128, 1000), (300, 5000), (1000, 257)])
+def test_gram_matches_numpy(gpu_lib, n, k):
+    bb = gpu_lib
+    rng = np.random.default_rng(n + k)
+    Y = rng.standard_normal((n, k))
+    w = rng.uniform(0.0, 3.0, k)
+    C = bb.gram(Y, w)
+    ref = (Y * w) @ Y.T
+    scale = np.abs(Y) ** 2 @ w
+    assert np.max(np.abs(C - ref) / np.sqrt(np.outer(scale, scale))) < 1e-13 * max(k, 64)
+
+
+def test_gram_mfma_layout_asymmetric(gpu_lib):
+    """Exact integer data, asymmetric Y: catches a transposed or mis-rowed MFMA C/D map."""
+    bb = gpu_lib
+    rng = np.random.default_rng(5)
+    Y = rng.integers(-3, 4, size=(256, 64)).astype(np.float64)
+    w = rng.integers(0, 3, size=64).astype(np.float64)
+    assert np.array_equal(bb.gram(Y, w), (Y * w) @ Y.T)
+
+
+@pytest.mark.parametrize("m,nrhs", [(20, 1), (64, 2), (130, 1), (700, 2)])
+def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
+    bb = gpu_lib
+    rng = np.random.default_rng(m)
+    B = rng.standard_normal((m, m + 5))
+    A = B @ B.T + 0.1 * np.eye(m)
+    b = rng.standard_normal((m, nrhs))
+    x = bb.chol_solve(A, b)
+    ref = np.linalg.solve(A, b)
+    assert rel_err(x, ref) < 1e-10 * np.linalg.cond(A) ** 0.5
+
+
+def test_chol_solve_detects_non_spd(gpu_lib):
+    bb = gpu_lib
+    A = np.array([[1.0, 2.0], [2.0, 1.0]])
+    with pytest.raises(RuntimeError):
+        bb.chol_solve(A, np.ones(2))
+
+
+def compare_chain(g, o, tol_mean=1e-8, tol_elem=1e-6):
+    for key in ("beta", "lambda", "sig2", "tau", "alpha"):
+        gv = np.asarray(g[key])
+        ov = np.asarray(o[key])
+        if key in ("beta", "lambda"):
+            gv = gv.T  # R-style M x P  ->  P x M
+        assert gv.shape == ov.shape, (key, gv.shape, ov.shape)
+        assert np.all(np.isfinite(gv)), key
+        e = np.max(np.abs(gv - ov) / np.maximum(np.abs(ov), 1e-8))
+        assert e < tol_elem, (key, e)
+    pm_g = np.asarray(g["beta"]).mean(axis=0)
+    pm_o = np.asarray(o["beta"]).mean(axis=1)
+    assert rel_err(pm_g, pm_o) < tol_mean
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),                                   # C1 defaults: sig2, tau unknown, alpha = 0.5
+    dict(sig2_true=1.5),
+    dict(tau_true=0.8),
+    dict(alpha=0.3, nu_shape=0.5, nu_rate=0.5),
+])
+def test_chain_small_p_matches_oracle(gpu_lib, kw):
+    """C1 (n=100, p=20): reference-literal p x p Cholesky path, full chain."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(100, 20)
+    bb.set_seed(SEED)
+    g = bb.bridge_reg_stb(y, X, nsamp=300, burn=100, **kw)
+    o = gibbs.bridge_regression_stable(
+        y, X, 300, burn=100, alpha=kw.get("alpha", 0.5), nu_shape=kw.get("nu_shape", 2.0),
+        nu_rate=kw.get("nu_rate", 2.0), true_sig2=kw.get("sig2_true", 0.0),
+        true_tau=kw.get("tau_true", 0.0), seed=SEED, stream=0, method="chol")
+    compare_chain(g, o)
+
+
+def test_chain_unknown_alpha_matches_oracle(gpu_lib):
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(80, 12, seed=3)
+    bb.set_seed(SEED + 1)
+    g = bb.bridge_reg_stb(y, X, nsamp=200, burn=50, alpha=0.0)
+    o = gibbs.bridge_regression_stable(y, X, 200, burn=50, alpha=0.0, seed=SEED + 1, stream=0,
+                                       method="chol")
+    compare_chain(g, o)
+
+
+def test_chain_ortho_matches_oracle(gpu_lib):
+    bb = gpu_lib
+    rng = np.random.default_rng(9)
+    Q, _ = np.linalg.qr(rng.standard_normal((120, 15)))
+    X = Q * 4.0
+    y = X @ np.r_[np.ones(3), np.zeros(12)] + rng.standard_normal(120)
+    bb.set_seed(SEED + 2)
+    g = bb.bridge_reg_stb(y, X, nsamp=200, burn=50, ortho=True)
+    o = gibbs.bridge_regression_stable(y, X, 200, burn=50, ortho=True, seed=SEED + 2, stream=0)
+    compare_chain(g, o)
+
+
+def test_chain_wide_p_woodbury_matches_oracle(gpu_lib):
+    """p > n: the Woodbury draw on the GPU vs the oracle's Woodbury restatement."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(60, 250, seed=11)
+    bb.set_seed(SEED + 3)
+    g = bb.bridge_reg_stb(y, X, nsamp=150, burn=30)
+    o = gibbs.bridge_regression_stable(y, X, 150, burn=30, seed=SEED + 3, stream=0,
+                                       method="woodbury")
+    compare_chain(g, o, tol_mean=1e-8, tol_elem=1e-5)
+
+
+def test_diabetes_end_to_end(gpu_lib):
+    """442 x 10 diabetes design (Efron et al.; the reference's man/diabetes.Rd data)."""
+    sk = pytest.importorskip("sklearn.datasets")
+    d = sk.load_diabetes(scaled=False)
+    X = d.data - d.data.mean(axis=0)
+    y = d.target - d.target.mean()
+    bb = gpu_lib
+    bb.set_seed(SEED + 4)
+    g = bb.bridge_reg_stb(y, X, nsamp=500, burn=100)
+    o = gibbs.bridge_regression_stable(y, X, 500, burn=100, seed=SEED + 4, stream=0,
+                                       method="chol")
+    compare_chain(g, o)
+    # posterior means close to least squares for this well-determined design
+    ls = np.linalg.lstsq(X, y, rcond=None)[0]
+    pm = g["beta"].mean(axis=0)
+    assert np.corrcoef(pm, ls)[0, 1] > 0.9
+
+
+def teacher_forced_sweep(X, y, beta, tau, sig2, alpha, t, seed, stream, hyper):
+    """One oracle sweep (tau, sig2, lambda, beta) from a given state, Woodbury form."""
+    n, p = X.shape
+    tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, hyper["nu_shape"],
+                              hyper["nu_rate"], seed, stream, t)
+    r = y - X @ beta
+    sig2 = oracle.sig2_from_rss(float(r @ r), n, hyper["sig2_shape"], hyper["sig2_scale"], seed,
+                                stream, t)
+    lam = oracle.sample_lambda(beta, alpha, tau, seed, stream, t)
+    z = oracle.normals(p, seed, stream, t, oracle.KIND_BETA_Z)
+    d = oracle.normals(n, seed, stream, t, oracle.KIND_DELTA)
+    b = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
+    return b, lam, tau, sig2
+
+
+@pytest.mark.parametrize("n,p", [(1000, 5000), (2000, 6000)])
+def test_teacher_forced_sweep_large(gpu_lib, n, p):
+    """C2-scale and C3-height sweeps from an identical state (one sweep each)."""
+    bb = gpu_lib
+    X, y, btrue = synthetic_problem(n, p, seed=n + p)
+    cfg = bb.EngineConfig(n=n, p=p, seed=SEED, stream=7, trace_capacity=2)
+    e = bb.Engine(cfg, X, y)
+    assert e.method() == 2
+    e.init_state()
+    rng = np.random.default_rng(1)
+    beta0 = btrue + 0.05 * rng.standard_normal(p)
+    e.set_state(beta0, 1.0, 1.0, 0.5)
+    t = 5
+    e.run(t, 1, first_slot=0, slot_step=0)
+    s = e.state()
+    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
+    b, lam, tau, sig2 = teacher_forced_sweep(X, y, beta0, 1.0, 1.0, 0.5, t, SEED, 7, hyper)
+    assert abs(s["tau"] - tau) / tau < 1e-12
+    assert abs(s["sig2"] - sig2) / sig2 < 1e-12
+    assert flips(s["lambda"], lam) == 0
+    assert np.max(np.abs(s["lambda"] - lam) / lam) < 1e-11
+    assert rel_err(s["beta"], b) < 1e-9
+    assert e.error_flags() == 0
+    e.close()
