@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = [
     "bb_engine_set_state", "bb_engine_method", "bb_engine_enable_timing",
     "bb_engine_kernel_times", "bb_engine_reset_timing", "bb_engine_error_flags",
     "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
+    "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
 ]
 
 
@@ -103,6 +104,12 @@ def library(build: bool = True) -> ctypes.CDLL:
                                    c.c_uint64, c.c_uint64, c.c_uint64, c.c_int]
     L.bb_gram.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_bench_lambda.argtypes = [_dp, c.c_int, c.c_double, c.c_double, c.c_int, c.c_int,
+                                  c.c_int, _dp, _dp]
+    L.bb_engine_phase_times.argtypes = [c.c_void_p, _dp, c.c_int, _ip]
+    L.bb_phase_count.restype = c.c_int
+    L.bb_phase_name.argtypes = [c.c_int]
+    L.bb_phase_name.restype = c.c_char_p
     L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
     L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
     _lib = L
@@ -292,6 +299,18 @@ def sample_lambda(beta, alpha, tau, seed, stream, t, j0=0, group=0):
     return lam
 
 
+def bench_lambda(beta, alpha, tau, group, noinline=1, reps=20):
+    """Average ms of one lambda-kernel launch (microbenchmark) and its last draws."""
+    L = library()
+    _require_gpu()
+    beta = np.ascontiguousarray(beta, dtype=np.float64)
+    lam = np.zeros_like(beta)
+    ms = ctypes.c_double()
+    _check(L.bb_bench_lambda(_p(beta), beta.shape[0], alpha, tau, group, noinline, reps,
+                             ctypes.byref(ms), _p(lam)), "bb_bench_lambda")
+    return ms.value, lam
+
+
 def gram(Y, w):
     """C = Y diag(w) Y' on the device (fp64 MFMA)."""
     L = library()
@@ -431,6 +450,16 @@ class Engine:
         _check(library().bb_engine_kernel_times(self._h, ctypes.byref(g), ctypes.byref(s),
                                                 ctypes.byref(n)), "bb_engine_kernel_times")
         return g.value, s.value, n.value
+
+    def phase_times(self):
+        """Average ms per sweep per phase (HIP events on the engine stream)."""
+        L = library()
+        k = L.bb_phase_count()
+        ms = np.zeros(k)
+        n = ctypes.c_int()
+        _check(L.bb_engine_phase_times(self._h, _p(ms), k, ctypes.byref(n)),
+               "bb_engine_phase_times")
+        return {L.bb_phase_name(i).decode(): float(ms[i]) for i in range(k) if ms[i] > 0}
 
     def error_flags(self) -> int:
         f = ctypes.c_uint32()

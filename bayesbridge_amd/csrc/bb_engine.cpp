@@ -117,6 +117,14 @@ void next_call_key(uint64_t *k0, uint64_t *k1) {
 // ---------------------------------------------------------------------------
 // Engine
 // ---------------------------------------------------------------------------
+enum Phase {
+    PH_PRE, PH_SCALARS, PH_LAMBDA, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL, PH_SOLVE,
+    PH_BETA, PH_XB, PH_ALPHA, PH_END, PH_COUNT
+};
+static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "gram", "xu",
+                                            "reduce", "form", "chol", "solve", "beta", "xb",
+                                            "alpha", "end"};
+
 struct bb_engine {
     bb_config cfg{};
     int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
@@ -134,7 +142,7 @@ struct bb_engine {
     int nparts = 0, nbS = 0;
     // woodbury
     double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *PT = nullptr,
-           *w = nullptr;
+           *w = nullptr, *Wd = nullptr;
     int S = 1;
     size_t slab_stride = 0;
     // chol / ortho
@@ -146,11 +154,18 @@ struct bb_engine {
     int cap = 1;
     // communicator
     ncclComm_t comm = nullptr;
-    // timing
+    // timing: per-sweep event marks at phase starts, on the engine stream
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<int, int>> gram_pairs, sweep_pairs;
+    std::vector<std::vector<std::pair<int, int>>> sweep_marks;  // (phase, event)
     size_t ev_next = 0;
+
+    void mark(int phase) {
+        if (!timing) return;
+        int e0 = ev();
+        HIPCHECK(hipEventRecord(ev_pool[e0], stream));
+        sweep_marks.back().push_back({phase, e0});
+    }
 
     ~bb_engine() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -189,62 +204,65 @@ struct bb_engine {
     }
 
     void sweep(uint64_t t, int slot, int mcmc_phase) {
-        int e_sw0 = -1;
-        if (timing) {
-            e_sw0 = ev();
-            HIPCHECK(hipEventRecord(ev_pool[e_sw0], stream));
-        }
-        pre_and_scalars(t, slot, 0);
+        if (timing) sweep_marks.emplace_back();
+        mark(PH_PRE);
+        launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
+        allreduce(red1, (size_t)nbS + n_pad);
+        mark(PH_SCALARS);
+        launch_scalars(stream, red1, nbS, y, n, p, sc, hy, cfg.seed, cfg.stream, t,
+                       slot_ptr(tr_tau, slot, 1), slot_ptr(tr_sig2, slot, 1),
+                       slot_ptr(tr_alpha, slot, 1), 0, err);
         double *trl = slot_ptr(tr_lam, slot, p_loc);
         double *trb = slot_ptr(tr_beta, slot, p_loc);
+        mark(PH_LAMBDA);
         if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
-            int eg0 = -1, eg1 = -1;
-            if (timing) {
-                eg0 = ev();
-                HIPCHECK(hipEventRecord(ev_pool[eg0], stream));
-            }
+            mark(PH_GRAM);
             launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
-            if (timing) {
-                eg1 = ev();
-                HIPCHECK(hipEventRecord(ev_pool[eg1], stream));
-                gram_pairs.push_back({eg0, eg1});
-            }
+            mark(PH_XU);
             launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
+            mark(PH_REDUCE);
             launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad), red2);
             allreduce(red2, (size_t)n_pad * n_pad + n_pad);
+            mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, PT);
-            chol_bsolve(stream, M, n_pad, n_pad, M + (size_t)n_pad * n_pad, w, 1);
+            mark(PH_CHOL);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd);
+            mark(PH_SOLVE);
+            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1);
+            mark(PH_BETA);
             launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
         } else {
             launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
                           group, lam, nullptr, nullptr, trl, err);
             if (method == 1) {
+                mark(PH_FORM);
                 launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
-                chol_factor(stream, A, p_pad, p_pad, 1, err, PT);
+                mark(PH_CHOL);
+                chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd);
+                mark(PH_SOLVE);
                 launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
-                chol_bsolve(stream, A, p_pad, p_pad, Y2, W2, 2);
+                chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2);
+                mark(PH_BETA);
                 launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
             } else {
+                mark(PH_BETA);
                 launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta,
                                   trb);
             }
         }
+        mark(PH_XB);
         launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
         if (!hy.know_alpha) {
             // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
             // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
+            mark(PH_ALPHA);
             const double pr_a = (method != 3 && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
             launch_alpha_mh(stream, beta, p, sc, pr_a, hy.alpha_b, cfg.seed, cfg.stream, t,
                             slot_ptr(tr_alpha, slot, 1));
         }
-        if (timing) {
-            int e_sw1 = ev();
-            HIPCHECK(hipEventRecord(ev_pool[e_sw1], stream));
-            sweep_pairs.push_back({e_sw0, e_sw1});
-        }
+        mark(PH_END);
     }
 
     uint32_t read_err() {
@@ -315,6 +333,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
         e->w = dalloc<double>(n_pad, o);
     }
     e->PT = dalloc<double>((size_t)kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
+    e->Wd = dalloc<double>((size_t)kNB * (n_pad > p_pad ? n_pad : p_pad), o);
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
     const bool small = c.p <= c.n && c.world == 1;
     if (e->method != 2 || small) {
@@ -366,10 +385,10 @@ void engine_init_state(bb_engine *e) {
         e->clear_err();
         launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, e->p_pad, e->A,
                       e->p_pad, e->p_pad);
-        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT);
+        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT, e->Wd);
         HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
                                 e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
-        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Y2, e->W2, 1);
+        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1);
         uint32_t f = e->read_err();
         ls_ok = (f & 8u) == 0;
         if (ls_ok) {
@@ -616,31 +635,60 @@ int bb_engine_enable_timing(bb_engine *e, int enable) {
 
 int bb_engine_reset_timing(bb_engine *e) {
     (void)hipStreamSynchronize(e->stream);
-    e->gram_pairs.clear();
-    e->sweep_pairs.clear();
+    e->sweep_marks.clear();
     e->ev_next = 0;
     return 0;
 }
+
+int bb_engine_phase_times(bb_engine *e, double *ms, int cap, int *samples) {
+    try {
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        std::vector<double> acc(PH_COUNT, 0.0);
+        for (auto &marks : e->sweep_marks)
+            for (size_t i = 0; i + 1 < marks.size(); ++i) {
+                float v = 0;
+                HIPCHECK(hipEventElapsedTime(&v, e->ev_pool[marks[i].second],
+                                             e->ev_pool[marks[i + 1].second]));
+                acc[marks[i].first] += v;
+            }
+        const double ns = e->sweep_marks.empty() ? 1.0 : (double)e->sweep_marks.size();
+        for (int i = 0; i < cap && i < PH_COUNT; ++i) ms[i] = acc[i] / ns;
+        if (samples) *samples = (int)e->sweep_marks.size();
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+const char *bb_phase_name(int i) { return (i >= 0 && i < PH_COUNT) ? kPhaseNames[i] : ""; }
+int bb_phase_count(void) { return PH_COUNT; }
 
 int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
                            int *samples) {
     try {
         HIPCHECK(hipStreamSynchronize(e->stream));
         double g = 0, s = 0;
-        for (auto &pr : e->gram_pairs) {
-            float ms = 0;
-            HIPCHECK(hipEventElapsedTime(&ms, e->ev_pool[pr.first], e->ev_pool[pr.second]));
-            g += ms;
+        int ng = 0;
+        for (auto &marks : e->sweep_marks) {
+            for (size_t i = 0; i + 1 < marks.size(); ++i)
+                if (marks[i].first == PH_GRAM) {
+                    float v = 0;
+                    HIPCHECK(hipEventElapsedTime(&v, e->ev_pool[marks[i].second],
+                                                 e->ev_pool[marks[i + 1].second]));
+                    g += v;
+                    ++ng;
+                }
+            if (marks.size() >= 2) {
+                float v = 0;
+                HIPCHECK(hipEventElapsedTime(&v, e->ev_pool[marks.front().second],
+                                             e->ev_pool[marks.back().second]));
+                s += v;
+            }
         }
-        for (auto &pr : e->sweep_pairs) {
-            float ms = 0;
-            HIPCHECK(hipEventElapsedTime(&ms, e->ev_pool[pr.first], e->ev_pool[pr.second]));
-            s += ms;
-        }
-        if (gram_ms_avg) *gram_ms_avg = e->gram_pairs.empty() ? 0.0 : g / e->gram_pairs.size();
-        if (sweep_ms_avg)
-            *sweep_ms_avg = e->sweep_pairs.empty() ? 0.0 : s / e->sweep_pairs.size();
-        if (samples) *samples = (int)e->sweep_pairs.size();
+        if (gram_ms_avg) *gram_ms_avg = ng ? g / ng : 0.0;
+        if (sweep_ms_avg) *sweep_ms_avg = e->sweep_marks.empty() ? 0.0 : s / e->sweep_marks.size();
+        if (samples) *samples = (int)e->sweep_marks.size();
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;
@@ -721,6 +769,44 @@ int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, do
     return rc;
 }
 
+int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int group,
+                    int noinline, int reps, double *ms_avg, double *lambda_out) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        double *db = dalloc<double>(p, owned), *dl = dalloc<double>(p, owned);
+        DevScalars *dsc = dalloc<DevScalars>(1, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        DevScalars s{};
+        s.tau = tau;
+        s.alpha = alpha;
+        HIPCHECK(hipMemcpy(dsc, &s, sizeof(s), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(db, beta, p * sizeof(double), hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        launch_lambda_variant(0, db, p, dsc, 1, 0, 1, group, noinline, dl, de);  // warm
+        HIPCHECK(hipEventRecord(e0, 0));
+        for (int r = 0; r < reps; ++r)
+            launch_lambda_variant(0, db, p, dsc, 1, 0, 2 + r, group, noinline, dl, de);
+        HIPCHECK(hipEventRecord(e1, 0));
+        HIPCHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+        *ms_avg = ms / reps;
+        if (lambda_out)
+            HIPCHECK(hipMemcpy(lambda_out, dl, p * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 int bb_gram(double *C, const double *Yh, const double *wh, int n, int k) {
     std::vector<void *> owned;
     int rc = 0;
@@ -772,10 +858,11 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
             for (int r = 0; r < m; ++r) h[(size_t)r + (size_t)(m_pad + q) * m_pad] = bh[r + (size_t)q * m];
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
         double *PT = dalloc<double>((size_t)kNB * (m_pad + kNB), owned);
+        double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
-        chol_factor(0, dA, m_pad, m_pad, 1, de, PT);
-        chol_bsolve(0, dA, m_pad, m_pad, dA + (size_t)m_pad * m_pad, W, nrhs);
+        chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd);
+        chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, nrhs);
         HIPCHECK(hipGetLastError());
         std::vector<double> hw((size_t)m_pad * nrhs);
         HIPCHECK(hipMemcpy(hw.data(), W, hw.size() * sizeof(double), hipMemcpyDeviceToHost));

@@ -42,6 +42,10 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
                    int group, double *lam, double *D, double *u, double *lam_trace,
                    uint32_t *err);
 
+void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
+                           uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,
+                           double *lam, uint32_t *err);
+
 // slabs[s] (ld = ldo) gets the upper triangle (column-major) of Y diag(w) Y' over
 // K-range s; Y is n_pad x K column-major with ld = ldy (n_pad multiple of 128).
 int gram_splits_for(int n_pad, int K);
@@ -81,13 +85,14 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 
 // In-place upper Cholesky A = U'U of the leading m_pad x m_pad block with the
 // forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
-// PT: scratch of kNB x (m_pad + nrhs_blocks * kNB) doubles.
+// PT: scratch of kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
+// kNB x kNB receiving U_kk^-T (used by chol_bsolve).
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT);
+                 double *PT, double *Wd);
 
-// Backward solve U W = Y (Y, W: m_pad x nrhs, ld = m_pad); Y is overwritten.
-void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, double *Y, double *W,
-                 int nrhs);
+// Backward solve U W = Y (Y, W: m_pad x nrhs <= 2, ld = m_pad); Y is overwritten.
+void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
+                 double *Y, double *W, int nrhs);
 
 // beta_j = u_j + D_j (X_j . w) / sig (Woodbury update); writes beta and trace.
 void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,

@@ -56,11 +56,14 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
 // ---------------------------------------------------------------------------
 // tilted stable draws
 // ---------------------------------------------------------------------------
+// Lanes per coefficient (inner-attempt speculation).  Measured on MI355X with the C3
+// h-distribution (tools/bench_lambda.py): p=50000 best at G=4..8, p=6250 at G=16;
+// tiny p (C1) wants the widest group for latency.
 int stable_group_for(long count) {
-    long target = 131072;  // lanes worth of attempts in flight (256 CUs x 4 SIMD x 2 x 64)
+    if (count <= 1024) return 64;
     long g = 1;
-    while (g < 64 && count * g * 2 <= target) g *= 2;
-    return (int)g;
+    while (g < 16 && count * g * 2 <= 100000) g *= 2;
+    return (int)(g < 4 ? 4 : g);
 }
 
 template <int G>
@@ -100,7 +103,7 @@ void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const
 
 // lambda_j = 2 retstable(beta_j^2 / tau^2, alpha / 2, 1)   (BridgeRegression.cpp:506-510);
 // Woodbury mode also forms D_j = tau^2 / lambda_j and u_j = sqrt(D_j) z_j.
-template <int G>
+template <int G, bool NI = (BB_STABLE_NOINLINE != 0)>
 __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, int p_pad,
                                                 uint64_t j0, const DevScalars *sc, Key key,
                                                 uint64_t t, int mode, double *lam, double *D,
@@ -112,7 +115,8 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
     const double alpha = sc->alpha;
     const double b = active ? beta[i] : 0.0;
     const double h = b * b / (tau * tau);
-    double x = stable_group_draw<G>(active, h, 0.5 * alpha, 1.0, key, t, j0 + (uint64_t)i, err);
+    double x = stable_group_draw<G, NI>(active, h, 0.5 * alpha, 1.0, key, t, j0 + (uint64_t)i,
+                                        err);
     if ((threadIdx.x & (G - 1)) == 0 && i < p_pad) {
         if (active) {
             const double l = 2 * x;
@@ -152,6 +156,30 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
             k_lambda<1><<<(p_pad + 255) / 256, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
                                                             mode, lam, D, u, lam_trace, err);
     }
+}
+
+// Microbenchmark: launch k_lambda with an explicit group size and inlining variant.
+void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
+                           uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,
+                           double *lam, uint32_t *err) {
+    Key key{k0, k1};
+    long threads = (long)p * group;
+    int blocks = (int)((threads + 255) / 256);
+#define BB_V(G)                                                                               \
+    case G:                                                                                   \
+        if (noinline)                                                                         \
+            k_lambda<G, true><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,   \
+                                                     lam, nullptr, nullptr, nullptr, err);    \
+        else                                                                                  \
+            k_lambda<G, false><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,  \
+                                                      lam, nullptr, nullptr, nullptr, err);   \
+        break;
+    switch (group) {
+        BB_V(1) BB_V(2) BB_V(4) BB_V(8) BB_V(16) BB_V(32) BB_V(64)
+        default:
+            break;
+    }
+#undef BB_V
 }
 
 // ---------------------------------------------------------------------------
@@ -504,89 +532,138 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 
 // ---------------------------------------------------------------------------
 // Blocked right-looking Cholesky A = U'U (upper, column-major, NB = 64) with the
-// forward solve folded into trailing right-hand-side column blocks.
-//
-// k_chol_panel (step k): workgroup q factors the augmented block [A_kk | A_kj],
-// j = k + q, in registers (thread = one row x 8 or 16 columns; row c of the block is
-// broadcast through LDS each step, one barrier per pivot).  q == 0 writes U_kk;
-// q > 0 writes U_kj = U_kk^-T A_kj and a row-major copy PT[s][j*64 + x] used by the
-// trailing update so that its MFMA operands are lane-contiguous.
+// forward solve folded into trailing right-hand-side column blocks.  Per step k:
+//   k_chol_diag   (1 workgroup)  eliminates [A_kk | I] -> U_kk and W_k = U_kk^-T;
+//   k_chol_panel  (MFMA)         U_kj = W_k A_kj for every column block j > k (RHS
+//                                blocks included = forward substitution), written to A
+//                                and row-major to PT so the update reads lane-contiguous;
+//   k_chol_update (MFMA)         A_ij -= U_ki' U_kj for k < i <= j.
+// W_k is kept (Wd[k]) for the backward solve (U_kk^-1 = W_k').
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void k_chol_panel(double *A, int lda, int k, double *PT,
-                                                    int ldpt, uint32_t *err) {
-    __shared__ double buf[2][128];
+__global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, double *Wd,
+                                                   uint32_t *err) {
+    __shared__ __attribute__((aligned(16))) double buf[2][128];
     __shared__ double dsq[64];
-    const int j = k + blockIdx.x;
-    const bool aug = (j != k);
-    const int ncol = aug ? 128 : 64;
-    const int nm = ncol / 8;
     const int tid = threadIdx.x;
     const int r = tid & 63;
-    const int cg = tid >> 6;  // 0..7
-    const int kb = k * kNB, jb = j * kNB;
+    const int cg = tid >> 6;  // 0..7 -> columns cg*16 .. cg*16+15 of [A_kk | I]
+    const int kb = k * kNB;
     double a[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-        const int cc = cg + 8 * m;
-        double v = 0.0;
-        if (m < nm) {
-            const double *colp = (cc < 64) ? A + (size_t)(kb + cc) * lda + kb
-                                           : A + (size_t)(jb + cc - 64) * lda + kb;
-            v = colp[r];
-        }
+        const int cc = cg * 16 + m;
+        double v;
+        if (cc < 64) v = (r <= cc) ? A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] : 0.0;
+        else v = (cc - 64 == r) ? 1.0 : 0.0;
         a[m] = v;
     }
     if (r == 0) {
 #pragma unroll
-        for (int m = 0; m < 16; ++m)
-            if (m < nm) buf[0][cg + 8 * m] = a[m];
+        for (int m = 0; m < 16; m += 2)
+            *(double2 *)&buf[0][cg * 16 + m] = make_double2(a[m], a[m + 1]);
     }
     __syncthreads();
     for (int c = 0; c < 64; ++c) {
         const double *bc = buf[c & 1];
         const double piv = bc[c];
-        if (tid == 0) {
-            dsq[c] = sqrt(piv);
-            if (!(piv > 0.0) && err) atomicOr(err, 8u);
-        }
-        if (r > c) {
-            const double l = bc[r] / piv;
+        const double inv = 1.0 / piv;
+        const double l = bc[r] * inv;  // row c, column r (upper part for r > c)
+        double rv[16];
 #pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                const int cc = cg + 8 * m;
-                if (m < nm && cc >= r) a[m] -= l * bc[cc];
-            }
+        for (int m = 0; m < 16; m += 2) {
+            const double2 t2 = *(const double2 *)&bc[cg * 16 + m];
+            rv[m] = t2.x;
+            rv[m + 1] = t2.y;
+        }
+        const bool upd = r > c;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const int cc = cg * 16 + m;
+            const double nv = a[m] - l * rv[m];
+            a[m] = (upd && cc >= r) ? nv : a[m];
         }
         if (r == c + 1) {
             double *bn = buf[(c + 1) & 1];
 #pragma unroll
-            for (int m = 0; m < 16; ++m)
-                if (m < nm) bn[cg + 8 * m] = a[m];
+            for (int m = 0; m < 16; m += 2)
+                *(double2 *)&bn[cg * 16 + m] = make_double2(a[m], a[m + 1]);
+        }
+        if (tid == 0) {
+            dsq[c] = sqrt(piv);
+            if (!(piv > 0.0) && err) atomicOr(err, 8u);
         }
         __syncthreads();
     }
     const double d = dsq[r];
+    double *W = Wd + (size_t)k * kNB * kNB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
-        const int cc = cg + 8 * m;
-        if (m >= nm) continue;
-        if (!aug) {
+        const int cc = cg * 16 + m;
+        if (cc < 64) {
             if (r < cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = a[m] / d;
             else if (r == cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = d;
-        } else if (cc >= 64) {
-            const double v = a[m] / d;
-            A[(size_t)(kb + r) + (size_t)(jb + cc - 64) * lda] = v;
-            PT[(size_t)r * ldpt + jb + cc - 64] = v;
+        } else {
+            W[(size_t)(cc - 64) * kNB + r] = a[m] / d;  // W[r][x], column-major
         }
     }
+}
+
+// U_kj = W_k A_kj for j = k + 1 + blockIdx.x.  Computed transposed, D'[x][r] =
+// sum_s A_kj[s][x] W[r][s], so the column-major store of U_kj is lane-contiguous.
+__global__ __launch_bounds__(256) void k_chol_panel(double *A, int lda, int k,
+                                                    const double *__restrict__ Wd, double *PT,
+                                                    int ldpt) {
+    __shared__ double As[64][65];  // As[s][x] = A_kj[s][x]
+    const int j = k + 1 + blockIdx.x;
+    const int kb = k * kNB, jb = j * kNB;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int sr = e & 63, x = e >> 6;
+        As[sr][x] = A[(size_t)(kb + sr) + (size_t)(jb + x) * lda];
+    }
+    __syncthreads();
+    const double *W = Wd + (size_t)k * kNB * kNB;
+    const int wx = (wid >> 1) * 32, wr = (wid & 1) * 32;
+    v4d acc[2][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[p][q] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+        const int sr = kk * 4 + (lane >> 4);
+        double av[2], bv[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) av[p] = As[sr][wx + p * 16 + (lane & 15)];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) bv[q] = W[(size_t)sr * kNB + wr + q * 16 + (lane & 15)];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
+    }
+    // D'[x][r]: col (lane&15) -> r, row (lane>>4)+4*rr -> x.  W[r][s] is read as W'[s][r]:
+    // column-major W gives W[r][s] at s*64 + r, i.e. B[k=s][j=r] lane-contiguous in r.
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int x = wx + p * 16 + (lane >> 4) + 4 * rr;
+                const int rw = wr + q * 16 + (lane & 15);
+                const double v = acc[p][q][rr];
+                A[(size_t)(kb + rw) + (size_t)(jb + x) * lda] = v;
+                PT[(size_t)rw * ldpt + jb + x] = v;
+            }
 }
 
 // Trailing update A_ij -= U_ki' U_kj for k < i <= j (i < nblk), j < ncb.
 // D[x][y] = sum_s U_kj[s][x] U_ki[s][y] via v_mfma_f64_16x16x4_f64 with operands read
 // lane-contiguously from PT; A_ij[y][x] -= D[x][y] (coalesced along y).
 __global__ __launch_bounds__(256) void k_chol_update(double *A, int lda, int k, int nblk,
-                                                     int ncb, const double *__restrict__ PT,
-                                                     int ldpt) {
+                                                     const double *__restrict__ PT, int ldpt) {
     const int a = nblk - k - 1;
     const int tri = a * (a + 1) / 2;
     const int t = blockIdx.x;
@@ -602,7 +679,6 @@ __global__ __launch_bounds__(256) void k_chol_update(double *A, int lda, int k, 
         j = nblk + t2 / a;
         i = k + 1 + t2 % a;
     }
-    (void)ncb;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wx = (wid >> 1) * 32, wy = (wid & 1) * 32;
     const int ib = i * kNB, jb = j * kNB;
@@ -639,53 +715,74 @@ __global__ __launch_bounds__(256) void k_chol_update(double *A, int lda, int k, 
             }
 }
 
-// Backward solve step k: every workgroup solves U_kk w_k = y_k in LDS (redundantly);
-// workgroup 0 stores w_k; workgroup i < k applies y_i -= U_ik w_k.
+// Backward solve step k: every workgroup forms w_k = U_kk^-1 y_k = W_k' y_k;
+// workgroup 0 stores it; workgroup i < k applies y_i -= U_ik w_k.
 __global__ __launch_bounds__(256) void k_bsolve_step(const double *A, int lda, int k,
-                                                     int m_pad, double *Y, double *W,
-                                                     int nrhs) {
-    __shared__ double U[64][65];
+                                                     int m_pad, const double *__restrict__ Wd,
+                                                     double *Y, double *Wout, int nrhs) {
     __shared__ double yv[2][64];
+    __shared__ double part[4][2][64];
     __shared__ double wv[2][64];
-    const int tid = threadIdx.x, r = tid & 63, q = tid >> 6;
+    const int tid = threadIdx.x, x = tid & 63, g = tid >> 6;  // g: 16-row slice
     const int kb = k * kNB;
-    for (int c = q; c < 64; c += 4) U[r][c] = A[(size_t)(kb + r) + (size_t)(kb + c) * lda];
-    if (q < nrhs) yv[q][r] = Y[(size_t)q * m_pad + kb + r];
+    if (tid < 64 * nrhs) yv[tid >> 6][tid & 63] = Y[(size_t)(tid >> 6) * m_pad + kb + (tid & 63)];
     __syncthreads();
-    for (int c = 63; c >= 0; --c) {
-        if (q < nrhs) {
-            const double wc = yv[q][c] / U[c][c];
-            if (r < c) yv[q][r] -= U[r][c] * wc;
-            if (r == c) wv[q][c] = wc;
+    const double *W = Wd + (size_t)k * kNB * kNB;
+    // w[x] = sum_r W[r][x] y[r]; W column-major: column x contiguous in r
+    for (int q = 0; q < nrhs; ++q) {
+        double acc = 0.0;
+        const double *col = W + (size_t)x * kNB + g * 16;
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) acc += col[rr] * yv[q][g * 16 + rr];
+        part[g][q][x] = acc;
+    }
+    __syncthreads();
+    if (tid < 64 * nrhs) {
+        const int q = tid >> 6;
+        wv[q][x] = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid < 64 * nrhs)
+        Wout[(size_t)(tid >> 6) * m_pad + kb + x] = wv[tid >> 6][x];
+    if (k > 0) {
+        const int ib = blockIdx.x * kNB;
+        // y_i[r] -= sum_c U_ik[r][c] w[c]; thread (r = x, slice g over c)
+        for (int q = 0; q < nrhs; ++q) {
+            double acc = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) {
+                const int c = g * 16 + cc;
+                acc += A[(size_t)(ib + x) + (size_t)(kb + c) * lda] * wv[q][c];
+            }
+            part[g][q][x] = acc;
         }
         __syncthreads();
-    }
-    if (blockIdx.x == 0 && q < nrhs) W[(size_t)q * m_pad + kb + r] = wv[q][r];
-    if (k > 0 && q < nrhs) {
-        const int ib = blockIdx.x * kNB;
-        double acc = 0.0;
-        for (int c = 0; c < 64; ++c) acc += A[(size_t)(ib + r) + (size_t)(kb + c) * lda] * wv[q][c];
-        Y[(size_t)q * m_pad + ib + r] -= acc;
+        if (tid < 64 * nrhs) {
+            const int q = tid >> 6;
+            const double acc = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+            Y[(size_t)q * m_pad + ib + x] -= acc;
+        }
     }
 }
 
-void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, double *Y, double *W,
-                 int nrhs) {
+void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
+                 double *Y, double *W, int nrhs) {
     const int nblk = m_pad / kNB;
     for (int k = nblk - 1; k >= 0; --k)
-        k_bsolve_step<<<k > 0 ? k : 1, 256, 0, s>>>(A, lda, k, m_pad, Y, W, nrhs);
+        k_bsolve_step<<<k > 0 ? k : 1, 256, 0, s>>>(A, lda, k, m_pad, Wd, Y, W, nrhs);
 }
 
-void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks,
-                    uint32_t *err, double *PT) {
+void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
+                 double *PT, double *Wd) {
     const int nblk = m_pad / kNB;
     const int ncb = nblk + nrhs_blocks;
     const int ldpt = ncb * kNB;
     for (int k = 0; k < nblk; ++k) {
-        k_chol_panel<<<ncb - k, 512, 0, s>>>(A, lda, k, PT, ldpt, err);
+        k_chol_diag<<<1, 512, 0, s>>>(A, lda, k, Wd, err);
+        if (ncb - k - 1 > 0) k_chol_panel<<<ncb - k - 1, 256, 0, s>>>(A, lda, k, Wd, PT, ldpt);
         const int a = nblk - k - 1;
         const int tiles = a * (a + 1) / 2 + a * nrhs_blocks;
-        if (tiles > 0) k_chol_update<<<tiles, 256, 0, s>>>(A, lda, k, nblk, ncb, PT, ldpt);
+        if (tiles > 0) k_chol_update<<<tiles, 256, 0, s>>>(A, lda, k, nblk, PT, ldpt);
     }
 }
 

@@ -7,7 +7,7 @@
 // Counter layout (DESIGN.md "RNG counter layout"): key = (seed, stream),
 // ctr = (t, kind << 56 | j, a, b).  A variate depends only on its counter, so any
 // lane may evaluate any attempt: the group sampler below evaluates G consecutive
-// outer attempts of one coefficient in G lanes and keeps the first accepted one,
+// inner attempts of one coefficient in G lanes and keeps the first accepted one,
 // which reproduces the sequential rejection loop exactly.
 //
 // All arithmetic is IEEE fp64; the library is compiled with -ffp-contract=off so
@@ -127,96 +127,103 @@ __device__ __forceinline__ double sinc_mm(double x) {  // retstable.cpp:18-29
     return sin(x) / x;
 }
 
-__device__ __forceinline__ double zolotarev_A(double x, double alpha) {  // :40-47
-    double ia = 1. - alpha;
-    return pow(ia * sinc_mm(ia * x), ia) * pow(alpha * sinc_mm(alpha * x), alpha) / sinc_mm(x);
+// x^y for x >= 0 as exp(y log x).  Every pow of retstable.cpp:94-271 has a non-negative
+// base (sinc of |x| < pi, lambda^alpha, 1 + alpha zeta / sqrt(gamma), A, b/a, X, m), and
+// exp(y log x) reproduces pow's special cases there (0^y, inf^-y, NaN for X < 0) at
+// ~|y log x| * 2^-53 relative error -- far below the GPU/oracle tolerance -- for roughly
+// half the instructions and registers of the correctly rounded ocml pow.
+__device__ __forceinline__ double powp(double x, double y) { return exp(y * log(x)); }
+
+__device__ __forceinline__ double zolotarev_A_p(double x, double alpha, double ia) {
+    return powp(ia * sinc_mm(ia * x), ia) * powp(alpha * sinc_mm(alpha * x), alpha) / sinc_mm(x);
 }
 
-__device__ __forceinline__ double b_over_b0(double x, double alpha) {  // :73-77
-    double ia = 1. - alpha;
-    double den = pow(sinc_mm(alpha * x), alpha) * pow(sinc_mm(ia * x), ia);
+__device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia) {
+    double den = powp(sinc_mm(alpha * x), alpha) * powp(sinc_mm(ia * x), ia);
     return sinc_mm(x) / den;
 }
 
-// Per-coefficient constants (retstable.cpp:121-147).
+// Per-coefficient constants (retstable.cpp:121-147), with the loop-invariant ratios of
+// the inner loop hoisted (same expressions, so the same bits).
 struct StableParams {
-    double h, alpha, V0, b, lambda_alpha, gamma, sgamma, xi, psi, w1, w2, w3, c1;
+    double h, alpha, ia, V0, b, lambda_alpha, gamma, sgamma, xi, psi, c1;
+    double thr_w1, thr_w3;  // w1/(w1+w2), w3/(w2+w3)
+    double neg_inv_alpha, inv_ia, inv_alpha;
 };
 
 __device__ __forceinline__ StableParams stable_params(double h, double alpha, double V0) {
     StableParams s;
     s.h = h;
     s.alpha = alpha;
+    s.ia = 1. - alpha;
     s.V0 = V0;
     s.c1 = sqrt(kPi2);
     const double c2 = 2. + s.c1;
     s.b = (1. - alpha) / alpha;
-    s.lambda_alpha = pow(h, alpha) * V0;
+    s.lambda_alpha = powp(h, alpha) * V0;
     s.gamma = s.lambda_alpha * alpha * (1. - alpha);
     s.sgamma = sqrt(s.gamma);
     double c3 = c2 * s.sgamma;
     s.xi = (1. + kSqrt2 * c3) / kPi;
     s.psi = c3 * exp(-s.gamma * kPi * kPi / 8.) / kSqrtPi;
-    s.w1 = s.c1 * s.xi / s.sgamma;
-    s.w2 = 2. * kSqrtPi * s.psi;
-    s.w3 = s.xi * kPi;
+    const double w1 = s.c1 * s.xi / s.sgamma;
+    const double w2 = 2. * kSqrtPi * s.psi;
+    const double w3 = s.xi * kPi;
+    s.thr_w1 = w1 / (w1 + w2);
+    s.thr_w3 = w3 / (w2 + w3);
+    s.neg_inv_alpha = -1 / alpha;
+    s.inv_ia = 1. / (1. - alpha);
+    s.inv_alpha = 1 / alpha;
     return s;
 }
 
-// One outer attempt o of coefficient j (retstable.cpp:155-256): runs the inner
-// loop (:162-207) on blocks (t, INNER|j, o, i), then the outer test on block
-// (t, OUTER|j, o, 0).  Returns true and sets X if accepted.
-__device__ inline bool stable_outer_attempt(const StableParams &s, Key key, uint64_t t,
-                                            uint64_t j, uint64_t o, double &X,
-                                            uint32_t *err) {
+// Inner attempt i of outer attempt o (retstable.cpp:162-207), block (t, INNER|j, o, i).
+// Returns whether (U, z, Z) is accepted by the inner test.
+__device__ __forceinline__ bool stable_inner_body(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, uint64_t i, double &U,
+                                             double &z, double &Z) {
     const double alpha = s.alpha, gamma = s.gamma, sgamma = s.sgamma;
-    double U = 0, z = 0, Z = 0;
-    bool inner_ok = false;
-    for (uint64_t i = 0; i < (1ull << 20); ++i) {
-        U4 r = uniforms(key, t, KIND_LAMBDA_INNER, j, o, i);
-        double V = r.r[0];
-        if (gamma >= 1) {
-            if (V < s.w1 / (s.w1 + s.w2)) U = fabs(bm_normal(r.r[2], r.r[3])) / sgamma;
-            else {
-                double W_ = r.r[2];
-                U = kPi * (1. - W_ * W_);
-            }
-        } else {
+    U4 r = uniforms(key, t, KIND_LAMBDA_INNER, j, o, i);
+    double V = r.r[0];
+    if (gamma >= 1) {
+        if (V < s.thr_w1) U = fabs(bm_normal(r.r[2], r.r[3])) / sgamma;
+        else {
             double W_ = r.r[2];
-            if (V < s.w3 / (s.w2 + s.w3)) U = kPi * W_;
-            else U = kPi * (1. - W_ * W_);
+            U = kPi * (1. - W_ * W_);
         }
-        double W = r.r[1];
-        double zeta = sqrt(b_over_b0(U, alpha));
-        z = 1 / (1 - pow(1 + alpha * zeta / sgamma, -1 / alpha));
-        double rho = kPi * exp(-s.lambda_alpha * (1. - 1. / (zeta * zeta))) /
-                     ((1. + s.c1) * sgamma / zeta + z);
-        double d = 0.;
-        if (U >= 0 && gamma >= 1) d += s.xi * exp(-gamma * U * U / 2.);
-        if (U > 0 && U < kPi) d += s.psi / sqrt(kPi - U);
-        if (U >= 0 && U <= kPi && gamma < 1) d += s.xi;
-        rho *= d;
-        Z = W * rho;
-        if (U < kPi && Z <= 1.) {
-            inner_ok = true;
-            break;
-        }
+    } else {
+        double W_ = r.r[2];
+        if (V < s.thr_w3) U = kPi * W_;
+        else U = kPi * (1. - W_ * W_);
     }
-    if (!inner_ok) {
-        if (err) atomicOr(err, 2u);
-        X = __builtin_nan("");
-        return true;  // give up on this coefficient (flagged)
-    }
-    double a = pow(zolotarev_A(U, alpha), 1. / (1. - alpha));  // :212-218
-    double m = pow(s.b / a, alpha) * s.lambda_alpha;
+    double W = r.r[1];
+    double zeta = sqrt(b_over_b0_p(U, alpha, s.ia));
+    z = 1 / (1 - powp(1 + alpha * zeta / sgamma, s.neg_inv_alpha));
+    double rho = kPi * exp(-s.lambda_alpha * (1. - 1. / (zeta * zeta))) /
+                 ((1. + s.c1) * sgamma / zeta + z);
+    double d = 0.;
+    if (U >= 0 && gamma >= 1) d += s.xi * exp(-gamma * U * U / 2.);
+    if (U > 0 && U < kPi) d += s.psi / sqrt(kPi - U);
+    if (U >= 0 && U <= kPi && gamma < 1) d += s.xi;
+    rho *= d;
+    Z = W * rho;
+    return (U < kPi && Z <= 1.);
+}
+
+// Outer test of outer attempt o (retstable.cpp:212-256) given the accepted inner triple.
+__device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, double U, double z,
+                                             double Z, double &X) {
+    const double alpha = s.alpha;
+    double a = powp(zolotarev_A_p(U, alpha, s.ia), s.inv_ia);
+    double m = powp(s.b / a, alpha) * s.lambda_alpha;
     double delta = sqrt(m * alpha / a);
     double a1 = delta * s.c1;
     double a2 = delta;
     double a3 = z / a;
     double ssum = a1 + a2 + a3;
-
     U4 r = uniforms(key, t, KIND_LAMBDA_OUTER, j, o, 0);
-    double V_ = r.r[0], N_ = 0., E_ = 0.;  // :224-238
+    double V_ = r.r[0], N_ = 0., E_ = 0.;
     double Xc;
     if (V_ < a1 / ssum) {
         N_ = bm_normal(r.r[1], r.r[2]);
@@ -229,23 +236,53 @@ __device__ inline bool stable_outer_attempt(const StableParams &s, Key key, uint
         }
     }
     double E = -log(Z);
-    double c = a * (Xc - m);  // :247-251
-    c += (m != 0) ? s.h * (pow(Xc, -1. * s.b) - pow(m, -1. * s.b)) : 0.0;
+    double c = a * (Xc - m);
+    c += (m != 0) ? s.h * (powp(Xc, -1. * s.b) - powp(m, -1. * s.b)) : 0.0;
     if (Xc < m) c -= N_ * N_ / 2.;
     else if (Xc > m + delta) c -= E_;
     X = Xc;
     return (Xc >= 0 && c <= E);
 }
 
-__device__ __forceinline__ double stable_finish(const StableParams &s, double X) {
-    return exp(1 / s.alpha * log(s.V0) - s.b * log(X));  // :270
+__device__ __noinline__ bool stable_inner_ni(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, uint64_t i, double &U,
+                                             double &z, double &Z) {
+    return stable_inner_body(s, key, t, j, o, i, U, z, Z);
+}
+__device__ __noinline__ bool stable_outer_ni(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, double U, double z,
+                                             double Z, double &X) {
+    return stable_outer_body(s, key, t, j, o, U, z, Z, X);
+}
+template <bool NI>
+__device__ __forceinline__ bool stable_inner(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, uint64_t i, double &U,
+                                             double &z, double &Z) {
+    if constexpr (NI) return stable_inner_ni(s, key, t, j, o, i, U, z, Z);
+    else return stable_inner_body(s, key, t, j, o, i, U, z, Z);
+}
+template <bool NI>
+__device__ __forceinline__ bool stable_outer(const StableParams &s, Key key, uint64_t t,
+                                             uint64_t j, uint64_t o, double U, double z,
+                                             double Z, double &X) {
+    if constexpr (NI) return stable_outer_ni(s, key, t, j, o, U, z, Z, X);
+    else return stable_outer_body(s, key, t, j, o, U, z, Z, X);
 }
 
-// Group sampler: the G lanes [gbase, gbase+G) of a wave cooperate on one
-// coefficient.  Every lane of the wave must call this (ballot/shuffle inside);
-// `active` marks lanes whose group has a coefficient.  Returns the draw in every
-// lane of the group.
-template <int G>
+#ifndef BB_STABLE_NOINLINE
+#define BB_STABLE_NOINLINE 0
+#endif
+
+__device__ __forceinline__ double stable_finish(const StableParams &s, double X) {
+    return exp(s.inv_alpha * log(s.V0) - s.b * log(X));  // :270
+}
+
+// Group sampler: the G lanes [gbase, gbase+G) of a wave cooperate on one coefficient by
+// evaluating G consecutive INNER attempts of the current outer attempt in parallel; the
+// lowest accepted inner attempt (counter order) feeds the outer test, which every lane of
+// the group evaluates on identical inputs.  This reproduces the sequential double
+// rejection loop exactly.  Every lane of the wave must call this (ballot/shuffle inside).
+template <int G, bool NI = (BB_STABLE_NOINLINE != 0)>
 __device__ inline double stable_group_draw(bool active, double h, double alpha, double V0,
                                            Key key, uint64_t t, uint64_t j, uint32_t *err) {
     const int lane = threadIdx.x & 63;
@@ -260,20 +297,35 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
         if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) atomicOr(err, 4u);  // :112-115
         s = stable_params(h, alpha, V0);
     }
-    uint64_t base = 0;
-    for (int round = 0; round < (1 << 20); ++round) {
+    uint64_t o = 0, ib = 0;
+    for (int iter = 0; iter < (1 << 22); ++iter) {
         bool acc = false;
-        double X = 0.0;
-        if (!done) acc = stable_outer_attempt(s, key, t, j, base + (uint64_t)g, X, err);
-        uint64_t m = (__ballot(acc) >> gbase) & gmask;
-        int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
-        double Xw = __shfl(X, gbase + win, 64);
-        if (!done && m) {
-            result = stable_finish(s, Xw);
-            done = true;
+        double U = 0.0, z = 0.0, Z = 0.0;
+        if (!done) acc = stable_inner<NI>(s, key, t, j, o, ib + (uint64_t)g, U, z, Z);
+        const uint64_t m = (__ballot(acc) >> gbase) & gmask;
+        const int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
+        const double Uw = __shfl(U, gbase + win, 64);
+        const double zw = __shfl(z, gbase + win, 64);
+        const double Zw = __shfl(Z, gbase + win, 64);
+        if (!done) {
+            if (!m) {
+                ib += G;
+            } else {
+                double X;
+                if (stable_outer<NI>(s, key, t, j, o, Uw, zw, Zw, X)) {
+                    result = stable_finish(s, X);
+                    done = true;
+                } else {
+                    ++o;
+                    ib = 0;
+                }
+            }
         }
-        base += G;
         if (__all(done)) break;
+    }
+    if (!done) {
+        atomicOr(err, 2u);
+        result = __builtin_nan("");
     }
     return result;
 }

@@ -167,6 +167,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     gram_ms, sweep_ms, nsamp = eng.kernel_times()
+    phases = eng.phase_times()
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
@@ -212,6 +213,7 @@ def main():
                          "traffic": None, "gram_ms_avg": gram_ms,
                          "sweep_ms_avg_events": sweep_ms,
                          "flops_per_launch": gram_flops},
+            "phases_ms": {k: round(v, 4) for k, v in phases.items()},
             "cpu_baseline": cpu,
             "setup_s": setup_s,
         }

@@ -165,6 +165,11 @@ int bb_engine_enable_timing(bb_engine *e, int enable);
 int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
                            int *samples);
 int bb_engine_reset_timing(bb_engine *e);
+/* Average milliseconds per sweep spent in each phase (ms[0 .. bb_phase_count()-1]),
+ * measured between HIP events recorded at phase starts on the engine stream. */
+int bb_engine_phase_times(bb_engine *e, double *ms, int cap, int *samples);
+int bb_phase_count(void);
+const char *bb_phase_name(int i);
 
 /* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags);
@@ -178,6 +183,12 @@ int bb_retstable_batch(double *x, const double *alpha, const double *V0, const d
 /* lambda_j = 2 * retstable(beta_j^2/tau^2, alpha/2, 1) for global j = j0 + i. */
 int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, double tau,
                      uint64_t seed, uint64_t stream, uint64_t t, uint64_t j0, int group);
+
+/* Microbenchmark of the lambda kernel: average ms over `reps` launches (sweep indices
+ * t = 2 .. reps+1, key (1, 0)) for an explicit group size and inlining variant; the
+ * last launch's draws are returned in lambda_out (may be NULL). */
+int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int group,
+                    int noinline, int reps, double *ms_avg, double *lambda_out);
 
 /* Gram C = Y diag(w) Y' (Y: n x k column-major) via the fp64 MFMA kernel;
  * C is n x n column-major, full symmetric result. */
