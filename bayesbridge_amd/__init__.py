@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = [
     "bb_engine_kernel_times", "bb_engine_reset_timing", "bb_engine_error_flags",
     "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
+    "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
 ]
 
 
@@ -104,6 +105,10 @@ def library(build: bool = True) -> ctypes.CDLL:
                                    c.c_uint64, c.c_uint64, c.c_uint64, c.c_int]
     L.bb_gram.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_group_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
+    L.bb_group_destroy.argtypes = [c.c_void_p]
+    L.bb_group_init_state.argtypes = [c.c_void_p]
+    L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
     L.bb_bench_lambda.argtypes = [_dp, c.c_int, c.c_double, c.c_double, c.c_int, c.c_int,
                                   c.c_int, _dp, _dp]
     L.bb_engine_phase_times.argtypes = [c.c_void_p, _dp, c.c_int, _ip]
@@ -469,6 +474,41 @@ class Engine:
     def close(self):
         if getattr(self, "_h", None):
             library().bb_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ShardGroup:
+    """Column shards of one chain as several engines on ONE device, exchanging through
+    on-device sums -- the sharded decomposition without RCCL (single-GPU testing)."""
+
+    def __init__(self, engines):
+        L = library()
+        self.engines = list(engines)
+        arr = (ctypes.c_void_p * len(self.engines))(*[e._h.value for e in self.engines])
+        h = ctypes.c_void_p()
+        _check(L.bb_group_create(arr, len(self.engines), ctypes.byref(h)), "bb_group_create")
+        self._h = h
+
+    def init_state(self):
+        _check(library().bb_group_init_state(self._h), "bb_group_init_state")
+
+    def run(self, t0, count, first_slot=-1, slot_step=1, mcmc_phase=1):
+        _check(library().bb_group_run(self._h, int(t0), int(count), int(first_slot),
+                                      int(slot_step), int(mcmc_phase)), "bb_group_run")
+
+    def sync(self):
+        for e in self.engines:
+            e.sync()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            library().bb_group_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -203,17 +204,23 @@ struct bb_engine {
                        slot_ptr(tr_alpha, slot, 1), tau_only, err);
     }
 
-    void sweep(uint64_t t, int slot, int mcmc_phase) {
+    // A sweep is three phases separated by the two exchange points of the column-sharded
+    // decomposition: red1 = [S_alpha partials | X beta] and
+    // red2 = [partial Gram | X u].  Single engines and RCCL ranks run them back to back
+    // through allreduce(); a shard group (bb_group_*) interleaves its members' phases.
+    void phase_a(uint64_t t) {
+        (void)t;
         if (timing) sweep_marks.emplace_back();
         mark(PH_PRE);
         launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
-        allreduce(red1, (size_t)nbS + n_pad);
+    }
+
+    void phase_b(uint64_t t, int slot) {
         mark(PH_SCALARS);
         launch_scalars(stream, red1, nbS, y, n, p, sc, hy, cfg.seed, cfg.stream, t,
                        slot_ptr(tr_tau, slot, 1), slot_ptr(tr_sig2, slot, 1),
                        slot_ptr(tr_alpha, slot, 1), 0, err);
         double *trl = slot_ptr(tr_lam, slot, p_loc);
-        double *trb = slot_ptr(tr_beta, slot, p_loc);
         mark(PH_LAMBDA);
         if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
@@ -224,7 +231,15 @@ struct bb_engine {
             launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
             mark(PH_REDUCE);
             launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad), red2);
-            allreduce(red2, (size_t)n_pad * n_pad + n_pad);
+        } else {
+            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
+                          group, lam, nullptr, nullptr, trl, err);
+        }
+    }
+
+    void phase_c(uint64_t t, int slot, int mcmc_phase) {
+        double *trb = slot_ptr(tr_beta, slot, p_loc);
+        if (method == 2) {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
             mark(PH_CHOL);
@@ -233,24 +248,19 @@ struct bb_engine {
             chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1);
             mark(PH_BETA);
             launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
+        } else if (method == 1) {
+            mark(PH_FORM);
+            launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
+            mark(PH_CHOL);
+            chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd);
+            mark(PH_SOLVE);
+            launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
+            chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2);
+            mark(PH_BETA);
+            launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
         } else {
-            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
-                          group, lam, nullptr, nullptr, trl, err);
-            if (method == 1) {
-                mark(PH_FORM);
-                launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
-                mark(PH_CHOL);
-                chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd);
-                mark(PH_SOLVE);
-                launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
-                chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2);
-                mark(PH_BETA);
-                launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
-            } else {
-                mark(PH_BETA);
-                launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta,
-                                  trb);
-            }
+            mark(PH_BETA);
+            launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta, trb);
         }
         mark(PH_XB);
         launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
@@ -263,6 +273,17 @@ struct bb_engine {
                             slot_ptr(tr_alpha, slot, 1));
         }
         mark(PH_END);
+    }
+
+    size_t red1_count() const { return (size_t)nbS + n_pad; }
+    size_t red2_count() const { return (size_t)n_pad * n_pad + n_pad; }
+
+    void sweep(uint64_t t, int slot, int mcmc_phase) {
+        phase_a(t);
+        allreduce(red1, red1_count());
+        phase_b(t, slot);
+        if (method == 2) allreduce(red2, red2_count());
+        phase_c(t, slot, mcmc_phase);
     }
 
     uint32_t read_err() {
@@ -377,7 +398,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
-void engine_init_state(bb_engine *e) {
+void engine_init_state_local(bb_engine *e) {
     const bb_config &c = e->cfg;
     // least squares start (BridgeWrapper.cpp:242-244, BridgeRegression.cpp:79-91)
     bool ls_ok = false;
@@ -413,8 +434,12 @@ void engine_init_state(bb_engine *e) {
     HIPCHECK(hipMemcpyAsync(e->tr_beta, e->beta, (size_t)e->p_loc * sizeof(double),
                             hipMemcpyDeviceToDevice, e->stream));
     launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
+    launch_record_scalars(e->stream, e->sc, e->tr_tau, e->tr_sig2, e->tr_alpha);
+}
+
+void engine_init_state(bb_engine *e) {
+    engine_init_state_local(e);
     if (e->method != 3 && !e->hy.know_tau) e->pre_and_scalars(0, 0, 1);  // :262
-    else launch_record_scalars(e->stream, e->sc, e->tr_tau, e->tr_sig2, e->tr_alpha);
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -705,6 +730,133 @@ int bb_engine_error_flags(bb_engine *e, uint32_t *flags) {
     }
     return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Shard groups: several column-shard engines driven by one host thread, with the two
+// per-sweep exchanges done as on-device sums (members on one device) -- used to test the
+// sharded decomposition on a single GPU.
+// ---------------------------------------------------------------------------
+struct bb_group {
+    std::vector<bb_engine *> members;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;
+    std::vector<hipEvent_t> mev;
+    double *tmp = nullptr;
+    size_t tmp_count = 0;
+    ~bb_group() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (tmp) (void)hipFree(tmp);
+        if (ev) (void)hipEventDestroy(ev);
+        for (auto e : mev) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    // sum buf(member) over members, result written back to every member's buf
+    void reduce(double *bb_engine::*buf, size_t count) {
+        for (size_t i = 0; i < members.size(); ++i) {
+            HIPCHECK(hipEventRecord(mev[i], members[i]->stream));
+            HIPCHECK(hipStreamWaitEvent(stream, mev[i], 0));
+        }
+        HIPCHECK(hipMemcpyAsync(tmp, members[0]->*buf, count * sizeof(double),
+                                hipMemcpyDeviceToDevice, stream));
+        for (size_t i = 1; i < members.size(); ++i)
+            launch_sum_into(stream, members[i]->*buf, tmp, count);
+        for (size_t i = 0; i < members.size(); ++i)
+            HIPCHECK(hipMemcpyAsync(members[i]->*buf, tmp, count * sizeof(double),
+                                    hipMemcpyDeviceToDevice, stream));
+        HIPCHECK(hipEventRecord(ev, stream));
+        for (auto *m : members) HIPCHECK(hipStreamWaitEvent(m->stream, ev, 0));
+    }
+};
+
+extern "C" {
+
+int bb_group_create(bb_engine **engines, int count, bb_group **out) {
+    *out = nullptr;
+    bb_group *g = new bb_group();
+    try {
+        if (count < 1) throw HipError("empty group");
+        for (int i = 0; i < count; ++i) {
+            if (engines[i]->cfg.world != count || engines[i]->cfg.rank != i)
+                throw HipError("group member rank/world mismatch");
+            if (engines[i]->cfg.device != engines[0]->cfg.device)
+                throw HipError("group members must share one device (use RCCL across devices)");
+            g->members.push_back(engines[i]);
+        }
+        HIPCHECK(hipSetDevice(engines[0]->cfg.device));
+        HIPCHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreateWithFlags(&g->ev, hipEventDisableTiming));
+        for (int i = 0; i < count; ++i) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            g->mev.push_back(e);
+        }
+        size_t c = 0;
+        for (auto *m : g->members) {
+            c = std::max(c, m->red1_count());
+            if (m->method == 2) c = std::max(c, m->red2_count());
+        }
+        g->tmp_count = c;
+        HIPCHECK(hipMalloc(&g->tmp, c * sizeof(double)));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        delete g;
+        return -1;
+    }
+    *out = g;
+    return 0;
+}
+
+void bb_group_destroy(bb_group *g) { delete g; }
+
+int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
+                 int mcmc_phase) {
+    try {
+        HIPCHECK(hipSetDevice(g->members[0]->cfg.device));
+        for (int k = 0; k < count; ++k) {
+            const uint64_t t = t0 + (uint64_t)k;
+            const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
+            for (auto *m : g->members) m->phase_a(t);
+            g->reduce(&bb_engine::red1, g->members[0]->red1_count());
+            for (auto *m : g->members) m->phase_b(t, slot);
+            if (g->members[0]->method == 2)
+                g->reduce(&bb_engine::red2, g->members[0]->red2_count());
+            for (auto *m : g->members) m->phase_c(t, slot, mcmc_phase);
+        }
+        HIPCHECK(hipGetLastError());
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_group_init_state(bb_group *g) {
+    // p > n (Woodbury) start: beta = 0, then the pre-burn tau draw from the summed red1
+    try {
+        for (auto *m : g->members) {
+            if (m->G != nullptr) throw HipError("group init supports the p > n path only");
+            engine_init_state_local(m);
+        }
+        bool draw_tau = g->members[0]->method != 3 && !g->members[0]->hy.know_tau;
+        if (draw_tau) {
+            for (auto *m : g->members)
+                launch_pre(m->stream, m->xb_part, m->nparts, m->n_pad, m->beta, m->p_loc, m->sc,
+                           m->red1, m->nbS);
+            g->reduce(&bb_engine::red1, g->members[0]->red1_count());
+            for (auto *m : g->members)
+                launch_scalars(m->stream, m->red1, m->nbS, m->y, m->n, m->p, m->sc, m->hy,
+                               m->cfg.seed, m->cfg.stream, 0, m->tr_tau, m->tr_sig2,
+                               m->tr_alpha, 1, m->err);
+        }
+        for (auto *m : g->members) HIPCHECK(hipStreamSynchronize(m->stream));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"
 
 // ---------------------------------------------------------------------------
 // kernel-level entry points

@@ -540,6 +540,15 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 //   k_chol_update (MFMA)         A_ij -= U_ki' U_kj for k < i <= j.
 // W_k is kept (Wd[k]) for the backward solve (U_kk^-1 = W_k').
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ double fast_rcp(double p) {
+    // v_rcp_f64 + two Newton steps: full double precision for the normal, positive pivots
+    // seen here (the IEEE division sequence costs ~3x the dependent latency).
+    double r = __builtin_amdgcn_rcp(p);
+    r = r * (2.0 - p * r);
+    r = r * (2.0 - p * r);
+    return r;
+}
+
 __global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, double *Wd,
                                                    uint32_t *err) {
     __shared__ __attribute__((aligned(16))) double buf[2][128];
@@ -548,6 +557,7 @@ __global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, do
     const int r = tid & 63;
     const int cg = tid >> 6;  // 0..7 -> columns cg*16 .. cg*16+15 of [A_kk | I]
     const int kb = k * kNB;
+    const int mstart = r - cg * 16;  // element m is in the upper part iff m >= mstart
     double a[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
@@ -565,9 +575,6 @@ __global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, do
     __syncthreads();
     for (int c = 0; c < 64; ++c) {
         const double *bc = buf[c & 1];
-        const double piv = bc[c];
-        const double inv = 1.0 / piv;
-        const double l = bc[r] * inv;  // row c, column r (upper part for r > c)
         double rv[16];
 #pragma unroll
         for (int m = 0; m < 16; m += 2) {
@@ -575,12 +582,13 @@ __global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, do
             rv[m] = t2.x;
             rv[m + 1] = t2.y;
         }
-        const bool upd = r > c;
+        const double lr = bc[r];
+        const double piv = bc[c];
+        const double l = lr * fast_rcp(piv) * (double)(r > c);
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const int cc = cg * 16 + m;
-            const double nv = a[m] - l * rv[m];
-            a[m] = (upd && cc >= r) ? nv : a[m];
+            const double lm = l * (double)(m >= mstart);
+            a[m] = __builtin_fma(-lm, rv[m], a[m]);
         }
         if (r == c + 1) {
             double *bn = buf[(c + 1) & 1];
@@ -588,22 +596,28 @@ __global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, do
             for (int m = 0; m < 16; m += 2)
                 *(double2 *)&bn[cg * 16 + m] = make_double2(a[m], a[m + 1]);
         }
-        if (tid == 0) {
-            dsq[c] = sqrt(piv);
-            if (!(piv > 0.0) && err) atomicOr(err, 8u);
-        }
         __syncthreads();
     }
+    // pivot r is a[r][r] (unchanged after step r), held by thread (r, cg = r / 16)
+    if (cg == (r >> 4)) {
+        double pv = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) pv = (m == (r & 15)) ? a[m] : pv;
+        dsq[r] = sqrt(pv);
+        if (!(pv > 0.0) && err) atomicOr(err, 8u);
+    }
+    __syncthreads();
     const double d = dsq[r];
+    const double dinv = 1.0 / d;
     double *W = Wd + (size_t)k * kNB * kNB;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const int cc = cg * 16 + m;
         if (cc < 64) {
-            if (r < cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = a[m] / d;
+            if (r < cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = a[m] * dinv;
             else if (r == cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = d;
         } else {
-            W[(size_t)(cc - 64) * kNB + r] = a[m] / d;  // W[r][x], column-major
+            W[(size_t)(cc - 64) * kNB + r] = a[m] * dinv;  // W[r][x], column-major
         }
     }
 }

@@ -156,6 +156,19 @@ int bb_engine_get_state(bb_engine *e, double *beta, double *lambda, double *tau,
 int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig2,
                         double alpha);
 
+/*
+ * Shard group: `count` engines on ONE device with cfg.rank = 0..count-1 and
+ * cfg.world = count, each holding a column shard, driven by one host thread with the
+ * per-sweep exchanges done as on-device sums.  Exercises the sharded decomposition on a
+ * single GPU (RCCL cannot place two ranks on one device).  p > n path only.
+ */
+typedef struct bb_group bb_group;
+int bb_group_create(bb_engine **engines, int count, bb_group **out);
+void bb_group_destroy(bb_group *g);
+int bb_group_init_state(bb_group *g);
+int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
+                 int mcmc_phase);
+
 /* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho. */
 int bb_engine_method(const bb_engine *e);
 

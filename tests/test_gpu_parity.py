@@ -292,3 +292,62 @@ def test_teacher_forced_sweep_large(gpu_lib, n, p):
     assert rel_err(s["beta"], b) < 1e-9
     assert e.error_flags() == 0
     e.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_group_matches_single_engine(gpu_lib, world):
+    """The column-sharded sweep (two exchanges per sweep) on one GPU vs the unsharded
+    engine, teacher-forced from identical states for several sweeps."""
+    bb = gpu_lib
+    n, p = 200, 1100
+    X, y, btrue = synthetic_problem(n, p, seed=21)
+    seed, stream = SEED + 9, 0
+    single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, method=2), X, y)
+    single.init_state()
+    per = (p + world - 1) // world
+    shards = []
+    for r in range(world):
+        j0, j1 = r * per, min(p, (r + 1) * per)
+        cfg = bb.EngineConfig(n=n, p=p, p_local=j1 - j0, j0=j0, rank=r, world=world, seed=seed,
+                              stream=stream, method=2)
+        shards.append(bb.Engine(cfg, np.asfortranarray(X[:, j0:j1]), y))
+    grp = bb.ShardGroup(shards)
+    grp.init_state()
+    rng = np.random.default_rng(3)
+    beta = btrue + 0.05 * rng.standard_normal(p)
+    tau, sig2 = 0.9, 1.1
+    for t in range(1, 6):
+        single.set_state(beta, tau, sig2, 0.5)
+        for r, e in enumerate(shards):
+            e.set_state(beta[r * per:min(p, (r + 1) * per)], tau, sig2, 0.5)
+        single.run(t, 1)
+        grp.run(t, 1)
+        grp.sync()
+        s1 = single.state()
+        parts = [e.state() for e in shards]
+        bg = np.concatenate([q["beta"] for q in parts])
+        lg = np.concatenate([q["lambda"] for q in parts])
+        for q in parts:
+            assert abs(q["tau"] - s1["tau"]) <= 1e-13 * s1["tau"]
+            assert abs(q["sig2"] - s1["sig2"]) <= 1e-12 * s1["sig2"]
+        # same counters; tau differs only by the summation order of S_alpha
+        assert flips(lg, s1["lambda"]) == 0
+        assert np.max(np.abs(lg - s1["lambda"]) / s1["lambda"]) < 1e-11
+        assert rel_err(bg, s1["beta"]) < 1e-10, (t, rel_err(bg, s1["beta"]))
+        beta, tau, sig2 = s1["beta"], s1["tau"], s1["sig2"]
+    grp.close()
+    single.close()
+
+
+def test_gpu_matches_golden_vectors(gpu_lib):
+    """The HIP path against the committed fixtures (tests/golden/oracle_vectors.npz)."""
+    import os
+
+    bb = gpu_lib
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_vectors.npz"))
+    x = bb.retstable_batch(g["rs_alpha"], g["rs_V0"], g["rs_h"], seed=SEED, stream=0, t=0)
+    assert flips(x, g["rs_x"]) == 0
+    assert np.max(np.abs(x - g["rs_x"]) / g["rs_x"]) < 1e-11
+    bb.set_seed(SEED)
+    ch = bb.bridge_reg_stb(g["chain_y"], g["chain_X"], nsamp=20, burn=5)
+    compare_chain(ch, {k: g["chain_" + k] for k in ("beta", "lambda", "sig2", "tau", "alpha")})
