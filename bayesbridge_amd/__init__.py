@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = [
     "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
+    "bb_bench_chol",
 ]
 
 
@@ -109,6 +110,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
+    L.bb_bench_chol.argtypes = [c.c_int, c.c_int, c.c_int, _dp, _dp]
     L.bb_bench_lambda.argtypes = [_dp, c.c_int, c.c_double, c.c_double, c.c_int, c.c_int,
                                   c.c_int, _dp, _dp]
     L.bb_engine_phase_times.argtypes = [c.c_void_p, _dp, c.c_int, _ip]
@@ -314,6 +316,16 @@ def bench_lambda(beta, alpha, tau, group, noinline=1, reps=20):
     _check(L.bb_bench_lambda(_p(beta), beta.shape[0], alpha, tau, group, noinline, reps,
                              ctypes.byref(ms), _p(lam)), "bb_bench_lambda")
     return ms.value, lam
+
+
+def bench_chol(m, diag_threads=512, reps=10):
+    """(factor ms, solve ms) of the blocked device Cholesky on an m x m SPD test matrix."""
+    L = library()
+    _require_gpu()
+    f, s = ctypes.c_double(), ctypes.c_double()
+    _check(L.bb_bench_chol(m, diag_threads, reps, ctypes.byref(f), ctypes.byref(s)),
+           "bb_bench_chol")
+    return f.value, s.value
 
 
 def gram(Y, w):

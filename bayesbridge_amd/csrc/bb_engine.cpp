@@ -353,7 +353,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
         e->w = dalloc<double>(n_pad, o);
     }
-    e->PT = dalloc<double>((size_t)kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
+    e->PT = dalloc<double>((size_t)2 * kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
     e->Wd = dalloc<double>((size_t)kNB * (n_pad > p_pad ? n_pad : p_pad), o);
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
     const bool small = c.p <= c.n && c.world == 1;
@@ -959,6 +959,61 @@ int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int gro
     return rc;
 }
 
+int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *ms_solve) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int m_pad = round_up(m, kNB);
+        // SPD test matrix: I * m + small symmetric perturbation, built on the host once
+        std::vector<double> h((size_t)m_pad * (m_pad + kNB), 0.0);
+        for (int c = 0; c < m_pad; ++c)
+            for (int r = 0; r <= c; ++r)
+                h[(size_t)r + (size_t)c * m_pad] =
+                    (r == c) ? (double)m_pad : 0.5 * std::sin(0.37 * r + 0.11 * c);
+        for (int r = 0; r < m_pad; ++r) h[(size_t)r + (size_t)m_pad * m_pad] = 1.0;
+        double *src = dalloc<double>(h.size(), owned), *dA = dalloc<double>(h.size(), owned);
+        HIPCHECK(hipMemcpy(src, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
+        double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
+        double *W = dalloc<double>((size_t)m_pad, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        set_chol_diag_threads(diag_threads);
+        hipEvent_t e0, e1, e2;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        HIPCHECK(hipEventCreate(&e2));
+        double tf = 0, ts = 0;
+        for (int it = 0; it <= reps; ++it) {
+            HIPCHECK(hipMemcpyAsync(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice, 0));
+            HIPCHECK(hipEventRecord(e0, 0));
+            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd);
+            HIPCHECK(hipEventRecord(e1, 0));
+            chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, 1);
+            HIPCHECK(hipEventRecord(e2, 0));
+            HIPCHECK(hipEventSynchronize(e2));
+            float a = 0, b = 0;
+            HIPCHECK(hipEventElapsedTime(&a, e0, e1));
+            HIPCHECK(hipEventElapsedTime(&b, e1, e2));
+            if (it > 0) {
+                tf += a;
+                ts += b;
+            }
+        }
+        set_chol_diag_threads(512);
+        *ms_factor = tf / reps;
+        *ms_solve = ts / reps;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 int bb_gram(double *C, const double *Yh, const double *wh, int n, int k) {
     std::vector<void *> owned;
     int rc = 0;
@@ -1009,7 +1064,7 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         for (int q = 0; q < nrhs; ++q)
             for (int r = 0; r < m; ++r) h[(size_t)r + (size_t)(m_pad + q) * m_pad] = bh[r + (size_t)q * m];
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        double *PT = dalloc<double>((size_t)kNB * (m_pad + kNB), owned);
+        double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);

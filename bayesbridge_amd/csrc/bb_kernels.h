@@ -85,10 +85,12 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 
 // In-place upper Cholesky A = U'U of the leading m_pad x m_pad block with the
 // forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
-// PT: scratch of kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
+// PT: scratch of 2 x kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
 // kNB x kNB receiving U_kk^-T (used by chol_bsolve).
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *PT, double *Wd);
+
+void set_chol_diag_threads(int nt);  // 128 / 256 / 512 / 1024 (tuning)
 
 // Backward solve U W = Y (Y, W: m_pad x nrhs <= 2, ld = m_pad); Y is overwritten.
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,

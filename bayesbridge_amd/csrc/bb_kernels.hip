@@ -532,111 +532,191 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 
 // ---------------------------------------------------------------------------
 // Blocked right-looking Cholesky A = U'U (upper, column-major, NB = 64) with the
-// forward solve folded into trailing right-hand-side column blocks.  Per step k:
-//   k_chol_diag   (1 workgroup)  eliminates [A_kk | I] -> U_kk and W_k = U_kk^-T;
-//   k_chol_panel  (MFMA)         U_kj = W_k A_kj for every column block j > k (RHS
-//                                blocks included = forward substitution), written to A
-//                                and row-major to PT so the update reads lane-contiguous;
-//   k_chol_update (MFMA)         A_ij -= U_ki' U_kj for k < i <= j.
-// W_k is kept (Wd[k]) for the backward solve (U_kk^-1 = W_k').
+// forward solve folded into trailing right-hand-side column blocks.  Two kernels per step
+// kp (k = kp - 1 is the previous step, whose row panel PT_k is already formed):
+//   k_chol_stepA: workgroup 0 applies step k's update to A_kp,kp and eliminates
+//                 [A_kp,kp | I] -> W_kp = U_kp,kp^-T (the serial pivot chain); the other
+//                 workgroups apply step k's update to every tile (i, j), kp <= i <= j
+//                 (RHS blocks included), reading U's block row k lane-contiguously from PT_k.
+//   k_chol_stepB: U_kp,j = W_kp A_kp,j for j > kp (MFMA), into A and row-major PT_kp
+//                 (RHS blocks: the forward substitution).
+// The backward solve uses W_kp = U_kp,kp^-T, so U_kp,kp itself is never stored.
+// Dependent fp64 ops cost ~48 cycles on gfx950 and the pivot loop is issue/latency bound
+// (tools/diag_latency.hip), so the loop carries no per-element masks: the published pivot
+// row has its strictly-lower part zeroed, which keeps every lower-part value finite, and
+// finished rows use a zero multiplier.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double fast_rcp(double p) {
-    // v_rcp_f64 + two Newton steps: full double precision for the normal, positive pivots
-    // seen here (the IEEE division sequence costs ~3x the dependent latency).
+    // v_rcp_f64 (~2^-26 accurate) + one Newton step: ~1 ulp for the normal positive pivots
     double r = __builtin_amdgcn_rcp(p);
-    r = r * (2.0 - p * r);
-    r = r * (2.0 - p * r);
-    return r;
+    return r * (2.0 - p * r);
 }
 
-__global__ __launch_bounds__(512) void k_chol_diag(double *A, int lda, int k, double *Wd,
-                                                   uint32_t *err) {
+constexpr int kLP = 129;  // LDS row pitch of the 64 x 128 augmented block
+
+__global__ __launch_bounds__(512) void k_chol_stepA(double *A, int lda, int k, int nblk,
+                                                    int nrhs_blocks,
+                                                    const double *__restrict__ PTin, int ldpt,
+                                                    double *Wd, uint32_t *err) {
+    __shared__ double L[64][kLP];
     __shared__ __attribute__((aligned(16))) double buf[2][128];
     __shared__ double dsq[64];
-    const int tid = threadIdx.x;
-    const int r = tid & 63;
-    const int cg = tid >> 6;  // 0..7 -> columns cg*16 .. cg*16+15 of [A_kk | I]
-    const int kb = k * kNB;
-    const int mstart = r - cg * 16;  // element m is in the upper part iff m >= mstart
-    double a[16];
+    const int kp = k + 1;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (blockIdx.x > 0) {
+        // ---- trailing update of tile (i, j), kp <= i <= j, (i, j) != (kp, kp) ----
+        const int a = nblk - kp;
+        const int tri = a * (a + 1) / 2;
+        const int t = blockIdx.x;
+        int i, j;
+        if (t < tri) {
+            int jj = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+            while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
+            while (jj * (jj + 1) / 2 > t) --jj;
+            j = kp + jj;
+            i = kp + (t - jj * (jj + 1) / 2);
+        } else {
+            const int t2 = t - tri;
+            j = nblk + t2 / a;
+            i = kp + t2 % a;
+        }
+        const int ib = i * kNB, jb = j * kNB;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int cc = cg * 16 + m;
-        double v;
-        if (cc < 64) v = (r <= cc) ? A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] : 0.0;
-        else v = (cc - 64 == r) ? 1.0 : 0.0;
-        a[m] = v;
+        for (int h = 0; h < 2; ++h) {
+            const int blk = wid * 2 + h;  // 16 MFMA blocks of 16x16
+            const int bx = blk >> 2, by = blk & 3;
+            v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+            for (int kk = 0; kk < 16; ++kk) {
+                const double *pr = PTin + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
+                const double av = pr[jb + bx * 16 + (lane & 15)];
+                const double bv = pr[ib + by * 16 + (lane & 15)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int x = bx * 16 + (lane >> 4) + 4 * rr;  // column within block j
+                const int y = by * 16 + (lane & 15);           // row within block i
+                A[(size_t)(ib + y) + (size_t)(jb + x) * lda] -= acc[rr];
+            }
+        }
+        return;
     }
-    if (r == 0) {
-#pragma unroll
-        for (int m = 0; m < 16; m += 2)
-            *(double2 *)&buf[0][cg * 16 + m] = make_double2(a[m], a[m + 1]);
+    (void)nrhs_blocks;
+    // ---- workgroup 0: update A_kp,kp, eliminate [A_kp,kp | I] ----
+    const int ib = kp * kNB;
+    for (int e = tid; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        L[y][x] = (y <= x) ? A[(size_t)(ib + y) + (size_t)(ib + x) * lda] : 0.0;
     }
     __syncthreads();
-    for (int c = 0; c < 64; ++c) {
-        const double *bc = buf[c & 1];
-        double rv[16];
+    if (k >= 0) {
 #pragma unroll
-        for (int m = 0; m < 16; m += 2) {
-            const double2 t2 = *(const double2 *)&bc[cg * 16 + m];
-            rv[m] = t2.x;
-            rv[m + 1] = t2.y;
-        }
-        const double lr = bc[r];
-        const double piv = bc[c];
-        const double l = lr * fast_rcp(piv) * (double)(r > c);
+        for (int h = 0; h < 2; ++h) {
+            const int blk = wid * 2 + h;
+            const int bx = blk >> 2, by = blk & 3;
+            v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+            for (int kk = 0; kk < 16; ++kk) {
+                const double *pr = PTin + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
+                const double av = pr[ib + bx * 16 + (lane & 15)];
+                const double bv = pr[ib + by * 16 + (lane & 15)];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const double lm = l * (double)(m >= mstart);
-            a[m] = __builtin_fma(-lm, rv[m], a[m]);
-        }
-        if (r == c + 1) {
-            double *bn = buf[(c + 1) & 1];
-#pragma unroll
-            for (int m = 0; m < 16; m += 2)
-                *(double2 *)&bn[cg * 16 + m] = make_double2(a[m], a[m + 1]);
+            for (int rr = 0; rr < 4; ++rr) {
+                const int x = bx * 16 + (lane >> 4) + 4 * rr;
+                const int y = by * 16 + (lane & 15);
+                if (y <= x) L[y][x] -= acc[rr];
+            }
         }
         __syncthreads();
     }
-    // pivot r is a[r][r] (unchanged after step r), held by thread (r, cg = r / 16)
-    if (cg == (r >> 4)) {
-        double pv = 0.0;
+    // wave w owns rows 8w .. 8w+7; lane l owns columns 2l, 2l+1 of [A | I] (128 columns)
+    const int r0 = wid * 8;
+    const int c0 = lane * 2;
+    double a[8][2];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) pv = (m == (r & 15)) ? a[m] : pv;
-        dsq[r] = sqrt(pv);
-        if (!(pv > 0.0) && err) atomicOr(err, 8u);
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? L[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (wid == 0) *(double2 *)&buf[0][c0] = make_double2(a[0][0], a[0][1]);
+    __syncthreads();
+    for (int cb = 0; cb < 64; cb += 8) {
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) {
+            const int c = cb + ci;
+            const double *bc = buf[ci & 1];
+            const double2 rv = *(const double2 *)&bc[c0];
+            double lr[8];
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                const double2 t2 = *(const double2 *)&bc[r0 + i];
+                lr[i] = t2.x;
+                lr[i + 1] = t2.y;
+            }
+            const double inv = fast_rcp(bc[c]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double li = (r0 + i > c) ? lr[i] * inv : 0.0;
+                a[i][0] = __builtin_fma(-li, rv.x, a[i][0]);
+                a[i][1] = __builtin_fma(-li, rv.y, a[i][1]);
+            }
+            const int nr = c + 1;  // publish row nr: wave nr/8, slot (ci + 1) & 7 (static)
+            if (nr < 64 && (nr >> 3) == wid) {
+                const int sl = (ci + 1) & 7;
+                const double v0 = (c0 < nr) ? 0.0 : a[sl][0];      // zero the strictly-lower
+                const double v1 = (c0 + 1 < nr) ? 0.0 : a[sl][1];  // part (cols < 64 only)
+                *(double2 *)&buf[(ci + 1) & 1][c0] = make_double2(v0, v1);
+            }
+            __syncthreads();
+        }
+    }
+    // pivots: row r's diagonal element sits in wave r/8, lane r/2, slot (r&7, r&1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q == r0 + i) {
+                const double pv = a[i][q];
+                dsq[r0 + i] = sqrt(pv);
+                if (!(pv > 0.0) && err) atomicOr(err, 8u);
+            }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double dinv = 1.0 / dsq[r0 + i];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) L[r0 + i][c0 + q - 64] = a[i][q] * dinv;
     }
     __syncthreads();
-    const double d = dsq[r];
-    const double dinv = 1.0 / d;
-    double *W = Wd + (size_t)k * kNB * kNB;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int cc = cg * 16 + m;
-        if (cc < 64) {
-            if (r < cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = a[m] * dinv;
-            else if (r == cc) A[(size_t)(kb + r) + (size_t)(kb + cc) * lda] = d;
-        } else {
-            W[(size_t)(cc - 64) * kNB + r] = a[m] * dinv;  // W[r][x], column-major
-        }
+    double *W = Wd + (size_t)kp * kNB * kNB;
+    for (int e = tid; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        W[(size_t)x * kNB + y] = L[y][x];  // W[y][x], column-major
     }
 }
 
-// U_kj = W_k A_kj for j = k + 1 + blockIdx.x.  Computed transposed, D'[x][r] =
+// U_kp,j = W_kp A_kp,j for j = kp + 1 + blockIdx.x.  Computed transposed, D'[x][r] =
 // sum_s A_kj[s][x] W[r][s], so the column-major store of U_kj is lane-contiguous.
-__global__ __launch_bounds__(256) void k_chol_panel(double *A, int lda, int k,
+__global__ __launch_bounds__(256) void k_chol_stepB(double *A, int lda, int kp,
                                                     const double *__restrict__ Wd, double *PT,
                                                     int ldpt) {
     __shared__ double As[64][65];  // As[s][x] = A_kj[s][x]
-    const int j = k + 1 + blockIdx.x;
-    const int kb = k * kNB, jb = j * kNB;
+    __shared__ double Us[64][65];  // Us[r][x] = U_kj[r][x] staging for the row-major PT store
+    const int j = kp + 1 + blockIdx.x;
+    const int kb = kp * kNB, jb = j * kNB;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int e = tid; e < 64 * 64; e += 256) {
         const int sr = e & 63, x = e >> 6;
         As[sr][x] = A[(size_t)(kb + sr) + (size_t)(jb + x) * lda];
     }
     __syncthreads();
-    const double *W = Wd + (size_t)k * kNB * kNB;
+    const double *W = Wd + (size_t)kp * kNB * kNB;
     const int wx = (wid >> 1) * 32, wr = (wid & 1) * 32;
     v4d acc[2][2];
 #pragma unroll
@@ -657,8 +737,6 @@ __global__ __launch_bounds__(256) void k_chol_panel(double *A, int lda, int k,
             for (int q = 0; q < 2; ++q)
                 acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
     }
-    // D'[x][r]: col (lane&15) -> r, row (lane>>4)+4*rr -> x.  W[r][s] is read as W'[s][r]:
-    // column-major W gives W[r][s] at s*64 + r, i.e. B[k=s][j=r] lane-contiguous in r.
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -669,65 +747,35 @@ __global__ __launch_bounds__(256) void k_chol_panel(double *A, int lda, int k,
                 const int rw = wr + q * 16 + (lane & 15);
                 const double v = acc[p][q][rr];
                 A[(size_t)(kb + rw) + (size_t)(jb + x) * lda] = v;
-                PT[(size_t)rw * ldpt + jb + x] = v;
+                Us[rw][x] = v;
             }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int x = e & 63, rw = e >> 6;
+        PT[(size_t)rw * ldpt + jb + x] = Us[rw][x];
+    }
 }
 
-// Trailing update A_ij -= U_ki' U_kj for k < i <= j (i < nblk), j < ncb.
-// D[x][y] = sum_s U_kj[s][x] U_ki[s][y] via v_mfma_f64_16x16x4_f64 with operands read
-// lane-contiguously from PT; A_ij[y][x] -= D[x][y] (coalesced along y).
-__global__ __launch_bounds__(256) void k_chol_update(double *A, int lda, int k, int nblk,
-                                                     const double *__restrict__ PT, int ldpt) {
-    const int a = nblk - k - 1;
-    const int tri = a * (a + 1) / 2;
-    const int t = blockIdx.x;
-    int i, j;
-    if (t < tri) {
-        int jj = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-        while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
-        while (jj * (jj + 1) / 2 > t) --jj;
-        j = k + 1 + jj;
-        i = k + 1 + (t - jj * (jj + 1) / 2);
-    } else {
-        const int t2 = t - tri;
-        j = nblk + t2 / a;
-        i = k + 1 + t2 % a;
+void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
+                 double *PT, double *Wd) {
+    const int nblk = m_pad / kNB;
+    const int ncb = nblk + nrhs_blocks;
+    const int ldpt = ncb * kNB;
+    double *pt[2] = {PT, PT + (size_t)kNB * ldpt};
+    for (int kp = 0; kp < nblk; ++kp) {
+        int grid = 1;
+        if (kp > 0) {
+            const int a = nblk - kp;
+            grid = a * (a + 1) / 2 + a * nrhs_blocks;
+        }
+        const double *pin = pt[(kp + 1) & 1];  // PT of step kp - 1
+        k_chol_stepA<<<grid, 512, 0, s>>>(A, lda, kp - 1, nblk, nrhs_blocks, pin, ldpt, Wd, err);
+        if (ncb - kp - 1 > 0)
+            k_chol_stepB<<<ncb - kp - 1, 256, 0, s>>>(A, lda, kp, Wd, pt[kp & 1], ldpt);
     }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wx = (wid >> 1) * 32, wy = (wid & 1) * 32;
-    const int ib = i * kNB, jb = j * kNB;
-    v4d acc[2][2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) acc[p][q] = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-    for (int kk = 0; kk < kNB / 4; ++kk) {
-        const int srow = kk * 4 + (lane >> 4);
-        const double *pr = PT + (size_t)srow * ldpt;
-        double av[2], bv[2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m) av[m] = pr[jb + wx + m * 16 + (lane & 15)];
-#pragma unroll
-        for (int m = 0; m < 2; ++m) bv[m] = pr[ib + wy + m * 16 + (lane & 15)];
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int x = wx + p * 16 + (lane >> 4) + 4 * rr;  // column within block j
-                const int y = wy + q * 16 + (lane & 15);           // row within block i
-                double *dst = A + (size_t)(ib + y) + (size_t)(jb + x) * lda;
-                *dst -= acc[p][q][rr];
-            }
 }
+
+void set_chol_diag_threads(int nt) { (void)nt; }
 
 // Backward solve step k: every workgroup forms w_k = U_kk^-1 y_k = W_k' y_k;
 // workgroup 0 stores it; workgroup i < k applies y_i -= U_ik w_k.
@@ -784,20 +832,6 @@ void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const doubl
     const int nblk = m_pad / kNB;
     for (int k = nblk - 1; k >= 0; --k)
         k_bsolve_step<<<k > 0 ? k : 1, 256, 0, s>>>(A, lda, k, m_pad, Wd, Y, W, nrhs);
-}
-
-void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT, double *Wd) {
-    const int nblk = m_pad / kNB;
-    const int ncb = nblk + nrhs_blocks;
-    const int ldpt = ncb * kNB;
-    for (int k = 0; k < nblk; ++k) {
-        k_chol_diag<<<1, 512, 0, s>>>(A, lda, k, Wd, err);
-        if (ncb - k - 1 > 0) k_chol_panel<<<ncb - k - 1, 256, 0, s>>>(A, lda, k, Wd, PT, ldpt);
-        const int a = nblk - k - 1;
-        const int tiles = a * (a + 1) / 2 + a * nrhs_blocks;
-        if (tiles > 0) k_chol_update<<<tiles, 256, 0, s>>>(A, lda, k, nblk, PT, ldpt);
-    }
 }
 
 // ---------------------------------------------------------------------------

@@ -288,7 +288,7 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
-    const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+    const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << (G & 63)) - 1ull);
     if (active && alpha == 1.) active = false;  // :104-110 returns V0, no RNG used
     double result = V0;
     bool done = !active;

@@ -203,6 +203,10 @@ int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, do
 int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int group,
                     int noinline, int reps, double *ms_avg, double *lambda_out);
 
+/* Microbenchmark of the blocked Cholesky (m x m SPD test matrix, 1 RHS): average ms of
+ * chol_factor and of chol_bsolve over `reps` runs with a given diagonal-kernel width. */
+int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *ms_solve);
+
 /* Gram C = Y diag(w) Y' (Y: n x k column-major) via the fp64 MFMA kernel;
  * C is n x n column-major, full symmetric result. */
 int bb_gram(double *C, const double *Y, const double *w, int n, int k);
