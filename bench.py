@@ -97,8 +97,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=2000)
-    ap.add_argument("--p", type=int, default=50000)
+    ap.add_argument("--rows", type=int, default=2000)
+    ap.add_argument("--cols", type=int, default=50000)
     ap.add_argument("--alpha", type=float, default=0.5)
     ap.add_argument("--cpu-sweeps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -120,8 +120,14 @@ def main():
 
     import bayesbridge_amd as bb
 
+    # every rank drives its own GPU; torch's current device must match for the
+    # torch.cuda.synchronize() fences of the timing protocol
+    ndev = max(1, torch.cuda.device_count())
+    device = local_rank % ndev
+    torch.cuda.set_device(device)
+
     bb.set_verbose(0)
-    n, p, alpha = args.n, args.p, args.alpha
+    n, p, alpha = args.rows, args.cols, args.alpha
     per = (p + world - 1) // world
     j0 = min(p, rank * per)
     j1 = min(p, j0 + per)
@@ -131,9 +137,10 @@ def main():
     y, _ = make_problem_y(n, p)
     cfg = bb.EngineConfig(n=n, p=p, p_local=p_loc, j0=j0, rank=rank, world=world,
                           true_alpha=alpha, method=2, trace_capacity=1, seed=0xB4E5B41D6E,
-                          stream=0, device=local_rank)
+                          stream=0, device=device)
     eng = bb.Engine(cfg, X, y)
     del X
+    force_rccl = os.environ.get("BB_FORCE_RCCL", "0") == "1"
     if world > 1:
         if rank == 0:
             uid = bb.Engine.comm_unique_id()
@@ -142,6 +149,9 @@ def main():
             obj = [None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0])
+    elif force_rccl:
+        # exercise the RCCL exchange path on one GPU (1-rank communicator)
+        eng.comm_init(bb.Engine.comm_unique_id())
     eng.init_state()
     setup_s = time.perf_counter() - t_setup0
     log(f"[rank {rank}] setup {setup_s:.2f} s  (n={n}, p={p}, p_local={p_loc}, "
@@ -203,6 +213,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SURVEY.md 8(d) Gaussian design, seed 20240501)",
             "config": {"workload": f"C3 Gaussian bridge n={n} p={p} alpha={alpha}",
+                       "rccl": bool(world > 1 or force_rccl),
                        "n": n, "p": p, "alpha": alpha,
                        "beta_step": "woodbury (exact, p > n)",
                        "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"

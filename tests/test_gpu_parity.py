@@ -351,3 +351,23 @@ def test_gpu_matches_golden_vectors(gpu_lib):
     bb.set_seed(SEED)
     ch = bb.bridge_reg_stb(g["chain_y"], g["chain_X"], nsamp=20, burn=5)
     compare_chain(ch, {k: g["chain_" + k] for k in ("beta", "lambda", "sig2", "tau", "alpha")})
+
+
+def test_rccl_one_rank_communicator_is_identity(gpu_lib):
+    """The RCCL exchange path (ncclCommInitRank + ncclAllReduce on the engine stream) with a
+    1-rank communicator must reproduce the communicator-free engine bit for bit."""
+    bb = gpu_lib
+    n, p = 150, 700
+    X, y, _ = synthetic_problem(n, p, seed=31)
+    outs = []
+    for use_comm in (False, True):
+        e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=11, method=2,
+                                      trace_capacity=8), X, y)
+        if use_comm:
+            e.comm_init(bb.Engine.comm_unique_id())
+        e.init_state()
+        e.run(1, 8, first_slot=0, slot_step=1)
+        outs.append(e.trace(0, 8))
+        e.close()
+    for k in ("beta", "lambda", "sig2", "tau"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
