@@ -110,7 +110,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
-    L.bb_bench_chol.argtypes = [c.c_int, c.c_int, c.c_int, _dp, _dp]
+    L.bb_bench_chol.argtypes = [c.c_int, c.c_int, _dp, _dp, c.c_void_p]
     L.bb_bench_lambda.argtypes = [_dp, c.c_int, c.c_double, c.c_double, c.c_int, c.c_int,
                                   c.c_int, _dp, _dp]
     L.bb_engine_phase_times.argtypes = [c.c_void_p, _dp, c.c_int, _ip]
@@ -318,14 +318,17 @@ def bench_lambda(beta, alpha, tau, group, noinline=1, reps=20):
     return ms.value, lam
 
 
-def bench_chol(m, diag_threads=512, reps=10):
-    """(factor ms, solve ms) of the blocked device Cholesky on an m x m SPD test matrix."""
+def bench_chol(m, reps=10, trace=False):
+    """(factor ms, solve ms[, stamps]) of the blocked device Cholesky on an m x m SPD test
+    matrix; with trace=True also the (steps, 8) s_memrealtime stamps (100 MHz ticks) of one
+    traced factorisation (see bb_bench_chol in include/bayesbridge.h)."""
     L = library()
     _require_gpu()
     f, s = ctypes.c_double(), ctypes.c_double()
-    _check(L.bb_bench_chol(m, diag_threads, reps, ctypes.byref(f), ctypes.byref(s)),
-           "bb_bench_chol")
-    return f.value, s.value
+    ts = np.zeros((-(-m // 64), 8), dtype=np.uint64) if trace else None
+    _check(L.bb_bench_chol(m, reps, ctypes.byref(f), ctypes.byref(s),
+                           ts.ctypes.data if trace else None), "bb_bench_chol")
+    return (f.value, s.value, ts) if trace else (f.value, s.value)
 
 
 def gram(Y, w):

@@ -144,6 +144,7 @@ struct bb_engine {
     // woodbury
     double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *PT = nullptr,
            *w = nullptr, *Wd = nullptr;
+    unsigned int *flags = nullptr;
     int S = 1;
     size_t slab_stride = 0;
     // chol / ortho
@@ -243,7 +244,7 @@ struct bb_engine {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
             mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd, flags);
             mark(PH_SOLVE);
             chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1);
             mark(PH_BETA);
@@ -252,7 +253,7 @@ struct bb_engine {
             mark(PH_FORM);
             launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
             mark(PH_CHOL);
-            chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd);
+            chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd, flags);
             mark(PH_SOLVE);
             launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
             chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2);
@@ -355,6 +356,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     }
     e->PT = dalloc<double>((size_t)2 * kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
     e->Wd = dalloc<double>((size_t)kNB * (n_pad > p_pad ? n_pad : p_pad), o);
+    e->flags = dalloc<unsigned int>((size_t)(n_pad > p_pad ? n_pad : p_pad) / kNB + 4, o);
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
     const bool small = c.p <= c.n && c.world == 1;
     if (e->method != 2 || small) {
@@ -406,7 +408,7 @@ void engine_init_state_local(bb_engine *e) {
         e->clear_err();
         launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, e->p_pad, e->A,
                       e->p_pad, e->p_pad);
-        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT, e->Wd);
+        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT, e->Wd, e->flags);
         HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
                                 e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
         chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1);
@@ -959,7 +961,8 @@ int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int gro
     return rc;
 }
 
-int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *ms_solve) {
+int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
+                  unsigned long long *trace) {
     std::vector<void *> owned;
     int rc = 0;
     try {
@@ -976,9 +979,9 @@ int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *
         HIPCHECK(hipMemcpy(src, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
         double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
+        unsigned int *fl = dalloc<unsigned int>((size_t)m_pad / kNB + 4, owned);
         double *W = dalloc<double>((size_t)m_pad, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
-        set_chol_diag_threads(diag_threads);
         hipEvent_t e0, e1, e2;
         HIPCHECK(hipEventCreate(&e0));
         HIPCHECK(hipEventCreate(&e1));
@@ -987,7 +990,7 @@ int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *
         for (int it = 0; it <= reps; ++it) {
             HIPCHECK(hipMemcpyAsync(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice, 0));
             HIPCHECK(hipEventRecord(e0, 0));
-            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd);
+            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
             HIPCHECK(hipEventRecord(e1, 0));
             chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, 1);
             HIPCHECK(hipEventRecord(e2, 0));
@@ -1000,9 +1003,17 @@ int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *
                 ts += b;
             }
         }
-        set_chol_diag_threads(512);
         *ms_factor = tf / reps;
         *ms_solve = ts / reps;
+        if (trace) {
+            const size_t nts = (size_t)8 * (m_pad / kNB);
+            unsigned long long *dt = dalloc<unsigned long long>(nts, owned);
+            HIPCHECK(hipMemset(dt, 0, nts * sizeof(unsigned long long)));
+            HIPCHECK(hipMemcpy(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice));
+            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl, dt);
+            HIPCHECK(hipDeviceSynchronize());
+            HIPCHECK(hipMemcpy(trace, dt, nts * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        }
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         (void)hipEventDestroy(e2);
@@ -1066,9 +1077,10 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
         double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
+        unsigned int *fl = dalloc<unsigned int>((size_t)m_pad / kNB + 4, owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
-        chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd);
+        chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
         chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, nrhs);
         HIPCHECK(hipGetLastError());
         std::vector<double> hw((size_t)m_pad * nrhs);

@@ -87,10 +87,11 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 // forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
 // PT: scratch of 2 x kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
 // kNB x kNB receiving U_kk^-T (used by chol_bsolve).
+// flags: >= m_pad/kNB unsigned ints of scratch (zeroed here for every factorisation).
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT, double *Wd);
+                 double *PT, double *Wd, unsigned int *flags,
+                 unsigned long long *trace = nullptr);
 
-void set_chol_diag_threads(int nt);  // 128 / 256 / 512 / 1024 (tuning)
 
 // Backward solve U W = Y (Y, W: m_pad x nrhs <= 2, ld = m_pad); Y is overwritten.
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,

@@ -532,19 +532,23 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 
 // ---------------------------------------------------------------------------
 // Blocked right-looking Cholesky A = U'U (upper, column-major, NB = 64) with the
-// forward solve folded into trailing right-hand-side column blocks.  Two kernels per step
-// kp (k = kp - 1 is the previous step, whose row panel PT_k is already formed):
-//   k_chol_stepA: workgroup 0 applies step k's update to A_kp,kp and eliminates
-//                 [A_kp,kp | I] -> W_kp = U_kp,kp^-T (the serial pivot chain); the other
-//                 workgroups apply step k's update to every tile (i, j), kp <= i <= j
-//                 (RHS blocks included), reading U's block row k lane-contiguously from PT_k.
-//   k_chol_stepB: U_kp,j = W_kp A_kp,j for j > kp (MFMA), into A and row-major PT_kp
-//                 (RHS blocks: the forward substitution).
-// The backward solve uses W_kp = U_kp,kp^-T, so U_kp,kp itself is never stored.
-// Dependent fp64 ops cost ~48 cycles on gfx950 and the pivot loop is issue/latency bound
-// (tools/diag_latency.hip), so the loop carries no per-element masks: the published pivot
-// row has its strictly-lower part zeroed, which keeps every lower-part value finite, and
-// finished rows use a zero multiplier.
+// forward solve folded into trailing right-hand-side column blocks.  ONE launch per block
+// step kp (panel PT_{kp-1} of the previous step is ready):
+//   workgroup 0      applies step kp-1's update to A_kp,kp and eliminates [A_kp,kp | I]
+//                    -> W_kp = U_kp,kp^-T, stores it and releases flags[kp];
+//   panel workgroups (j > kp, RHS blocks included) apply step kp-1's update to A_kp,j in
+//                    LDS, acquire flags[kp], then form U_kp,j = W_kp A_kp,j (MFMA) into A and
+//                    row-major into PT_kp (RHS blocks: the forward substitution);
+//   trailing workgroups apply step kp-1's update to every tile (i, j), kp < i <= j.
+// The flag hand-off follows the agent-scope release/acquire recipe (cdna_hip_programming
+// Guideline 16); flags are zeroed per factorisation; spins are bounded (error bit 16).
+// Pivot chain (tools/diag_latency.hip: a dependent fp64 op ~48 cycles, an LDS
+// write/barrier/read round trip ~270): the wave owning rows 8b..8b+7 factors them with
+// v_readlane broadcasts (no barrier), publishes the 8 rows once, and the other waves apply a
+// rank-8 update -- valid because a symmetric elimination's multipliers depend only on the
+// final pivot rows.  Pivot rows are published with their strictly-lower part zeroed so every
+// value stays finite without per-element masks.  U_kp,kp itself is never stored: the
+// backward solve uses W_kp.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double fast_rcp(double p) {
     // v_rcp_f64 (~2^-26 accurate) + one Newton step: ~1 ulp for the normal positive pivots
@@ -552,87 +556,185 @@ __device__ __forceinline__ double fast_rcp(double p) {
     return r * (2.0 - p * r);
 }
 
-constexpr int kLP = 129;  // LDS row pitch of the 64 x 128 augmented block
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
-__global__ __launch_bounds__(512) void k_chol_stepA(double *A, int lda, int k, int nblk,
-                                                    int nrhs_blocks,
-                                                    const double *__restrict__ PTin, int ldpt,
-                                                    double *Wd, uint32_t *err) {
-    __shared__ double L[64][kLP];
-    __shared__ __attribute__((aligned(16))) double buf[2][128];
-    __shared__ double dsq[64];
-    const int kp = k + 1;
+// Trailing update of one 64x64 tile in global memory: A_ij -= U_ki' U_kj (PT = U's block
+// row k, row-major), 8 waves x 2 MFMA blocks of 16x16.
+__device__ __forceinline__ void tile_update_global(double *A, int lda, int ib, int jb,
+                                                  const double *__restrict__ PT, int ldpt) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int blk = wid * 2 + h;
+        const int bx = blk >> 2, by = blk & 3;
+        v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kk = 0; kk < 16; ++kk) {
+            const double *pr = PT + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
+            const double av = pr[jb + bx * 16 + (lane & 15)];
+            const double bv = pr[ib + by * 16 + (lane & 15)];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int x = bx * 16 + (lane >> 4) + 4 * rr;  // column within block j
+            const int y = by * 16 + (lane & 15);           // row within block i
+            A[(size_t)(ib + y) + (size_t)(jb + x) * lda] -= acc[rr];
+        }
+    }
+}
+
+// Same update applied to a 64x64 tile held in LDS as T[row][col] (pitch 65).
+__device__ __forceinline__ void tile_update_lds(double (*T)[65], int ib, int jb,
+                                               const double *__restrict__ PT, int ldpt,
+                                               bool upper_only) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int blk = wid * 2 + h;
+        const int bx = blk >> 2, by = blk & 3;
+        v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kk = 0; kk < 16; ++kk) {
+            const double *pr = PT + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
+            const double av = pr[jb + bx * 16 + (lane & 15)];
+            const double bv = pr[ib + by * 16 + (lane & 15)];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int x = bx * 16 + (lane >> 4) + 4 * rr;
+            const int y = by * 16 + (lane & 15);
+            if (!upper_only || y <= x) T[y][x] -= acc[rr];
+        }
+    }
+}
+
+// Diagnostic timestamps (s_memrealtime, 100 MHz) of the step's critical path, written only
+// when a trace buffer is given (bb_chol_trace): [kp][0..4] workgroup 0 start / tile loaded /
+// updated / eliminated / flag released, [kp][5..7] panel workgroup 1 start / acquired / done.
+#define CHOL_TS(slot)                                                                      \
+    do {                                                                                    \
+        if (trace && threadIdx.x == 0) trace[kp * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+
+__global__ __launch_bounds__(512) void k_chol_step(double *A, int lda, int kp, int nblk,
+                                                   int ncb, const double *__restrict__ PTin,
+                                                   double *PTout, int ldpt, double *Wd,
+                                                   unsigned int *flags, uint32_t *err,
+                                                   unsigned long long *trace) {
+    __shared__ double T[64][65];                                   // one 64x64 tile
+    __shared__ __attribute__((aligned(16))) double rows[2][8][128];  // published pivot rows
+    __shared__ double rinv[2][8];
+    __shared__ double piv[64];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (blockIdx.x > 0) {
-        // ---- trailing update of tile (i, j), kp <= i <= j, (i, j) != (kp, kp) ----
-        const int a = nblk - kp;
+    const int npanel = ncb - kp - 1;
+    const int ib = kp * kNB;
+    if ((int)blockIdx.x > npanel) {
+        // ---- trailing update of tile (i, j), kp < i <= j (RHS blocks included) ----
+        const int a = nblk - kp - 1;
         const int tri = a * (a + 1) / 2;
-        const int t = blockIdx.x;
+        const int t = blockIdx.x - npanel - 1;
         int i, j;
         if (t < tri) {
             int jj = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
             while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
             while (jj * (jj + 1) / 2 > t) --jj;
-            j = kp + jj;
-            i = kp + (t - jj * (jj + 1) / 2);
+            j = kp + 1 + jj;
+            i = kp + 1 + (t - jj * (jj + 1) / 2);
         } else {
             const int t2 = t - tri;
             j = nblk + t2 / a;
-            i = kp + t2 % a;
+            i = kp + 1 + t2 % a;
         }
-        const int ib = i * kNB, jb = j * kNB;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int blk = wid * 2 + h;  // 16 MFMA blocks of 16x16
-            const int bx = blk >> 2, by = blk & 3;
-            v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-            for (int kk = 0; kk < 16; ++kk) {
-                const double *pr = PTin + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
-                const double av = pr[jb + bx * 16 + (lane & 15)];
-                const double bv = pr[ib + by * 16 + (lane & 15)];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int x = bx * 16 + (lane >> 4) + 4 * rr;  // column within block j
-                const int y = by * 16 + (lane & 15);           // row within block i
-                A[(size_t)(ib + y) + (size_t)(jb + x) * lda] -= acc[rr];
-            }
-        }
+        tile_update_global(A, lda, i * kNB, j * kNB, PTin, ldpt);
         return;
     }
-    (void)nrhs_blocks;
-    // ---- workgroup 0: update A_kp,kp, eliminate [A_kp,kp | I] ----
-    const int ib = kp * kNB;
-    for (int e = tid; e < 64 * 64; e += 512) {
-        const int y = e & 63, x = e >> 6;
-        L[y][x] = (y <= x) ? A[(size_t)(ib + y) + (size_t)(ib + x) * lda] : 0.0;
-    }
-    __syncthreads();
-    if (k >= 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int blk = wid * 2 + h;
-            const int bx = blk >> 2, by = blk & 3;
-            v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-            for (int kk = 0; kk < 16; ++kk) {
-                const double *pr = PTin + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
-                const double av = pr[ib + bx * 16 + (lane & 15)];
-                const double bv = pr[ib + by * 16 + (lane & 15)];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int x = bx * 16 + (lane >> 4) + 4 * rr;
-                const int y = by * 16 + (lane & 15);
-                if (y <= x) L[y][x] -= acc[rr];
-            }
+    if (blockIdx.x > 0) {
+        // ---- panel workgroup: U_kp,j = W_kp (A_kp,j - step kp-1 update) ----
+        const int j = kp + blockIdx.x;
+        const int jb = j * kNB;
+        if (blockIdx.x != 1) trace = nullptr;
+        CHOL_TS(5);
+        for (int e = tid; e < 64 * 64; e += 512) {
+            const int y = e & 63, x = e >> 6;
+            T[y][x] = A[(size_t)(ib + y) + (size_t)(jb + x) * lda];
         }
         __syncthreads();
+        if (kp > 0) {
+            tile_update_lds(T, ib, jb, PTin, ldpt, false);
+            __syncthreads();
+        }
+        if (tid == 0) {
+            unsigned spins = 0;
+            while (__hip_atomic_load(&flags[kp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   0u) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24)) {
+                    atomicOr(err, 16u);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        CHOL_TS(6);
+        __syncthreads();
+        // D'[x][r] = sum_s T[s][x] W[r][s]: 8 waves x 2 blocks of 16x16 over the 64x64 result
+        const double *W = Wd + (size_t)kp * kNB * kNB;
+        v4d acc[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+        const int bxx = (wid >> 1) * 16;      // x block (0..48)
+        const int brr = (wid & 1) * 32;       // r base (0 / 32), two 16-wide blocks
+#pragma unroll 4
+        for (int kk = 0; kk < 16; ++kk) {
+            const int sr = kk * 4 + (lane >> 4);
+            const double av = T[sr][bxx + (lane & 15)];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const double bv = W[(size_t)sr * kNB + brr + h * 16 + (lane & 15)];
+                acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // T is overwritten with U below
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const int x = bxx + (lane >> 4) + 4 * rr;
+                const int rw = brr + h * 16 + (lane & 15);
+                const double v = acc[h][rr];
+                A[(size_t)(ib + rw) + (size_t)(jb + x) * lda] = v;
+                T[rw][x] = v;
+            }
+        __syncthreads();
+        for (int e = tid; e < 64 * 64; e += 512) {
+            const int x = e & 63, rw = e >> 6;
+            PTout[(size_t)rw * ldpt + jb + x] = T[rw][x];
+        }
+        CHOL_TS(7);
+        return;
     }
-    // wave w owns rows 8w .. 8w+7; lane l owns columns 2l, 2l+1 of [A | I] (128 columns)
+    // ---- workgroup 0: update A_kp,kp, eliminate [A_kp,kp | I], publish W_kp ----
+    CHOL_TS(0);
+    for (int e = tid; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        T[y][x] = (y <= x) ? A[(size_t)(ib + y) + (size_t)(ib + x) * lda] : 0.0;
+    }
+    __syncthreads();
+    CHOL_TS(1);
+    if (kp > 0) {
+        tile_update_lds(T, ib, ib, PTin, ldpt, true);
+        __syncthreads();
+    }
+    CHOL_TS(2);
+    // wave w owns rows 8w .. 8w+7; lane l owns columns 2l, 2l+1 of [A | I]
     const int r0 = wid * 8;
     const int c0 = lane * 2;
     double a[8][2];
@@ -641,141 +743,111 @@ __global__ __launch_bounds__(512) void k_chol_stepA(double *A, int lda, int k, i
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int row = r0 + i, col = c0 + q;
-            a[i][q] = (col < 64) ? L[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
         }
-    if (wid == 0) *(double2 *)&buf[0][c0] = make_double2(a[0][0], a[0][1]);
-    __syncthreads();
-    for (int cb = 0; cb < 64; cb += 8) {
+    for (int b = 0; b < 8; ++b) {
+        const int sb = b & 1;
+        if (wid == b) {
+            // wave-local factorisation of rows 8b .. 8b+7
+            double invs[8];
 #pragma unroll
-        for (int ci = 0; ci < 8; ++ci) {
-            const int c = cb + ci;
-            const double *bc = buf[ci & 1];
-            const double2 rv = *(const double2 *)&bc[c0];
-            double lr[8];
+            for (int ci = 0; ci < 8; ++ci) {
+                const int c = 8 * b + ci;
+                a[ci][0] = (c0 < c) ? 0.0 : a[ci][0];
+                a[ci][1] = (c0 + 1 < c) ? 0.0 : a[ci][1];
+                const double pv = readlane_d(a[ci][ci & 1], 4 * b + (ci >> 1));
+                const double inv = fast_rcp(pv);
+                invs[ci] = inv;
+                if (lane == 0) piv[c] = pv;
 #pragma unroll
-            for (int i = 0; i < 8; i += 2) {
-                const double2 t2 = *(const double2 *)&bc[r0 + i];
-                lr[i] = t2.x;
-                lr[i + 1] = t2.y;
+                for (int i = ci + 1; i < 8; ++i) {
+                    const double li = readlane_d(a[ci][i & 1], 4 * b + (i >> 1)) * inv;
+                    a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
+                    a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+                }
             }
-            const double inv = fast_rcp(bc[c]);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const double li = (r0 + i > c) ? lr[i] * inv : 0.0;
-                a[i][0] = __builtin_fma(-li, rv.x, a[i][0]);
-                a[i][1] = __builtin_fma(-li, rv.y, a[i][1]);
+            for (int ci = 0; ci < 8; ++ci)
+                *(double2 *)&rows[sb][ci][c0] = make_double2(a[ci][0], a[ci][1]);
+            if (lane < 8) {
+                double v = 0.0;
+#pragma unroll
+                for (int ci = 0; ci < 8; ++ci) v = (lane == ci) ? invs[ci] : v;
+                rinv[sb][lane] = v;
             }
-            const int nr = c + 1;  // publish row nr: wave nr/8, slot (ci + 1) & 7 (static)
-            if (nr < 64 && (nr >> 3) == wid) {
-                const int sl = (ci + 1) & 7;
-                const double v0 = (c0 < nr) ? 0.0 : a[sl][0];      // zero the strictly-lower
-                const double v1 = (c0 + 1 < nr) ? 0.0 : a[sl][1];  // part (cols < 64 only)
-                *(double2 *)&buf[(ci + 1) & 1][c0] = make_double2(v0, v1);
-            }
-            __syncthreads();
         }
+        __syncthreads();
+        if (wid > b) {
+            // rank-8 update of my rows with the published pivot rows 8b .. 8b+7
+            double m[8][8];
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double iv = rinv[sb][ci];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    const double2 t2 = *(const double2 *)&rows[sb][ci][r0 + i];
+                    m[ci][i] = t2.x * iv;
+                    m[ci][i + 1] = t2.y * iv;
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double2 rv = *(const double2 *)&rows[sb][ci][c0];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    a[i][0] = __builtin_fma(-m[ci][i], rv.x, a[i][0]);
+                    a[i][1] = __builtin_fma(-m[ci][i], rv.y, a[i][1]);
+                }
+            }
+        }
+        // the next block's publisher writes rows[sb ^ 1]; rows[sb] is rewritten two blocks
+        // later, after the barrier that follows every wave's reads of it
     }
-    // pivots: row r's diagonal element sits in wave r/8, lane r/2, slot (r&7, r&1)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-            if (c0 + q == r0 + i) {
-                const double pv = a[i][q];
-                dsq[r0 + i] = sqrt(pv);
-                if (!(pv > 0.0) && err) atomicOr(err, 8u);
-            }
-    __syncthreads();
+    CHOL_TS(3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const double dinv = 1.0 / dsq[r0 + i];
+        const double pv = piv[r0 + i];
+        if (!(pv > 0.0) && err && lane == 0) atomicOr(err, 8u);
+        const double dinv = 1.0 / sqrt(pv);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            if (c0 + q >= 64) L[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
     }
     __syncthreads();
     double *W = Wd + (size_t)kp * kNB * kNB;
     for (int e = tid; e < 64 * 64; e += 512) {
         const int y = e & 63, x = e >> 6;
-        W[(size_t)x * kNB + y] = L[y][x];  // W[y][x], column-major
+        W[(size_t)x * kNB + y] = T[y][x];  // W[y][x], column-major
     }
-}
-
-// U_kp,j = W_kp A_kp,j for j = kp + 1 + blockIdx.x.  Computed transposed, D'[x][r] =
-// sum_s A_kj[s][x] W[r][s], so the column-major store of U_kj is lane-contiguous.
-__global__ __launch_bounds__(256) void k_chol_stepB(double *A, int lda, int kp,
-                                                    const double *__restrict__ Wd, double *PT,
-                                                    int ldpt) {
-    __shared__ double As[64][65];  // As[s][x] = A_kj[s][x]
-    __shared__ double Us[64][65];  // Us[r][x] = U_kj[r][x] staging for the row-major PT store
-    const int j = kp + 1 + blockIdx.x;
-    const int kb = kp * kNB, jb = j * kNB;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int e = tid; e < 64 * 64; e += 256) {
-        const int sr = e & 63, x = e >> 6;
-        As[sr][x] = A[(size_t)(kb + sr) + (size_t)(jb + x) * lda];
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const double *W = Wd + (size_t)kp * kNB * kNB;
-    const int wx = (wid >> 1) * 32, wr = (wid & 1) * 32;
-    v4d acc[2][2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) acc[p][q] = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-    for (int kk = 0; kk < 16; ++kk) {
-        const int sr = kk * 4 + (lane >> 4);
-        double av[2], bv[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) av[p] = As[sr][wx + p * 16 + (lane & 15)];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) bv[q] = W[(size_t)sr * kNB + wr + q * 16 + (lane & 15)];
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[p], bv[q], acc[p][q], 0, 0, 0);
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[kp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int x = wx + p * 16 + (lane >> 4) + 4 * rr;
-                const int rw = wr + q * 16 + (lane & 15);
-                const double v = acc[p][q][rr];
-                A[(size_t)(kb + rw) + (size_t)(jb + x) * lda] = v;
-                Us[rw][x] = v;
-            }
-    __syncthreads();
-    for (int e = tid; e < 64 * 64; e += 256) {
-        const int x = e & 63, rw = e >> 6;
-        PT[(size_t)rw * ldpt + jb + x] = Us[rw][x];
-    }
+    CHOL_TS(4);
 }
 
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT, double *Wd) {
+                 double *PT, double *Wd, unsigned int *flags, unsigned long long *trace) {
     const int nblk = m_pad / kNB;
     const int ncb = nblk + nrhs_blocks;
     const int ldpt = ncb * kNB;
     double *pt[2] = {PT, PT + (size_t)kNB * ldpt};
+    (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * ((nblk + 3) & ~3), s);
     for (int kp = 0; kp < nblk; ++kp) {
-        int grid = 1;
-        if (kp > 0) {
-            const int a = nblk - kp;
-            grid = a * (a + 1) / 2 + a * nrhs_blocks;
-        }
+        const int npanel = ncb - kp - 1;
+        const int a = nblk - kp - 1;
+        const int tiles = kp > 0 ? (a * (a + 1) / 2 + a * nrhs_blocks) : 0;
+        // tiles of rows > kp receive step kp-1's update; at kp = 0 there is none
+        const int ntrail = (kp > 0) ? tiles : 0;
         const double *pin = pt[(kp + 1) & 1];  // PT of step kp - 1
-        k_chol_stepA<<<grid, 512, 0, s>>>(A, lda, kp - 1, nblk, nrhs_blocks, pin, ldpt, Wd, err);
-        if (ncb - kp - 1 > 0)
-            k_chol_stepB<<<ncb - kp - 1, 256, 0, s>>>(A, lda, kp, Wd, pt[kp & 1], ldpt);
+        k_chol_step<<<1 + npanel + ntrail, 512, 0, s>>>(A, lda, kp, nblk, ncb, pin, pt[kp & 1],
+                                                      ldpt, Wd, flags, err, trace);
     }
 }
 
-void set_chol_diag_threads(int nt) { (void)nt; }
 
 // Backward solve step k: every workgroup forms w_k = U_kk^-1 y_k = W_k' y_k;
 // workgroup 0 stores it; workgroup i < k applies y_i -= U_ik w_k.

@@ -204,8 +204,12 @@ int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int gro
                     int noinline, int reps, double *ms_avg, double *lambda_out);
 
 /* Microbenchmark of the blocked Cholesky (m x m SPD test matrix, 1 RHS): average ms of
- * chol_factor and of chol_bsolve over `reps` runs with a given diagonal-kernel width. */
-int bb_bench_chol(int m, int diag_threads, int reps, double *ms_factor, double *ms_solve);
+ * chol_factor and of chol_bsolve over `reps` runs.  If `trace` is not NULL it receives
+ * 8 * ceil(m/64) s_memrealtime stamps (100 MHz) of an extra traced factorisation: per block
+ * step, the diagonal workgroup's start / tile loaded / tile updated / eliminated / W
+ * released, then panel workgroup 1's start / W acquired / done. */
+int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
+                  unsigned long long *trace);
 
 /* Gram C = Y diag(w) Y' (Y: n x k column-major) via the fp64 MFMA kernel;
  * C is n x n column-major, full symmetric result. */
