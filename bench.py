@@ -92,6 +92,25 @@ def cpu_baseline(n, p, alpha, sweeps, log_every=True):
     return per, threads
 
 
+def pmc_traffic(n, p, world):
+    """HBM bytes per k_gram launch from the newest committed PMC summary of this workload
+    (profiles/rNN_pmc.json, written by tools/profile_round.sh + tools/profile_summary.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 read correction).  None if absent or
+    for a different workload / world size."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if w.get("n") == n and w.get("p") == p and world == 1 and "k_gram" in d:
+            best = (d["k_gram"]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -189,6 +208,8 @@ def main():
     gram_flops = float(n) * (n + 1) * p_loc
     achieved = gram_flops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
 
+    traffic = pmc_traffic(n, p, world)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sweeps > 0:
         log(f"[cpu_baseline] timing {args.cpu_sweeps} oracle sweeps at n={n}, p={p} ...")
@@ -221,7 +242,11 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "k_gram (v_mfma_f64_16x16x4_f64)",
                          "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                         "traffic": None, "gram_ms_avg": gram_ms,
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
+                         "traffic_source": traffic[1] if traffic else None,
+                         "algorithmic_bytes_per_launch": 8.0 * n * p_loc,
+                         "gram_ms_avg": gram_ms,
                          "sweep_ms_avg_events": sweep_ms,
                          "flops_per_launch": gram_flops},
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},

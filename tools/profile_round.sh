@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round profile of the bench workload (run on the GPU box):
+#   1. rocprofv3 --kernel-trace --stats       -> per-kernel average durations
+#   2. rocprofv3 --pmc FETCH_SIZE  (own pass) -> HBM read KB per dispatch
+#   3. rocprofv3 --pmc WRITE_SIZE  (own pass) -> HBM write KB per dispatch
+# No --pmc pass is combined with any trace domain.  Each step has its own time limit and
+# a failure ends the script.  Summaries: python tools/profile_summary.py <round>.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+ROUND=${ROUND:-r01}
+OUT=gpurun_out/prof_$ROUND
+mkdir -p "$OUT"
+ARGS="--no-cpu-baseline $*"
+set -o pipefail
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
+    -- python3 bench.py --steps 10 --warmup 2 $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
+    || { echo "kernel-trace pass failed ($?)"; exit 1; }
+echo "kernel-trace pass ok"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
+    -- python3 bench.py --steps 2 --warmup 1 $ARGS > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err" \
+    || { echo "FETCH_SIZE pass failed ($?)"; exit 1; }
+echo "FETCH_SIZE pass ok"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
+    -- python3 bench.py --steps 2 --warmup 1 $ARGS > "$OUT/write_bench.json" 2> "$OUT/write_bench.err" \
+    || { echo "WRITE_SIZE pass failed ($?)"; exit 1; }
+echo "WRITE_SIZE pass ok"

@@ -1,0 +1,99 @@
+"""Turn a tools/profile_round.sh output directory into the committed round summaries:
+  profiles/<round>_kernel_stats.csv   rocprofv3 --stats table (copied as is)
+  profiles/<round>_kernel_stats.txt   the same, sorted, with % of GPU time
+  profiles/<round>_pmc.json           per-kernel average FETCH_SIZE / WRITE_SIZE per dispatch
+
+FETCH_SIZE / WRITE_SIZE are KB (x1024).  On gfx950 FETCH_SIZE reports 1/2 of the bytes of a
+wide coalesced streaming read (MI355X_MICROARCH.md HBM section), so read bytes are taken as
+2 x FETCH_SIZE x 1024; the k_xv pass, which streams X exactly once with known bytes, is
+reported beside it as an in-run calibration of that factor.
+Usage: python tools/profile_summary.py r01 [n] [p]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def one(pattern):
+    hits = glob.glob(pattern, recursive=True)
+    if not hits:
+        raise SystemExit(f"missing {pattern}")
+    return hits[0]
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").strip()
+
+
+def pmc_avgs(path, counter):
+    tot, cnt = {}, {}
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r["Kernel_Name"])
+        tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
+        cnt[k] = cnt.get(k, 0) + 1
+    return {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
+
+
+def main():
+    rnd = sys.argv[1]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
+    p = int(sys.argv[3]) if len(sys.argv) > 3 else 50000
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    ks = one(os.path.join(src, "kt", "**", "*kernel_stats.csv"))
+    shutil.copy(ks, os.path.join(dst, f"{rnd}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(ks)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    lines = [f"# rocprofv3 --kernel-trace --stats of: python3 bench.py --steps 10 --warmup 2 "
+             f"--no-cpu-baseline (n={n}, p={p}, 1 GPU)",
+             f"{'kernel':48s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'tot_ms':>9s}  share"]
+    avg_us = {}
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        k = short(r["Name"])
+        avg_us[k] = float(r["AverageNs"]) / 1e3
+        lines.append(f"{k[:48]:48s} {r['Calls']:>6s} {float(r['AverageNs']) / 1e3:10.2f} "
+                     f"{float(r['MinNs']) / 1e3:10.2f} {float(r['TotalDurationNs']) / 1e6:9.2f} "
+                     f"{100 * float(r['TotalDurationNs']) / tot:5.1f}%")
+    open(os.path.join(dst, f"{rnd}_kernel_stats.txt"), "w").write("\n".join(lines) + "\n")
+    fetch = pmc_avgs(one(os.path.join(src, "fetch", "**", "*counter_collection.csv")), "FETCH_SIZE")
+    write = pmc_avgs(one(os.path.join(src, "write", "**", "*counter_collection.csv")), "WRITE_SIZE")
+    n_pad = -(-n // 128) * 128
+    p_pad = -(-p // 256) * 256
+    x_bytes = 8.0 * n_pad * p_pad
+    out = {"round": rnd, "workload": {"n": n, "p": p, "n_pad": n_pad, "p_pad": p_pad},
+           "units": "bytes per dispatch (average over the profiled dispatches)",
+           "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 1/2 reporting of wide "
+                         "streaming reads); write_bytes = WRITE_SIZE x 1024",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f_kb, fc = fetch.get(k, (float("nan"), 0))
+        w_kb, wc = write.get(k, (float("nan"), 0))
+        out["kernels"][k] = {"fetch_kb": f_kb, "write_kb": w_kb, "dispatches": max(fc, wc),
+                             "read_bytes": 2 * 1024 * f_kb, "write_bytes": 1024 * w_kb,
+                             "hbm_bytes": 2 * 1024 * f_kb + 1024 * w_kb,
+                             "avg_us": avg_us.get(k)}
+    if "bb::k_xv" in out["kernels"]:
+        kx = out["kernels"]["bb::k_xv"]
+        out["calibration_k_xv"] = {"algorithmic_read_bytes": x_bytes,
+                                   "fetch_x1024": 1024 * kx["fetch_kb"],
+                                   "ratio_algorithmic_over_fetch": x_bytes / (1024 * kx["fetch_kb"])}
+    if "bb::k_gram" in out["kernels"]:
+        g = out["kernels"]["bb::k_gram"]
+        out["k_gram"] = {"hbm_bytes_per_launch": g["hbm_bytes"],
+                         "algorithmic_bytes_per_launch": x_bytes + 8.0 * p_pad + 8.0 * n_pad ** 2,
+                         "avg_us": g["avg_us"]}
+    json.dump(out, open(os.path.join(dst, f"{rnd}_pmc.json"), "w"), indent=1)
+    print("\n".join(lines[:16]))
+    print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
