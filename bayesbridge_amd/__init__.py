@@ -40,7 +40,10 @@ class bb_config(ctypes.Structure):
                 ("true_sig2", ctypes.c_double), ("true_tau", ctypes.c_double),
                 ("true_alpha", ctypes.c_double), ("ortho", ctypes.c_int),
                 ("method", ctypes.c_int), ("trace_capacity", ctypes.c_int),
-                ("seed", ctypes.c_uint64), ("stream", ctypes.c_uint64), ("device", ctypes.c_int)]
+                ("seed", ctypes.c_uint64), ("stream", ctypes.c_uint64), ("device", ctypes.c_int),
+                ("gram_mode", ctypes.c_int)]
+
+GRAM_FP64, GRAM_OZAKI = 0, 1
 
 
 EXPORTED_SYMBOLS = [
@@ -54,7 +57,7 @@ EXPORTED_SYMBOLS = [
     "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
-    "bb_bench_chol",
+    "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode",
 ]
 
 
@@ -96,6 +99,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_get_state.argtypes = [c.c_void_p, _dp, _dp, _dp, _dp, _dp]
     L.bb_engine_set_state.argtypes = [c.c_void_p, _dp, c.c_double, c.c_double, c.c_double]
     L.bb_engine_method.argtypes = [c.c_void_p]
+    L.bb_engine_gram_mode.argtypes = [c.c_void_p]
     L.bb_engine_enable_timing.argtypes = [c.c_void_p, c.c_int]
     L.bb_engine_reset_timing.argtypes = [c.c_void_p]
     L.bb_engine_kernel_times.argtypes = [c.c_void_p, _dp, _dp, _ip]
@@ -105,6 +109,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_sample_lambda.argtypes = [_dp, _dp, c.c_int, c.c_double, c.c_double, c.c_uint64,
                                    c.c_uint64, c.c_uint64, c.c_uint64, c.c_int]
     L.bb_gram.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_gram_ozaki.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_group_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
     L.bb_group_destroy.argtypes = [c.c_void_p]
@@ -331,15 +336,21 @@ def bench_chol(m, reps=10, trace=False):
     return (f.value, s.value, ts) if trace else (f.value, s.value)
 
 
-def gram(Y, w):
-    """C = Y diag(w) Y' on the device (fp64 MFMA)."""
+def gram(Y, w, mode=GRAM_FP64):
+    """C = Y diag(w) Y' on the device: fp64 MFMA (mode 0) or Ozaki-II int8 MFMA (mode 1,
+    w >= 0)."""
     L = library()
     _require_gpu()
     Y = np.asfortranarray(Y, dtype=np.float64)
     w = np.ascontiguousarray(w, dtype=np.float64)
     n, k = Y.shape
     C = np.zeros((n, n), order="F")
-    _check(L.bb_gram(_p(C), _p(Y), _p(w), n, k), "bb_gram")
+    if mode == GRAM_OZAKI:
+        if np.any(w < 0):
+            raise ValueError("the Ozaki Gram needs w >= 0")
+        _check(L.bb_gram_ozaki(_p(C), _p(Y), _p(w), n, k), "bb_gram_ozaki")
+    else:
+        _check(L.bb_gram(_p(C), _p(Y), _p(w), n, k), "bb_gram")
     return C
 
 
@@ -381,12 +392,15 @@ class EngineConfig:
     seed: int = 0xB4E5B41D6E
     stream: int = 0
     device: int = 0
+    gram_mode: Optional[int] = None  # None: library default (env BB_GRAM_MODE)
 
     def to_c(self) -> bb_config:
         c = bb_config()
         library().bb_config_default(ctypes.byref(c))
         for name, _ in bb_config._fields_:
             v = getattr(self, name)
+            if v is None:
+                continue
             setattr(c, name, int(v) if isinstance(v, bool) else v)
         if c.p_local <= 0:
             c.p_local = c.p
@@ -434,6 +448,9 @@ class Engine:
 
     def method(self) -> int:
         return int(library().bb_engine_method(self._h))
+
+    def gram_mode(self) -> int:
+        return int(library().bb_engine_gram_mode(self._h))
 
     def trace(self, slot0: int, count: int):
         pl = self.p_local

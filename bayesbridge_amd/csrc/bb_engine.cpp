@@ -19,6 +19,7 @@
 
 #include "../../include/bayesbridge.h"
 #include "bb_kernels.h"
+#include "bb_ozaki.h"
 
 using namespace bb;
 
@@ -119,10 +120,12 @@ void next_call_key(uint64_t *k0, uint64_t *k1) {
 // Engine
 // ---------------------------------------------------------------------------
 enum Phase {
-    PH_PRE, PH_SCALARS, PH_LAMBDA, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL, PH_SOLVE,
-    PH_BETA, PH_XB, PH_ALPHA, PH_END, PH_COUNT
+    PH_PRE, PH_SCALARS, PH_LAMBDA, PH_OZPREP, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL,
+    PH_SOLVE, PH_BETA, PH_XB, PH_ALPHA, PH_END, PH_COUNT
 };
-static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "gram", "xu",
+// "gram" times the Gram GEMM kernel alone (k_gram, or k_oz_gemm after "ozprep" = row scales
+// + residues); "reduce" is the split/slab combine (k_slab_sum or the CRT k_oz_crt).
+static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "ozprep", "gram", "xu",
                                             "reduce", "form", "chol", "solve", "beta", "xb",
                                             "alpha", "end"};
 
@@ -147,6 +150,12 @@ struct bb_engine {
     unsigned int *flags = nullptr;
     int S = 1;
     size_t slab_stride = 0;
+    // Ozaki-II Gram (gram_mode 1)
+    int n_oz = 0, oz_b = 0, oz_S = 1;
+    double *oz_xmax = nullptr, *oz_rscale = nullptr;
+    unsigned long long *oz_rowbits = nullptr;
+    int *oz_escale = nullptr;
+    int8_t *oz_R = nullptr, *oz_P = nullptr;
     // chol / ortho
     double *G = nullptr, *cvec = nullptr, *A = nullptr, *Y2 = nullptr, *W2 = nullptr,
            *gdiag = nullptr;
@@ -226,12 +235,26 @@ struct bb_engine {
         if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
-            mark(PH_GRAM);
-            launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
+            if (cfg.gram_mode == 1) {
+                mark(PH_OZPREP);
+                launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowbits, oz_rscale,
+                                oz_escale);
+                launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R);
+                mark(PH_GRAM);
+                launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P);
+            } else {
+                mark(PH_GRAM);
+                launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
+            }
             mark(PH_XU);
             launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
             mark(PH_REDUCE);
-            launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad), red2);
+            if (cfg.gram_mode == 1)
+                launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
+                              xv_chunks(p_pad), red2);
+            else
+                launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
+                                red2);
         } else {
             launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
                           group, lam, nullptr, nullptr, trl, err);
@@ -346,9 +369,23 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     e->tr_alpha = dalloc<double>(e->cap, o);
 
     if (e->method == 2) {
-        e->S = gram_splits_for(n_pad, p_pad);
-        e->slab_stride = (size_t)n_pad * n_pad;
-        e->slabs = dalloc<double>(e->slab_stride * e->S, o);
+        if (c.gram_mode == 1) {
+            e->n_oz = oz_rows(n_pad);
+            const int nkc = p_pad / kOzKC;
+            e->oz_b = oz_bits_for(p_pad);
+            e->oz_S = oz_splits_for(e->n_oz, nkc);
+            e->oz_xmax = dalloc<double>((size_t)nkc * e->n_oz, o);
+            e->oz_rowbits = dalloc<unsigned long long>(e->n_oz, o);
+            e->oz_rscale = dalloc<double>(e->n_oz, o);
+            e->oz_escale = dalloc<int>(e->n_oz, o);
+            e->oz_R = dalloc<int8_t>(oz_residue_bytes(e->n_oz, p_pad), o);
+            e->oz_P = dalloc<int8_t>(oz_partial_bytes(e->n_oz, e->oz_S), o);
+            launch_oz_xmax(e->stream, e->X, n_pad, n_pad, e->n_oz, p_pad, e->oz_xmax);
+        } else {
+            e->S = gram_splits_for(n_pad, p_pad);
+            e->slab_stride = (size_t)n_pad * n_pad;
+            e->slabs = dalloc<double>(e->slab_stride * e->S, o);
+        }
         e->xu_part = dalloc<double>((size_t)xv_chunks(p_pad) * n_pad, o);
         e->red2 = dalloc<double>((size_t)n_pad * n_pad + n_pad, o);
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
@@ -499,6 +536,8 @@ void bb_config_default(bb_config *c) {
     c->true_alpha = 0.5;
     c->trace_capacity = 1;
     c->seed = 0xB4E5B41D6EULL;
+    const char *gm = getenv("BB_GRAM_MODE");
+    c->gram_mode = (gm && strcmp(gm, "ozaki") == 0) ? 1 : 0;
 }
 
 int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
@@ -654,6 +693,7 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
 }
 
 int bb_engine_method(const bb_engine *e) { return e->method; }
+int bb_engine_gram_mode(const bb_engine *e) { return e->cfg.gram_mode; }
 
 int bb_engine_enable_timing(bb_engine *e, int enable) {
     e->timing = enable != 0;
@@ -1043,6 +1083,50 @@ int bb_gram(double *C, const double *Yh, const double *wh, int n, int k) {
         double *red = dalloc<double>(stride + n_pad, owned);
         launch_gram(0, dY, n_pad, dw, n_pad, k_pad, S, sl, n_pad, stride);
         launch_slab_sum(0, sl, S, stride, n_pad, nullptr, 0, red);
+        HIPCHECK(hipGetLastError());
+        std::vector<double> h(stride);
+        HIPCHECK(hipMemcpy(h.data(), red, stride * sizeof(double), hipMemcpyDeviceToHost));
+        for (int c = 0; c < n; ++c)
+            for (int r = 0; r < n; ++r)
+                C[(size_t)r + (size_t)c * n] =
+                    r <= c ? h[(size_t)r + (size_t)c * n_pad] : h[(size_t)c + (size_t)r * n_pad];
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile);
+        const int n_oz = oz_rows(n_pad);
+        const int k_pad = round_up(k, 256);
+        const int nkc = k_pad / kOzKC;
+        double *dY = dalloc<double>((size_t)n_pad * k_pad, owned);
+        double *dw = dalloc<double>(k_pad, owned);
+        HIPCHECK(hipMemcpy2D(dY, (size_t)n_pad * sizeof(double), Yh, (size_t)n * sizeof(double),
+                             (size_t)n * sizeof(double), (size_t)k, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dw, wh, (size_t)k * sizeof(double), hipMemcpyHostToDevice));
+        const int b = oz_bits_for(k_pad);
+        const int S = oz_splits_for(n_oz, nkc);
+        double *xmax = dalloc<double>((size_t)nkc * n_oz, owned);
+        unsigned long long *rowbits = dalloc<unsigned long long>(n_oz, owned);
+        double *rscale = dalloc<double>(n_oz, owned);
+        int *escale = dalloc<int>(n_oz, owned);
+        int8_t *R = dalloc<int8_t>(oz_residue_bytes(n_oz, k_pad), owned);
+        int8_t *P = dalloc<int8_t>(oz_partial_bytes(n_oz, S), owned);
+        const size_t stride = (size_t)n_pad * n_pad;
+        double *red = dalloc<double>(stride + n_pad, owned);
+        launch_oz_xmax(0, dY, n_pad, n_pad, n_oz, k_pad, xmax);
+        launch_oz_scale(0, dw, k_pad, xmax, n_oz, b, rowbits, rscale, escale);
+        launch_oz_residues(0, dY, n_pad, n_pad, n_oz, k_pad, dw, rscale, R);
+        launch_oz_gemm(0, R, n_oz, k_pad, S, P);
+        launch_oz_crt(0, P, S, n_oz, n_pad, escale, nullptr, 0, red);
         HIPCHECK(hipGetLastError());
         std::vector<double> h(stride);
         HIPCHECK(hipMemcpy(h.data(), red, stride * sizeof(double), hipMemcpyDeviceToHost));

@@ -1,0 +1,60 @@
+// Ozaki-II (CRT) fp64-accurate Gram on int8 MFMA.
+//
+// G = X diag(D) X' = Y Y' with Y = X diag(sqrt(D)).  Each row i of Y is scaled by a power of
+// two and rounded to an integer Yh_i with |Yh_ij| <= 2^b (b <= 53, so the rounding is the
+// fp64 rounding of the scaled value, relative to the row's bound).  The exact integer Gram
+// C = Yh Yh' (|C| <= K 2^2b < M/2) is recovered from its residues modulo kOzMods pairwise
+// coprime moduli m_k <= 247:  C mod m_k = (Yh mod m_k)(Yh mod m_k)' mod m_k, each an int8
+// GEMM with exact int32 accumulation on v_mfma_i32_32x32x32_i8.  Garner's mixed-radix
+// reconstruction (balanced digits) gives C exactly as a 128-bit integer, which is rounded
+// once to fp64 and scaled back: G_ik = C_ik 2^(e_i + e_k).
+//
+// Work: kOzMods symmetric int8 GEMMs (lower 256x256 tiles only) = kOzMods/2 full GEMM
+// equivalents at 64x the per-clock rate of the fp64 MFMA Gram, plus one streaming pass over X
+// (read 8 B, write kOzMods B per element).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bb {
+
+constexpr int kOzMods = 16;
+constexpr int kOzT = 256;  // GEMM tile (rows of Y)
+constexpr int kOzKC = 64;  // K bytes per residue chunk
+
+struct OzConsts {
+    int m[kOzMods];
+    double inv_m[kOzMods];
+    float inv_mf[kOzMods];
+    int invP[kOzMods];             // (prod_{i<k} m_i)^-1 mod m_k  (k >= 1)
+    int Pmod[kOzMods][kOzMods];    // Pmod[j][k] = (prod_{i<j} m_i) mod m_k  (j < k)
+    double log2M;
+};
+
+// Host: moduli and Garner constants (computed once).
+const OzConsts &oz_consts();
+// Largest b with K 2^(2b+1) < M (capped at 53): the integer bits per scaled element.
+int oz_bits_for(int K);
+int oz_rows(int n_pad);                    // n_pad rounded up to kOzT
+int oz_splits_for(int n_oz, int nkc);      // K splits of the int8 GEMM
+size_t oz_residue_bytes(int n_oz, int p_pad);
+size_t oz_partial_bytes(int n_oz, int nsplit);
+
+// Setup: xmax[c * n_oz + i] = max_{j in chunk c} |X_ij| (c = 64-column chunk; rows >= n_pad 0).
+void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
+                    double *xmax);
+// Per sweep: row exponents from the bound max_c xmax[c][i] * max_{j in c} sqrt(D_j):
+// rscale[i] = 2^(b - e_i), escale[i] = e_i - b.  rowbits: n_oz words of scratch, zero on
+// entry and left zero.
+void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
+                     int b, unsigned long long *rowbits, double *rscale, int *escale);
+// Residues R[k][c][i][0..63] = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8).
+void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
+                        const double *D, const double *rscale, int8_t *R);
+// P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
+void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P);
+// red2[r + c n_pad] (r <= c < n_pad) = G(r, c); red2[n_pad^2 + r] = sum_q xu_part[q][r].
+void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
+                   const int *escale, const double *xu_part, int nxu, double *red2);
+
+}  // namespace bb

@@ -1,0 +1,529 @@
+// bb_ozaki.hip -- fp64-accurate Woodbury Gram X diag(D) X' on the int8 matrix cores of gfx950
+// (Ozaki scheme II: exact int8 GEMMs modulo pairwise coprime moduli + CRT).  See bb_ozaki.h
+// for the arithmetic; DESIGN.md s5 for the roofline.  Replaces the fp64 MFMA k_gram on the
+// p > n beta step (the reference's Gram is BridgeRegression.cpp:24, X'X, for its p x p path).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "bb_ozaki.h"
+
+namespace bb {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// Host constants.
+// ---------------------------------------------------------------------------
+static const int kMods[kOzMods] = {247, 245, 244, 243, 241, 239, 233, 229,
+                                   227, 223, 211, 199, 197, 193, 191, 181};
+
+static long long inv_mod(long long a, long long m) {
+    long long g = m, x = 0, x1 = 1, a1 = ((a % m) + m) % m;
+    while (a1) {
+        long long q = g / a1, t = g - q * a1;
+        g = a1;
+        a1 = t;
+        t = x - q * x1;
+        x = x1;
+        x1 = t;
+    }
+    return ((x % m) + m) % m;
+}
+
+const OzConsts &oz_consts() {
+    static OzConsts c = [] {
+        OzConsts o{};
+        o.log2M = 0.0;
+        for (int k = 0; k < kOzMods; ++k) {
+            o.m[k] = kMods[k];
+            o.inv_m[k] = 1.0 / kMods[k];
+            o.inv_mf[k] = 1.0f / (float)kMods[k];
+            o.log2M += std::log2((double)kMods[k]);
+            long long P = 1;  // prod_{i<k} m_i mod m_k
+            for (int j = 0; j < k; ++j) {
+                o.Pmod[j][k] = (int)P;
+                P = (P * kMods[j]) % kMods[k];
+            }
+            o.invP[k] = k ? (int)inv_mod(P, kMods[k]) : 1;
+        }
+        return o;
+    }();
+    return c;
+}
+
+int oz_bits_for(int K) {
+    const double l = oz_consts().log2M - 1.0 - std::log2((double)(K > 1 ? K : 1)) - 1e-6;
+    int b = (int)std::floor(l / 2.0);
+    return b > 53 ? 53 : b;
+}
+
+int oz_rows(int n_pad) { return (n_pad + kOzT - 1) / kOzT * kOzT; }
+
+int oz_splits_for(int n_oz, int nkc) {
+    const int nt = n_oz / kOzT;
+    const int tiles = nt * (nt + 1) / 2;
+    // grid = tiles x kOzMods x S workgroups, one per CU at a time: pick the S (power of two,
+    // >= 16 chunks per split) with the best last-round fill over 256 CUs
+    int best = 1;
+    double best_eff = 0.0;
+    for (int S = 1; S <= 64; S *= 2) {
+        if (S > 1 && nkc / S < 16) break;
+        const double wg = (double)tiles * kOzMods * S;
+        const double rounds = std::ceil(wg / 256.0);
+        double eff = wg / (rounds * 256.0);
+        // more splits cost partial traffic; prefer fewer unless clearly fuller
+        if (eff > best_eff + 0.05) {
+            best_eff = eff;
+            best = S;
+        }
+    }
+    return best;
+}
+
+size_t oz_residue_bytes(int n_oz, int p_pad) { return (size_t)kOzMods * n_oz * p_pad; }
+
+size_t oz_partial_bytes(int n_oz, int nsplit) {
+    const int nt = n_oz / kOzT;
+    return (size_t)nsplit * kOzMods * (nt * (nt + 1) / 2) * kOzT * kOzT;
+}
+
+// ---------------------------------------------------------------------------
+// Setup: per-(64-column chunk, row) max |X|.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_oz_xmax(const double *__restrict__ X, int ldx, int n_pad,
+                                                 int n_oz, double *__restrict__ xmax) {
+    const int c = blockIdx.x;
+    const int i = blockIdx.y * 256 + threadIdx.x;
+    double m = 0.0;
+    if (i < n_pad)
+        for (int j = 0; j < kOzKC; ++j) m = fmax(m, fabs(X[(size_t)i + (size_t)(c * kOzKC + j) * ldx]));
+    xmax[(size_t)c * n_oz + i] = m;
+}
+
+void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
+                    double *xmax) {
+    dim3 grid(p_pad / kOzKC, n_oz / 256);
+    k_oz_xmax<<<grid, 256, 0, s>>>(X, ldx, n_pad, n_oz, xmax);
+}
+
+// ---------------------------------------------------------------------------
+// Per sweep: chunk maxima of sqrt(D), then row exponents.
+// ---------------------------------------------------------------------------
+// One wave per (64 rows, 16 chunks): chunk maxima of sqrt(D) by wave reductions, then the
+// lane's row bound over those chunks, folded into rowbits[i] with atomicMax on the bit
+// pattern (non-negative doubles order like their bits; max is order-independent, so the
+// result is deterministic).  k_oz_finalize turns the bound into exponents and re-zeroes it.
+constexpr int kOzBoundChunks = 16;
+
+__global__ __launch_bounds__(64) void k_oz_bound(const double *__restrict__ D, int nkc,
+                                                 const double *__restrict__ xmax, int n_oz,
+                                                 unsigned long long *__restrict__ rowbits) {
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    const int cg = blockIdx.y * kOzBoundChunks;
+    double sdm[kOzBoundChunks];
+#pragma unroll
+    for (int q = 0; q < kOzBoundChunks; ++q) {
+        const int c = cg + q;
+        double v = c < nkc ? sqrt(D[(size_t)c * kOzKC + lane]) : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+        sdm[q] = v;
+    }
+    double m = 0.0;
+#pragma unroll
+    for (int q = 0; q < kOzBoundChunks; ++q) {
+        const int c = cg + q;
+        if (c < nkc) m = fmax(m, xmax[(size_t)c * n_oz + i] * sdm[q]);
+    }
+    if (m > 0.0) atomicMax(&rowbits[i], (unsigned long long)__double_as_longlong(m));
+}
+
+__global__ __launch_bounds__(256) void k_oz_finalize(unsigned long long *__restrict__ rowbits,
+                                                     int n_oz, int b, double *__restrict__ rscale,
+                                                     int *__restrict__ escale) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_oz) return;
+    const double m = __longlong_as_double((long long)rowbits[i]);
+    rowbits[i] = 0ull;
+    int e = 0;
+    if (m > 0.0) (void)frexp(m, &e);  // m < 2^e
+    if (e < -960) e = -960;
+    rscale[i] = ldexp(1.0, b - e);
+    escale[i] = e - b;
+}
+
+void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
+                     int b, unsigned long long *rowbits, double *rscale, int *escale) {
+    const int nkc = p_pad / kOzKC;
+    dim3 grid(n_oz / 64, (nkc + kOzBoundChunks - 1) / kOzBoundChunks);
+    k_oz_bound<<<grid, 64, 0, s>>>(D, nkc, xmax, n_oz, rowbits);
+    k_oz_finalize<<<(n_oz + 255) / 256, 256, 0, s>>>(rowbits, n_oz, b, rscale, escale);
+}
+
+// ---------------------------------------------------------------------------
+// Residues.  Wave = (64 rows, one 64-column chunk); lane = row.  Each lane rounds its 64
+// scaled values once, then emits 64 bytes per modulus: r = v - m rint(v/m) via the
+// 1.5*2^52 magic constant (|v| <= 2^53, m <= 247 => |r| <= 125, int8), the byte taken from
+// the low word of r + magic.  Stores: 64 B per lane, 4 KB contiguous per wave and modulus.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double oz_readlane_d(double v, int lane) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+constexpr int kOzResCols = 32;  // columns per wave (half a chunk): keeps occupancy >= 4
+
+__global__ __launch_bounds__(256) void k_oz_residues(const double *__restrict__ X, int ldx,
+                                                     int n_pad, int n_oz, int nkc,
+                                                     const double *__restrict__ D,
+                                                     const double *__restrict__ rscale,
+                                                     int8_t *__restrict__ R, OzConsts C) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kc = blockIdx.x * 2 + (w >> 1);
+    const int half = w & 1;
+    const int row = blockIdx.y * 64 + lane;
+    if (kc >= nkc) return;
+    const int col0 = kc * kOzKC + half * kOzResCols;
+    const double sdl = sqrt(D[(size_t)col0 + (lane & (kOzResCols - 1))]);
+    const double rs = rscale[row];
+    // rows >= n_pad (tile padding) load a valid row and are zeroed through rs = 0
+    const double rsl = row < n_pad ? rs : 0.0;
+    const double *xp = X + (size_t)min(row, n_pad - 1) + (size_t)col0 * ldx;
+    double v[kOzResCols];
+#pragma unroll
+    for (int j = 0; j < kOzResCols; ++j) v[j] = xp[(size_t)j * ldx];
+#pragma unroll
+    for (int j = 0; j < kOzResCols; ++j) v[j] = rint(v[j] * oz_readlane_d(sdl, j) * rsl);
+    // low 32 bits of each integer x (|x| <= 2^53): x = xh 2^32 + xl, 0 <= xl < 2^32
+    unsigned int xl[kOzResCols];
+#pragma unroll
+    for (int j = 0; j < kOzResCols; ++j) {
+        const double xh = floor(v[j] * 2.3283064365386963e-10);  // 2^-32
+        xl[j] = (unsigned int)__builtin_fma(-xh, 4294967296.0, v[j]);
+    }
+    const double magic = 6755399441055744.0;  // 1.5 * 2^52
+#pragma unroll 1
+    for (int k = 0; k < kOzMods; ++k) {
+        // q = rint(x / m) sits in the low word of fma(x, 1/m, 1.5*2^52) (two's complement);
+        // r = x - q m is the balanced residue (|r| <= 125), and its byte is
+        // (xl + q (256 - m)) mod 256 -- one fp64 FMA and one v_mad_u32_u24 per element
+        const double im = C.inv_m[k];
+        const unsigned int cm = 256u - (unsigned int)C.m[k];
+        int8_t *dst = R + (((size_t)k * nkc + kc) * n_oz + row) * kOzKC + half * kOzResCols;
+#pragma unroll
+        for (int q = 0; q < kOzResCols / 16; ++q) {
+            unsigned int wd[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                unsigned int b4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int j = q * 16 + d * 4 + e;
+                    const unsigned int ql =
+                        (unsigned int)__double_as_longlong(__builtin_fma(v[j], im, magic));
+                    b4[e] = __umul24(ql, cm) + xl[j];
+                }
+                const unsigned int lo = __builtin_amdgcn_perm(b4[1], b4[0], 0x0c0c0400u);
+                const unsigned int hi = __builtin_amdgcn_perm(b4[3], b4[2], 0x0c0c0400u);
+                wd[d] = lo | (hi << 16);
+            }
+            *(v4i *)(dst + q * 16) = (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+        }
+    }
+}
+
+void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
+                        const double *D, const double *rscale, int8_t *R) {
+    const int nkc = p_pad / kOzKC;
+    dim3 grid((nkc + 1) / 2, n_oz / 64);
+    k_oz_residues<<<grid, 256, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts());
+}
+
+// ---------------------------------------------------------------------------
+// int8 GEMM per (modulus, lower tile, K split): C = R_I R_K' (exact int32), stored mod m.
+// 256 threads = 4 waves in 2x2, each wave 128x128 = 4x4 v_mfma_i32_32x32x32_i8 blocks (256
+// accumulator registers; one workgroup per CU).
+// Staging: a 4-stage LDS ring (32 KB per stage: A then B, 256 rows x 64 B each) filled by
+// global_load_lds_dwordx4 three chunks ahead; one wave-instruction moves 16 rows (1 KB,
+// lane-linear in LDS).  The 16-byte unit u of row r is stored at unit u ^ ((r >> 2) & 3)
+// (swizzle applied on the per-lane SOURCE address, undone on the fragment read) so that a
+// ds_read_b128 phase of 16 rows hits 16 distinct bank groups.  Per chunk: counted
+// s_waitcnt vmcnt (two stages stay in flight), raw s_barrier, issue chunk + 3, 16
+// ds_read_b128, 32 MFMAs.
+// Operand lane map: lane l holds row (l & 31), bytes 16 (l >> 5) .. +15 of the 32-byte K
+// step -- A and B use the same K map, so the product is the exact dot product.  C/D map:
+// col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (l >> 5).
+// XCD grouping: block b runs on XCD b % 8; all tiles of one (modulus, split) unit are given
+// to one XCD so that their shared row blocks stay in that XCD's L2.
+// ---------------------------------------------------------------------------
+constexpr int kOzStages = 4;
+constexpr int kOzOpBytes = kOzT * kOzKC;          // 16 KB per operand per stage
+constexpr int kOzStageBytes = 2 * kOzOpBytes;     // 32 KB
+
+__device__ __forceinline__ void oz_glds(const int8_t *src, int8_t *lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                     (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ int oz_swz(int row, int unit) {
+    return row * kOzKC + ((unit ^ ((row >> 2) & 3)) << 4);
+}
+
+__global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R, int n_oz,
+                                                    int nkc, int nsplit, int8_t *__restrict__ P,
+                                                    OzConsts C) {
+    __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int u = xcd + 8 * (q / ntiles);
+    const int tile = q % ntiles;
+    const int mod = u % kOzMods;
+    const int split = u / kOzMods;
+    if (split >= nsplit) return;
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int K = tile - I * (I + 1) / 2;
+    const int per = (nkc + nsplit - 1) / nsplit;
+    const int c0 = split * per;
+    const int nch = max(0, min(nkc, c0 + per) - c0);
+    const size_t kstride = (size_t)n_oz * kOzKC;
+    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
+    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+
+    // this wave's 4 glds per operand: rows 16 (4 wid + i) + (lane >> 2), stored unit lane & 3
+    int srcoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 16 * (4 * wid + i) + (lane >> 2);
+        srcoff[i] = row * kOzKC + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
+    }
+    auto issue = [&](int kc, int stage) {
+        int8_t *sb = smem + stage * kOzStageBytes;
+        const int8_t *ga = baseA + (size_t)kc * kstride;
+        const int8_t *gb = baseB + (size_t)kc * kstride;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) oz_glds(ga + srcoff[i], sb + (4 * wid + i) * 1024);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) oz_glds(gb + srcoff[i], sb + kOzOpBytes + (4 * wid + i) * 1024);
+    };
+
+    v16i acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+    auto wait_chunk = [&](int rem) {  // rem = chunks issued beyond the awaited one (<= 2)
+        if (rem >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else if (rem == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto read_frags = [&](int chunk, v4i (&fa)[2][4], v4i (&fb)[2][4]) {
+        const int8_t *A_ = smem + (chunk % kOzStages) * kOzStageBytes;
+        const int8_t *B_ = A_ + kOzOpBytes;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int un = ks * 2 + (lane >> 5);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                fa[ks][i] = *(const v4i *)&A_[oz_swz(wr * 128 + i * 32 + (lane & 31), un)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                fb[ks][j] = *(const v4i *)&B_[oz_swz(wc * 128 + j * 32 + (lane & 31), un)];
+        }
+    };
+    auto mfmas = [&](v4i (&fa)[2][4], v4i (&fb)[2][4]) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ks][i], fb[ks][j],
+                                                                      acc[i][j], 0, 0, 0);
+    };
+    // One step: (my reads of chunk `it` are done) -> chunk it+1 landed for every wave and
+    // chunk it's stage free -> refill that stage with chunk it+4 -> request chunk it+1's
+    // fragments -> MFMAs of chunk it from registers, overlapping those LDS reads.
+    auto step = [&](int it, v4i (&fa_c)[2][4], v4i (&fb_c)[2][4], v4i (&fa_n)[2][4],
+                    v4i (&fb_n)[2][4]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (it + 1 < nch) wait_chunk(min(2, nch - 2 - it));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + kOzStages < nch) issue(c0 + it + kOzStages, (it + kOzStages) % kOzStages);
+        if (it + 1 < nch) read_frags(it + 1, fa_n, fb_n);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(fa_c, fb_c);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    v4i fa0[2][4], fb0[2][4], fa1[2][4], fb1[2][4];
+    if (nch > 0) {
+#pragma unroll
+        for (int st = 0; st < kOzStages - 1; ++st)
+            if (st < nch) issue(c0 + st, st);
+        wait_chunk(min(2, nch - 1));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kOzStages - 1 < nch) issue(c0 + kOzStages - 1, kOzStages - 1);
+        read_frags(0, fa0, fb0);
+    }
+    int it = 0;
+    for (; it + 1 < nch; it += 2) {
+        step(it, fa0, fb0, fa1, fb1);
+        step(it + 1, fa1, fb1, fa0, fb0);
+    }
+    if (it < nch) step(it, fa0, fb0, fa1, fb1);
+    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
+    const int m = C.m[mod];
+    const double im = C.inv_m[mod];
+    const int hi = m / 2, lo = hi - m + 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rowl = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int col = wc * 128 + j * 32 + (lane & 31);
+                const int cval = acc[i][j][r];
+                int rr = cval - (int)rint((double)cval * im) * m;
+                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
+                out[rowl * kOzT + col] = (int8_t)rr;
+            }
+}
+
+void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P) {
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int nkc = p_pad / kOzKC;
+    // kOzMods * nsplit units, a multiple of 8 (kOzMods = 16): unit u -> XCD u % 8
+    k_oz_gemm<<<ntiles * kOzMods * nsplit, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, oz_consts());
+}
+
+// ---------------------------------------------------------------------------
+// CRT: per lower-triangle element, sum the split residues, Garner (balanced digits) ->
+// exact 128-bit C -> fp64 -> scale; written to red2 as the upper triangle of a column-major
+// n_pad x n_pad matrix (the layout k_form_m reads).  Extra threads sum the X u partials.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int oz_smod(int v, int m, float imf) {
+    int r = v - (int)rintf((float)v * imf) * m;
+    const int hi = m / 2, lo = hi - m + 1;
+    r = r > hi ? r - m : r;
+    r = r < lo ? r + m : r;
+    return r;
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, int nsplit, int nt,
+                                                int n_pad, const int *__restrict__ escale,
+                                                const double *__restrict__ xu_part, int nxu,
+                                                double *__restrict__ red2, OzConsts C) {
+    const int ntiles = nt * (nt + 1) / 2;
+    const long nquad = (long)ntiles * kOzT * kOzT / 4;
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= nquad) {
+        const long r = gid - nquad;
+        if (r < n_pad) {
+            double v = 0.0;
+            for (int q = 0; q < nxu; ++q) v += xu_part[(size_t)q * n_pad + r];
+            red2[(size_t)n_pad * n_pad + r] = v;
+        }
+        return;
+    }
+    const int tile = (int)(gid >> 14);
+    const int e0 = (int)(gid & 16383) * 4;  // 4 consecutive columns of one tile row
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int K = tile - I * (I + 1) / 2;
+    const int gi = I * kOzT + (e0 >> 8), gk0 = K * kOzT + (e0 & 255);
+    if (gi < gk0 || gi >= n_pad) return;
+    // residue sums of the 4 elements for every modulus
+    int rs[kOzMods][4];
+#pragma unroll
+    for (int k = 0; k < kOzMods; ++k) {
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        const int nsp = NS > 0 ? NS : nsplit;
+#pragma unroll
+        for (int sp = 0; sp < (NS > 0 ? NS : 1); ++sp) {
+            const int w = *(const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
+                                                 (size_t)(kOzT * kOzT) + e0);
+            s0 += (int)(int8_t)(w & 0xff);
+            s1 += (int)(int8_t)((w >> 8) & 0xff);
+            s2 += (int)(int8_t)((w >> 16) & 0xff);
+            s3 += w >> 24;
+        }
+        for (int sp = (NS > 0 ? NS : 1); sp < nsp; ++sp) {
+            const int w = *(const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
+                                                 (size_t)(kOzT * kOzT) + e0);
+            s0 += (int)(int8_t)(w & 0xff);
+            s1 += (int)(int8_t)((w >> 8) & 0xff);
+            s2 += (int)(int8_t)((w >> 16) & 0xff);
+            s3 += w >> 24;
+        }
+        rs[k][0] = s0;
+        rs[k][1] = s1;
+        rs[k][2] = s2;
+        rs[k][3] = s3;
+    }
+    const int ei = escale[gi];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int gk = gk0 + q;
+        if (gk > gi) break;
+        int a[kOzMods];
+#pragma unroll
+        for (int k = 0; k < kOzMods; ++k) {
+            const int r = oz_smod(rs[k][q], C.m[k], C.inv_mf[k]);
+            if (k == 0) {
+                a[0] = r;
+            } else {
+                int acc = 0;
+#pragma unroll
+                for (int j = 0; j < k; ++j) acc += a[j] * C.Pmod[j][k];
+                const int sk = oz_smod(acc, C.m[k], C.inv_mf[k]);
+                a[k] = oz_smod((r - sk) * C.invP[k], C.m[k], C.inv_mf[k]);
+            }
+        }
+        __int128 X = a[kOzMods - 1];
+#pragma unroll
+        for (int k = kOzMods - 2; k >= 0; --k) X = X * (__int128)C.m[k] + (__int128)a[k];
+        const bool neg = X < 0;
+        if (neg) X = -X;
+        const unsigned long long hi = (unsigned long long)(X >> 64);
+        const unsigned long long lo = (unsigned long long)X;
+        double v = __builtin_fma((double)hi, 18446744073709551616.0, (double)lo);
+        v = neg ? -v : v;
+        red2[(size_t)gk + (size_t)gi * n_pad] = ldexp(v, ei + escale[gk]);
+    }
+}
+
+void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
+                   const int *escale, const double *xu_part, int nxu, double *red2) {
+    const int nt = n_oz / kOzT;
+    const long ntot = (long)(nt * (nt + 1) / 2) * kOzT * kOzT / 4 + n_pad;
+    const unsigned g = (unsigned)((ntot + 255) / 256);
+    const OzConsts &C = oz_consts();
+    switch (nsplit) {
+        case 1: k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C); break;
+        case 2: k_oz_crt<2><<<g, 256, 0, s>>>(P, 2, nt, n_pad, escale, xu_part, nxu, red2, C); break;
+        case 4: k_oz_crt<4><<<g, 256, 0, s>>>(P, 4, nt, n_pad, escale, xu_part, nxu, red2, C); break;
+        default:
+            k_oz_crt<0><<<g, 256, 0, s>>>(P, nsplit, nt, n_pad, escale, xu_part, nxu, red2, C);
+    }
+}
+
+}  // namespace bb

@@ -7,6 +7,9 @@ Workload (BASELINE.json metric): Gaussian bridge regression, n=2000, p=50000, al
 are sharded across one process per GPU with one RCCL all-reduce per exchange step
 (strong scaling: the total problem is fixed).
 
+Defaults follow SURVEY.md 8(d): M = 1000 timed sweeps after B = 100 burn-in sweeps, every
+timed sweep recording beta / lambda / sig2 / tau into the device-resident trace.
+
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
   roofline     -- the fp64 MFMA Gram kernel (dominant kernel): algorithmic flops per
                   launch / average launch duration from HIP events on the engine stream
@@ -28,6 +31,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (spec)
+# dense int8 MFMA: 2048 ops/clk/SIMD (v_mfma_i32_32x32x32_i8 = 32 cycles) x 1024 SIMDs x 2.4 GHz
+INT8_MFMA_PEAK_TOPS = 2048 * 1024 * 2.4e9 / 1e12
 DATA_SEED = 20240501
 
 
@@ -92,7 +97,7 @@ def cpu_baseline(n, p, alpha, sweeps, log_every=True):
     return per, threads
 
 
-def pmc_traffic(n, p, world):
+def pmc_traffic(n, p, world, kernel):
     """HBM bytes per k_gram launch from the newest committed PMC summary of this workload
     (profiles/rNN_pmc.json, written by tools/profile_round.sh + tools/profile_summary.py:
     separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 read correction).  None if absent or
@@ -106,21 +111,26 @@ def pmc_traffic(n, p, world):
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        if w.get("n") == n and w.get("p") == p and world == 1 and "k_gram" in d:
-            best = (d["k_gram"]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+        gk = d.get("gram_kernels", {})
+        if w.get("n") == n and w.get("p") == p and world == 1 and kernel in gk:
+            best = (gk[kernel]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
     return best
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # M = 1000 timed sweeps after B = 100 burn-in sweeps
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--rows", type=int, default=2000)
     ap.add_argument("--cols", type=int, default=50000)
     ap.add_argument("--alpha", type=float, default=0.5)
     ap.add_argument("--cpu-sweeps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
+                    help="Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
+                         "BB_GRAM_MODE, else the library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,8 +165,11 @@ def main():
     X = make_columns(n, j0, j1)
     y, _ = make_problem_y(n, p)
     cfg = bb.EngineConfig(n=n, p=p, p_local=p_loc, j0=j0, rank=rank, world=world,
-                          true_alpha=alpha, method=2, trace_capacity=1, seed=0xB4E5B41D6E,
-                          stream=0, device=device)
+                          true_alpha=alpha, method=2,
+                          trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
+                          stream=0, device=device,
+                          gram_mode=None if args.gram is None else
+                          (bb.GRAM_OZAKI if args.gram == "ozaki" else bb.GRAM_FP64))
     eng = bb.Engine(cfg, X, y)
     del X
     force_rccl = os.environ.get("BB_FORCE_RCCL", "0") == "1"
@@ -186,7 +199,9 @@ def main():
     eng.enable_timing(True)
     eng.reset_timing()
     t0 = time.perf_counter()
-    eng.run(t, args.steps, first_slot=-1)
+    # the timed loop records every sweep's beta / lambda / sig2 / tau into the device trace
+    # ring, as the reference's MCMC loop writes its output slots (BridgeWrapper.cpp:287-298)
+    eng.run(t, args.steps, first_slot=0)
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -204,11 +219,23 @@ def main():
 
     value = args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-    # algorithmic fp64 flops of one Gram launch on this rank: n(n+1) p_local
+    # Dominant kernel = the Gram GEMM.  fp64 path: algorithmic fp64 flops of one k_gram
+    # launch on this rank, n(n+1) p_local.  Ozaki path: algorithmic int8 ops of
+    # one k_oz_gemm launch, kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
+    gram_mode = eng.gram_mode()
     gram_flops = float(n) * (n + 1) * p_loc
-    achieved = gram_flops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+    if gram_mode == bb.GRAM_OZAKI:
+        kernel_ops = 16.0 * n * (n + 1) * p_loc
+        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm (v_mfma_i32_32x32x32_i8)"
+    else:
+        kernel_ops = gram_flops
+        peak, unit, kname = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", "k_gram (v_mfma_f64_16x16x4_f64)"
+    achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
+    fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
 
-    traffic = pmc_traffic(n, p, world)
+    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm" if gram_mode == bb.GRAM_OZAKI
+                          else "bb::k_gram")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sweeps > 0:
@@ -237,18 +264,22 @@ def main():
                        "rccl": bool(world > 1 or force_rccl),
                        "n": n, "p": p, "alpha": alpha,
                        "beta_step": "woodbury (exact, p > n)",
+                       "gram": ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
+                                else "fp64 mfma"),
                        "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
                                                                   if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": "k_gram (v_mfma_f64_16x16x4_f64)",
-                         "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+            "roofline": {"bound": "mfma", "kernel": kname,
+                         "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
                          "traffic_source": traffic[1] if traffic else None,
                          "algorithmic_bytes_per_launch": 8.0 * n * p_loc,
                          "gram_ms_avg": gram_ms,
                          "sweep_ms_avg_events": sweep_ms,
-                         "flops_per_launch": gram_flops},
+                         "ops_per_launch": kernel_ops,
+                         "gram_fp64_equivalent_tflops": fp64_equiv,
+                         "gram_total_ms": gram_total_ms},
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},
             "cpu_baseline": cpu,
             "setup_s": setup_s,

@@ -107,6 +107,8 @@ typedef struct bb_config {
     int trace_capacity; /* number of trace slots kept on device (>= 1) */
     uint64_t seed, stream;
     int device;
+    int gram_mode;      /* Woodbury Gram: 0 fp64 MFMA, 1 Ozaki-II on int8 MFMA (fp64-accurate);
+                           the default is taken from env BB_GRAM_MODE ("fp64"/"ozaki") */
 } bb_config;
 
 void bb_config_default(bb_config *cfg);
@@ -171,6 +173,8 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
 
 /* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho. */
 int bb_engine_method(const bb_engine *e);
+/* Gram implementation in use on the Woodbury path: 0 fp64 MFMA, 1 Ozaki-II int8. */
+int bb_engine_gram_mode(const bb_engine *e);
 
 /* Per-kernel timing: milliseconds of the last sweep's Gram kernel and of the
  * whole last sweep, measured with HIP events on the engine's stream. */
@@ -214,6 +218,10 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
 /* Gram C = Y diag(w) Y' (Y: n x k column-major) via the fp64 MFMA kernel;
  * C is n x n column-major, full symmetric result. */
 int bb_gram(double *C, const double *Y, const double *w, int n, int k);
+
+/* The same Gram through the Ozaki-II int8 path (w >= 0): exact integer Gram of the
+ * row-scaled, fp64-rounded Y diag(sqrt(w)), rounded once to fp64. */
+int bb_gram_ozaki(double *C, const double *Y, const double *w, int n, int k);
 
 /* SPD solve via the blocked device Cholesky: A (m x m, column-major, only the
  * upper triangle read) -> x = A^-1 b for nrhs right-hand sides (m x nrhs). */

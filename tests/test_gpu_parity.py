@@ -112,6 +112,39 @@ def test_gram_mfma_layout_asymmetric(gpu_lib):
     assert np.array_equal(bb.gram(Y, w), (Y * w) @ Y.T)
 
 
+def test_gram_ozaki_exact_on_integers(gpu_lib):
+    """Integer Y, square-integer w: the Ozaki-II Gram is exact (every scaled input
+    sqrt(w_j) Y_ij is an integer times a power of two, the CRT recovers the exact integer product), so it must equal the int64
+    product bit for bit -- this also pins the int8 MFMA operand and C/D lane maps, the tile
+    decode and the split-K / XCD grouping (n not a multiple of the 256 tile, ragged k)."""
+    bb = gpu_lib
+    rng = np.random.default_rng(17)
+    for n, k in [(300, 1000), (77, 5000), (600, 333)]:
+        Yi = rng.integers(-60, 61, size=(n, k))
+        wi = rng.choice([0, 1, 4, 9], size=k)  # perfect squares: sqrt(w) Y stays integral
+        ref = (Yi * wi) @ Yi.T
+        C = bb.gram(Yi.astype(np.float64), wi.astype(np.float64), mode=bb.GRAM_OZAKI)
+        assert np.array_equal(C, ref.astype(np.float64)), (n, k)
+
+
+@pytest.mark.parametrize("n,k", [(200, 3000), (450, 700)])
+def test_gram_ozaki_fp64_accuracy(gpu_lib, n, k):
+    """Random Y and weights over 10 decades (like D = tau^2/lambda): the Ozaki Gram's error
+    against an 80-bit long-double reference, relative to (|Y| w |Y|')_ik, is at fp64 level and
+    no worse than 4x the fp64 MFMA Gram's."""
+    bb = gpu_lib
+    rng = np.random.default_rng(n * 7 + k)
+    Y = rng.standard_normal((n, k))
+    w = 10.0 ** rng.uniform(-8, 2, k)
+    Yl = Y.astype(np.longdouble)
+    ref = (Yl * w.astype(np.longdouble)) @ Yl.T
+    scale = (np.abs(Y) * w) @ np.abs(Y).T
+    e_oz = np.max(np.abs(bb.gram(Y, w, mode=bb.GRAM_OZAKI) - ref) / scale)
+    e_64 = np.max(np.abs(bb.gram(Y, w) - ref) / scale)
+    assert e_oz < 2e-15, (e_oz, e_64)
+    assert e_oz < 4 * max(e_64, 1e-16), (e_oz, e_64)
+
+
 @pytest.mark.parametrize("m,nrhs", [(20, 1), (64, 2), (130, 1), (700, 2)])
 def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
     bb = gpu_lib
@@ -187,9 +220,10 @@ def test_chain_ortho_matches_oracle(gpu_lib):
     compare_chain(g, o)
 
 
+@pytest.mark.parametrize("gram_mode", [0, 1], ids=["fp64", "ozaki"])
 @pytest.mark.parametrize("n,p,kw", [(60, 250, {}), (100, 160, dict(true_sig2=1.0)),
                                      (200, 1000, {})])
-def test_chain_wide_p_woodbury_teacher_forced(gpu_lib, n, p, kw):
+def test_chain_wide_p_woodbury_teacher_forced(gpu_lib, n, p, kw, gram_mode):
     """p > n: every GPU sweep starts from the oracle's previous state (teacher forcing).
 
     Free-running p > n chains are chaotic under fp64 roundoff -- the CPU oracle decouples
@@ -203,7 +237,7 @@ def test_chain_wide_p_woodbury_teacher_forced(gpu_lib, n, p, kw):
     o = gibbs.bridge_regression_stable(y, X, 40, burn=0, seed=seed, stream=stream,
                                        method="woodbury", record_state=True, **kw)
     cfg = bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, method=2, trace_capacity=1,
-                          true_sig2=kw.get("true_sig2", 0.0))
+                          true_sig2=kw.get("true_sig2", 0.0), gram_mode=gram_mode)
     e = bb.Engine(cfg, X, y)
     e.init_state()
     st = o["states"]
@@ -268,12 +302,13 @@ def teacher_forced_sweep(X, y, beta, tau, sig2, alpha, t, seed, stream, hyper):
     return b, lam, tau, sig2
 
 
+@pytest.mark.parametrize("gram_mode", [0, 1], ids=["fp64", "ozaki"])
 @pytest.mark.parametrize("n,p", [(1000, 5000), (2000, 6000)])
-def test_teacher_forced_sweep_large(gpu_lib, n, p):
+def test_teacher_forced_sweep_large(gpu_lib, n, p, gram_mode):
     """C2-scale and C3-height sweeps from an identical state (one sweep each)."""
     bb = gpu_lib
     X, y, btrue = synthetic_problem(n, p, seed=n + p)
-    cfg = bb.EngineConfig(n=n, p=p, seed=SEED, stream=7, trace_capacity=2)
+    cfg = bb.EngineConfig(n=n, p=p, seed=SEED, stream=7, trace_capacity=2, gram_mode=gram_mode)
     e = bb.Engine(cfg, X, y)
     assert e.method() == 2
     e.init_state()

@@ -85,11 +85,17 @@ def main():
         out["calibration_k_xv"] = {"algorithmic_read_bytes": x_bytes,
                                    "fetch_x1024": 1024 * kx["fetch_kb"],
                                    "ratio_algorithmic_over_fetch": x_bytes / (1024 * kx["fetch_kb"])}
-    if "bb::k_gram" in out["kernels"]:
-        g = out["kernels"]["bb::k_gram"]
-        out["k_gram"] = {"hbm_bytes_per_launch": g["hbm_bytes"],
-                         "algorithmic_bytes_per_launch": x_bytes + 8.0 * p_pad + 8.0 * n_pad ** 2,
-                         "avg_us": g["avg_us"]}
+    # the Gram GEMM kernels: fp64 k_gram reads X (+D) and writes n_pad^2 partials per split;
+    # k_oz_gemm reads the 16 int8 residue planes (16 n_oz p_pad bytes) and writes partials
+    n_oz = -(-n_pad // 256) * 256
+    algo = {"bb::k_gram": x_bytes + 8.0 * p_pad + 8.0 * n_pad ** 2,
+            "bb::k_oz_gemm": 16.0 * n_oz * p_pad}
+    out["gram_kernels"] = {}
+    for k, a in algo.items():
+        if k in out["kernels"]:
+            g = out["kernels"][k]
+            out["gram_kernels"][k] = {"hbm_bytes_per_launch": g["hbm_bytes"],
+                                      "algorithmic_bytes_per_launch": a, "avg_us": g["avg_us"]}
     json.dump(out, open(os.path.join(dst, f"{rnd}_pmc.json"), "w"), indent=1)
     print("\n".join(lines[:16]))
     print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
