@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = [
     "bb_retstable_batch", "bb_sample_lambda", "bb_gram", "bb_chol_solve",
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
-    "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode",
+    "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode", "bb_bench_ozaki",
 ]
 
 
@@ -110,6 +110,7 @@ def library(build: bool = True) -> ctypes.CDLL:
                                    c.c_uint64, c.c_uint64, c.c_uint64, c.c_int]
     L.bb_gram.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_gram_ozaki.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_bench_ozaki.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, _dp]
     L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_group_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
     L.bb_group_destroy.argtypes = [c.c_void_p]
@@ -334,6 +335,15 @@ def bench_chol(m, reps=10, trace=False):
     _check(L.bb_bench_chol(m, reps, ctypes.byref(f), ctypes.byref(s),
                            ts.ctypes.data if trace else None), "bb_bench_chol")
     return (f.value, s.value, ts) if trace else (f.value, s.value)
+
+
+def bench_ozaki(n, k, nsplit=0, dbg=0, reps=10):
+    """Average ms of the Ozaki int8 GEMM kernel alone (random residues)."""
+    L = library()
+    _require_gpu()
+    ms = ctypes.c_double()
+    _check(L.bb_bench_ozaki(n, k, nsplit, dbg, reps, ctypes.byref(ms)), "bb_bench_ozaki")
+    return ms.value
 
 
 def gram(Y, w, mode=GRAM_FP64):

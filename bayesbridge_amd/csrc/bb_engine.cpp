@@ -1142,6 +1142,45 @@ int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
     return rc;
 }
 
+int bb_bench_ozaki(int n, int k, int nsplit, int dbg, int reps, double *ms) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_oz = oz_rows(round_up(n, kGramTile));
+        const int k_pad = round_up(k, 256);
+        const int S = nsplit > 0 ? nsplit : oz_splits_for(n_oz, k_pad / kOzKC);
+        int8_t *R = dalloc<int8_t>(oz_residue_bytes(n_oz, k_pad), owned);
+        int8_t *P = dalloc<int8_t>(oz_partial_bytes(n_oz, S), owned);
+        // random residues in [-120, 120]
+        std::vector<int8_t> h(oz_residue_bytes(n_oz, k_pad));
+        uint64_t st = 0x9E3779B97F4A7C15ULL;
+        for (auto &v : h) {
+            st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+            v = (int8_t)((int)((st >> 33) % 241) - 120);
+        }
+        HIPCHECK(hipMemcpy(R, h.data(), h.size(), hipMemcpyHostToDevice));
+        hipEvent_t e0, e1;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg);
+        HIPCHECK(hipEventRecord(e0, 0));
+        for (int r = 0; r < reps; ++r) launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg);
+        HIPCHECK(hipEventRecord(e1, 0));
+        HIPCHECK(hipEventSynchronize(e1));
+        float t = 0;
+        HIPCHECK(hipEventElapsedTime(&t, e0, e1));
+        *ms = t / reps;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs) {
     std::vector<void *> owned;
     int rc = 0;

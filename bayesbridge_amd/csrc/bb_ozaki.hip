@@ -178,15 +178,18 @@ __device__ __forceinline__ double oz_readlane_d(double v, int lane) {
 
 constexpr int kOzResCols = 32;  // columns per wave (half a chunk): keeps occupancy >= 4
 
-__global__ __launch_bounds__(256) void k_oz_residues(const double *__restrict__ X, int ldx,
+// Workgroup = one 64-column chunk x 256 rows (8 waves: 4 row slices x 2 column halves), so
+// the X reads are 2 KB contiguous per column and each modulus plane is written as one 16 KB
+// contiguous block.
+__global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ X, int ldx,
                                                      int n_pad, int n_oz, int nkc,
                                                      const double *__restrict__ D,
                                                      const double *__restrict__ rscale,
                                                      int8_t *__restrict__ R, OzConsts C) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int kc = blockIdx.x * 2 + (w >> 1);
+    const int kc = blockIdx.x;
     const int half = w & 1;
-    const int row = blockIdx.y * 64 + lane;
+    const int row = blockIdx.y * 256 + (w >> 1) * 64 + lane;
     if (kc >= nkc) return;
     const int col0 = kc * kOzKC + half * kOzResCols;
     const double sdl = sqrt(D[(size_t)col0 + (lane & (kOzResCols - 1))]);
@@ -240,8 +243,8 @@ __global__ __launch_bounds__(256) void k_oz_residues(const double *__restrict__ 
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R) {
     const int nkc = p_pad / kOzKC;
-    dim3 grid((nkc + 1) / 2, n_oz / 64);
-    k_oz_residues<<<grid, 256, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts());
+    dim3 grid(nkc, n_oz / 256);
+    k_oz_residues<<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts());
 }
 
 // ---------------------------------------------------------------------------
@@ -274,6 +277,9 @@ __device__ __forceinline__ int oz_swz(int row, int unit) {
     return row * kOzKC + ((unit ^ ((row >> 2) & 3)) << 4);
 }
 
+// dbg (timing ablations for tools/bench_ozaki.py only; 0 in production): bit 0 skips the
+// in-loop LDS-DMA refills, bit 1 the fragment reads, bit 2 the waits and barrier.
+template <int dbg>
 __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R, int n_oz,
                                                     int nkc, int nsplit, int8_t *__restrict__ P,
                                                     OzConsts C) {
@@ -306,14 +312,15 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
         const int row = 16 * (4 * wid + i) + (lane >> 2);
         srcoff[i] = row * kOzKC + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
     }
+    // glds number g (0..7) of a stage: operand g >> 2, wave-slice g & 3
+    auto glds_one = [&](int kc, int stage, int g) {
+        int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
+        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride;
+        oz_glds(src + srcoff[g & 3], sb + (4 * wid + (g & 3)) * 1024);
+    };
     auto issue = [&](int kc, int stage) {
-        int8_t *sb = smem + stage * kOzStageBytes;
-        const int8_t *ga = baseA + (size_t)kc * kstride;
-        const int8_t *gb = baseB + (size_t)kc * kstride;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) oz_glds(ga + srcoff[i], sb + (4 * wid + i) * 1024);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) oz_glds(gb + srcoff[i], sb + kOzOpBytes + (4 * wid + i) * 1024);
+        for (int g = 0; g < 8; ++g) glds_one(kc, stage, g);
     };
 
     v16i acc[4][4];
@@ -324,60 +331,66 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
 
-    auto wait_chunk = [&](int rem) {  // rem = chunks issued beyond the awaited one (<= 2)
-        if (rem >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if (rem == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    auto frag_a = [&](int chunk, int ks, int i) {
+        const int8_t *A_ = smem + (chunk % kOzStages) * kOzStageBytes;
+        return *(const v4i *)&A_[oz_swz(wr * 128 + i * 32 + (lane & 31), ks * 2 + (lane >> 5))];
+    };
+    auto frag_b = [&](int chunk, int ks, int j) {
+        const int8_t *B_ = smem + (chunk % kOzStages) * kOzStageBytes + kOzOpBytes;
+        return *(const v4i *)&B_[oz_swz(wc * 128 + j * 32 + (lane & 31), ks * 2 + (lane >> 5))];
     };
     auto read_frags = [&](int chunk, v4i (&fa)[2][4], v4i (&fb)[2][4]) {
-        const int8_t *A_ = smem + (chunk % kOzStages) * kOzStageBytes;
-        const int8_t *B_ = A_ + kOzOpBytes;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int un = ks * 2 + (lane >> 5);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                fa[ks][i] = *(const v4i *)&A_[oz_swz(wr * 128 + i * 32 + (lane & 31), un)];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                fb[ks][j] = *(const v4i *)&B_[oz_swz(wc * 128 + j * 32 + (lane & 31), un)];
-        }
-    };
-    auto mfmas = [&](v4i (&fa)[2][4], v4i (&fb)[2][4]) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ks][i], fb[ks][j],
-                                                                      acc[i][j], 0, 0, 0);
+            for (int i = 0; i < 4; ++i) {
+                fa[ks][i] = frag_a(chunk, ks, i);
+                fb[ks][i] = frag_b(chunk, ks, i);
+            }
     };
     // One step: (my reads of chunk `it` are done) -> chunk it+1 landed for every wave and
-    // chunk it's stage free -> refill that stage with chunk it+4 -> request chunk it+1's
-    // fragments -> MFMAs of chunk it from registers, overlapping those LDS reads.
+    // chunk it's stage free -> 8 groups of {4 MFMAs of chunk it from registers, 2 fragment
+    // reads of chunk it+1, 1 LDS-DMA load of chunk it+4 into the freed stage}, pinned by
+    // sched_barrier: one wave per SIMD issues in order, so a block of loads would idle the
+    // matrix pipe.  Past the end the refill re-loads the last chunk into the freed stage
+    // and the extra reads land in dead registers, keeping every step identical (two
+    // stages always in flight at the wait: vmcnt(16)).
     auto step = [&](int it, v4i (&fa_c)[2][4], v4i (&fb_c)[2][4], v4i (&fa_n)[2][4],
                     v4i (&fb_n)[2][4]) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (it + 1 < nch) wait_chunk(min(2, nch - 2 - it));
-        __builtin_amdgcn_s_barrier();
+        if (!(dbg & 4)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
         asm volatile("" ::: "memory");
-        if (it + kOzStages < nch) issue(c0 + it + kOzStages, (it + kOzStages) % kOzStages);
-        if (it + 1 < nch) read_frags(it + 1, fa_n, fb_n);
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(fa_c, fb_c);
-        __builtin_amdgcn_sched_barrier(0);
+        const int kc_next = c0 + min(it + kOzStages, nch - 1);
+        const int st_next = (it + kOzStages) % kOzStages;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const int ks = g >> 2, i = g & 3;
+            acc[i][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][0],
+                                                              acc[i][0], 0, 0, 0);
+            if (!(dbg & 1)) glds_one(kc_next, st_next, g);
+            if (!(dbg & 2)) fa_n[ks][i] = frag_a(it + 1, ks, i);
+            acc[i][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][1],
+                                                              acc[i][1], 0, 0, 0);
+            if (!(dbg & 2)) fb_n[ks][i] = frag_b(it + 1, ks, i);
+            acc[i][2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][2],
+                                                              acc[i][2], 0, 0, 0);
+            acc[i][3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][3],
+                                                              acc[i][3], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     };
 
     v4i fa0[2][4], fb0[2][4], fa1[2][4], fb1[2][4];
     if (nch > 0) {
 #pragma unroll
-        for (int st = 0; st < kOzStages - 1; ++st)
-            if (st < nch) issue(c0 + st, st);
-        wait_chunk(min(2, nch - 1));
+        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kOzStages - 1 < nch) issue(c0 + kOzStages - 1, kOzStages - 1);
+        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
         read_frags(0, fa0, fb0);
     }
     int it = 0;
@@ -386,6 +399,8 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
         step(it + 1, fa1, fb1, fa0, fb0);
     }
     if (it < nch) step(it, fa0, fb0, fa1, fb1);
+    // the refills issued past the end must land before the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
     const int m = C.m[mod];
     const double im = C.inv_m[mod];
@@ -405,12 +420,24 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
             }
 }
 
-void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P) {
+void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
+                    int dbg) {
     const int nt = n_oz / kOzT;
     const int ntiles = nt * (nt + 1) / 2;
     const int nkc = p_pad / kOzKC;
     // kOzMods * nsplit units, a multiple of 8 (kOzMods = 16): unit u -> XCD u % 8
-    k_oz_gemm<<<ntiles * kOzMods * nsplit, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, oz_consts());
+    const unsigned g = ntiles * kOzMods * nsplit;
+    const OzConsts &C = oz_consts();
+    switch (dbg) {
+#define BB_OZ(D)                                                                  \
+    case D:                                                                       \
+        k_oz_gemm<D><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);                \
+        break;
+        BB_OZ(1) BB_OZ(2) BB_OZ(3) BB_OZ(4) BB_OZ(7)
+#undef BB_OZ
+        default:
+            k_oz_gemm<0><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
+    }
 }
 
 // ---------------------------------------------------------------------------

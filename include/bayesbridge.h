@@ -219,6 +219,10 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
  * C is n x n column-major, full symmetric result. */
 int bb_gram(double *C, const double *Y, const double *w, int n, int k);
 
+/* Microbenchmark of the Ozaki int8 GEMM alone on random residues (n x k, nsplit K splits, 0 =
+ * automatic); dbg != 0 selects timing ablations (results then meaningless). */
+int bb_bench_ozaki(int n, int k, int nsplit, int dbg, int reps, double *ms);
+
 /* The same Gram through the Ozaki-II int8 path (w >= 0): exact integer Gram of the
  * row-scaled, fp64-rounded Y diag(sqrt(w)), rounded once to fp64. */
 int bb_gram_ozaki(double *C, const double *Y, const double *w, int n, int k);
