@@ -393,7 +393,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     }
     e->PT = dalloc<double>((size_t)2 * kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
     e->Wd = dalloc<double>((size_t)kNB * (n_pad > p_pad ? n_pad : p_pad), o);
-    e->flags = dalloc<unsigned int>((size_t)(n_pad > p_pad ? n_pad : p_pad) / kNB + 4, o);
+    e->flags = dalloc<unsigned int>(chol_flag_words(n_pad > p_pad ? n_pad : p_pad, 1), o);
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
     const bool small = c.p <= c.n && c.world == 1;
     if (e->method != 2 || small) {
@@ -536,8 +536,9 @@ void bb_config_default(bb_config *c) {
     c->true_alpha = 0.5;
     c->trace_capacity = 1;
     c->seed = 0xB4E5B41D6EULL;
+    // Woodbury Gram: Ozaki-II int8 (fp64-accurate, ~2x faster at C3) unless BB_GRAM_MODE=fp64
     const char *gm = getenv("BB_GRAM_MODE");
-    c->gram_mode = (gm && strcmp(gm, "ozaki") == 0) ? 1 : 0;
+    c->gram_mode = (gm && strcmp(gm, "fp64") == 0) ? 0 : 1;
 }
 
 int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
@@ -1019,7 +1020,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
         HIPCHECK(hipMemcpy(src, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
         double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
-        unsigned int *fl = dalloc<unsigned int>((size_t)m_pad / kNB + 4, owned);
+        unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
         hipEvent_t e0, e1, e2;
@@ -1200,7 +1201,7 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
         double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
-        unsigned int *fl = dalloc<unsigned int>((size_t)m_pad / kNB + 4, owned);
+        unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
         chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);

@@ -87,7 +87,9 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 // forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
 // PT: scratch of 2 x kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
 // kNB x kNB receiving U_kk^-T (used by chol_bsolve).
-// flags: >= m_pad/kNB unsigned ints of scratch (zeroed here for every factorisation).
+// flags: chol_flag_words(m_pad, nrhs_blocks) unsigned ints of scratch (zeroed here for
+// every factorisation).  Env BB_CHOL=steps selects the one-launch-per-block-step variant.
+size_t chol_flag_words(int m_pad, int nrhs_blocks);
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *PT, double *Wd, unsigned int *flags,
                  unsigned long long *trace = nullptr);

@@ -16,6 +16,10 @@
 // reference's chol(U, VInv, 'U') convention (A = U'U).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include "bb_kernels.h"
 #include "bb_sampler.h"
 
@@ -551,9 +555,10 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 // backward solve uses W_kp.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double fast_rcp(double p) {
-    // v_rcp_f64 (~2^-26 accurate) + one Newton step: ~1 ulp for the normal positive pivots
-    double r = __builtin_amdgcn_rcp(p);
-    return r * (2.0 - p * r);
+    // v_rcp_f64 (~2^-26 accurate) + one Newton step in FMA form: ~1 ulp for the normal
+    // positive pivots, two dependent FMAs after the reciprocal
+    const double r = __builtin_amdgcn_rcp(p);
+    return __builtin_fma(r, __builtin_fma(-p, r, 1.0), r);
 }
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -829,8 +834,386 @@ __global__ __launch_bounds__(512) void k_chol_step(double *A, int lda, int kp, i
     CHOL_TS(4);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent dataflow Cholesky (the default): ONE launch factors the whole matrix.
+//   workgroup 0 (the chain) owns the critical path: for k = 0 .. nblk-1 it eliminates the
+//     diagonal block D_k (held in LDS, all updates applied) -> W_k = U_kk^-T, publishes W_k,
+//     then takes the hand-off tiles A_{k,k+1}, A_{k+1,k+1} (updated by their owners through
+//     step k-1), forms U_{k,k+1} = W_k A_{k,k+1} (published: it feeds the updates of step k)
+//     and D_{k+1} = A_{k+1,k+1} - U_{k,k+1}' U_{k,k+1} locally -- no launch boundary and no
+//     flag round trip between two consecutive eliminations;
+//   workgroups 1.. own the other tiles (i <= j, RHS block columns included), taken in
+//     row-major order, round-robin: a tile is loaded into LDS, receives its updates
+//     A_ij -= U_ki' U_kj (k < i; MFMA) as the panels U_k* are published, then either becomes
+//     U_ij = W_i A_ij (published) or, for the hand-off tiles (i,i) / (i,i+1), is written
+//     back and handed to the chain.
+// Every dependency points to an earlier tile row or to the chain at a step <= the tile's
+// row, and each owner takes its tiles in row-major order, so the schedule cannot deadlock
+// with every workgroup resident (grid <= CUs, one 512-thread workgroup per CU).
+// Flags (zeroed per factorisation): fW[k], fP[k][j] (U_kj published), fR[k][0/1] (tile
+// (k,k) / (k,k+1) handed over); agent-scope release/acquire, spins bounded (error bit 16).
+// ---------------------------------------------------------------------------
+struct CholFlags {
+    unsigned int *W, *P, *R;
+    int ncb;
+};
+
+__device__ __forceinline__ void flag_release(unsigned int *f) {
+    // caller: every wave's stores issued; all waves drain them before the barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ void flag_acquire2(const unsigned int *f1, const unsigned int *f2,
+                                              uint32_t *err) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
+               (f2 && __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++spins > (1u << 23)) {
+                atomicOr(err, 16u);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
+// Load tile (row block i, col block j) of column-major A into L[y][x].
+__device__ __forceinline__ void tile_load(double (*L)[65], const double *A, int lda, int i, int j,
+                                          bool upper_only) {
+    for (int e = threadIdx.x; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        const double v = A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda];
+        L[y][x] = (!upper_only || y <= x) ? v : 0.0;
+    }
+}
+
+__device__ __forceinline__ void tile_store(const double (*L)[65], double *A, int lda, int i,
+                                           int j) {
+    for (int e = threadIdx.x; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda] = L[y][x];
+    }
+}
+
+// C[y][x] = sum_s P[s][y] Q[s][x] over 64 s (P'Q), 8 waves x 2 blocks of 16x16 (fp64 MFMA);
+// the lane's results are acc[h][r] at y = by*16 + (lane>>4) + 4r, x = bx*16 + (lane&15).
+__device__ __forceinline__ void mm_tn(const double (*P)[65], const double (*Q)[65], v4d acc[2]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
+        acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kk = 0; kk < 16; ++kk) {
+            const int sr = kk * 4 + (lane >> 4);
+            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(P[sr][by * 16 + (lane & 15)],
+                                                         Q[sr][bx * 16 + (lane & 15)], acc[h],
+                                                         0, 0, 0);
+        }
+    }
+}
+
+#define MM_FOR(h, r, y, x)                                                                  \
+    for (int h = 0; h < 2; ++h)                                                             \
+        for (int r = 0; r < 4; ++r)                                                         \
+            if (const int blk_ = (threadIdx.x >> 6) * 2 + h, y = (blk_ & 3) * 16 +           \
+                                                             ((threadIdx.x & 63) >> 4) + 4 * r, \
+                      x = (blk_ >> 2) * 16 + (threadIdx.x & 15); true)
+
+// Eliminate the SPD diagonal block held (upper triangle, lower zero) in T; on return T[y][x]
+// holds W = U^-T (lower triangular).  Same wave-local 8-pivot scheme as k_chol_step.
+__device__ void diag_eliminate(double (*T)[65], double (*rows)[8][128], double (*rinv)[8],
+                               double *piv, uint32_t *err) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    for (int b = 0; b < 8; ++b) {
+        const int sb = b & 1;
+        if (wid == b) {
+            double invs[8];
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const int c = 8 * b + ci;
+                a[ci][0] = (c0 < c) ? 0.0 : a[ci][0];
+                a[ci][1] = (c0 + 1 < c) ? 0.0 : a[ci][1];
+                const double pv = readlane_d(a[ci][ci & 1], 4 * b + (ci >> 1));
+                const double inv = fast_rcp(pv);
+                invs[ci] = inv;
+                if (lane == 0) piv[c] = pv;
+#pragma unroll
+                for (int i = ci + 1; i < 8; ++i) {
+                    const double li = readlane_d(a[ci][i & 1], 4 * b + (i >> 1)) * inv;
+                    a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
+                    a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci)
+                *(double2 *)&rows[sb][ci][c0] = make_double2(a[ci][0], a[ci][1]);
+            if (lane < 8) {
+                double v = 0.0;
+#pragma unroll
+                for (int ci = 0; ci < 8; ++ci) v = (lane == ci) ? invs[ci] : v;
+                rinv[sb][lane] = v;
+            }
+        }
+        __syncthreads();
+        if (wid > b) {
+            double m[8][8];
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double iv = rinv[sb][ci];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    const double2 t2 = *(const double2 *)&rows[sb][ci][r0 + i];
+                    m[ci][i] = t2.x * iv;
+                    m[ci][i + 1] = t2.y * iv;
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double2 rv = *(const double2 *)&rows[sb][ci][c0];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    a[i][0] = __builtin_fma(-m[ci][i], rv.x, a[i][0]);
+                    a[i][1] = __builtin_fma(-m[ci][i], rv.y, a[i][1]);
+                }
+            }
+        }
+    }
+    // (T was read into registers before the first pivot block's barrier)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pv = piv[r0 + i];
+        if (!(pv > 0.0) && err && lane == 0) atomicOr(err, 8u);
+        const double dinv = 1.0 / sqrt(pv);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int nblk, int ncb,
+                                                         double *Wd, CholFlags F,
+                                                         uint32_t *err,
+                                                         unsigned long long *trace) {
+    __shared__ double T[64][65];  // tile being updated / the chain's diagonal block -> W
+    __shared__ double S[64][65];  // staging: U_ki / the chain's A_{k,k+1} -> U_{k,k+1}
+    __shared__ double Q[64][65];  // staging: U_kj / W_i / the chain's next diagonal block
+    __shared__ __attribute__((aligned(16))) double rows[2][8][128];
+    __shared__ double rinv[2][8];
+    __shared__ double piv[64];
+    const int tid = threadIdx.x;
+    v4d acc[2];
+    if (blockIdx.x == 0) {
+        // ------------------------------ the chain ------------------------------
+        tile_load(T, A, lda, 0, 0, true);
+        __syncthreads();
+#define CHAIN_TS(slot)                                                                  \
+    do {                                                                                \
+        if (trace && tid == 0) trace[k * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();  \
+    } while (0)
+        for (int k = 0; k < nblk; ++k) {
+            CHAIN_TS(0);
+            diag_eliminate(T, rows, rinv, piv, err);
+            CHAIN_TS(1);
+            double *W = Wd + (size_t)k * kNB * kNB;
+            for (int e = tid; e < 64 * 64; e += 512) {  // stores drain behind the next work
+                const int y = e & 63, x = e >> 6;
+                W[(size_t)x * kNB + y] = T[y][x];  // W[y][x], column-major
+            }
+            CHAIN_TS(2);
+            if (k + 1 < nblk) {
+                // hand-off tiles, updated by their owners through step k-1
+                flag_acquire2(&F.R[2 * k + 1], &F.R[2 * (k + 1)], err);
+                CHAIN_TS(3);
+                {
+                    // all 16 loads of the two tiles in flight before the first LDS write
+                    double vs[8], vq[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                        vs[q] = A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda];
+                        vq[q] = A[(size_t)((k + 1) * kNB + y) + (size_t)((k + 1) * kNB + x) * lda];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                        S[y][x] = vs[q];
+                        Q[y][x] = (y <= x) ? vq[q] : 0.0;
+                    }
+                }
+                __syncthreads();
+                CHAIN_TS(4);
+                // U_{k,k+1}[r][x] = sum_s W[r][s] S[s][x]   (W[r][s] = T[r][s])
+                {
+                    const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
+                        acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+                        for (int kk = 0; kk < 16; ++kk) {
+                            const int sr = kk * 4 + (lane >> 4);
+                            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                T[by * 16 + (lane & 15)][sr], S[sr][bx * 16 + (lane & 15)],
+                                acc[h], 0, 0, 0);
+                        }
+                    }
+                }
+                __syncthreads();  // all reads of S (and of W in T) done
+                MM_FOR(h, r, y, x) {
+                    const double v = acc[h][r];
+                    S[y][x] = v;  // U_{k,k+1}
+                    A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda] = v;
+                }
+                __syncthreads();
+                CHAIN_TS(5);
+                // D_{k+1} = A_{k+1,k+1} - U' U  (upper part) -> T
+                mm_tn(S, S, acc);
+                MM_FOR(h, r, y, x) {
+                    T[y][x] = (y <= x) ? Q[y][x] - acc[h][r] : 0.0;
+                }
+                CHAIN_TS(6);
+                // publish W_k and U_{k,k+1} together (their stores have drained meanwhile)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&F.W[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                flag_release(&F.W[k]);
+            }
+            CHAIN_TS(7);
+        }
+#undef CHAIN_TS
+        return;
+    }
+    // ------------------------------ tile owners ------------------------------
+    const int nowner = gridDim.x - 1;
+    int n = blockIdx.x - 1;
+    int ti = 0, tj = 0, base = 0;  // tile (ti, tj) = the n-th tile in row-major order
+    for (;; n += nowner) {
+        while (ti < nblk && n - base >= ncb - ti) {
+            base += ncb - ti;
+            ++ti;
+        }
+        if (ti >= nblk) break;
+        tj = ti + (n - base);
+        const int i = ti, j = tj;
+        if (i == 0 && j == 0) continue;  // the chain starts from A_00 itself
+        const bool diag = (j == i);
+        const bool handoff = diag || (j == i + 1 && j < nblk);
+        const int nupd = diag ? i - 1 : i;  // (i,i): updates 0..i-2, the chain applies i-1
+        tile_load(T, A, lda, i, j, diag);
+        __syncthreads();
+        for (int k = 0; k < nupd; ++k) {
+            flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], err);
+            tile_load(S, A, lda, k, i, false);
+            if (!diag) tile_load(Q, A, lda, k, j, false);
+            __syncthreads();
+            mm_tn(S, diag ? S : Q, acc);
+            MM_FOR(h, r, y, x) {
+                if (!diag || y <= x) T[y][x] -= acc[h][r];
+            }
+            __syncthreads();
+        }
+        if (handoff) {
+            tile_store(T, A, lda, i, j);
+            flag_release(&F.R[2 * i + (diag ? 0 : 1)]);
+            continue;
+        }
+        // U_ij = W_i A_ij
+        flag_acquire2(&F.W[i], nullptr, err);
+        {
+            const double *W = Wd + (size_t)i * kNB * kNB;
+            for (int e = tid; e < 64 * 64; e += 512) {
+                const int y = e & 63, x = e >> 6;
+                Q[y][x] = W[(size_t)x * kNB + y];  // Q[r][s] = W[r][s]
+            }
+        }
+        __syncthreads();
+        {
+            const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
+                acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+                for (int kk = 0; kk < 16; ++kk) {
+                    const int sr = kk * 4 + (lane >> 4);
+                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                        Q[by * 16 + (lane & 15)][sr], T[sr][bx * 16 + (lane & 15)], acc[h], 0,
+                        0, 0);
+                }
+            }
+        }
+        MM_FOR(h, r, y, x) {
+            A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda] = acc[h][r];
+        }
+        flag_release(&F.P[i * F.ncb + j]);
+    }
+}
+
+size_t chol_flag_words(int m_pad, int nrhs_blocks) {
+    const size_t nblk = (size_t)m_pad / kNB, ncb = nblk + nrhs_blocks;
+    return nblk + nblk * ncb + 2 * nblk + 4;
+}
+
+static int chol_mode() {
+    static int m = [] {
+        const char *e = getenv("BB_CHOL");
+        return (e && strcmp(e, "steps") == 0) ? 1 : 0;
+    }();
+    return m;
+}
+
+static int device_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
+
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *PT, double *Wd, unsigned int *flags, unsigned long long *trace) {
+    if (chol_mode() == 0) {
+        const int nblk = m_pad / kNB;
+        const int ncb = nblk + nrhs_blocks;
+        const size_t words = chol_flag_words(m_pad, nrhs_blocks);
+        (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * words, s);
+        CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb};
+        const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
+        const int grid = std::min(device_cus(), 1 + ntiles);
+        k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+        return;
+    }
     const int nblk = m_pad / kNB;
     const int ncb = nblk + nrhs_blocks;
     const int ldpt = ncb * kNB;

@@ -108,7 +108,7 @@ typedef struct bb_config {
     uint64_t seed, stream;
     int device;
     int gram_mode;      /* Woodbury Gram: 0 fp64 MFMA, 1 Ozaki-II on int8 MFMA (fp64-accurate);
-                           the default is taken from env BB_GRAM_MODE ("fp64"/"ozaki") */
+                           default 1, or 0 when env BB_GRAM_MODE=fp64 */
 } bb_config;
 
 void bb_config_default(bb_config *cfg);
