@@ -486,8 +486,10 @@ class Engine:
         _check(library().bb_engine_set_state(self._h, _p(beta), tau, sig2, alpha),
                "bb_engine_set_state")
 
-    def enable_timing(self, on: bool = True):
-        library().bb_engine_enable_timing(self._h, 1 if on else 0)
+    def enable_timing(self, on: bool = True, phases: bool = True):
+        """HIP-event timing on the engine stream: every phase start (phases=True) or only
+        the Gram kernel's bracket (two events per sweep, used inside timed loops)."""
+        library().bb_engine_enable_timing(self._h, (2 if phases else 1) if on else 0)
 
     def reset_timing(self):
         library().bb_engine_reset_timing(self._h)

@@ -167,12 +167,20 @@ struct bb_engine {
     ncclComm_t comm = nullptr;
     // timing: per-sweep event marks at phase starts, on the engine stream
     bool timing = false;
+    int timing_level = 2;  // 1: Gram bracket only, 2: every phase
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::vector<std::pair<int, int>>> sweep_marks;  // (phase, event)
     size_t ev_next = 0;
 
     void mark(int phase) {
         if (!timing) return;
+        // level 1: only the Gram kernel's bracket (start of PH_GRAM and the next mark), so
+        // a timed run carries two events per sweep instead of one per phase
+        if (timing_level == 1) {
+            const bool open = !sweep_marks.back().empty() &&
+                              sweep_marks.back().back().first == PH_GRAM;
+            if (phase != PH_GRAM && !open) return;
+        }
         int e0 = ev();
         HIPCHECK(hipEventRecord(ev_pool[e0], stream));
         sweep_marks.back().push_back({phase, e0});
@@ -239,19 +247,21 @@ struct bb_engine {
                 mark(PH_OZPREP);
                 launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowbits, oz_rscale,
                                 oz_escale);
-                launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R);
+                // the residue pass over X also forms the X u partials
+                launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R, u,
+                                   xu_part);
                 mark(PH_GRAM);
                 launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P);
             } else {
                 mark(PH_GRAM);
                 launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
+                mark(PH_XU);
+                launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
             }
-            mark(PH_XU);
-            launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
             mark(PH_REDUCE);
             if (cfg.gram_mode == 1)
                 launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
-                              xv_chunks(p_pad), red2);
+                              oz_xu_parts(p_pad), red2);
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
                                 red2);
@@ -263,6 +273,7 @@ struct bb_engine {
 
     void phase_c(uint64_t t, int slot, int mcmc_phase) {
         double *trb = slot_ptr(tr_beta, slot, p_loc);
+        bool xb_fused = false;
         if (method == 2) {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
@@ -271,7 +282,15 @@ struct bb_engine {
             mark(PH_SOLVE);
             chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1);
             mark(PH_BETA);
-            launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
+            if (beta_xb_supported(n_pad)) {
+                // beta and the X beta partials of the next sweep in one pass over X
+                launch_beta_woodbury_xb(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb,
+                                        xb_part);
+                nparts = beta_xb_parts(p_loc);
+                xb_fused = true;
+            } else {
+                launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
+            }
         } else if (method == 1) {
             mark(PH_FORM);
             launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
@@ -286,8 +305,11 @@ struct bb_engine {
             mark(PH_BETA);
             launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta, trb);
         }
-        mark(PH_XB);
-        launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
+        if (!xb_fused) {
+            mark(PH_XB);
+            launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
+            nparts = xv_chunks(p_loc);
+        }
         if (!hy.know_alpha) {
             // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
             // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
@@ -358,7 +380,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     e->sc = dalloc<DevScalars>(1, o);
     e->err = dalloc<uint32_t>(4, o);
     e->nparts = xv_chunks(p_pad);
-    e->xb_part = dalloc<double>((size_t)e->nparts * n_pad, o);
+    e->xb_part = dalloc<double>(
+        (size_t)std::max(xv_chunks(p_pad), beta_xb_parts(c.p_local)) * n_pad, o);
     e->nbS = pre_blocks_s(c.p_local);
     e->red1 = dalloc<double>((size_t)e->nbS + n_pad, o);
     e->group = stable_group_for(c.p_local);
@@ -473,6 +496,7 @@ void engine_init_state_local(bb_engine *e) {
     HIPCHECK(hipMemcpyAsync(e->tr_beta, e->beta, (size_t)e->p_loc * sizeof(double),
                             hipMemcpyDeviceToDevice, e->stream));
     launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
+    e->nparts = xv_chunks(e->p_loc);
     launch_record_scalars(e->stream, e->sc, e->tr_tau, e->tr_sig2, e->tr_alpha);
 }
 
@@ -685,6 +709,7 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
         s.alpha = alpha;
         HIPCHECK(hipMemcpy(e->sc, &s, sizeof(s), hipMemcpyHostToDevice));
         launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
+        e->nparts = xv_chunks(e->p_loc);
         HIPCHECK(hipStreamSynchronize(e->stream));
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -698,6 +723,7 @@ int bb_engine_gram_mode(const bb_engine *e) { return e->cfg.gram_mode; }
 
 int bb_engine_enable_timing(bb_engine *e, int enable) {
     e->timing = enable != 0;
+    e->timing_level = enable == 1 ? 1 : 2;
     return 0;
 }
 

@@ -104,6 +104,14 @@ void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, co
                           const double *u, const double *D, const DevScalars *sc, int p_loc,
                           double *beta, double *beta_trace);
 
+// Fused variant for n_pad <= 2048: also writes the X beta partials part[g * n_pad + r]
+// (g < beta_xb_parts(p_loc)) that k_pre sums, so no separate X beta pass is needed.
+int beta_xb_parts(int p_loc);
+bool beta_xb_supported(int n_pad);
+void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,
+                             const double *u, const double *D, const DevScalars *sc, int p_loc,
+                             double *beta, double *beta_trace, double *part);
+
 // Build the 2-RHS backward-solve input [U'^-1 c | z] (chol path).
 void launch_chol_rhs(hipStream_t s, const double *A, int lda, int rhs_col, int p, int p_pad,
                      uint64_t k0, uint64_t k1, uint64_t t, double *Y2);

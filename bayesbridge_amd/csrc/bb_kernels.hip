@@ -1330,6 +1330,105 @@ void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, co
                                                           beta, beta_trace);
 }
 
+// Fused Woodbury beta update + X beta partials (one pass over X instead of two):
+// wave = one column at a time: s = X_j . w (same per-lane order + wave tree as k_beta_wb),
+// beta_j = u_j + D_j s / sig, then the lane's rows accumulate X_j beta_j in registers
+// (rows 2 lane + 128 i, i < NR).  The next column's loads are issued before the current
+// column's reduction.  The workgroup's 8 wave accumulators are summed in wave order through
+// LDS into part[blockIdx.x][row], which k_pre sums next sweep.  NR = n_pad / 128 <= 16.
+template <int NR>
+__global__ __launch_bounds__(512) void k_beta_wb_xb(const double *__restrict__ X, int ldx,
+                                                    int n_pad, const double *__restrict__ w,
+                                                    const double *__restrict__ u,
+                                                    const double *__restrict__ D,
+                                                    const DevScalars *sc, int p_loc,
+                                                    double *__restrict__ beta,
+                                                    double *__restrict__ trace,
+                                                    double *__restrict__ part) {
+    __shared__ double ws[NR * 128];
+    for (int i = threadIdx.x; i < NR * 128; i += 512) ws[i] = w[i];
+    __syncthreads();
+    const double sig = sqrt(sc->sig2);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nw = gridDim.x * 8;
+    double2 acc[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) acc[i] = make_double2(0.0, 0.0);
+    int j = blockIdx.x * 8 + wid;
+    double2 xn[NR];
+    if (j < p_loc) {
+        const double *col = X + (size_t)j * ldx + 2 * lane;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) xn[i] = *(const double2 *)(col + 128 * i);
+    }
+    for (; j < p_loc; j += nw) {
+        double2 x[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) x[i] = xn[i];
+        const int jn = j + nw;
+        if (jn < p_loc) {
+            const double *col = X + (size_t)jn * ldx + 2 * lane;
+#pragma unroll
+            for (int i = 0; i < NR; ++i) xn[i] = *(const double2 *)(col + 128 * i);
+        }
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            s += x[i].x * ws[128 * i + 2 * lane];
+            s += x[i].y * ws[128 * i + 2 * lane + 1];
+        }
+        s = wave_allsum(s);
+        const double b = u[j] + D[j] * s / sig;
+        if (lane == 0) {
+            beta[j] = b;
+            if (trace) trace[j] = b;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            acc[i].x = __builtin_fma(x[i].x, b, acc[i].x);
+            acc[i].y = __builtin_fma(x[i].y, b, acc[i].y);
+        }
+    }
+    // wave-ordered sum of the 8 accumulators (ws is reused as the running sum)
+    __syncthreads();
+    for (int q = 0; q < 8; ++q) {
+        if (wid == q) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                double2 *d = (double2 *)&ws[128 * i + 2 * lane];
+                *d = q == 0 ? acc[i] : make_double2(d->x + acc[i].x, d->y + acc[i].y);
+            }
+        }
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < NR * 128; i += 512)
+        part[(size_t)blockIdx.x * n_pad + i] = ws[i];
+}
+
+int beta_xb_parts(int p_loc) {
+    int g = (p_loc + 31) / 32;
+    return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
+bool beta_xb_supported(int n_pad) { return n_pad % 128 == 0 && n_pad <= 2048; }
+
+void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,
+                             const double *u, const double *D, const DevScalars *sc, int p_loc,
+                             double *beta, double *beta_trace, double *part) {
+    const int g = beta_xb_parts(p_loc);
+    switch (n_pad / 128) {
+#define BXB(NR)                                                                             \
+    case NR:                                                                                \
+        k_beta_wb_xb<NR><<<g, 512, 0, s>>>(X, ldx, n_pad, w, u, D, sc, p_loc, beta, beta_trace, \
+                                           part);                                           \
+        break;
+        BXB(1) BXB(2) BXB(3) BXB(4) BXB(5) BXB(6) BXB(7) BXB(8)
+        BXB(9) BXB(10) BXB(11) BXB(12) BXB(13) BXB(14) BXB(15) BXB(16)
+#undef BXB
+        default: break;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_chol_rhs(const double *A, int lda, int rhs_col, int p,
                                                   int p_pad, Key key, uint64_t t, double *Y2) {
     const int r = blockIdx.x * 256 + threadIdx.x;

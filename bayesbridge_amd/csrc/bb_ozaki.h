@@ -48,9 +48,13 @@ void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz
 // entry and left zero.
 void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
                      int b, unsigned long long *rowbits, double *rscale, int *escale);
-// Residues R[k][c][i][0..63] = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8).
+// Residues R[k][c][i][0..63] = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8).  When u is
+// given, the same pass writes the X.u partials xu_part[g * n_pad + i] (g = 256-column group,
+// oz_xu_parts(p_pad) of them; rows < n_pad).
+int oz_xu_parts(int p_pad);
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
-                        const double *D, const double *rscale, int8_t *R);
+                        const double *D, const double *rscale, int8_t *R,
+                        const double *u = nullptr, double *xu_part = nullptr);
 // P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
                     int dbg = 0);

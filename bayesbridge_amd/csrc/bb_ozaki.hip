@@ -176,75 +176,100 @@ __device__ __forceinline__ double oz_readlane_d(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-constexpr int kOzResCols = 32;  // columns per wave (half a chunk): keeps occupancy >= 4
+constexpr int kOzResCols = 32;   // columns per wave (half a chunk): keeps occupancy >= 4
+constexpr int kOzResChunks = 4;  // 64-column chunks per workgroup (= one kXvCols X.u partial)
 
-// Workgroup = one 64-column chunk x 256 rows (8 waves: 4 row slices x 2 column halves), so
-// the X reads are 2 KB contiguous per column and each modulus plane is written as one 16 KB
-// contiguous block.
+// Workgroup = kOzResChunks 64-column chunks x 256 rows (8 waves: 4 row slices x 2 column
+// halves), so the X reads are 2 KB contiguous per column and each modulus plane is written
+// as one 16 KB contiguous block per chunk.  The same pass over X also forms the X.u partial
+// sums of the Woodbury draw (u = sqrt(D) z): part[g][row] over the 256 columns of group g,
+// summed per lane in column order, then the two column halves -- so the separate X.u pass
+// (k_xv) disappears from the Ozaki sweep.
 __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ X, int ldx,
                                                      int n_pad, int n_oz, int nkc,
                                                      const double *__restrict__ D,
                                                      const double *__restrict__ rscale,
-                                                     int8_t *__restrict__ R, OzConsts C) {
+                                                     int8_t *__restrict__ R, OzConsts C,
+                                                     const double *__restrict__ u,
+                                                     double *__restrict__ xu_part) {
+    __shared__ double xu_half[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int kc = blockIdx.x;
     const int half = w & 1;
     const int row = blockIdx.y * 256 + (w >> 1) * 64 + lane;
-    if (kc >= nkc) return;
-    const int col0 = kc * kOzKC + half * kOzResCols;
-    const double sdl = sqrt(D[(size_t)col0 + (lane & (kOzResCols - 1))]);
     const double rs = rscale[row];
     // rows >= n_pad (tile padding) load a valid row and are zeroed through rs = 0
     const double rsl = row < n_pad ? rs : 0.0;
-    const double *xp = X + (size_t)min(row, n_pad - 1) + (size_t)col0 * ldx;
-    double v[kOzResCols];
+    double xu = 0.0;
+    for (int cc = 0; cc < kOzResChunks; ++cc) {
+        const int kc = blockIdx.x * kOzResChunks + cc;
+        if (kc >= nkc) break;
+        const int col0 = kc * kOzKC + half * kOzResCols;
+        const int cl = col0 + (lane & (kOzResCols - 1));
+        const double sdl = sqrt(D[cl]);
+        const double ul = u ? u[cl] : 0.0;
+        const double *xp = X + (size_t)min(row, n_pad - 1) + (size_t)col0 * ldx;
+        double v[kOzResCols];
 #pragma unroll
-    for (int j = 0; j < kOzResCols; ++j) v[j] = xp[(size_t)j * ldx];
+        for (int j = 0; j < kOzResCols; ++j) v[j] = xp[(size_t)j * ldx];
+        if (u) {
 #pragma unroll
-    for (int j = 0; j < kOzResCols; ++j) v[j] = rint(v[j] * oz_readlane_d(sdl, j) * rsl);
-    // low 32 bits of each integer x (|x| <= 2^53): x = xh 2^32 + xl, 0 <= xl < 2^32
-    unsigned int xl[kOzResCols];
+            for (int j = 0; j < kOzResCols; ++j) xu += v[j] * oz_readlane_d(ul, j);
+        }
 #pragma unroll
-    for (int j = 0; j < kOzResCols; ++j) {
-        const double xh = floor(v[j] * 2.3283064365386963e-10);  // 2^-32
-        xl[j] = (unsigned int)__builtin_fma(-xh, 4294967296.0, v[j]);
-    }
-    const double magic = 6755399441055744.0;  // 1.5 * 2^52
+        for (int j = 0; j < kOzResCols; ++j) v[j] = rint(v[j] * oz_readlane_d(sdl, j) * rsl);
+        // low 32 bits of each integer x (|x| <= 2^53): x = xh 2^32 + xl, 0 <= xl < 2^32
+        unsigned int xl[kOzResCols];
+#pragma unroll
+        for (int j = 0; j < kOzResCols; ++j) {
+            const double xh = floor(v[j] * 2.3283064365386963e-10);  // 2^-32
+            xl[j] = (unsigned int)__builtin_fma(-xh, 4294967296.0, v[j]);
+        }
+        const double magic = 6755399441055744.0;  // 1.5 * 2^52
 #pragma unroll 1
-    for (int k = 0; k < kOzMods; ++k) {
-        // q = rint(x / m) sits in the low word of fma(x, 1/m, 1.5*2^52) (two's complement);
-        // r = x - q m is the balanced residue (|r| <= 125), and its byte is
-        // (xl + q (256 - m)) mod 256 -- one fp64 FMA and one v_mad_u32_u24 per element
-        const double im = C.inv_m[k];
-        const unsigned int cm = 256u - (unsigned int)C.m[k];
-        int8_t *dst = R + (((size_t)k * nkc + kc) * n_oz + row) * kOzKC + half * kOzResCols;
+        for (int k = 0; k < kOzMods; ++k) {
+            // q = rint(x / m) sits in the low word of fma(x, 1/m, 1.5*2^52) (two's
+            // complement); r = x - q m is the balanced residue (|r| <= 125), and its byte is
+            // (xl + q (256 - m)) mod 256 -- one fp64 FMA and one v_mad_u32_u24 per element
+            const double im = C.inv_m[k];
+            const unsigned int cm = 256u - (unsigned int)C.m[k];
+            int8_t *dst = R + (((size_t)k * nkc + kc) * n_oz + row) * kOzKC + half * kOzResCols;
 #pragma unroll
-        for (int q = 0; q < kOzResCols / 16; ++q) {
-            unsigned int wd[4];
+            for (int q = 0; q < kOzResCols / 16; ++q) {
+                unsigned int wd[4];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                unsigned int b4[4];
+                for (int d = 0; d < 4; ++d) {
+                    unsigned int b4[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int j = q * 16 + d * 4 + e;
-                    const unsigned int ql =
-                        (unsigned int)__double_as_longlong(__builtin_fma(v[j], im, magic));
-                    b4[e] = __umul24(ql, cm) + xl[j];
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = q * 16 + d * 4 + e;
+                        const unsigned int ql =
+                            (unsigned int)__double_as_longlong(__builtin_fma(v[j], im, magic));
+                        b4[e] = __umul24(ql, cm) + xl[j];
+                    }
+                    const unsigned int lo = __builtin_amdgcn_perm(b4[1], b4[0], 0x0c0c0400u);
+                    const unsigned int hi = __builtin_amdgcn_perm(b4[3], b4[2], 0x0c0c0400u);
+                    wd[d] = lo | (hi << 16);
                 }
-                const unsigned int lo = __builtin_amdgcn_perm(b4[1], b4[0], 0x0c0c0400u);
-                const unsigned int hi = __builtin_amdgcn_perm(b4[3], b4[2], 0x0c0c0400u);
-                wd[d] = lo | (hi << 16);
+                *(v4i *)(dst + q * 16) = (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
             }
-            *(v4i *)(dst + q * 16) = (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
         }
     }
+    if (!u) return;
+    if (half == 1) xu_half[w >> 1][lane] = xu;
+    __syncthreads();
+    if (half == 0 && row < n_pad)
+        xu_part[(size_t)blockIdx.x * n_pad + row] = xu + xu_half[w >> 1][lane];
 }
 
+int oz_xu_parts(int p_pad) { return (p_pad / kOzKC + kOzResChunks - 1) / kOzResChunks; }
+
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
-                        const double *D, const double *rscale, int8_t *R) {
+                        const double *D, const double *rscale, int8_t *R, const double *u,
+                        double *xu_part) {
     const int nkc = p_pad / kOzKC;
-    dim3 grid(nkc, n_oz / 256);
-    k_oz_residues<<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts());
+    dim3 grid(oz_xu_parts(p_pad), n_oz / 256);
+    k_oz_residues<<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts(), u,
+                                       xu_part);
 }
 
 // ---------------------------------------------------------------------------

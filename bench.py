@@ -196,7 +196,8 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    eng.enable_timing(True)
+    # inside the timed region only the Gram kernel is bracketed by HIP events (two per sweep)
+    eng.enable_timing(True, phases=False)
     eng.reset_timing()
     t0 = time.perf_counter()
     # the timed loop records every sweep's beta / lambda / sig2 / tau into the device trace
@@ -205,13 +206,23 @@ def main():
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    t += args.steps
     if dist:
         dist.barrier()
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    gram_ms, sweep_ms, nsamp = eng.kernel_times()
+    gram_ms, _, nsamp = eng.kernel_times()
+    # per-phase breakdown from a short untimed run with an event at every phase start
+    eng.enable_timing(True, phases=True)
+    eng.reset_timing()
+    nph = max(1, min(args.steps, 20))
+    eng.run(t, nph, first_slot=-1)
+    eng.sync()
+    t += nph
     phases = eng.phase_times()
+    _, sweep_ms, _ = eng.kernel_times()
+    eng.enable_timing(False)
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:

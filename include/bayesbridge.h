@@ -176,8 +176,9 @@ int bb_engine_method(const bb_engine *e);
 /* Gram implementation in use on the Woodbury path: 0 fp64 MFMA, 1 Ozaki-II int8. */
 int bb_engine_gram_mode(const bb_engine *e);
 
-/* Per-kernel timing: milliseconds of the last sweep's Gram kernel and of the
- * whole last sweep, measured with HIP events on the engine's stream. */
+/* Per-kernel timing with HIP events on the engine's stream.  enable: 0 off, 1 only the
+ * Gram kernel is bracketed (two events per sweep, for timed runs), 2 every phase start.
+ * kernel_times: average ms of the Gram kernel and of the event-covered part of a sweep. */
 int bb_engine_enable_timing(bb_engine *e, int enable);
 int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
                            int *samples);
