@@ -327,11 +327,13 @@ def bench_lambda(beta, alpha, tau, group, noinline=1, reps=20):
 def bench_chol(m, reps=10, trace=False):
     """(factor ms, solve ms[, stamps]) of the blocked device Cholesky on an m x m SPD test
     matrix; with trace=True also the (steps, 8) s_memrealtime stamps (100 MHz ticks) of one
-    traced factorisation (see bb_bench_chol in include/bayesbridge.h)."""
+    traced factorisation (see bb_bench_chol in include/bayesbridge.h), followed by the same
+    points in shader clocks (s_memtime), then the elimination's 8 producer-group start and 8
+    end stamps (100 MHz): shape (steps + 1, 32); the last row holds owner stamps."""
     L = library()
     _require_gpu()
     f, s = ctypes.c_double(), ctypes.c_double()
-    ts = np.zeros((-(-m // 64), 8), dtype=np.uint64) if trace else None
+    ts = np.zeros((-(-m // 64) + 1, 32), dtype=np.uint64) if trace else None
     _check(L.bb_bench_chol(m, reps, ctypes.byref(f), ctypes.byref(s),
                            ts.ctypes.data if trace else None), "bb_bench_chol")
     return (f.value, s.value, ts) if trace else (f.value, s.value)

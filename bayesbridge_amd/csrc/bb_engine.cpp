@@ -1073,7 +1073,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
         *ms_factor = tf / reps;
         *ms_solve = ts / reps;
         if (trace) {
-            const size_t nts = (size_t)8 * (m_pad / kNB);
+            const size_t nts = (size_t)32 * (m_pad / kNB + 1);
             unsigned long long *dt = dalloc<unsigned long long>(nts, owned);
             HIPCHECK(hipMemset(dt, 0, nts * sizeof(unsigned long long)));
             HIPCHECK(hipMemcpy(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice));

@@ -620,12 +620,16 @@ __device__ __forceinline__ void tile_update_lds(double (*T)[65], int ib, int jb,
     }
 }
 
-// Diagnostic timestamps (s_memrealtime, 100 MHz) of the step's critical path, written only
-// when a trace buffer is given (bb_chol_trace): [kp][0..4] workgroup 0 start / tile loaded /
+// Diagnostic timestamps of the step's critical path, written only when a trace buffer is
+// given (bb_bench_chol): [kp][0..7] s_memrealtime (100 MHz), [kp][8..15] the same points in
+// shader clocks (s_memtime).  Slots: [kp][0..4] workgroup 0 start / tile loaded /
 // updated / eliminated / flag released, [kp][5..7] panel workgroup 1 start / acquired / done.
 #define CHOL_TS(slot)                                                                      \
     do {                                                                                    \
-        if (trace && threadIdx.x == 0) trace[kp * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        if (trace && threadIdx.x == 0) {                                                  \
+            trace[kp * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();                     \
+            trace[kp * 32 + 8 + (slot)] = __builtin_amdgcn_s_memtime();                     \
+        }                                                                                   \
     } while (0)
 
 __global__ __launch_bounds__(512) void k_chol_step(double *A, int lda, int kp, int nblk,
@@ -858,15 +862,25 @@ struct CholFlags {
     int ncb;
 };
 
+// Cross-workgroup hand-offs inside the persistent kernel follow the write-through recipe of
+// cdna_hip_programming.md Guideline 16 (R1, "every load sc1"): every handed-off double is
+// stored with an agent-scope relaxed atomic (global_store ... sc1, written through the XCD's
+// L2) and every load of handed-off data is an agent-scope relaxed atomic load (sc1, bypasses
+// the CU's L1), so neither side needs an L2 write-back (buffer_wbl2, ~2-6 us) or an L1
+// invalidate (buffer_inv, ~1.7 us) per hop.  Release = every storing wave drains its stores,
+// barrier, one lane stores the flag (relaxed, agent).
+__device__ __forceinline__ double ld_sc1(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void flag_release(unsigned int *f) {
-    // caller: every wave's stores issued; all waves drain them before the barrier
+    // caller: every wave's sc1 stores issued; each wave drains them before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void flag_acquire2(const unsigned int *f1, const unsigned int *f2,
@@ -875,32 +889,42 @@ __device__ __forceinline__ void flag_acquire2(const unsigned int *f1, const unsi
         unsigned spins = 0;
         while (__hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
                (f2 && __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++spins > (1u << 23)) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 25)) {
                 atomicOr(err, 16u);
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
+    // the payload is read with sc1 loads only: no L1 invalidate, just keep the compiler
+    // from hoisting them above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __syncthreads();
 }
 
-// Load tile (row block i, col block j) of column-major A into L[y][x].
+// Load tile (row block i, col block j) of column-major A into L[y][x] (all 8 sc1 loads of
+// a thread in flight before the first LDS write).
 __device__ __forceinline__ void tile_load(double (*L)[65], const double *A, int lda, int i, int j,
                                           bool upper_only) {
-    for (int e = threadIdx.x; e < 64 * 64; e += 512) {
-        const int y = e & 63, x = e >> 6;
-        const double v = A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda];
-        L[y][x] = (!upper_only || y <= x) ? v : 0.0;
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + q * 512, y = e & 63, x = e >> 6;
+        v[q] = ld_sc1(&A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + q * 512, y = e & 63, x = e >> 6;
+        L[y][x] = (!upper_only || y <= x) ? v[q] : 0.0;
     }
 }
 
 __device__ __forceinline__ void tile_store(const double (*L)[65], double *A, int lda, int i,
                                            int j) {
-    for (int e = threadIdx.x; e < 64 * 64; e += 512) {
-        const int y = e & 63, x = e >> 6;
-        A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda] = L[y][x];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int e = threadIdx.x + q * 512, y = e & 63, x = e >> 6;
+        st_sc1(&A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda], L[y][x]);
     }
 }
 
@@ -929,12 +953,54 @@ __device__ __forceinline__ void mm_tn(const double (*P)[65], const double (*Q)[6
                                                              ((threadIdx.x & 63) >> 4) + 4 * r, \
                       x = (blk_ >> 2) * 16 + (threadIdx.x & 15); true)
 
-// Eliminate the SPD diagonal block held (upper triangle, lower zero) in T; on return T[y][x]
-// holds W = U^-T (lower triangular).  Same wave-local 8-pivot scheme as k_chol_step.
-__device__ void diag_eliminate(double (*T)[65], double (*rows)[8][128], double (*rinv)[8],
-                               double *piv, uint32_t *err) {
+// Eliminate the SPD diagonal block held in T (upper triangle used; the lower part may hold
+// anything finite); on return T[y][x] holds W = U^-T (lower triangular) and piv[] the pivots.
+// Wave w owns rows 8w .. 8w+7 of [A | I] (lane = columns 2l, 2l+1).  Pipelined groups
+// (tools/elim_bench.hip, V6: 9.3 us vs 13.7 us for the barrier-per-group scheme):
+//   the producing wave w factors its 8 rows in-wave (readlane broadcasts with compile-time
+//   lane indices, priority 3) and publishes every pivot row the moment it is final: the
+//   scaled row [A | I] / p into ROWS and the unscaled A part (the multipliers) into MUL, then
+//   bumps an LDS counter;
+//   every later wave applies each published row to its own rows as soon as the counter
+//   passes it (no workgroup barrier between groups), so the next producer starts one
+//   rank-1 update after the previous group's last pivot.
+// The multipliers of a symmetric elimination come from the pivot row's upper part, and the
+// I part of pivot row c is zero beyond column c, so no entry needs masking.
+// ROWS (64 x 128) may alias any LDS except T/MUL; MUL (64 x 64) aliases T (T is read into
+// registers first; W is written back after a barrier).  cnt: an LDS int.
+template <int W>
+__device__ __forceinline__ void elim_produce(double (&a)[8][2], double (*ROWS)[128],
+                                            double (*MUL)[64], double *piv,
+                                            volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(-m, rs0, a[i][0]);
+            a[i][1] = __builtin_fma(-m, rs1, a[i][1]);
+        }
+        if (W < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(rs0, rs1);
+            if (lane < 32) *(double2 *)&MUL[c][c0] = make_double2(a[ci][0], a[ci][1]);
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[128], double *piv,
+                                               int *cnt, uint32_t *err,
+                                               unsigned long long *gts = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int r0 = wid * 8, c0 = lane * 2;
+    double(*MUL)[64] = (double(*)[64]) & T[0][0];
     double a[8][2];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -943,69 +1009,62 @@ __device__ void diag_eliminate(double (*T)[65], double (*rows)[8][128], double (
             const int row = r0 + i, col = c0 + q;
             a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
         }
-    for (int b = 0; b < 8; ++b) {
-        const int sb = b & 1;
-        if (wid == b) {
-            double invs[8];
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const int c = 8 * b + ci;
-                a[ci][0] = (c0 < c) ? 0.0 : a[ci][0];
-                a[ci][1] = (c0 + 1 < c) ? 0.0 : a[ci][1];
-                const double pv = readlane_d(a[ci][ci & 1], 4 * b + (ci >> 1));
-                const double inv = fast_rcp(pv);
-                invs[ci] = inv;
-                if (lane == 0) piv[c] = pv;
-#pragma unroll
-                for (int i = ci + 1; i < 8; ++i) {
-                    const double li = readlane_d(a[ci][i & 1], 4 * b + (i >> 1)) * inv;
-                    a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
-                    a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+    if (tid == 0) *cnt = 0;
+    __syncthreads();  // T is in registers: MUL may overwrite it
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    // ---- apply the pivot rows of the earlier groups as they are published ----
+    // (the counter is read only when the rows already seen are used up, so a wave that
+    // lags applies its backlog without LDS round trips)
+    int avail = 0;
+    for (int c = 0; c < r0; ++c) {
+        if (c >= avail) {
+            for (unsigned spins = 0; (avail = *vc) <= c;) {
+                if (++spins > (1u << 22)) {  // bounded: a broken hand-off flags, never hangs
+                    if (lane == 0 && err) atomicOr(err, 16u);
+                    avail = r0;
+                    break;
                 }
             }
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci)
-                *(double2 *)&rows[sb][ci][c0] = make_double2(a[ci][0], a[ci][1]);
-            if (lane < 8) {
-                double v = 0.0;
-#pragma unroll
-                for (int ci = 0; ci < 8; ++ci) v = (lane == ci) ? invs[ci] : v;
-                rinv[sb][lane] = v;
-            }
+            asm volatile("" ::: "memory");
         }
-        __syncthreads();
-        if (wid > b) {
-            double m[8][8];
+        const double2 v = *(const double2 *)&ROWS[c][c0];
 #pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const double iv = rinv[sb][ci];
-#pragma unroll
-                for (int i = 0; i < 8; i += 2) {
-                    const double2 t2 = *(const double2 *)&rows[sb][ci][r0 + i];
-                    m[ci][i] = t2.x * iv;
-                    m[ci][i + 1] = t2.y * iv;
-                }
-            }
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const double2 rv = *(const double2 *)&rows[sb][ci][c0];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    a[i][0] = __builtin_fma(-m[ci][i], rv.x, a[i][0]);
-                    a[i][1] = __builtin_fma(-m[ci][i], rv.y, a[i][1]);
-                }
-            }
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&MUL[c][r0 + i];
+            a[i][0] = __builtin_fma(-mm.x, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-mm.x, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-mm.y, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-mm.y, v.y, a[i + 1][1]);
         }
     }
-    // (T was read into registers before the first pivot block's barrier)
+    // ---- my group: 8 pivots in-wave (compile-time lane indices) ----
+    if (gts && lane == 0) gts[wid] = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: elim_produce<0>(a, ROWS, MUL, piv, vc); break;
+        case 1: elim_produce<1>(a, ROWS, MUL, piv, vc); break;
+        case 2: elim_produce<2>(a, ROWS, MUL, piv, vc); break;
+        case 3: elim_produce<3>(a, ROWS, MUL, piv, vc); break;
+        case 4: elim_produce<4>(a, ROWS, MUL, piv, vc); break;
+        case 5: elim_produce<5>(a, ROWS, MUL, piv, vc); break;
+        case 6: elim_produce<6>(a, ROWS, MUL, piv, vc); break;
+        default: elim_produce<7>(a, ROWS, MUL, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (gts && lane == 0) gts[8 + wid] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // every wave is done with MUL (= T)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const double pv = piv[r0 + i];
-        if (!(pv > 0.0) && err && lane == 0) atomicOr(err, 8u);
-        const double dinv = 1.0 / sqrt(pv);
+        if (lane == 0 && err && !(pv > 0.0)) atomicOr(err, 8u);
+        // 1/sqrt(p): v_rsq_f64 + two Newton steps (full fp64 accuracy, no IEEE sequences)
+        double r = __builtin_amdgcn_rsq(pv);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
 #pragma unroll
         for (int q = 0; q < 2; ++q)
-            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * r;
     }
     __syncthreads();
 }
@@ -1014,30 +1073,38 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                                                          double *Wd, CholFlags F,
                                                          uint32_t *err,
                                                          unsigned long long *trace) {
-    __shared__ double T[64][65];  // tile being updated / the chain's diagonal block -> W
-    __shared__ double S[64][65];  // staging: U_ki / the chain's A_{k,k+1} -> U_{k,k+1}
-    __shared__ double Q[64][65];  // staging: U_kj / W_i / the chain's next diagonal block
-    __shared__ __attribute__((aligned(16))) double rows[2][8][128];
-    __shared__ double rinv[2][8];
+    // T: tile being updated / the chain's diagonal block -> W; S: staging U_ki / the chain's
+    // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
+    // During the chain's elimination S and Q together hold the published pivot rows.
+    __shared__ __attribute__((aligned(16))) double Lb[3][64][65];
     __shared__ double piv[64];
+    __shared__ int cnt;
+    double(*T)[65] = Lb[0];
+    double(*S)[65] = Lb[1];
+    double(*Q)[65] = Lb[2];
     const int tid = threadIdx.x;
     v4d acc[2];
     if (blockIdx.x == 0) {
         // ------------------------------ the chain ------------------------------
+        const int lane = tid & 63, wid = tid >> 6;
+        double(*ROWS)[128] = (double(*)[128]) & Lb[1][0][0];
         tile_load(T, A, lda, 0, 0, true);
         __syncthreads();
 #define CHAIN_TS(slot)                                                                  \
     do {                                                                                \
-        if (trace && tid == 0) trace[k * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();  \
+        if (trace && tid == 0) {                                                        \
+            trace[k * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();                    \
+            trace[k * 32 + 8 + (slot)] = __builtin_amdgcn_s_memtime();                    \
+        }                                                                               \
     } while (0)
         for (int k = 0; k < nblk; ++k) {
             CHAIN_TS(0);
-            diag_eliminate(T, rows, rinv, piv, err);
+            diag_eliminate(T, ROWS, piv, &cnt, err, trace ? trace + k * 32 + 16 : nullptr);
             CHAIN_TS(1);
             double *W = Wd + (size_t)k * kNB * kNB;
             for (int e = tid; e < 64 * 64; e += 512) {  // stores drain behind the next work
                 const int y = e & 63, x = e >> 6;
-                W[(size_t)x * kNB + y] = T[y][x];  // W[y][x], column-major
+                st_sc1(&W[(size_t)x * kNB + y], T[y][x]);  // W[y][x], column-major
             }
             CHAIN_TS(2);
             if (k + 1 < nblk) {
@@ -1050,54 +1117,78 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const int e = tid + q * 512, y = e & 63, x = e >> 6;
-                        vs[q] = A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda];
-                        vq[q] = A[(size_t)((k + 1) * kNB + y) + (size_t)((k + 1) * kNB + x) * lda];
+                        vs[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda]);
+                        vq[q] = ld_sc1(
+                            &A[(size_t)((k + 1) * kNB + y) + (size_t)((k + 1) * kNB + x) * lda]);
                     }
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const int e = tid + q * 512, y = e & 63, x = e >> 6;
                         S[y][x] = vs[q];
-                        Q[y][x] = (y <= x) ? vq[q] : 0.0;
+                        Q[y][x] = vq[q];
                     }
                 }
                 __syncthreads();
                 CHAIN_TS(4);
-                // U_{k,k+1}[r][x] = sum_s W[r][s] S[s][x]   (W[r][s] = T[r][s])
-                {
-                    const int lane = tid & 63, wid = tid >> 6;
+                // U_{k,k+1}[r][x] = sum_{s <= r} W[r][s] S[s][x]  (W = T lower triangular):
+                // block row by needs K steps 0 .. 4 by + 3 only; wave w takes column block
+                // w >> 1 and the row-block pair {0, 3} or {1, 2} (20 MFMAs per wave)
+                const int ubx = wid >> 1;
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
-                        acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-                        for (int kk = 0; kk < 16; ++kk) {
-                            const int sr = kk * 4 + (lane >> 4);
-                            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                T[by * 16 + (lane & 15)][sr], S[sr][bx * 16 + (lane & 15)],
-                                acc[h], 0, 0, 0);
-                        }
+                for (int h = 0; h < 2; ++h) {
+                    const int by = (wid & 1) ? (h ? 2 : 1) : (h ? 3 : 0);
+                    acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+                    for (int kk = 0; kk < 4 * (by + 1); ++kk) {
+                        const int sr = kk * 4 + (lane >> 4);
+                        acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            T[by * 16 + (lane & 15)][sr], S[sr][ubx * 16 + (lane & 15)], acc[h],
+                            0, 0, 0);
                     }
                 }
                 __syncthreads();  // all reads of S (and of W in T) done
-                MM_FOR(h, r, y, x) {
-                    const double v = acc[h][r];
-                    S[y][x] = v;  // U_{k,k+1}
-                    A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda] = v;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int by = (wid & 1) ? (h ? 2 : 1) : (h ? 3 : 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int y = by * 16 + (lane >> 4) + 4 * r, x = ubx * 16 + (lane & 15);
+                        const double v = acc[h][r];
+                        S[y][x] = v;  // U_{k,k+1}
+                        st_sc1(&A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda], v);
+                    }
                 }
                 __syncthreads();
                 CHAIN_TS(5);
-                // D_{k+1} = A_{k+1,k+1} - U' U  (upper part) -> T
-                mm_tn(S, S, acc);
-                MM_FOR(h, r, y, x) {
-                    T[y][x] = (y <= x) ? Q[y][x] - acc[h][r] : 0.0;
+                // D_{k+1} = A_{k+1,k+1} - U' U on the 10 upper 16x16 blocks (waves 0, 1 take
+                // two); the strictly lower blocks of T are zeroed
+                {
+                    const int nb = wid < 2 ? 2 : 1;
+                    for (int h = 0; h < nb; ++h) {
+                        const int blk = h ? 8 + wid : wid;
+                        // upper blocks in order (0,0) (0,1) (1,1) (0,2) (1,2) (2,2) (0,3) ...
+                        const int bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
+                        const int by = blk - bx * (bx + 1) / 2;
+                        v4d d = (v4d){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+                        for (int kk = 0; kk < 16; ++kk) {
+                            const int sr = kk * 4 + (lane >> 4);
+                            d = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                                S[sr][by * 16 + (lane & 15)], S[sr][bx * 16 + (lane & 15)], d, 0,
+                                0, 0);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int y = by * 16 + (lane >> 4) + 4 * r, x = bx * 16 + (lane & 15);
+                            T[y][x] = (y <= x) ? Q[y][x] - d[r] : 0.0;
+                            if (by != bx) T[x][y] = 0.0;  // the mirrored lower block
+                        }
+                    }
                 }
                 CHAIN_TS(6);
-                // publish W_k and U_{k,k+1} together (their stores have drained meanwhile)
+                // publish W_k and U_{k,k+1} together (their sc1 stores have drained meanwhile)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_store(&F.W[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(&F.P[k * F.ncb + k + 1], 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1126,31 +1217,56 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         const bool diag = (j == i);
         const bool handoff = diag || (j == i + 1 && j < nblk);
         const int nupd = diag ? i - 1 : i;  // (i,i): updates 0..i-2, the chain applies i-1
+        // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1)
+        constexpr int kt = 6;
+        unsigned long long *otr = nullptr;
+        if (trace && nblk > kt + 1) {
+            if (i == kt && j == kt + 1) otr = trace + (size_t)nblk * 32 + 8;
+            if (i == kt - 1 && j == kt + 1) otr = trace + (size_t)nblk * 32;
+        }
+#define OWN_TS(slot)                                                                \
+    do {                                                                            \
+        if (otr && tid == 0) otr[slot] = __builtin_amdgcn_s_memrealtime();          \
+    } while (0)
         tile_load(T, A, lda, i, j, diag);
         __syncthreads();
         for (int k = 0; k < nupd; ++k) {
+            if (k == nupd - 1) OWN_TS(0);
             flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], err);
+            if (k == nupd - 1) OWN_TS(1);
             tile_load(S, A, lda, k, i, false);
             if (!diag) tile_load(Q, A, lda, k, j, false);
             __syncthreads();
+            if (k == nupd - 1) OWN_TS(2);
             mm_tn(S, diag ? S : Q, acc);
             MM_FOR(h, r, y, x) {
                 if (!diag || y <= x) T[y][x] -= acc[h][r];
             }
             __syncthreads();
+            if (k == nupd - 1) OWN_TS(3);
         }
         if (handoff) {
             tile_store(T, A, lda, i, j);
             flag_release(&F.R[2 * i + (diag ? 0 : 1)]);
+            OWN_TS(4);
             continue;
         }
         // U_ij = W_i A_ij
+        OWN_TS(4);
         flag_acquire2(&F.W[i], nullptr, err);
+        OWN_TS(5);
         {
             const double *W = Wd + (size_t)i * kNB * kNB;
-            for (int e = tid; e < 64 * 64; e += 512) {
-                const int y = e & 63, x = e >> 6;
-                Q[y][x] = W[(size_t)x * kNB + y];  // Q[r][s] = W[r][s]
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                v[q] = ld_sc1(&W[(size_t)x * kNB + y]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                Q[y][x] = v[q];  // Q[r][s] = W[r][s]
             }
         }
         __syncthreads();
@@ -1169,10 +1285,13 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 }
             }
         }
+        OWN_TS(6);
         MM_FOR(h, r, y, x) {
-            A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda] = acc[h][r];
+            st_sc1(&A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda], acc[h][r]);
         }
         flag_release(&F.P[i * F.ncb + j]);
+        OWN_TS(7);
+#undef OWN_TS
     }
 }
 

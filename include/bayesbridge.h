@@ -210,9 +210,11 @@ int bb_bench_lambda(const double *beta, int p, double alpha, double tau, int gro
 
 /* Microbenchmark of the blocked Cholesky (m x m SPD test matrix, 1 RHS): average ms of
  * chol_factor and of chol_bsolve over `reps` runs.  If `trace` is not NULL it receives
- * 8 * ceil(m/64) s_memrealtime stamps (100 MHz) of an extra traced factorisation: per block
- * step, the diagonal workgroup's start / tile loaded / tile updated / eliminated / W
- * released, then panel workgroup 1's start / W acquired / done. */
+ * 32 * ceil(m/64) stamps of an extra traced factorisation: per block step, 8 points of the
+ * chain workgroup's critical path (elimination start / done / W stored / hand-off acquired
+ * / tiles loaded / U formed / next diagonal block formed / released) in s_memrealtime ticks
+ * (100 MHz), the same 8 points in shader clocks (s_memtime), then the diagonal
+ * elimination's 8 producer-group starts and 8 ends (s_memrealtime). */
 int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
                   unsigned long long *trace);
 

@@ -1,0 +1,659 @@
+// Microbenchmark (not product code): the Cholesky chain's 64x64 diagonal elimination
+// [A | I] -> (pivots, W = U^-T).  V0 = the barrier-per-8-pivot scheme of k_chol_persistent;
+// V1 = pipelined: the producing wave publishes each pivot row to LDS as soon as it is
+// final and the later waves apply it right away (LDS counter, no workgroup barrier), so the
+// hand-off between 8-row groups costs one rank-1 update instead of a barrier + rank-8.
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/elim_bench tools/elim_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+__device__ __forceinline__ double fast_rcp(double p) {
+    const double r = __builtin_amdgcn_rcp(p);
+    return __builtin_fma(r, __builtin_fma(-p, r, 1.0), r);
+}
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// ---------------- V0 (copy of the product's diag_eliminate) ----------------
+__device__ void elim_v0(double (*T)[65], double (*rows)[8][128], double (*rinv)[8], double *piv) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    for (int b = 0; b < 8; ++b) {
+        const int sb = b & 1;
+        if (wid == b) {
+            double invs[8];
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const int c = 8 * b + ci;
+                a[ci][0] = (c0 < c) ? 0.0 : a[ci][0];
+                a[ci][1] = (c0 + 1 < c) ? 0.0 : a[ci][1];
+                const double pv = readlane_d(a[ci][ci & 1], 4 * b + (ci >> 1));
+                const double inv = fast_rcp(pv);
+                invs[ci] = inv;
+                if (lane == 0) piv[c] = pv;
+#pragma unroll
+                for (int i = ci + 1; i < 8; ++i) {
+                    const double li = readlane_d(a[ci][i & 1], 4 * b + (i >> 1)) * inv;
+                    a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
+                    a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci)
+                *(double2 *)&rows[sb][ci][c0] = make_double2(a[ci][0], a[ci][1]);
+            if (lane < 8) {
+                double v = 0.0;
+#pragma unroll
+                for (int ci = 0; ci < 8; ++ci) v = (lane == ci) ? invs[ci] : v;
+                rinv[sb][lane] = v;
+            }
+        }
+        __syncthreads();
+        if (wid > b) {
+            double m[8][8];
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double iv = rinv[sb][ci];
+#pragma unroll
+                for (int i = 0; i < 8; i += 2) {
+                    const double2 t2 = *(const double2 *)&rows[sb][ci][r0 + i];
+                    m[ci][i] = t2.x * iv;
+                    m[ci][i + 1] = t2.y * iv;
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 8; ++ci) {
+                const double2 rv = *(const double2 *)&rows[sb][ci][c0];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    a[i][0] = __builtin_fma(-m[ci][i], rv.x, a[i][0]);
+                    a[i][1] = __builtin_fma(-m[ci][i], rv.y, a[i][1]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pv = piv[r0 + i];
+        const double dinv = 1.0 / sqrt(pv);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+    }
+    __syncthreads();
+}
+
+// ---------------- V1: pipelined row publication ----------------
+// PUB[c][0..64]: packed pivot row c of [D | I]: D[c][j] at j >= c, I[c][j] at j < c,
+// I[c][c] at 64.  RINV[c] = 1 / pivot c.  *cnt = published rows.
+__device__ unsigned long long g_ts[16];
+template <int SLEEP>
+__device__ void elim_v1(double (*T)[65], double (*PUB)[66], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    const bool dl = lane < 32;          // lane holds D columns c0, c0+1 (else I columns)
+    const int jc = dl ? c0 : c0 - 64;   // column index within its part
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    // ---- consume the pivot rows of the earlier groups ----
+    for (int c = 0; c < r0; ++c) {
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= c) {
+            if (SLEEP) __builtin_amdgcn_s_sleep(SLEEP);
+        }
+        asm volatile("" ::: "memory");
+        const double iv = RINV[c];
+        double v0, v1;
+        {
+            const double2 t = *(const double2 *)&PUB[c][jc];
+            if (dl) {
+                v0 = jc >= c ? t.x : 0.0;
+                v1 = jc + 1 >= c ? t.y : 0.0;
+            } else {
+                const double dg = PUB[c][64];
+                v0 = jc < c ? t.x : (jc == c ? dg : 0.0);
+                v1 = jc + 1 < c ? t.y : (jc + 1 == c ? dg : 0.0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&PUB[c][r0 + i];
+            const double m0 = mm.x * iv, m1 = mm.y * iv;
+            a[i][0] = __builtin_fma(-m0, v0, a[i][0]);
+            a[i][1] = __builtin_fma(-m0, v1, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-m1, v0, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-m1, v1, a[i + 1][1]);
+        }
+    }
+    // ---- my group: 8 pivots in-wave ----
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = r0 + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * wid + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        // the next row first (it carries the chain)
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double li = readlane_d(a[ci][i & 1], 4 * wid + (i >> 1)) * inv;
+            a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
+            a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+        }
+        // publish row c (packed) for the later waves
+        if (wid < 7) {
+            if (dl) {
+                if (jc >= c) PUB[c][jc] = a[ci][0];
+                if (jc + 1 >= c) PUB[c][jc + 1] = a[ci][1];
+            } else {
+                if (jc < c) PUB[c][jc] = a[ci][0];
+                if (jc + 1 < c) PUB[c][jc + 1] = a[ci][1];
+                if (jc == c) PUB[c][64] = a[ci][0];
+                if (jc + 1 == c) PUB[c][64] = a[ci][1];
+            }
+            if (lane == 0) RINV[c] = inv;
+            asm volatile("" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_store(cnt, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pv = readlane_d(a[i][i & 1], 4 * wid + (i >> 1));
+        const double dinv = 1.0 / sqrt(pv);
+        if (!dl) {
+            T[r0 + i][jc] = a[i][0] * dinv;
+            T[r0 + i][jc + 1] = a[i][1] * dinv;
+        }
+    }
+    __syncthreads();
+}
+
+
+// ---------------- V3: pipelined, unpacked rows (one ds_write_b128 per lane per row) ----------------
+__device__ void elim_v3(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    for (int c = 0; c < r0; ++c) {
+        while (*vc <= c) {
+        }
+        asm volatile("" ::: "memory");
+        const double iv = RINV[c];
+        const double2 v = *(const double2 *)&ROWS[c][c0];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[c][r0 + i];
+            const double m0 = mm.x * iv, m1 = mm.y * iv;
+            a[i][0] = __builtin_fma(-m0, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-m0, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-m1, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-m1, v.y, a[i + 1][1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = r0 + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * wid + (ci >> 1));
+        const double inv = fast_rcp(pv);
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double li = readlane_d(a[ci][i & 1], 4 * wid + (i >> 1)) * inv;
+            a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
+            a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
+        }
+        if (wid < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(a[ci][0], a[ci][1]);
+            if (lane == 0) RINV[c] = inv;
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double dinv = 1.0 / sqrt(piv[r0 + i]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+    }
+    __syncthreads();
+}
+
+// ---------------- V4: V3 + compile-time lane indices + pre-scaled pivot row ----------------
+template <int W>
+__device__ __forceinline__ void produce_v4(double (&a)[8][2], double (*ROWS)[128], double *RINV,
+                                          double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(-m, rs0, a[i][0]);
+            a[i][1] = __builtin_fma(-m, rs1, a[i][1]);
+        }
+        if (W < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(a[ci][0], a[ci][1]);
+            if (lane == 0) RINV[c] = inv;
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ void elim_v4(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    for (int c = 0; c < r0; ++c) {
+        while (*vc <= c) {
+        }
+        asm volatile("" ::: "memory");
+        const double iv = RINV[c];
+        const double2 v = *(const double2 *)&ROWS[c][c0];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[c][r0 + i];
+            const double m0 = mm.x * iv, m1 = mm.y * iv;
+            a[i][0] = __builtin_fma(-m0, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-m0, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-m1, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-m1, v.y, a[i + 1][1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v4<0>(a, ROWS, RINV, piv, vc); break;
+        case 1: produce_v4<1>(a, ROWS, RINV, piv, vc); break;
+        case 2: produce_v4<2>(a, ROWS, RINV, piv, vc); break;
+        case 3: produce_v4<3>(a, ROWS, RINV, piv, vc); break;
+        case 4: produce_v4<4>(a, ROWS, RINV, piv, vc); break;
+        case 5: produce_v4<5>(a, ROWS, RINV, piv, vc); break;
+        case 6: produce_v4<6>(a, ROWS, RINV, piv, vc); break;
+        default: produce_v4<7>(a, ROWS, RINV, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double dinv = 1.0 / sqrt(piv[r0 + i]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+    }
+    __syncthreads();
+}
+
+// ---------------- V6: V4 + scaled rows published (ROWS2), consumers need no products ----------------
+template <int W>
+__device__ __forceinline__ void produce_v6(double (&a)[8][2], double (*ROWS)[128], double *RINV,
+                                          double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(-m, rs0, a[i][0]);
+            a[i][1] = __builtin_fma(-m, rs1, a[i][1]);
+        }
+        if (W < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(rs0, rs1);
+            if (lane < 32)
+                *(double2 *)&ROWS[64 + (c >> 1)][(c & 1) * 64 + c0] =
+                    make_double2(a[ci][0], a[ci][1]);
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ void elim_v6(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    for (int c = 0; c < r0; ++c) {
+        while (*vc <= c) {
+        }
+        asm volatile("" ::: "memory");
+        const double2 v = *(const double2 *)&ROWS[c][c0];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[64 + (c >> 1)][(c & 1) * 64 + r0 + i];
+            const double m0 = mm.x, m1 = mm.y;
+            a[i][0] = __builtin_fma(-m0, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-m0, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-m1, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-m1, v.y, a[i + 1][1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v6<0>(a, ROWS, RINV, piv, vc); break;
+        case 1: produce_v6<1>(a, ROWS, RINV, piv, vc); break;
+        case 2: produce_v6<2>(a, ROWS, RINV, piv, vc); break;
+        case 3: produce_v6<3>(a, ROWS, RINV, piv, vc); break;
+        case 4: produce_v6<4>(a, ROWS, RINV, piv, vc); break;
+        case 5: produce_v6<5>(a, ROWS, RINV, piv, vc); break;
+        case 6: produce_v6<6>(a, ROWS, RINV, piv, vc); break;
+        default: produce_v6<7>(a, ROWS, RINV, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double dinv = 1.0 / sqrt(piv[r0 + i]);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
+    }
+    __syncthreads();
+}
+
+// ---------------- V5: D-only elimination (1 column per lane), no W ----------------
+template <int W>
+__device__ __forceinline__ void produce_v5(double (&a)[8], double (*ROWS)[128], double *RINV,
+                                          double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci], c);
+        const double inv = fast_rcp(pv);
+        const double rs = a[ci] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci], 8 * W + i);
+            a[i] = __builtin_fma(-m, rs, a[i]);
+        }
+        if (W < 7) {
+            ROWS[c][lane] = a[ci];
+            ROWS[c][64 + lane] = rs;
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ void elim_v5(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8;
+    double a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = T[r0 + i][lane];
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    for (int c = 0; c < r0; ++c) {
+        while (*vc <= c) {
+        }
+        asm volatile("" ::: "memory");
+        const double v = ROWS[c][64 + lane];  // scaled pivot row
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[c][r0 + i];  // unscaled multipliers
+            a[i] = __builtin_fma(-mm.x, v, a[i]);
+            a[i + 1] = __builtin_fma(-mm.y, v, a[i + 1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v5<0>(a, ROWS, RINV, piv, vc); break;
+        case 1: produce_v5<1>(a, ROWS, RINV, piv, vc); break;
+        case 2: produce_v5<2>(a, ROWS, RINV, piv, vc); break;
+        case 3: produce_v5<3>(a, ROWS, RINV, piv, vc); break;
+        case 4: produce_v5<4>(a, ROWS, RINV, piv, vc); break;
+        case 5: produce_v5<5>(a, ROWS, RINV, piv, vc); break;
+        case 6: produce_v5<6>(a, ROWS, RINV, piv, vc); break;
+        default: produce_v5<7>(a, ROWS, RINV, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+    // U rows (scaled) into T, for reference
+#pragma unroll
+    for (int i = 0; i < 8; ++i) T[r0 + i][lane] = a[i] / sqrt(piv[r0 + i]);
+    __syncthreads();
+}
+template <int V>
+__global__ __launch_bounds__(512) void k_elim(const double *A, double *W, double *P,
+                                              unsigned long long *t, int reps) {
+    __shared__ double T[64][65];
+    __shared__ __attribute__((aligned(16))) double PUB[64][66];
+    __shared__ __attribute__((aligned(16))) double rows[2][8][128];
+    __shared__ double rinv[2][8];
+    __shared__ double RINV[64];
+    __shared__ double piv[64];
+    __shared__ int cnt;
+    __shared__ __attribute__((aligned(16))) double ROWS[96][128];
+    unsigned long long tot = 0;
+    for (int it = 0; it < reps; ++it) {
+        for (int e = threadIdx.x; e < 64 * 64; e += 512) {
+            const int y = e & 63, x = e >> 6;
+            T[y][x] = (y <= x) ? A[y + 64 * x] : 0.0;
+        }
+        __syncthreads();
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        if (V == 0) elim_v0(T, rows, rinv, piv);
+        else if (V == 1) elim_v1<0>(T, PUB, RINV, piv, &cnt);
+        else if (V == 3) elim_v3(T, ROWS, RINV, piv, &cnt);
+        else if (V == 4) elim_v4(T, ROWS, RINV, piv, &cnt);
+        else if (V == 5) elim_v5(T, ROWS, RINV, piv, &cnt);
+        else if (V == 6) elim_v6(T, ROWS, RINV, piv, &cnt);
+        else if (V == 2) elim_v1<1>(T, PUB, RINV, piv, &cnt);
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        tot += t1 - t0;
+    }
+    for (int e = threadIdx.x; e < 64 * 64; e += 512) {
+        const int y = e & 63, x = e >> 6;
+        W[y + 64 * x] = T[y][x];
+    }
+    if (threadIdx.x < 64) P[threadIdx.x] = piv[threadIdx.x];
+    if (threadIdx.x == 0) t[0] = tot;
+}
+
+
+// V6 on block 0 while blocks 1.. spin on a global flag with s_sleep (the persistent
+// Cholesky's idle owners); reports shader cycles and wall (100 MHz) ticks of block 0.
+__global__ __launch_bounds__(512) void k_elim_loaded(const double *A, unsigned int *flag,
+                                                     unsigned long long *t, int reps, int spin) {
+    __shared__ double T[64][65];
+    __shared__ __attribute__((aligned(16))) double ROWS[96][128];
+    __shared__ double RINV[64];
+    __shared__ double piv[64];
+    __shared__ int cnt;
+    if (blockIdx.x > 0) {
+        if (!spin) return;
+        if (threadIdx.x == 0)
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                __builtin_amdgcn_s_sleep(8);
+        __syncthreads();
+        return;
+    }
+    unsigned long long tot = 0, rt = 0;
+    for (int it = 0; it < reps; ++it) {
+        for (int e = threadIdx.x; e < 64 * 64; e += 512) {
+            const int y = e & 63, x = e >> 6;
+            T[y][x] = (y <= x) ? A[y + 64 * x] : 0.0;
+        }
+        __syncthreads();
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+        elim_v6(T, ROWS, RINV, piv, &cnt);
+        tot += __builtin_amdgcn_s_memtime() - t0;
+        rt += __builtin_amdgcn_s_memrealtime() - r0;
+    }
+    if (threadIdx.x == 0) {
+        t[0] = tot;
+        t[1] = rt;
+        __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+int main() {
+    std::vector<double> h(64 * 64);
+    for (int x = 0; x < 64; ++x)
+        for (int y = 0; y < 64; ++y)
+            h[y + 64 * x] = (x == y) ? 64.0 + 0.5 * y : 0.3 * std::sin(0.7 * x + 0.3 * y) + 0.2 * std::cos(0.11 * (x + y));
+    for (int x = 0; x < 64; ++x)
+        for (int y = x + 1; y < 64; ++y) h[y + 64 * x] = h[x + 64 * y];
+    double *dA, *dW, *dP;
+    unsigned long long *dt;
+    hipMalloc(&dA, 64 * 64 * 8);
+    hipMalloc(&dW, 64 * 64 * 8 * 7);
+    hipMalloc(&dP, 64 * 8 * 7);
+    hipMalloc(&dt, 8);
+    hipMemcpy(dA, h.data(), 64 * 64 * 8, hipMemcpyHostToDevice);
+    std::vector<double> W[7], P[7];
+    const int reps = 200;
+    for (int v = 0; v < 7; ++v) {
+        unsigned long long t = 0;
+        for (int rep = 0; rep < 2; ++rep) {
+            if (v == 0) k_elim<0><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 1) k_elim<1><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 2) k_elim<2><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 3) k_elim<3><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 4) k_elim<4><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 5) k_elim<5><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 6) k_elim<6><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
+        }
+        W[v].resize(4096);
+        P[v].resize(64);
+        hipMemcpy(W[v].data(), dW + v * 4096, 4096 * 8, hipMemcpyDeviceToHost);
+        hipMemcpy(P[v].data(), dP + v * 64, 64 * 8, hipMemcpyDeviceToHost);
+        printf("V%d: %.0f cycles per 64x64 elimination (%.2f us at 2.4 GHz), %.0f cycles/pivot\n", v,
+               (double)t / reps, (double)t / reps / 2400.0, (double)t / reps / 64);
+        if (v >= 1) {
+            unsigned long long ts[16];
+            hipMemcpyFromSymbol(ts, HIP_SYMBOL(g_ts), sizeof(ts));
+            for (int w = 0; w < 8; ++w)
+                printf("   wave %d group: start %+6lld  length %5lld  gap from prev end %5lld\n", w,
+                       (long long)(ts[2 * w] - ts[0]), (long long)(ts[2 * w + 1] - ts[2 * w]),
+                       w ? (long long)(ts[2 * w] - ts[2 * w - 1]) : 0ll);
+        }
+    }
+    {
+        unsigned int *fl;
+        unsigned long long *t2, h2[2];
+        hipMalloc(&fl, 4);
+        hipMalloc(&t2, 16);
+        for (int spin = 0; spin < 2; ++spin) {
+            for (int rep = 0; rep < 2; ++rep) {
+                hipMemset(fl, 0, 4);
+                k_elim_loaded<<<256, 512>>>(dA, fl, t2, reps, spin);
+                hipMemcpy(h2, t2, 16, hipMemcpyDeviceToHost);
+            }
+            printf("V6 on block 0 of 256 (others %s): %.0f cycles, %.2f us wall, clock %.0f MHz\n",
+                   spin ? "spinning" : "exited", (double)h2[0] / reps, (double)h2[1] / reps / 100.0,
+                   (double)h2[0] / ((double)h2[1] / 100.0));
+        }
+    }
+    // check: W = U^-T satisfies W A W' = I (lower W)
+    for (int v = 0; v < 7; ++v) {
+        if (v == 5) continue;
+        double err = 0, dw = 0;
+        for (int i = 0; i < 64; ++i)
+            for (int j = 0; j < 64; ++j) {
+                double s = 0;
+                for (int k = 0; k < 64; ++k)
+                    for (int l = 0; l < 64; ++l) s += W[v][i + 64 * k] * h[k + 64 * l] * W[v][j + 64 * l];
+                err = std::fmax(err, std::fabs(s - (i == j ? 1.0 : 0.0)));
+                dw = std::fmax(dw, std::fabs(W[v][i + 64 * j] - W[0][i + 64 * j]));
+            }
+        double dp = 0;
+        for (int i = 0; i < 64; ++i) dp = std::fmax(dp, std::fabs(P[v][i] - P[0][i]) / P[0][i]);
+        printf("V%d: max |W A W' - I| = %.3e, max |W - W_v0| = %.3e, pivots rel diff %.3e\n", v, err,
+               dw, dp);
+    }
+    return 0;
+}
