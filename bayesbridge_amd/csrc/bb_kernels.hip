@@ -374,19 +374,30 @@ __global__ __launch_bounds__(256) void k_pre(const double *part, int nparts, int
         v = block_sum<256>(v, sh);
         if (threadIdx.x == 0) red1[blockIdx.x] = v;
     } else {
-        const int r = (blockIdx.x - nbS) * 256 + threadIdx.x;
-        if (r < n_pad) {
-            double v = 0.0;
-            for (int q = 0; q < nparts; ++q) v += part[(size_t)q * n_pad + r];
-            red1[nbS + r] = v;
+        // 16 rows per workgroup, 16 threads per row each summing every 16th partial, then
+        // the 16 segment sums in segment order (fixed tree; 16x the loads in flight of a
+        // one-thread-per-row loop over up to 256 partials)
+        __shared__ double seg_sum[16][17];
+        const int rl = threadIdx.x & 15, seg = threadIdx.x >> 4;
+        const int r = (blockIdx.x - nbS) * 16 + rl;
+        double v = 0.0;
+        if (r < n_pad)
+            for (int q = seg; q < nparts; q += 16) v += part[(size_t)q * n_pad + r];
+        seg_sum[seg][rl] = v;
+        __syncthreads();
+        if (threadIdx.x < 16 && r < n_pad) {
+            double t = 0.0;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) t += seg_sum[g][rl];
+            red1[nbS + r] = t;
         }
     }
 }
 
 void launch_pre(hipStream_t s, const double *part, int nparts, int n_pad, const double *beta,
                 int p_loc, const DevScalars *sc, double *red1, int nbS) {
-    k_pre<<<nbS + (n_pad + 255) / 256, 256, 0, s>>>(part, nparts, n_pad, beta, p_loc, sc, red1,
-                                                     nbS);
+    k_pre<<<nbS + (n_pad + 15) / 16, 256, 0, s>>>(part, nparts, n_pad, beta, p_loc, sc, red1,
+                                                   nbS);
 }
 
 // tau | beta (BridgeRegression.cpp:453-465) and sig2 | beta (:436-450).
@@ -1401,11 +1412,101 @@ __global__ __launch_bounds__(256) void k_bsolve_step(const double *A, int lda, i
     }
 }
 
+// Backward solve of kBsNB consecutive blocks per launch (kb, kb-1, .., kb-nb+1): every
+// workgroup redundantly runs the short chain w_k = W_k' (y_k - sum_{k' in (k, kb]} U_kk' w_k')
+// (from L2-resident tiles; no inter-workgroup hand-off), workgroup 0 stores the w's, and
+// workgroup i < kb-nb+1 applies y_i -= sum_k U_ik w_k.  nblk/kBsNB launches instead of nblk.
+constexpr int kBsNB = 4;
+
+__global__ __launch_bounds__(256) void k_bsolve_multi(const double *A, int lda, int kb, int nb,
+                                                      int m_pad, const double *__restrict__ Wd,
+                                                      double *Y, double *Wout, int nrhs) {
+    __shared__ double yv[2][kBsNB][64];
+    __shared__ double wv[2][kBsNB][64];
+    __shared__ double part[4][2][64];
+    const int tid = threadIdx.x, x = tid & 63, g = tid >> 6;  // g: 16-row slice
+    for (int e = tid; e < 2 * kBsNB * 64; e += 256) {
+        const int q = e / (kBsNB * 64), sb = (e / 64) % kBsNB;
+        if (q < nrhs && sb < nb) yv[q][sb][e & 63] = Y[(size_t)q * m_pad + (kb - sb) * kNB + (e & 63)];
+    }
+    __syncthreads();
+    for (int sb = 0; sb < nb; ++sb) {
+        const int k = kb - sb;
+        if (sb > 0) {
+            // y_k -= sum_{s' < sb} U_{k, kb-s'} w_{s'}  (thread: row x, column slice g)
+            for (int q = 0; q < nrhs; ++q) {
+                double acc = 0.0;
+                for (int s2 = 0; s2 < sb; ++s2) {
+                    const double *col = A + (size_t)(k * kNB + x) + (size_t)((kb - s2) * kNB) * lda;
+#pragma unroll
+                    for (int cc = 0; cc < 16; ++cc) {
+                        const int c = g * 16 + cc;
+                        acc += col[(size_t)c * lda] * wv[q][s2][c];
+                    }
+                }
+                part[g][q][x] = acc;
+            }
+            __syncthreads();
+            if (tid < 64 * nrhs) {
+                const int q = tid >> 6;
+                yv[q][sb][x] -= ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+            }
+            __syncthreads();
+        }
+        // w[x] = sum_r W[r][x] y[r]; W column-major: column x contiguous in r
+        const double *W = Wd + (size_t)k * kNB * kNB;
+        for (int q = 0; q < nrhs; ++q) {
+            double acc = 0.0;
+            const double *col = W + (size_t)x * kNB + g * 16;
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) acc += col[rr] * yv[q][sb][g * 16 + rr];
+            part[g][q][x] = acc;
+        }
+        __syncthreads();
+        if (tid < 64 * nrhs) {
+            const int q = tid >> 6;
+            wv[q][sb][x] = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+        }
+        __syncthreads();
+    }
+    if (blockIdx.x == 0)
+        for (int e = tid; e < 2 * kBsNB * 64; e += 256) {
+            const int q = e / (kBsNB * 64), sb = (e / 64) % kBsNB;
+            if (q < nrhs && sb < nb)
+                Wout[(size_t)q * m_pad + (kb - sb) * kNB + (e & 63)] = wv[q][sb][e & 63];
+        }
+    const int nrow = kb - nb + 1;  // row blocks still to update
+    if (nrow > 0) {
+        const int ib = blockIdx.x * kNB;
+        for (int q = 0; q < nrhs; ++q) {
+            double acc = 0.0;
+            for (int sb = 0; sb < nb; ++sb) {
+                const double *col = A + (size_t)(ib + x) + (size_t)((kb - sb) * kNB) * lda;
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) {
+                    const int c = g * 16 + cc;
+                    acc += col[(size_t)c * lda] * wv[q][sb][c];
+                }
+            }
+            part[g][q][x] = acc;
+        }
+        __syncthreads();
+        if (tid < 64 * nrhs) {
+            const int q = tid >> 6;
+            const double acc = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+            Y[(size_t)q * m_pad + ib + x] -= acc;
+        }
+    }
+}
+
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
                  double *Y, double *W, int nrhs) {
     const int nblk = m_pad / kNB;
-    for (int k = nblk - 1; k >= 0; --k)
-        k_bsolve_step<<<k > 0 ? k : 1, 256, 0, s>>>(A, lda, k, m_pad, Wd, Y, W, nrhs);
+    for (int kb = nblk - 1; kb >= 0; kb -= kBsNB) {
+        const int nb = std::min(kBsNB, kb + 1);
+        const int nrow = kb - nb + 1;
+        k_bsolve_multi<<<nrow > 0 ? nrow : 1, 256, 0, s>>>(A, lda, kb, nb, m_pad, Wd, Y, W, nrhs);
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -48,7 +48,8 @@ void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz
 // entry and left zero.
 void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
                      int b, unsigned long long *rowbits, double *rscale, int *escale);
-// Residues R[k][c][i][0..63] = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8).  When u is
+// Residues r = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8), plane k, 64-column chunk c,
+// stored as [16-row block][16-byte unit 0..3][row in block][16 B].  When u is
 // given, the same pass writes the X.u partials xu_part[g * n_pad + i] (g = 256-column group,
 // oz_xu_parts(p_pad) of them; rows < n_pad).
 int oz_xu_parts(int p_pad);

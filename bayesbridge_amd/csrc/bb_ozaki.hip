@@ -167,7 +167,8 @@ void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xm
 // Residues.  Wave = (64 rows, one 64-column chunk); lane = row.  Each lane rounds its 64
 // scaled values once, then emits 64 bytes per modulus: r = v - m rint(v/m) via the
 // 1.5*2^52 magic constant (|v| <= 2^53, m <= 247 => |r| <= 125, int8), the byte taken from
-// the low word of r + magic.  Stores: 64 B per lane, 4 KB contiguous per wave and modulus.
+// the low word of r + magic.  Stores: four 16-byte units per lane into the blocked layout
+// (16 consecutive lanes write one contiguous 256 B run), 4 KB per wave and modulus.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double oz_readlane_d(double v, int lane) {
     const long long bits = __double_as_longlong(v);
@@ -232,7 +233,11 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
             // (xl + q (256 - m)) mod 256 -- one fp64 FMA and one v_mad_u32_u24 per element
             const double im = C.inv_m[k];
             const unsigned int cm = 256u - (unsigned int)C.m[k];
-            int8_t *dst = R + (((size_t)k * nkc + kc) * n_oz + row) * kOzKC + half * kOzResCols;
+            // plane (k, kc) is [16-row block][unit 0..3][row in block][16 B]: one store
+            // instruction writes the 64 rows' 16-byte unit as four 256-B runs, and one GEMM
+            // LDS-DMA instruction (16 rows x 4 units) reads one 1 KB block
+            int8_t *dst = R + ((size_t)k * nkc + kc) * n_oz * kOzKC + (size_t)(row >> 4) * 1024 +
+                          (size_t)(row & 15) * 16 + (size_t)(2 * half) * 256;
 #pragma unroll
             for (int q = 0; q < kOzResCols / 16; ++q) {
                 unsigned int wd[4];
@@ -250,7 +255,8 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
                     const unsigned int hi = __builtin_amdgcn_perm(b4[3], b4[2], 0x0c0c0400u);
                     wd[d] = lo | (hi << 16);
                 }
-                *(v4i *)(dst + q * 16) = (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+                *(v4i *)(dst + q * 256) =
+                    (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
             }
         }
     }
@@ -298,8 +304,9 @@ __device__ __forceinline__ void oz_glds(const int8_t *src, int8_t *lds) {
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
 
+// byte offset of (row, 16-byte unit) in a residue tile image: [16-row block][unit][row][16 B]
 __device__ __forceinline__ int oz_swz(int row, int unit) {
-    return row * kOzKC + ((unit ^ ((row >> 2) & 3)) << 4);
+    return (row >> 4) * 1024 + unit * 256 + (row & 15) * 16;
 }
 
 // dbg (timing ablations for tools/bench_ozaki.py only; 0 in production): bit 0 skips the
@@ -325,18 +332,20 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
     const int c0 = split * per;
     const int nch = max(0, min(nkc, c0 + per) - c0);
     const size_t kstride = (size_t)n_oz * kOzKC;
+    // residue plane (mod, chunk) layout: [16-row block][unit 0..3][row in block][16 B]
+    // (k_oz_residues); a 256-row tile is 16 consecutive 1 KB blocks
     const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
     const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 1, wc = wid & 1;
 
     // this wave's 4 glds per operand: rows 16 (4 wid + i) + (lane >> 2), stored unit lane & 3
+    // (one instruction copies the 1 KB block of 16 rows lane-linearly: the LDS image keeps
+    // the global [unit][row][16 B] order, whose 16-row runs make every ds_read_b128 lane
+    // group hit 16 distinct 16-byte bank slots without a swizzle)
     int srcoff[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = 16 * (4 * wid + i) + (lane >> 2);
-        srcoff[i] = row * kOzKC + (((lane & 3) ^ ((row >> 2) & 3)) << 4);
-    }
+    for (int i = 0; i < 4; ++i) srcoff[i] = (4 * wid + i) * 1024 + lane * 16;
     // glds number g (0..7) of a stage: operand g >> 2, wave-slice g & 3
     auto glds_one = [&](int kc, int stage, int g) {
         int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;

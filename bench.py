@@ -245,7 +245,7 @@ def main():
     gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
     fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
 
-    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm" if gram_mode == bb.GRAM_OZAKI
+    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm<0>" if gram_mode == bb.GRAM_OZAKI
                           else "bb::k_gram")
 
     cpu = None
@@ -285,7 +285,8 @@ def main():
                          "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
                          "traffic_source": traffic[1] if traffic else None,
-                         "algorithmic_bytes_per_launch": 8.0 * n * p_loc,
+                         "algorithmic_bytes_per_launch": (16.0 * n * p_loc if gram_mode == bb.GRAM_OZAKI
+                                                          else 8.0 * n * p_loc),
                          "gram_ms_avg": gram_ms,
                          "sweep_ms_avg_events": sweep_ms,
                          "ops_per_launch": kernel_ops,

@@ -5,8 +5,9 @@
 
 FETCH_SIZE / WRITE_SIZE are KB (x1024).  On gfx950 FETCH_SIZE reports 1/2 of the bytes of a
 wide coalesced streaming read (MI355X_MICROARCH.md HBM section), so read bytes are taken as
-2 x FETCH_SIZE x 1024; the k_xv pass, which streams X exactly once with known bytes, is
-reported beside it as an in-run calibration of that factor.
+2 x FETCH_SIZE x 1024; the fused beta pass (k_beta_wb_xb, or k_xv on the fp64-Gram path),
+which streams X exactly once with known bytes, is reported beside it as an in-run
+calibration of that factor.
 Usage: python tools/profile_summary.py r01 [n] [p]
 """
 import csv
@@ -80,16 +81,20 @@ def main():
                              "read_bytes": 2 * 1024 * f_kb, "write_bytes": 1024 * w_kb,
                              "hbm_bytes": 2 * 1024 * f_kb + 1024 * w_kb,
                              "avg_us": avg_us.get(k)}
-    if "bb::k_xv" in out["kernels"]:
-        kx = out["kernels"]["bb::k_xv"]
-        out["calibration_k_xv"] = {"algorithmic_read_bytes": x_bytes,
-                                   "fetch_x1024": 1024 * kx["fetch_kb"],
-                                   "ratio_algorithmic_over_fetch": x_bytes / (1024 * kx["fetch_kb"])}
+    for kname in ("bb::k_beta_wb_xb<16>", "bb::k_xv"):
+        if kname in out["kernels"]:
+            kx = out["kernels"][kname]
+            out["calibration"] = {"kernel": kname, "algorithmic_read_bytes": x_bytes,
+                                  "fetch_x1024": 1024 * kx["fetch_kb"],
+                                  "ratio_algorithmic_over_fetch":
+                                      x_bytes / (1024 * kx["fetch_kb"])}
+            break
     # the Gram GEMM kernels: fp64 k_gram reads X (+D) and writes n_pad^2 partials per split;
     # k_oz_gemm reads the 16 int8 residue planes (16 n_oz p_pad bytes) and writes partials
     n_oz = -(-n_pad // 256) * 256
     algo = {"bb::k_gram": x_bytes + 8.0 * p_pad + 8.0 * n_pad ** 2,
-            "bb::k_oz_gemm": 16.0 * n_oz * p_pad}
+            "bb::k_oz_gemm<0>": 16.0 * n_oz * p_pad,
+            "bb::k_oz_residues": x_bytes + 16.0 * n_oz * p_pad}
     out["gram_kernels"] = {}
     for k, a in algo.items():
         if k in out["kernels"]:
