@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "bb_ozaki.h"
 
@@ -280,6 +281,7 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
 
 // ---------------------------------------------------------------------------
 // int8 GEMM per (modulus, lower tile, K split): C = R_I R_K' (exact int32), stored mod m.
+// (32x32x32 form; production runs k_oz_gemm16 below, which shares this staging protocol.)
 // 256 threads = 4 waves in 2x2, each wave 128x128 = 4x4 v_mfma_i32_32x32x32_i8 blocks (256
 // accumulator registers; one workgroup per CU).
 // Staging: a 4-stage LDS ring (32 KB per stage: A then B, 256 rows x 64 B each) filled by
@@ -296,6 +298,7 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
 // to one XCD so that their shared row blocks stay in that XCD's L2.
 // ---------------------------------------------------------------------------
 constexpr int kOzStages = 4;
+constexpr int kOzStages16 = 4;  // k_oz_gemm16 (5 stages, the whole 160 KB LDS, measured no better)
 constexpr int kOzOpBytes = kOzT * kOzKC;          // 16 KB per operand per stage
 constexpr int kOzStageBytes = 2 * kOzOpBytes;     // 32 KB
 
@@ -327,6 +330,7 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
     int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
     while ((I + 1) * (I + 2) / 2 <= tile) ++I;
     while (I * (I + 1) / 2 > tile) --I;
+    I = __builtin_amdgcn_readfirstlane(I);
     const int K = tile - I * (I + 1) / 2;
     const int per = (nkc + nsplit - 1) / nsplit;
     const int c0 = split * per;
@@ -336,21 +340,20 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
     // (k_oz_residues); a 256-row tile is 16 consecutive 1 KB blocks
     const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
     const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wid >> 1, wc = wid & 1;
 
-    // this wave's 4 glds per operand: rows 16 (4 wid + i) + (lane >> 2), stored unit lane & 3
+    // this wave's 4 glds per operand: 16-row blocks 4 wid + i
     // (one instruction copies the 1 KB block of 16 rows lane-linearly: the LDS image keeps
     // the global [unit][row][16 B] order, whose 16-row runs make every ds_read_b128 lane
     // group hit 16 distinct 16-byte bank slots without a swizzle)
-    int srcoff[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) srcoff[i] = (4 * wid + i) * 1024 + lane * 16;
+    const int voff = wid * 4096 + lane * 16;  // the only per-lane part of a piece's source
     // glds number g (0..7) of a stage: operand g >> 2, wave-slice g & 3
     auto glds_one = [&](int kc, int stage, int g) {
         int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
-        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride;
-        oz_glds(src + srcoff[g & 3], sb + (4 * wid + (g & 3)) * 1024);
+        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
+        oz_glds(src + voff, sb + (4 * wid + (g & 3)) * 1024);
     };
     auto issue = [&](int kc, int stage) {
 #pragma unroll
@@ -454,6 +457,166 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
             }
 }
 
+// ---------------------------------------------------------------------------
+// The same tile, staging and schedule on v_mfma_i32_16x16x64_i8: one K step is a whole
+// 64-byte chunk, and a 16-row operand fragment (lane l: row l & 15, unit l >> 4) is exactly
+// one 1 KB block of the residue image, read lane-linearly.  Per wave 8 x 8 accumulator
+// blocks of 16 x 16 (256 registers), 64 MFMAs of 16 cycles per chunk.  C/D map: col =
+// l & 15, row = 4 (l >> 4) + reg.
+// ---------------------------------------------------------------------------
+// v_mfma_i32_16x16x64_i8 with the accumulator pinned to AGPRs (the builtin lets the register
+// allocator shuttle 64 four-register accumulators between the files every K step).  Every
+// accumulator is re-used only 64 MFMAs later; the epilogue waits out the last writes.
+__device__ __forceinline__ void oz_mfma16(v4i &acc, const v4i &a, const v4i &b) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// NW = 4: waves in 2 x 2, each 128 x 128 (8 x 8 blocks, 256 accumulator registers, one wave
+// per SIMD).  NW = 8: waves in 2 x 4, each 128 x 64 (8 x 4 blocks, 128 registers), two waves
+// per SIMD, so that one wave's MFMAs run while the other issues its LDS-DMA pieces.
+// s_waitcnt vmcnt(N) (expcnt, lgkmcnt left open): every piece older than the newest N landed
+template <int N>
+__device__ __forceinline__ void oz_wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
+template <int dbg, int NW, int ST>
+__global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restrict__ R, int n_oz,
+                                                          int nkc, int nsplit,
+                                                          int8_t *__restrict__ P, OzConsts C) {
+    constexpr int WN = NW / 2;        // wave columns
+    constexpr int FJ = 16 / WN;       // 16 x 16 column blocks per wave: 8 (NW 4) or 4 (NW 8)
+    constexpr int PP = 32 / NW;       // LDS-DMA pieces per wave and stage (32 per stage)
+    constexpr int PH = PP / 2;        // pieces per operand
+    __shared__ __attribute__((aligned(1024))) int8_t smem[ST * kOzStageBytes];
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int u = xcd + 8 * (q / ntiles);
+    const int tile = q % ntiles;
+    const int mod = u % kOzMods;
+    const int split = u / kOzMods;
+    if (split >= nsplit) return;
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    I = __builtin_amdgcn_readfirstlane(I);
+    const int K = tile - I * (I + 1) / 2;
+    const int per = (nkc + nsplit - 1) / nsplit;
+    const int c0 = split * per;
+    const int nch = max(0, min(nkc, c0 + per) - c0);
+    const size_t kstride = (size_t)n_oz * kOzKC;
+    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
+    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid / WN, wc = wid % WN;
+
+    // piece g of a stage: operand g / PH, 16-row block PH wid + g % PH (1 KB, lane-linear)
+    const int voff = wid * PH * 1024 + lane * 16;  // the only per-lane part of a source
+    auto glds_one = [&](int kc, int stage, int g) {
+        int8_t *sb = smem + stage * kOzStageBytes + (g / PH) * kOzOpBytes;
+        const int8_t *src = ((g / PH) ? baseB : baseA) + (size_t)kc * kstride + (g % PH) * 1024;
+        oz_glds(src + voff, sb + (PH * wid + (g % PH)) * 1024);
+    };
+    auto issue = [&](int kc, int stage) {
+#pragma unroll
+        for (int g = 0; g < PP; ++g) glds_one(kc, stage, g);
+    };
+
+    v4i acc[8][FJ];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+
+    auto frag_a = [&](int chunk, int i) {
+        const int8_t *A_ = smem + (chunk % ST) * kOzStageBytes;
+        return *(const v4i *)&A_[(wr * 8 + i) * 1024 + lane * 16];
+    };
+    auto frag_b = [&](int chunk, int j) {
+        const int8_t *B_ = smem + (chunk % ST) * kOzStageBytes + kOzOpBytes;
+        return *(const v4i *)&B_[(wc * FJ + j) * 1024 + lane * 16];
+    };
+    auto read_frags = [&](int chunk, v4i (&fa)[8], v4i (&fb)[FJ]) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i] = frag_a(chunk, i);
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) fb[j] = frag_b(chunk, j);
+    };
+    // same protocol as k_oz_gemm: 8 groups of {FJ MFMAs, PP/8 LDS-DMA pieces, the next
+    // chunk's A fragment g and (spread evenly) B fragments}
+    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[FJ], v4i (&fa_n)[8], v4i (&fb_n)[FJ]) {
+        if (!(dbg & 4)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            oz_wait_vm<PP * (ST - 2)>();
+            __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        const int kc_next = (dbg & 8) ? c0 : c0 + min(it + ST, nch - 1);
+        const int st_next = (it + ST) % ST;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            oz_mfma16(acc[g][0], fa_c[g], fb_c[0]);
+            if (!(dbg & 1) && (PP == 8 || (g & 1))) glds_one(kc_next, st_next, PP == 8 ? g : g >> 1);
+            oz_mfma16(acc[g][1], fa_c[g], fb_c[1]);
+            if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
+            oz_mfma16(acc[g][2], fa_c[g], fb_c[2]);
+            if (!(dbg & 2) && (FJ == 8 || !(g & 1))) fb_n[g * FJ / 8] = frag_b(it + 1, g * FJ / 8);
+            oz_mfma16(acc[g][3], fa_c[g], fb_c[3]);
+#pragma unroll
+            for (int j = 4; j < FJ; ++j) oz_mfma16(acc[g][j], fa_c[g], fb_c[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    v4i fa0[8], fb0[FJ], fa1[8], fb1[FJ];
+    if (nch > 0) {
+#pragma unroll
+        for (int st = 0; st < ST - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        oz_wait_vm<PP * (ST - 2)>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(c0 + min(ST - 1, nch - 1), ST - 1);
+        read_frags(0, fa0, fb0);
+    }
+    int it = 0;
+    for (; it + 1 < nch; it += 2) {
+        step(it, fa0, fb0, fa1, fb1);
+        step(it + 1, fa1, fb1, fa0, fb0);
+    }
+    if (it < nch) step(it, fa0, fb0, fa1, fb1);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
+    const int m = C.m[mod];
+    const double im = C.inv_m[mod];
+    const int hi = m / 2, lo = hi - m + 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rowl = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+                const int col = wc * FJ * 16 + j * 16 + (lane & 15);
+                const int cval = acc[i][j][r];
+                int rr = cval - (int)rint((double)cval * im) * m;
+                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
+                out[rowl * kOzT + col] = (int8_t)rr;
+            }
+}
+
+static int oz_shape() {
+    static const int s = [] {
+        const char *e = getenv("BB_OZ_SHAPE");
+        return e ? atoi(e) : 16;
+    }();
+    return s;
+}
+
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
                     int dbg) {
     const int nt = n_oz / kOzT;
@@ -462,6 +625,25 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
     // kOzMods * nsplit units, a multiple of 8 (kOzMods = 16): unit u -> XCD u % 8
     const unsigned g = ntiles * kOzMods * nsplit;
     const OzConsts &C = oz_consts();
+    const int shape = oz_shape();
+    if (shape == 16 || shape == 8) {
+        const int nw = shape == 8 ? 8 : 4;
+#define BB_OZ16(D, W) k_oz_gemm16<D, W, kOzStages16><<<g, W * 64, 0, s>>>(R, n_oz, nkc, nsplit, P, C)
+#define BB_OZ(D)                                 \
+    case D:                                      \
+        if (nw == 8) BB_OZ16(D, 8);              \
+        else BB_OZ16(D, 4);                      \
+        break;
+        switch (dbg) {
+            BB_OZ(1) BB_OZ(2) BB_OZ(3) BB_OZ(4) BB_OZ(7) BB_OZ(8)
+            default:
+                if (nw == 8) BB_OZ16(0, 8);
+                else BB_OZ16(0, 4);
+        }
+#undef BB_OZ
+#undef BB_OZ16
+        return;
+    }
     switch (dbg) {
 #define BB_OZ(D)                                                                  \
     case D:                                                                       \

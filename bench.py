@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (spec)
-# dense int8 MFMA: 2048 ops/clk/SIMD (v_mfma_i32_32x32x32_i8 = 32 cycles) x 1024 SIMDs x 2.4 GHz
+# dense int8 MFMA: 2048 ops/clk/SIMD (v_mfma_i32_16x16x64_i8 = 16 cycles) x 1024 SIMDs x 2.4 GHz
 INT8_MFMA_PEAK_TOPS = 2048 * 1024 * 2.4e9 / 1e12
 DATA_SEED = 20240501
 
@@ -112,8 +112,11 @@ def pmc_traffic(n, p, world, kernel):
             continue
         w = d.get("workload", {})
         gk = d.get("gram_kernels", {})
-        if w.get("n") == n and w.get("p") == p and world == 1 and kernel in gk:
-            best = (gk[kernel]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+        if w.get("n") != n or w.get("p") != p or world != 1:
+            continue
+        for k in gk:  # exact name, or the prefix of a template instantiation
+            if k == kernel or k.startswith(kernel + "<"):
+                best = (gk[k]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
     return best
 
 
@@ -237,7 +240,7 @@ def main():
     gram_flops = float(n) * (n + 1) * p_loc
     if gram_mode == bb.GRAM_OZAKI:
         kernel_ops = 16.0 * n * (n + 1) * p_loc
-        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm (v_mfma_i32_32x32x32_i8)"
+        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm16 (v_mfma_i32_16x16x64_i8)"
     else:
         kernel_ops = gram_flops
         peak, unit, kname = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", "k_gram (v_mfma_f64_16x16x4_f64)"
@@ -245,7 +248,7 @@ def main():
     gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
     fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
 
-    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm<0>" if gram_mode == bb.GRAM_OZAKI
+    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16" if gram_mode == bb.GRAM_OZAKI
                           else "bb::k_gram")
 
     cpu = None
