@@ -16,6 +16,9 @@
 // reference's chol(U, VInv, 'U') convention (A = U'U).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -865,12 +868,14 @@ __global__ __launch_bounds__(512) void k_chol_step(double *A, int lda, int kp, i
 // Every dependency points to an earlier tile row or to the chain at a step <= the tile's
 // row, and each owner takes its tiles in row-major order, so the schedule cannot deadlock
 // with every workgroup resident (grid <= CUs, one 512-thread workgroup per CU).
-// Flags (zeroed per factorisation): fW[k], fP[k][j] (U_kj published), fR[k][0/1] (tile
-// (k,k) / (k,k+1) handed over); agent-scope release/acquire, spins bounded (error bit 16).
+// Flags: fW[k], fP[k][j] (U_kj published), fR[k][0/1] (tile (k,k) / (k,k+1) handed over);
+// a flag is set by storing the factorisation's epoch (1, 2, ... per flag buffer), so the
+// buffer is never re-zeroed; agent-scope release/acquire, spins bounded (error bit 16).
 // ---------------------------------------------------------------------------
 struct CholFlags {
     unsigned int *W, *P, *R;
     int ncb;
+    unsigned int ep;  // this factorisation's epoch
 };
 
 // Cross-workgroup hand-offs inside the persistent kernel follow the write-through recipe of
@@ -887,19 +892,19 @@ __device__ __forceinline__ void st_sc1(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void flag_release(unsigned int *f) {
+__device__ __forceinline__ void flag_release(unsigned int *f, unsigned int ep) {
     // caller: every wave's sc1 stores issued; each wave drains them before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(f, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void flag_acquire2(const unsigned int *f1, const unsigned int *f2,
-                                              uint32_t *err) {
+                                              unsigned int ep, uint32_t *err) {
     if (threadIdx.x == 0) {
         unsigned spins = 0;
-        while (__hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u ||
-               (f2 && __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)) {
+        while (__hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep ||
+               (f2 && __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep)) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1u << 25)) {
                 atomicOr(err, 16u);
@@ -1120,7 +1125,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             CHAIN_TS(2);
             if (k + 1 < nblk) {
                 // hand-off tiles, updated by their owners through step k-1
-                flag_acquire2(&F.R[2 * k + 1], &F.R[2 * (k + 1)], err);
+                flag_acquire2(&F.R[2 * k + 1], &F.R[2 * (k + 1)], F.ep, err);
                 CHAIN_TS(3);
                 {
                     // all 16 loads of the two tiles in flight before the first LDS write
@@ -1200,12 +1205,12 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
-                    __hip_atomic_store(&F.W[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], 1u, __ATOMIC_RELAXED,
+                    __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
             } else {
-                flag_release(&F.W[k]);
+                flag_release(&F.W[k], F.ep);
             }
             CHAIN_TS(7);
         }
@@ -1243,7 +1248,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         __syncthreads();
         for (int k = 0; k < nupd; ++k) {
             if (k == nupd - 1) OWN_TS(0);
-            flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], err);
+            flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], F.ep, err);
             if (k == nupd - 1) OWN_TS(1);
             tile_load(S, A, lda, k, i, false);
             if (!diag) tile_load(Q, A, lda, k, j, false);
@@ -1258,13 +1263,13 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         }
         if (handoff) {
             tile_store(T, A, lda, i, j);
-            flag_release(&F.R[2 * i + (diag ? 0 : 1)]);
+            flag_release(&F.R[2 * i + (diag ? 0 : 1)], F.ep);
             OWN_TS(4);
             continue;
         }
         // U_ij = W_i A_ij
         OWN_TS(4);
-        flag_acquire2(&F.W[i], nullptr, err);
+        flag_acquire2(&F.W[i], nullptr, F.ep, err);
         OWN_TS(5);
         {
             const double *W = Wd + (size_t)i * kNB * kNB;
@@ -1300,7 +1305,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         MM_FOR(h, r, y, x) {
             st_sc1(&A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda], acc[h][r]);
         }
-        flag_release(&F.P[i * F.ncb + j]);
+        flag_release(&F.P[i * F.ncb + j], F.ep);
         OWN_TS(7);
 #undef OWN_TS
     }
@@ -1337,8 +1342,20 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
         const int nblk = m_pad / kNB;
         const int ncb = nblk + nrhs_blocks;
         const size_t words = chol_flag_words(m_pad, nrhs_blocks);
-        (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * words, s);
-        CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb};
+        // epoch per flag buffer (host side): zero the buffer only when first seen and on wrap
+        static std::mutex mu;
+        static std::unordered_map<const unsigned int *, unsigned int> epochs;
+        unsigned int ep;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            unsigned int &e = epochs[flags];
+            if (e == 0u || e == 0xffffffffu) {
+                (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * words, s);
+                e = 0u;
+            }
+            ep = ++e;
+        }
+        CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb, ep};
         const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
         const int grid = std::min(device_cus(), 1 + ntiles);
         k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);

@@ -17,8 +17,47 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 // ---------------------------------------------------------------------------
 // Host constants.
 // ---------------------------------------------------------------------------
-static const int kMods[kOzMods] = {247, 245, 244, 243, 241, 239, 233, 229,
-                                   227, 223, 211, 199, 197, 193, 191, 181};
+static constexpr int kMods[kOzMods] = {247, 245, 244, 243, 241, 239, 233, 229,
+                                       227, 223, 211, 199, 197, 193, 191, 181};
+
+// Compile-time Garner tables: the CRT kernel folds them into instruction literals (as
+// kernel arguments they spill out of SGPRs and are re-fetched by scalar loads per element).
+struct OzTab {
+    int m[kOzMods];
+    int invP[kOzMods];
+    int Pmod[kOzMods][kOzMods];
+    float inv_mf[kOzMods];
+};
+
+constexpr long long cx_inv_mod(long long a, long long m) {
+    long long g = m, x = 0, x1 = 1, a1 = ((a % m) + m) % m;
+    while (a1) {
+        long long q = g / a1, t = g - q * a1;
+        g = a1;
+        a1 = t;
+        t = x - q * x1;
+        x = x1;
+        x1 = t;
+    }
+    return ((x % m) + m) % m;
+}
+
+constexpr OzTab oz_make_tab() {
+    OzTab t{};
+    for (int k = 0; k < kOzMods; ++k) {
+        t.m[k] = kMods[k];
+        t.inv_mf[k] = 1.0f / (float)kMods[k];
+        long long P = 1;
+        for (int j = 0; j < k; ++j) {
+            t.Pmod[j][k] = (int)P;
+            P = (P * kMods[j]) % kMods[k];
+        }
+        t.invP[k] = k ? (int)cx_inv_mod(P, kMods[k]) : 1;
+    }
+    return t;
+}
+
+constexpr OzTab kOzTab = oz_make_tab();
 
 static long long inv_mod(long long a, long long m) {
     long long g = m, x = 0, x1 = 1, a1 = ((a % m) + m) % m;
@@ -680,9 +719,15 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
     if (gid >= nquad) {
         const long r = gid - nquad;
         if (r < n_pad) {
-            double v = 0.0;
-            for (int q = 0; q < nxu; ++q) v += xu_part[(size_t)q * n_pad + r];
-            red2[(size_t)n_pad * n_pad + r] = v;
+            // 8 interleaved partial sums (fixed order): 8 loads in flight per round trip
+            double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            int q = 0;
+            for (; q + 8 <= nxu; q += 8)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] += xu_part[(size_t)(q + t) * n_pad + r];
+            for (int t = 0; q < nxu; ++q, ++t) v[t] += xu_part[(size_t)q * n_pad + r];
+            red2[(size_t)n_pad * n_pad + r] =
+                ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
         }
         return;
     }
@@ -694,28 +739,37 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
     const int K = tile - I * (I + 1) / 2;
     const int gi = I * kOzT + (e0 >> 8), gk0 = K * kOzT + (e0 & 255);
     if (gi < gk0 || gi >= n_pad) return;
-    // residue sums of the 4 elements for every modulus
+    // residue sums of the 4 elements for every modulus: every word is loaded before any is
+    // used (interleaved with the sums, the loads become 16 dependent round trips per wave)
     int rs[kOzMods][4];
+    constexpr int NL = NS > 0 ? NS : 1;
+    int w[kOzMods][NL];
+#pragma unroll
+    for (int k = 0; k < kOzMods; ++k)
+#pragma unroll
+        for (int sp = 0; sp < NL; ++sp)
+            w[k][sp] = __builtin_nontemporal_load(
+                (const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
+                                      (size_t)(kOzT * kOzT) + e0));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < kOzMods; ++k) {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        const int nsp = NS > 0 ? NS : nsplit;
 #pragma unroll
-        for (int sp = 0; sp < (NS > 0 ? NS : 1); ++sp) {
-            const int w = *(const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
-                                                 (size_t)(kOzT * kOzT) + e0);
-            s0 += (int)(int8_t)(w & 0xff);
-            s1 += (int)(int8_t)((w >> 8) & 0xff);
-            s2 += (int)(int8_t)((w >> 16) & 0xff);
-            s3 += w >> 24;
+        for (int sp = 0; sp < NL; ++sp) {
+            const int v = w[k][sp];
+            s0 += (int)(int8_t)(v & 0xff);
+            s1 += (int)(int8_t)((v >> 8) & 0xff);
+            s2 += (int)(int8_t)((v >> 16) & 0xff);
+            s3 += v >> 24;
         }
-        for (int sp = (NS > 0 ? NS : 1); sp < nsp; ++sp) {
-            const int w = *(const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
+        for (int sp = NL; sp < (NS > 0 ? NS : nsplit); ++sp) {
+            const int v = *(const int *)(P + (((size_t)sp * kOzMods + k) * ntiles + tile) *
                                                  (size_t)(kOzT * kOzT) + e0);
-            s0 += (int)(int8_t)(w & 0xff);
-            s1 += (int)(int8_t)((w >> 8) & 0xff);
-            s2 += (int)(int8_t)((w >> 16) & 0xff);
-            s3 += w >> 24;
+            s0 += (int)(int8_t)(v & 0xff);
+            s1 += (int)(int8_t)((v >> 8) & 0xff);
+            s2 += (int)(int8_t)((v >> 16) & 0xff);
+            s3 += v >> 24;
         }
         rs[k][0] = s0;
         rs[k][1] = s1;
@@ -730,20 +784,20 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
         int a[kOzMods];
 #pragma unroll
         for (int k = 0; k < kOzMods; ++k) {
-            const int r = oz_smod(rs[k][q], C.m[k], C.inv_mf[k]);
+            const int r = oz_smod(rs[k][q], kOzTab.m[k], kOzTab.inv_mf[k]);
             if (k == 0) {
                 a[0] = r;
             } else {
                 int acc = 0;
 #pragma unroll
-                for (int j = 0; j < k; ++j) acc += a[j] * C.Pmod[j][k];
-                const int sk = oz_smod(acc, C.m[k], C.inv_mf[k]);
-                a[k] = oz_smod((r - sk) * C.invP[k], C.m[k], C.inv_mf[k]);
+                for (int j = 0; j < k; ++j) acc += a[j] * kOzTab.Pmod[j][k];
+                const int sk = oz_smod(acc, kOzTab.m[k], kOzTab.inv_mf[k]);
+                a[k] = oz_smod((r - sk) * kOzTab.invP[k], kOzTab.m[k], kOzTab.inv_mf[k]);
             }
         }
         __int128 X = a[kOzMods - 1];
 #pragma unroll
-        for (int k = kOzMods - 2; k >= 0; --k) X = X * (__int128)C.m[k] + (__int128)a[k];
+        for (int k = kOzMods - 2; k >= 0; --k) X = X * (__int128)kOzTab.m[k] + (__int128)a[k];
         const bool neg = X < 0;
         if (neg) X = -X;
         const unsigned long long hi = (unsigned long long)(X >> 64);
