@@ -76,6 +76,8 @@ T *dalloc(size_t count, std::vector<void *> &owned) {
     if (count == 0) count = 1;
     HIPCHECK(hipMalloc(&p, count * sizeof(T)));
     HIPCHECK(hipMemset(p, 0, count * sizeof(T)));
+    // the engine's streams are non-blocking: the zero fill must land before their first use
+    HIPCHECK(hipDeviceSynchronize());
     owned.push_back(p);
     return (T *)p;
 }
@@ -264,7 +266,7 @@ struct bb_engine {
                               oz_xu_parts(p_pad), red2);
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
-                                red2);
+                                red2, 1);
         } else {
             launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
                           group, lam, nullptr, nullptr, trl, err);
@@ -322,7 +324,7 @@ struct bb_engine {
     }
 
     size_t red1_count() const { return (size_t)nbS + n_pad; }
-    size_t red2_count() const { return (size_t)n_pad * n_pad + n_pad; }
+    size_t red2_count() const { return tri_count(n_pad) + n_pad; }
 
     void sweep(uint64_t t, int slot, int mcmc_phase) {
         phase_a(t);
@@ -410,7 +412,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
             e->slabs = dalloc<double>(e->slab_stride * e->S, o);
         }
         e->xu_part = dalloc<double>((size_t)xv_chunks(p_pad) * n_pad, o);
-        e->red2 = dalloc<double>((size_t)n_pad * n_pad + n_pad, o);
+        e->red2 = dalloc<double>(tri_count(n_pad) + n_pad, o);
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
         e->w = dalloc<double>(n_pad, o);
     }
@@ -440,7 +442,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
                         (size_t)p_pad * p_pad);
             double *red = nullptr;
             HIPCHECK(hipMalloc(&red, ((size_t)p_pad * p_pad + p_pad) * sizeof(double)));
-            launch_slab_sum(e->stream, sl, Sg, (size_t)p_pad * p_pad, p_pad, nullptr, 0, red);
+            launch_slab_sum(e->stream, sl, Sg, (size_t)p_pad * p_pad, p_pad, nullptr, 0, red, 0);
             e->G = dalloc<double>((size_t)p_pad * p_pad, o);
             HIPCHECK(hipMemcpyAsync(e->G, red, (size_t)p_pad * p_pad * sizeof(double),
                                     hipMemcpyDeviceToDevice, e->stream));
@@ -1109,14 +1111,13 @@ int bb_gram(double *C, const double *Yh, const double *wh, int n, int k) {
         double *sl = dalloc<double>(stride * S, owned);
         double *red = dalloc<double>(stride + n_pad, owned);
         launch_gram(0, dY, n_pad, dw, n_pad, k_pad, S, sl, n_pad, stride);
-        launch_slab_sum(0, sl, S, stride, n_pad, nullptr, 0, red);
+        launch_slab_sum(0, sl, S, stride, n_pad, nullptr, 0, red, 1);
         HIPCHECK(hipGetLastError());
-        std::vector<double> h(stride);
-        HIPCHECK(hipMemcpy(h.data(), red, stride * sizeof(double), hipMemcpyDeviceToHost));
+        std::vector<double> h(tri_count(n_pad));
+        HIPCHECK(hipMemcpy(h.data(), red, h.size() * sizeof(double), hipMemcpyDeviceToHost));
         for (int c = 0; c < n; ++c)
             for (int r = 0; r < n; ++r)
-                C[(size_t)r + (size_t)c * n] =
-                    r <= c ? h[(size_t)r + (size_t)c * n_pad] : h[(size_t)c + (size_t)r * n_pad];
+                C[(size_t)r + (size_t)c * n] = r <= c ? h[tri_index(r, c)] : h[tri_index(c, r)];
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         rc = -1;
@@ -1155,12 +1156,11 @@ int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
         launch_oz_gemm(0, R, n_oz, k_pad, S, P);
         launch_oz_crt(0, P, S, n_oz, n_pad, escale, nullptr, 0, red);
         HIPCHECK(hipGetLastError());
-        std::vector<double> h(stride);
-        HIPCHECK(hipMemcpy(h.data(), red, stride * sizeof(double), hipMemcpyDeviceToHost));
+        std::vector<double> h(tri_count(n_pad));
+        HIPCHECK(hipMemcpy(h.data(), red, h.size() * sizeof(double), hipMemcpyDeviceToHost));
         for (int c = 0; c < n; ++c)
             for (int r = 0; r < n; ++r)
-                C[(size_t)r + (size_t)c * n] =
-                    r <= c ? h[(size_t)r + (size_t)c * n_pad] : h[(size_t)c + (size_t)r * n_pad];
+                C[(size_t)r + (size_t)c * n] = r <= c ? h[tri_index(r, c)] : h[tri_index(c, r)];
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         rc = -1;

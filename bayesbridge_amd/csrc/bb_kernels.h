@@ -28,6 +28,11 @@ constexpr int kNB = 64;         // Cholesky block
 constexpr int kXvCols = 256;    // columns per block of the X.v partial-sum kernel
 constexpr int kXvRows = 512;    // rows per block of the X.v partial-sum kernel
 
+// Packed upper triangle, column-major: element (r, c), r <= c, at c (c + 1) / 2 + r.  The
+// Woodbury Gram travels in this form (red2), so its all-reduce moves n(n+1)/2 doubles.
+__host__ __device__ inline size_t tri_index(int r, int c) { return (size_t)c * (c + 1) / 2 + r; }
+__host__ __device__ inline size_t tri_count(int n) { return (size_t)n * (n + 1) / 2; }
+
 enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
 
 // Number of lanes cooperating on one tilted-stable draw for a problem of `count` draws.
@@ -68,9 +73,10 @@ void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y,
                     double *tau_tr, double *sig2_tr, double *alpha_tr, int tau_only,
                     uint32_t *err);
 
-// red2 = [sum_s slabs (upper, n_pad^2) | sum_q xu_part (n_pad)].
+// red2 = [sum_s slabs, upper triangle | sum_q xu_part (n_pad)]; packed = 1: the triangle is
+// packed (tri_index, the Woodbury red2), 0: full column-major n_pad^2 (lower part zero).
 void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
-                     const double *xu_part, int nxu, double *red2);
+                     const double *xu_part, int nxu, double *red2, int packed);
 
 // M (upper, ld = ldm) = I + red2 / sig2; column rhs_col = y/sig - (xu/sig + delta).
 void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,

@@ -453,28 +453,31 @@ void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_slab_sum(const double *slabs, int S, size_t stride,
                                                   int n_pad, const double *xu_part, int nxu,
-                                                  double *red2) {
+                                                  double *red2, int packed) {
     const size_t nn = (size_t)n_pad * n_pad;
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx < nn) {
         const int r = (int)(idx % n_pad), c = (int)(idx / n_pad);
-        double v = 0.0;
-        if (r <= c)
+        if (r <= c) {
+            double v = 0.0;
             for (int q = 0; q < S; ++q) v += slabs[(size_t)q * stride + idx];
-        red2[idx] = v;
+            red2[packed ? tri_index(r, c) : idx] = v;
+        } else if (!packed) {
+            red2[idx] = 0.0;
+        }
     } else if (idx < nn + (size_t)n_pad) {
         const int r = (int)(idx - nn);
         double v = 0.0;
         for (int q = 0; q < nxu; ++q) v += xu_part[(size_t)q * n_pad + r];
-        red2[idx] = v;
+        red2[(packed ? tri_count(n_pad) : nn) + r] = v;
     }
 }
 
 void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
-                     const double *xu_part, int nxu, double *red2) {
+                     const double *xu_part, int nxu, double *red2, int packed) {
     const size_t tot = (size_t)n_pad * n_pad + n_pad;
     k_slab_sum<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(slabs, S, slab_stride, n_pad,
-                                                             xu_part, nxu, red2);
+                                                             xu_part, nxu, red2, packed);
 }
 
 __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n_pad,
@@ -487,13 +490,13 @@ __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n
     const double sig2 = sc->sig2;
     double *dst = M + (size_t)r + (size_t)c * ldm;
     if (c < n_pad) {
-        if (r <= c) *dst = red2[idx] / sig2 + (r == c ? 1.0 : 0.0);
+        if (r <= c) *dst = red2[tri_index(r, c)] / sig2 + (r == c ? 1.0 : 0.0);
     } else if (c == rhs_col) {
         double v = 0.0;
         if (r < n) {
             const double sig = sqrt(sig2);
             const double delta = normal_at(key, t, KIND_DELTA, (uint64_t)r);
-            const double xu = red2[(size_t)n_pad * n_pad + r];
+            const double xu = red2[tri_count(n_pad) + r];
             v = y[r] / sig - (xu / sig + delta);
         }
         *dst = v;

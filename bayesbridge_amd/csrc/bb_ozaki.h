@@ -60,7 +60,8 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
 // P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
                     int dbg = 0);
-// red2[r + c n_pad] (r <= c < n_pad) = G(r, c); red2[n_pad^2 + r] = sum_q xu_part[q][r].
+// red2[tri_index(r, c)] (r <= c < n_pad) = G(r, c); red2[tri_count(n_pad) + r] = sum_q
+// xu_part[q][r].
 void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
                    const int *escale, const double *xu_part, int nxu, double *red2);
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "bb_kernels.h"
 #include "bb_ozaki.h"
 
 namespace bb {
@@ -697,8 +698,8 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
 
 // ---------------------------------------------------------------------------
 // CRT: per lower-triangle element, sum the split residues, Garner (balanced digits) ->
-// exact 128-bit C -> fp64 -> scale; written to red2 as the upper triangle of a column-major
-// n_pad x n_pad matrix (the layout k_form_m reads).  Extra threads sum the X u partials.
+// exact 128-bit C -> fp64 -> scale; written to red2 as the packed upper triangle
+// (tri_index, the layout k_form_m reads).  Extra threads sum the X u partials.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int oz_smod(int v, int m, float imf) {
     int r = v - (int)rintf((float)v * imf) * m;
@@ -726,7 +727,7 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
 #pragma unroll
                 for (int t = 0; t < 8; ++t) v[t] += xu_part[(size_t)(q + t) * n_pad + r];
             for (int t = 0; q < nxu; ++q, ++t) v[t] += xu_part[(size_t)q * n_pad + r];
-            red2[(size_t)n_pad * n_pad + r] =
+            red2[tri_count(n_pad) + r] =
                 ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
         }
         return;
@@ -804,7 +805,7 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
         const unsigned long long lo = (unsigned long long)X;
         double v = __builtin_fma((double)hi, 18446744073709551616.0, (double)lo);
         v = neg ? -v : v;
-        red2[(size_t)gk + (size_t)gi * n_pad] = ldexp(v, ei + escale[gk]);
+        red2[tri_index(gk, gi)] = ldexp(v, ei + escale[gk]);
     }
 }
 
