@@ -282,7 +282,7 @@ struct bb_engine {
             mark(PH_CHOL);
             chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd, flags);
             mark(PH_SOLVE);
-            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1);
+            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
             mark(PH_BETA);
             if (beta_xb_supported(n_pad)) {
                 // beta and the X beta partials of the next sweep in one pass over X
@@ -300,7 +300,7 @@ struct bb_engine {
             chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd, flags);
             mark(PH_SOLVE);
             launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
-            chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2);
+            chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2, flags, err);
             mark(PH_BETA);
             launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
         } else {
@@ -473,7 +473,7 @@ void engine_init_state_local(bb_engine *e) {
         chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT, e->Wd, e->flags);
         HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
                                 e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
-        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1);
+        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1, e->flags, e->err);
         uint32_t f = e->read_err();
         ls_ok = (f & 8u) == 0;
         if (ls_ok) {
@@ -1061,7 +1061,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
             HIPCHECK(hipEventRecord(e0, 0));
             chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
             HIPCHECK(hipEventRecord(e1, 0));
-            chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, 1);
+            chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, 1, fl, de);
             HIPCHECK(hipEventRecord(e2, 0));
             HIPCHECK(hipEventSynchronize(e2));
             float a = 0, b = 0;
@@ -1231,7 +1231,7 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
         chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
-        chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, nrhs);
+        chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, nrhs, fl, de);
         HIPCHECK(hipGetLastError());
         std::vector<double> hw((size_t)m_pad * nrhs);
         HIPCHECK(hipMemcpy(hw.data(), W, hw.size() * sizeof(double), hipMemcpyDeviceToHost));

@@ -69,7 +69,9 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
 int stable_group_for(long count) {
     if (count <= 1024) return 64;
     long g = 1;
-    while (g < 16 && count * g * 2 <= 100000) g *= 2;
+    // measured at a steady-state C3 chain (tools/bench_lambda_steady.py): p = 50000 -> 4,
+    // p = 6250 (8-way shard) -> 8
+    while (g < 16 && count * g * 2 <= 50000) g *= 2;
     return (int)(g < 4 ? 4 : g);
 }
 
@@ -1314,9 +1316,29 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     }
 }
 
-size_t chol_flag_words(int m_pad, int nrhs_blocks) {
+// [W: nblk | P: nblk x ncb | R: 2 nblk | 4 pad | backward-solve: nblk]
+static size_t bsolve_flag_offset(int m_pad, int nrhs_blocks) {
     const size_t nblk = (size_t)m_pad / kNB, ncb = nblk + nrhs_blocks;
     return nblk + nblk * ncb + 2 * nblk + 4;
+}
+
+size_t chol_flag_words(int m_pad, int nrhs_blocks) {
+    return bsolve_flag_offset(m_pad, nrhs_blocks) + (size_t)m_pad / kNB;
+}
+
+// Host-side epoch per flag buffer: advance = true starts a new use (zeroing `words` flags
+// when the buffer is first seen and on wrap); false returns the current epoch (0: none).
+static unsigned int flag_epoch(unsigned int *flags, size_t words, hipStream_t s, bool advance) {
+    static std::mutex mu;
+    static std::unordered_map<const unsigned int *, unsigned int> epochs;
+    std::lock_guard<std::mutex> lk(mu);
+    unsigned int &e = epochs[flags];
+    if (!advance) return e;
+    if (e == 0u || e == 0xffffffffu) {
+        (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * words, s);
+        e = 0u;
+    }
+    return ++e;
 }
 
 static int chol_mode() {
@@ -1345,19 +1367,7 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
         const int nblk = m_pad / kNB;
         const int ncb = nblk + nrhs_blocks;
         const size_t words = chol_flag_words(m_pad, nrhs_blocks);
-        // epoch per flag buffer (host side): zero the buffer only when first seen and on wrap
-        static std::mutex mu;
-        static std::unordered_map<const unsigned int *, unsigned int> epochs;
-        unsigned int ep;
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            unsigned int &e = epochs[flags];
-            if (e == 0u || e == 0xffffffffu) {
-                (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * words, s);
-                e = 0u;
-            }
-            ep = ++e;
-        }
+        const unsigned int ep = flag_epoch(flags, words, s, true);
         CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb, ep};
         const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
         const int grid = std::min(device_cus(), 1 + ntiles);
@@ -1519,9 +1529,86 @@ __global__ __launch_bounds__(256) void k_bsolve_multi(const double *A, int lda, 
     }
 }
 
+// Backward solve in ONE launch: workgroup b owns row block i = nblk-1-b.  It keeps y_i in
+// LDS, and for j = nblk-1 .. i+1 prefetches its tile U_ij into registers, waits for w_j's
+// flag (set-once, tagged with the factorisation's epoch), applies y_i -= U_ij w_j, then
+// forms w_i = W_i' y_i, stores it write-through (sc1) and sets its flag.  The critical path
+// is one hop + one 64 x 64 matvec per block instead of a launch per kBsNB blocks; every
+// workgroup waits only on higher blocks, all are co-resident (nblk <= CUs).
+__global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda, int nblk,
+                                                        int m_pad, const double *__restrict__ Wd,
+                                                        const double *Y, double *Wout, int nrhs,
+                                                        unsigned int *fl, unsigned int ep,
+                                                        uint32_t *err) {
+    __shared__ double yv[2][64];
+    __shared__ double wv[2][64];
+    __shared__ double part[4][2][64];
+    const int i = nblk - 1 - (int)blockIdx.x;
+    const int tid = threadIdx.x, x = tid & 63, g = tid >> 6;  // g: 16-wide slice
+    if (tid < 64 * nrhs) yv[tid >> 6][x] = Y[(size_t)(tid >> 6) * m_pad + i * kNB + x];
+    // W_i column x, rows g*16 .. +15 (column-major: contiguous)
+    double wreg[16];
+    {
+        const double *col = Wd + (size_t)i * kNB * kNB + (size_t)x * kNB + g * 16;
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) wreg[rr] = col[rr];
+    }
+    __syncthreads();
+    for (int j = nblk - 1; j > i; --j) {
+        // U_ij row x, columns g*16 .. +15 (loads in flight across the wait)
+        double ureg[16];
+        const double *row = A + (size_t)(i * kNB + x) + (size_t)(j * kNB + g * 16) * lda;
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) ureg[cc] = row[(size_t)cc * lda];
+        flag_acquire2(&fl[j], nullptr, ep, err);
+        if (tid < 64 * nrhs) wv[tid >> 6][x] = ld_sc1(&Wout[(size_t)(tid >> 6) * m_pad + j * kNB + x]);
+        __syncthreads();
+        for (int q = 0; q < nrhs; ++q) {
+            double acc = 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) acc += ureg[cc] * wv[q][g * 16 + cc];
+            part[g][q][x] = acc;
+        }
+        __syncthreads();
+        if (tid < 64 * nrhs) {
+            const int q = tid >> 6;
+            yv[q][x] -= ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+        }
+        __syncthreads();
+    }
+    for (int q = 0; q < nrhs; ++q) {
+        double acc = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) acc += wreg[rr] * yv[q][g * 16 + rr];
+        part[g][q][x] = acc;
+    }
+    __syncthreads();
+    if (tid < 64 * nrhs) {
+        const int q = tid >> 6;
+        const double w = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
+        st_sc1(&Wout[(size_t)q * m_pad + i * kNB + x], w);
+    }
+    flag_release(&fl[i], ep);
+}
+
+static bool bsolve_persistent() {
+    static const bool on = [] {
+        const char *e = getenv("BB_BSOLVE");
+        return !(e && std::strcmp(e, "multi") == 0);
+    }();
+    return on;
+}
+
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
-                 double *Y, double *W, int nrhs) {
+                 double *Y, double *W, int nrhs, unsigned int *flags, uint32_t *err) {
     const int nblk = m_pad / kNB;
+    if (flags && err && bsolve_persistent() && nblk <= device_cus()) {
+        // the solve's flags have their own epoch sequence (one per solve)
+        unsigned int *bf = flags + bsolve_flag_offset(m_pad, 1);
+        const unsigned int ep = flag_epoch(bf, (size_t)nblk, s, true);
+        k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err);
+        return;
+    }
     for (int kb = nblk - 1; kb >= 0; kb -= kBsNB) {
         const int nb = std::min(kBsNB, kb + 1);
         const int nrow = kb - nb + 1;
