@@ -1660,65 +1660,78 @@ void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, co
 // Fused Woodbury beta update + X beta partials (one pass over X instead of two):
 // wave = one column at a time: s = X_j . w (same per-lane order + wave tree as k_beta_wb),
 // beta_j = u_j + D_j s / sig, then the lane's rows accumulate X_j beta_j in registers
-// (rows 2 lane + 128 i, i < NR).  The next column's loads are issued before the current
-// column's reduction.  The workgroup's 8 wave accumulators are summed in wave order through
-// LDS into part[blockIdx.x][row], which k_pre sums next sweep.  NR = n_pad / 128 <= 16.
+// (rows 2 lane + 128 i, i < NR).  Four waves per workgroup (one per SIMD, so the wave has
+// the whole 512-entry register file and nothing spills); each wave keeps the next TWO
+// columns' loads in flight (three register buffers rotating), so the per-column memory
+// latency is hidden behind two columns of work.  The workgroup's 4 wave accumulators are
+// summed in wave order through LDS into part[blockIdx.x][row], which k_pre sums next
+// sweep.  NR = n_pad / 128 <= 16.
+constexpr int kBxbWaves = 4;
+
 template <int NR>
-__global__ __launch_bounds__(512) void k_beta_wb_xb(const double *__restrict__ X, int ldx,
-                                                    int n_pad, const double *__restrict__ w,
-                                                    const double *__restrict__ u,
-                                                    const double *__restrict__ D,
-                                                    const DevScalars *sc, int p_loc,
-                                                    double *__restrict__ beta,
-                                                    double *__restrict__ trace,
-                                                    double *__restrict__ part) {
+__global__ __launch_bounds__(64 * kBxbWaves, 1) void k_beta_wb_xb(
+    const double *__restrict__ X, int ldx, int n_pad, const double *__restrict__ w,
+    const double *__restrict__ u, const double *__restrict__ D, const DevScalars *sc, int p_loc,
+    double *__restrict__ beta, double *__restrict__ trace, double *__restrict__ part) {
     __shared__ double ws[NR * 128];
-    for (int i = threadIdx.x; i < NR * 128; i += 512) ws[i] = w[i];
+    for (int i = threadIdx.x; i < NR * 128; i += 64 * kBxbWaves) ws[i] = w[i];
     __syncthreads();
     const double sig = sqrt(sc->sig2);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nw = gridDim.x * 8;
+    const int nw = gridDim.x * kBxbWaves;
     double2 acc[NR];
 #pragma unroll
     for (int i = 0; i < NR; ++i) acc[i] = make_double2(0.0, 0.0);
-    int j = blockIdx.x * 8 + wid;
-    double2 xn[NR];
-    if (j < p_loc) {
-        const double *col = X + (size_t)j * ldx + 2 * lane;
+    // a buffer holds column j and its (u_j, D_j): every load of a column is issued together,
+    // so the counted waits for the oldest buffer never drain the two refills behind it
+    // (past the end the last column is re-read: branch-free, so the waits stay counted)
+    auto load = [&](int j, double2 (&xv)[NR], double2 &ud) {
+        const int jj = min(j, p_loc - 1);
+        const double *col = X + (size_t)jj * ldx + 2 * lane;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) xn[i] = *(const double2 *)(col + 128 * i);
-    }
-    for (; j < p_loc; j += nw) {
-        double2 x[NR];
-#pragma unroll
-        for (int i = 0; i < NR; ++i) x[i] = xn[i];
-        const int jn = j + nw;
-        if (jn < p_loc) {
-            const double *col = X + (size_t)jn * ldx + 2 * lane;
-#pragma unroll
-            for (int i = 0; i < NR; ++i) xn[i] = *(const double2 *)(col + 128 * i);
-        }
+        for (int i = 0; i < NR; ++i) xv[i] = *(const double2 *)(col + 128 * i);
+        ud = make_double2(u[jj], D[jj]);
+    };
+    // consume column j from xc, then refill xc with column j + 3 nw
+    auto step = [&](int j, double2 (&xc)[NR], double2 &ud) {
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            s += x[i].x * ws[128 * i + 2 * lane];
-            s += x[i].y * ws[128 * i + 2 * lane + 1];
+            s += xc[i].x * ws[128 * i + 2 * lane];
+            s += xc[i].y * ws[128 * i + 2 * lane + 1];
         }
         s = wave_allsum(s);
-        const double b = u[j] + D[j] * s / sig;
+        const double bj = ud.x + ud.y * s / sig;
         if (lane == 0) {
-            beta[j] = b;
-            if (trace) trace[j] = b;
+            beta[j] = bj;
+            if (trace) trace[j] = bj;
         }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            acc[i].x = __builtin_fma(x[i].x, b, acc[i].x);
-            acc[i].y = __builtin_fma(x[i].y, b, acc[i].y);
+            acc[i].x = __builtin_fma(xc[i].x, bj, acc[i].x);
+            acc[i].y = __builtin_fma(xc[i].y, bj, acc[i].y);
         }
+        // keep the refill behind the last use of xc (else the scheduler hoists it and both
+        // generations of the buffer are live at once)
+        __builtin_amdgcn_sched_barrier(0);
+        load(j + 3 * nw, xc, ud);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    double2 xa[NR], xb[NR], xcol[NR], uda, udb, udc;
+    int j = blockIdx.x * kBxbWaves + wid;
+    load(j, xa, uda);
+    load(j + nw, xb, udb);
+    load(j + 2 * nw, xcol, udc);
+    for (; j + 2 * nw < p_loc; j += 3 * nw) {
+        step(j, xa, uda);
+        step(j + nw, xb, udb);
+        step(j + 2 * nw, xcol, udc);
     }
-    // wave-ordered sum of the 8 accumulators (ws is reused as the running sum)
+    if (j < p_loc) step(j, xa, uda);
+    if (j + nw < p_loc) step(j + nw, xb, udb);
+    // wave-ordered sum of the accumulators (ws is reused as the running sum)
     __syncthreads();
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < kBxbWaves; ++q) {
         if (wid == q) {
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
@@ -1728,7 +1741,7 @@ __global__ __launch_bounds__(512) void k_beta_wb_xb(const double *__restrict__ X
         }
         __syncthreads();
     }
-    for (int i = threadIdx.x; i < NR * 128; i += 512)
+    for (int i = threadIdx.x; i < NR * 128; i += 64 * kBxbWaves)
         part[(size_t)blockIdx.x * n_pad + i] = ws[i];
 }
 
@@ -1746,8 +1759,8 @@ void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad,
     switch (n_pad / 128) {
 #define BXB(NR)                                                                             \
     case NR:                                                                                \
-        k_beta_wb_xb<NR><<<g, 512, 0, s>>>(X, ldx, n_pad, w, u, D, sc, p_loc, beta, beta_trace, \
-                                           part);                                           \
+        k_beta_wb_xb<NR><<<g, 64 * kBxbWaves, 0, s>>>(X, ldx, n_pad, w, u, D, sc, p_loc, beta,  \
+                                                      beta_trace, part);                   \
         break;
         BXB(1) BXB(2) BXB(3) BXB(4) BXB(5) BXB(6) BXB(7) BXB(8)
         BXB(9) BXB(10) BXB(11) BXB(12) BXB(13) BXB(14) BXB(15) BXB(16)
