@@ -37,6 +37,7 @@ enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
 
 // Number of lanes cooperating on one tilted-stable draw for a problem of `count` draws.
 int stable_group_for(long count);
+bool stable_noinline_for(long count);
 
 void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const double *V0,
                             const double *h, int num, uint64_t k0, uint64_t k1, uint64_t t,

@@ -66,7 +66,14 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
 // Lanes per coefficient (inner-attempt speculation).  Measured on MI355X with the C3
 // h-distribution (tools/bench_lambda.py): p=50000 best at G=4..8, p=6250 at G=16;
 // tiny p (C1) wants the widest group for latency.
+// Large batches are throughput-bound: the sampler in non-inlined calls (111 VGPRs, 4 waves
+// per SIMD) with G = 8 beats the inlined one (248 VGPRs, 1 wave per SIMD); small batches are
+// bound by the slowest draw, where the inlined body wins (tools/bench_lambda_steady.py:
+// p = 50000 187 vs 226 us, 25000 129 vs 142 us, 12500 98 vs 98 us, 6250 88 vs 67 us).
+bool stable_noinline_for(long count) { return count >= 20000; }
+
 int stable_group_for(long count) {
+    if (stable_noinline_for(count)) return 8;
     if (count <= 1024) return 64;
     long g = 1;
     // measured at a steady-state C3 chain (tools/bench_lambda_steady.py): p = 50000 -> 4,
@@ -112,8 +119,10 @@ void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const
 
 // lambda_j = 2 retstable(beta_j^2 / tau^2, alpha / 2, 1)   (BridgeRegression.cpp:506-510);
 // Woodbury mode also forms D_j = tau^2 / lambda_j and u_j = sqrt(D_j) z_j.
-template <int G, bool NI = (BB_STABLE_NOINLINE != 0)>
-__global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, int p_pad,
+// OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained).
+template <int G, bool NI = (BB_STABLE_NOINLINE != 0), int OCC = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_lambda(
+    const double *beta, int p_loc, int p_pad,
                                                 uint64_t j0, const DevScalars *sc, Key key,
                                                 uint64_t t, int mode, double *lam, double *D,
                                                 double *u, double *lam_trace, uint32_t *err) {
@@ -153,11 +162,16 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     Key key{k0, k1};
     long threads = (long)p_pad * group;
     int blocks = (int)((threads + 255) / 256);
+    const bool ni = stable_noinline_for(p_loc);
     switch (group) {
 #define BB_CASE(G)                                                                            \
     case G:                                                                                   \
-        k_lambda<G><<<blocks, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,  \
-                                           u, lam_trace, err);                                \
+        if (ni)                                                                               \
+            k_lambda<G, true><<<blocks, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, \
+                                                     lam, D, u, lam_trace, err);              \
+        else                                                                                  \
+            k_lambda<G, false><<<blocks, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,      \
+                                                      mode, lam, D, u, lam_trace, err);       \
         break;
         BB_CASE(1) BB_CASE(2) BB_CASE(4) BB_CASE(8) BB_CASE(16) BB_CASE(32) BB_CASE(64)
 #undef BB_CASE
@@ -176,9 +190,17 @@ void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevSc
     int blocks = (int)((threads + 255) / 256);
 #define BB_V(G)                                                                               \
     case G:                                                                                   \
-        if (noinline)                                                                         \
+        if (noinline == 1)                                                                    \
             k_lambda<G, true><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,   \
                                                      lam, nullptr, nullptr, nullptr, err);    \
+        else if (noinline == 2)                                                               \
+            k_lambda<G, false, 2><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t,            \
+                                                         LAMBDA_ONLY, lam, nullptr, nullptr,  \
+                                                         nullptr, err);                       \
+        else if (noinline == 4)                                                               \
+            k_lambda<G, false, 4><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t,            \
+                                                         LAMBDA_ONLY, lam, nullptr, nullptr,  \
+                                                         nullptr, err);                       \
         else                                                                                  \
             k_lambda<G, false><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,  \
                                                       lam, nullptr, nullptr, nullptr, err);   \

@@ -30,10 +30,13 @@ def main():
     beta, tau = st["beta"], st["tau"]
     print(f"state after {args.sweeps} sweeps: tau={tau:.3e}, "
           f"mean abs beta={float(abs(beta).mean()):.3e}", flush=True)
-    for part in (p, p // 8):
-        for g in (1, 2, 4, 8, 16, 32):
-            ms, _ = bb.bench_lambda(beta[:part], 0.5, tau, g, 0, 20)
-            print(f"p={part:6d} G={g:2d}: {ms * 1e3:8.1f} us/launch", flush=True)
+    # variant 0: inlined sampler; 1: sampler in non-inlined calls (fewer registers)
+    for part in (p, p // 2, p // 4, p // 8):
+        for var in (0, 1):
+            for g in (2, 4, 8, 16):
+                ms, _ = bb.bench_lambda(beta[:part], 0.5, tau, g, var, 20)
+                print(f"p={part:6d} variant={var} G={g:2d}: {ms * 1e3:8.1f} us/launch",
+                      flush=True)
 
 
 if __name__ == "__main__":
