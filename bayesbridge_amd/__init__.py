@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = [
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
     "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode", "bb_bench_ozaki",
+    "bridge_EM", "bb_bridge_em",
 ]
 
 
@@ -125,6 +126,9 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_phase_name.restype = c.c_char_p
     L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
     L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
+    L.bridge_EM.argtypes = [_dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _ip, _ip]
+    L.bb_bridge_em.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int, c.c_double, c.c_double,
+                               c.c_double, c.c_double, c.c_int, c.c_int]
     _lib = L
     return L
 
@@ -256,6 +260,66 @@ def bridge_reg(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=
         raise NotImplementedError("bridge.reg(method='triangle') is not part of this build")
     print('Unrecognized method.  Use "triangles" or "stable".')
     return None
+
+
+def check_em(lambda_max, tol, max_iter):
+    """BridgeWrapper.R:73-82 (check.EM)."""
+    checks = [_is_above(lambda_max, 0.0, "lambda.max"), _is_above(tol, 0.0, "tolerance"),
+              _is_above(max_iter, 1.0, "max.iter")]
+    return all(checks)
+
+
+def bridge_em(y, X, alpha=0.5, ratio=1.0, lambda_max=None, tol=1e-9, max_iter=30,
+              use_cg=False, ret_solves=False):
+    """bridge.EM (BridgeWrapper.R:89-133) through ``.C("bridge_EM", ...)``.
+
+    Bridge posterior mode by EM with sig = 1 and tau = ratio; lambda.max defaults to
+    1e9 * ratio.  Returns beta (P), or {"beta", "num.solves"} with ret_solves.
+    """
+    L = library()
+    _require_gpu()
+    if lambda_max is None:
+        lambda_max = 1e9 * ratio
+    y = np.asarray(y, dtype=np.float64).ravel()
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    N = y.shape[0]
+    R, P = X.shape
+    if ratio < 0:
+        print("bridge.EM: ratio < 0")
+        return 0
+    if alpha < 0:
+        print("bridge.EM: alpha < 0")
+        return 0
+    ok = check_parameters(N, R, 1, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0) and check_em(
+        lambda_max, tol, max_iter)
+    if not ok:
+        raise ValueError("bridge_em: invalid parameters")
+    beta = np.zeros(P)
+    Xf = np.asfortranarray(X)
+    d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
+    it = ctypes.c_int(int(max_iter))
+    L.bridge_EM(_p(beta), _p(y), _p(Xf), d(ratio), d(alpha), ctypes.byref(ctypes.c_int(P)),
+                ctypes.byref(ctypes.c_int(N)), d(lambda_max), d(tol), ctypes.byref(it),
+                ctypes.byref(ctypes.c_int(1 if use_cg else 0)))
+    if ret_solves:
+        return {"beta": beta, "num.solves": it.value}
+    return beta
+
+
+def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=False):
+    """trace.beta (Code/R/bridge-trace.R:22-54) without the plot: bridge.EM over a grid of
+    ratios with lambda.max = ratio / tol.  Returns {"beta" (L x P), "grid", "log.grid"}."""
+    if ratio_grid is None:
+        ratio_grid = np.exp(np.arange(-20.0, 20.0 + 1e-9, 0.1))
+    ratio_grid = np.asarray(ratio_grid, dtype=np.float64)
+    X = np.asarray(X, dtype=np.float64)
+    beta = np.zeros((ratio_grid.size, X.shape[1]))
+    for i, r in enumerate(ratio_grid):
+        beta[i] = bridge_em(y, X, alpha, ratio=r, lambda_max=r / tol, tol=tol,
+                            max_iter=max_iter, use_cg=use_cg)
+    return {"beta": beta, "grid": ratio_grid, "log.grid": np.log(ratio_grid)}
 
 
 def retstable_ld(num=1, alpha=1.0, V0=1.0, h=1.0):

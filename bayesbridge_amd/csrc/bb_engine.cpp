@@ -1252,6 +1252,146 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
 }
 
 // ---------------------------------------------------------------------------
+// Bridge EM (restating BR::EM, Code/C/BridgeRegression.cpp:600-708, with sig = 1 and
+// tau = ratio as the EM wrapper passes them, BridgeWrapper.cpp:57-73).  X'X and X'y are
+// formed once on the device; every maximisation step assembles the masked system on the
+// device (k_em_form), factors it with the persistent Cholesky and back-solves, or runs
+// conjugate gradients (k_em_cg).  The expectation step (lambda_j, the active set, the
+// distance) is an O(p) host loop over the same order as the reference.
+// Returns the number of "solves" (total_iter) or, when every coefficient was dropped, the
+// EM iteration count (the reference's early `return iter`); -1 after an error.
+// ---------------------------------------------------------------------------
+int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, int p, double ratio,
+                 double alpha, double lambda_max, double tol, int max_iter, int use_cg) {
+    std::vector<void *> owned;
+    int ret = -1;
+    std::fill(beta_out, beta_out + p, 0.0);
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile), p_pad = round_up(p, 256);
+        double *dX = dalloc<double>((size_t)n_pad * p_pad, owned);
+        double *dy = dalloc<double>(n_pad, owned);
+        HIPCHECK(hipMemcpy2D(dX, (size_t)n_pad * sizeof(double), Xh, (size_t)n * sizeof(double),
+                             (size_t)n * sizeof(double), (size_t)p, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dy, yh, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+        // G = X'X (transpose, Gram over rows with unit weights), b = X'y
+        double *Xt = dalloc<double>((size_t)p_pad * n_pad, owned);
+        launch_transpose(0, dX, n_pad, n_pad, p_pad, Xt, p_pad);
+        double *ones = dalloc<double>(n_pad, owned);
+        {
+            std::vector<double> h1(n_pad, 1.0);
+            HIPCHECK(hipMemcpy(ones, h1.data(), n_pad * sizeof(double), hipMemcpyHostToDevice));
+        }
+        const int Sg = gram_splits_for(p_pad, n_pad);
+        const size_t gstride = (size_t)p_pad * p_pad;
+        double *sl = dalloc<double>(gstride * Sg, owned);
+        launch_gram(0, Xt, p_pad, ones, p_pad, n_pad, Sg, sl, p_pad, gstride);
+        double *G = dalloc<double>(gstride + p_pad, owned);
+        launch_slab_sum(0, sl, Sg, gstride, p_pad, nullptr, 0, G, 0);
+        double *bvec = dalloc<double>(p_pad, owned);
+        launch_coldot(0, dX, n_pad, n_pad, dy, p, bvec);
+        double *A = dalloc<double>((size_t)p_pad * (p_pad + kNB), owned);
+        double *PT = dalloc<double>((size_t)2 * kNB * (p_pad + kNB), owned);
+        double *Wd = dalloc<double>((size_t)kNB * p_pad, owned);
+        unsigned int *fl = dalloc<unsigned int>(chol_flag_words(p_pad, 1), owned);
+        double *W = dalloc<double>(p_pad, owned);
+        double *dlam = dalloc<double>(p_pad, owned);
+        int *dmask = dalloc<int>(p_pad, owned);
+        double *work = dalloc<double>((size_t)3 * p_pad, owned);
+        int *dit = dalloc<int>(1, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+
+        std::vector<int> mask(p, 1);
+        std::vector<double> nb(p_pad, 0.0), ob(p, 0.0), lam(p_pad, 0.0);
+        auto upload_mask = [&]() {
+            std::vector<int> m(p_pad, 0);
+            std::copy(mask.begin(), mask.end(), m.begin());
+            HIPCHECK(hipMemcpy(dmask, m.data(), p_pad * sizeof(int), hipMemcpyHostToDevice));
+        };
+        // direct maximisation: A = XX_act (+ c2 diag(lam)), solve by Cholesky (symsolve)
+        auto solve_direct = [&](bool with_lam) {
+            launch_em_form(0, G, p_pad, with_lam ? dlam : nullptr, dmask, bvec, p, p_pad, A,
+                           p_pad, p_pad);
+            HIPCHECK(hipMemset(de, 0, sizeof(uint32_t)));
+            chol_factor(0, A, p_pad, p_pad, 1, de, PT, Wd, fl);
+            chol_bsolve(0, A, p_pad, p_pad, Wd, A + (size_t)p_pad * p_pad, W, 1, fl, de);
+            HIPCHECK(hipGetLastError());
+            uint32_t f = 0;
+            HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+            if (f & 8u) throw HipError("symsolve: matrix is not positive definite");
+            if (f) throw HipError("device solver reported an error");
+            HIPCHECK(hipMemcpy(nb.data(), W, p_pad * sizeof(double), hipMemcpyDeviceToHost));
+        };
+        const double sig = 1.0, tau = ratio;
+        const double c1 = alpha * std::exp((2 - alpha) * (std::log(tau) - std::log(sig)));
+        const double c2 = std::exp(-2 * (std::log(tau) - std::log(sig)));
+        int pa = p;             // active count
+        long total_iter = p;    // the first symsolve
+        upload_mask();
+        solve_direct(false);    // one maximisation step with A = X'X
+        double dist = tol + 1.0;
+        int iter = 0;
+        while (dist > tol && iter < max_iter) {
+            // expectation step over the active coordinates, in order
+            int num = 0;
+            for (int j = 0; j < p; ++j) {
+                if (!mask[j]) continue;
+                const double l = c1 * std::exp((alpha - 2) * std::log(std::fabs(nb[j])));
+                if (l < lambda_max) {
+                    lam[j] = c2 * l;
+                    ob[j] = nb[j];
+                    ++num;
+                } else {
+                    mask[j] = 0;
+                }
+            }
+            if (num < pa) {
+                if (num == 0) {
+                    ret = iter;
+                    for (void *q : owned) (void)hipFree(q);
+                    owned.clear();
+                    return ret;
+                }
+                pa = num;
+                upload_mask();
+            }
+            HIPCHECK(hipMemcpy(dlam, lam.data(), p_pad * sizeof(double), hipMemcpyHostToDevice));
+            if (!use_cg) {
+                solve_direct(true);
+                total_iter += pa;
+            } else {
+                // x0 = old beta on the active set (0 elsewhere)
+                std::vector<double> x0(p_pad, 0.0);
+                for (int j = 0; j < p; ++j)
+                    if (mask[j]) x0[j] = ob[j];
+                HIPCHECK(hipMemcpy(W, x0.data(), p_pad * sizeof(double), hipMemcpyHostToDevice));
+                launch_em_form(0, G, p_pad, dlam, dmask, bvec, p, p_pad, A, p_pad, p_pad);
+                launch_em_cg(0, A, p_pad, p_pad, A + (size_t)p_pad * p_pad, W, tol, pa, work,
+                             dit);
+                HIPCHECK(hipGetLastError());
+                int it = 0;
+                HIPCHECK(hipMemcpy(&it, dit, sizeof(int), hipMemcpyDeviceToHost));
+                HIPCHECK(hipMemcpy(nb.data(), W, p_pad * sizeof(double), hipMemcpyDeviceToHost));
+                total_iter += it;
+            }
+            double d2 = 0.0;
+            for (int j = 0; j < p; ++j)
+                if (mask[j]) d2 += (nb[j] - ob[j]) * (nb[j] - ob[j]);
+            dist = std::sqrt(d2);
+            ++iter;
+        }
+        for (int j = 0; j < p; ++j) beta_out[j] = mask[j] ? nb[j] : 0.0;
+        ret = (int)total_iter;
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        std::fill(beta_out, beta_out + p, 0.0);
+        ret = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return ret;
+}
+
+// ---------------------------------------------------------------------------
 // Reference .C entry points
 // ---------------------------------------------------------------------------
 void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num) {
@@ -1259,6 +1399,22 @@ void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num) {
     next_call_key(&k0, &k1);
     int rc = bb_retstable_batch(x, alpha, V0, h, *num, k0, k1, 0, 0);
     if (rc != 0) fprintf(stderr, "Error: retstable_LD: %s\n", g_last_error.c_str());
+}
+
+// BridgeWrapper.cpp:544-568 (decl. BridgeWrapper.h:166-176); R passes use.cg through
+// as.integer, so it is read as int (BridgeWrapper.R:116-123).  max_iter returns the number
+// of solves; errors print as the reference's EM wrapper does (BridgeWrapper.cpp:64-70).
+void bridge_EM(double *betap, const double *yp, const double *Xp, const double *ratio,
+               const double *alpha, const int *P, const int *N, const double *lambda_max,
+               const double *tol, int *max_iter, const int *use_cg) {
+    if (*use_cg && g_verbose) printf("Using conjugate gradient method.\n");
+    const int it = bb_bridge_em(betap, yp, Xp, *N, *P, *ratio, *alpha, *lambda_max, *tol,
+                                *max_iter, *use_cg);
+    if (it < 0) {
+        printf("Error: %s\n", g_last_error.c_str());
+        printf("Aborting EM.\n");
+    }
+    *max_iter = it;
 }
 
 void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,

@@ -86,6 +86,13 @@ void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const do
 
 // A (upper) = G + diag(lambda sig2 / tau^2) (or G alone if lam == nullptr); column
 // rhs_col = c.  Padding: identity.
+// Bridge EM maximisation system over the p_pad index space (mask 0 / padding coordinates
+// become identity rows with a zero right-hand side); dlam = c2 lam per coordinate or null.
+void launch_em_form(hipStream_t s, const double *G, int ldg, const double *dlam, const int *mask,
+                    const double *b, int p, int p_pad, double *A, int lda, int rhs_col);
+// Conjugate gradients on that system from x (in/out); work: 3 n doubles; *out_it = iterations.
+void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *b, double *x,
+                  double tol, int max_it, double *work, int *out_it);
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
                    int rhs_col);

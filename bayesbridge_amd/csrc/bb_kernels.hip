@@ -119,10 +119,8 @@ void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const
 
 // lambda_j = 2 retstable(beta_j^2 / tau^2, alpha / 2, 1)   (BridgeRegression.cpp:506-510);
 // Woodbury mode also forms D_j = tau^2 / lambda_j and u_j = sqrt(D_j) z_j.
-// OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained).
-template <int G, bool NI = (BB_STABLE_NOINLINE != 0), int OCC = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void k_lambda(
-    const double *beta, int p_loc, int p_pad,
+template <int G, bool NI = (BB_STABLE_NOINLINE != 0)>
+__global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, int p_pad,
                                                 uint64_t j0, const DevScalars *sc, Key key,
                                                 uint64_t t, int mode, double *lam, double *D,
                                                 double *u, double *lam_trace, uint32_t *err) {
@@ -193,14 +191,6 @@ void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevSc
         if (noinline == 1)                                                                    \
             k_lambda<G, true><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,   \
                                                      lam, nullptr, nullptr, nullptr, err);    \
-        else if (noinline == 2)                                                               \
-            k_lambda<G, false, 2><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t,            \
-                                                         LAMBDA_ONLY, lam, nullptr, nullptr,  \
-                                                         nullptr, err);                       \
-        else if (noinline == 4)                                                               \
-            k_lambda<G, false, 4><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t,            \
-                                                         LAMBDA_ONLY, lam, nullptr, nullptr,  \
-                                                         nullptr, err);                       \
         else                                                                                  \
             k_lambda<G, false><<<blocks, 256, 0, s>>>(beta, p, p, 0, sc, key, t, LAMBDA_ONLY,  \
                                                       lam, nullptr, nullptr, nullptr, err);   \
@@ -565,6 +555,116 @@ __global__ __launch_bounds__(256) void k_form_a(const double *G, int ldg, const 
     } else {
         *dst = 0.0;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Bridge EM (BridgeRegression.cpp:600-708): the maximisation step's system for the
+// active coordinates, A = XX_active + c2 diag(lam_active), b_active, laid out over the
+// full p_pad index space with every dropped (mask 0) or padding coordinate as an identity
+// row/column and a zero right-hand side -- the active block's elimination is then exactly
+// the one of the compacted system, and the dropped unknowns solve to 0.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_em_form(const double *G, int ldg, const double *dlam,
+                                                 const int *mask, const double *b, int p,
+                                                 int p_pad, double *A, int lda, int rhs_col) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t tot = (size_t)p_pad * (p_pad + kNB);
+    if (idx >= tot) return;
+    const int r = (int)(idx % p_pad), c = (int)(idx / p_pad);
+    double *dst = A + (size_t)r + (size_t)c * lda;
+    const bool ar = r < p && mask[r];
+    if (c < p_pad) {
+        if (r <= c) {
+            const bool ac = c < p && mask[c];
+            double v;
+            if (ar && ac)
+                v = G[(size_t)r + (size_t)c * ldg] + (r == c && dlam ? dlam[r] : 0.0);
+            else
+                v = (r == c) ? 1.0 : 0.0;
+            *dst = v;
+        }
+    } else if (c == rhs_col) {
+        *dst = ar ? b[r] : 0.0;
+    } else {
+        *dst = 0.0;
+    }
+}
+
+void launch_em_form(hipStream_t s, const double *G, int ldg, const double *dlam, const int *mask,
+                    const double *b, int p, int p_pad, double *A, int lda, int rhs_col) {
+    const size_t tot = (size_t)p_pad * (p_pad + kNB);
+    k_em_form<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(G, ldg, dlam, mask, b, p, p_pad, A,
+                                                            lda, rhs_col);
+}
+
+// Conjugate gradients on the masked system (upper triangle of A, column-major), one
+// workgroup: r = b - A x, d = r; while it < max_it and |r| > tol: a = r.r / d.Ad,
+// x += a d, r -= a Ad, d = r + (r'.r' / r.r) d.  Dot products are fixed-order block trees,
+// so the iteration count and the result are deterministic.  out_it = iterations taken.
+constexpr int kEmCgThreads = 1024;
+
+__device__ double em_block_dot(const double *u, const double *v, int n, double *sh) {
+    double a = 0.0;
+    for (int i = threadIdx.x; i < n; i += kEmCgThreads) a += u[i] * v[i];
+    a = wave_allsum(a);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[w] = a;
+    __syncthreads();
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < kEmCgThreads / 64; ++i) r += sh[i];
+    return r;  // every thread
+}
+
+__device__ void em_matvec(const double *A, int lda, int n, const double *v, double *out) {
+    for (int r = threadIdx.x; r < n; r += kEmCgThreads) {
+        double a = 0.0;
+        for (int c = 0; c < n; ++c) {
+            const double m = c >= r ? A[(size_t)r + (size_t)c * lda] : A[(size_t)c + (size_t)r * lda];
+            a += m * v[c];
+        }
+        out[r] = a;
+    }
+}
+
+__global__ __launch_bounds__(kEmCgThreads) void k_em_cg(const double *A, int lda, int n,
+                                                        const double *b, double *x, double tol,
+                                                        int max_it, double *work, int *out_it) {
+    __shared__ double sh[kEmCgThreads / 64];
+    double *r = work, *d = work + n, *ad = work + 2 * (size_t)n;
+    em_matvec(A, lda, n, x, ad);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kEmCgThreads) {
+        r[i] = b[i] - ad[i];
+        d[i] = r[i];
+    }
+    __syncthreads();
+    double rr = em_block_dot(r, r, n, sh);
+    int it = 0;
+    while (it < max_it && sqrt(rr) > tol) {
+        em_matvec(A, lda, n, d, ad);
+        __syncthreads();
+        const double dad = em_block_dot(d, ad, n, sh);
+        const double a = rr / dad;
+        for (int i = threadIdx.x; i < n; i += kEmCgThreads) {
+            x[i] += a * d[i];
+            r[i] -= a * ad[i];
+        }
+        __syncthreads();
+        const double rn = em_block_dot(r, r, n, sh);
+        const double bt = rn / rr;
+        for (int i = threadIdx.x; i < n; i += kEmCgThreads) d[i] = r[i] + bt * d[i];
+        __syncthreads();
+        rr = rn;
+        ++it;
+    }
+    if (threadIdx.x == 0) *out_it = it;
+}
+
+void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *b, double *x,
+                  double tol, int max_it, double *work, int *out_it) {
+    k_em_cg<<<1, kEmCgThreads, 0, s>>>(A, lda, n, b, x, tol, max_it, work, out_it);
 }
 
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,

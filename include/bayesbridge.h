@@ -60,6 +60,18 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
  */
 void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num);
 
+/*
+ * Bridge EM point estimate (sig = 1, tau = ratio): replaces Code/C/BridgeWrapper.cpp:544-568
+ * (decl. BridgeWrapper.h:166-176; algorithm BR::EM, BridgeRegression.cpp:600-708), called
+ * by bridge.EM (BridgeWrapper.R:89-133) and trace.beta (bridge-trace.R).  betap (P) gets
+ * the estimate; max_iter is the iteration cap on entry and the number of solves on return
+ * (-1 after an error, which prints "Aborting EM.").  `use_cg` is declared `const bool*`
+ * in the reference but R passes as.integer(use.cg); it is read as an int.
+ */
+void bridge_EM(double *betap, const double *yp, const double *Xp, const double *ratio,
+               const double *alpha, const int *P, const int *N, const double *lambda_max,
+               const double *tol, int *max_iter, const int *use_cg);
+
 /* ------------------------------------------------------------------------ */
 /* Part 2: extensions                                                        */
 /* ------------------------------------------------------------------------ */
@@ -233,6 +245,11 @@ int bb_gram_ozaki(double *C, const double *Y, const double *w, int n, int k);
 /* SPD solve via the blocked device Cholesky: A (m x m, column-major, only the
  * upper triangle read) -> x = A^-1 b for nrhs right-hand sides (m x nrhs). */
 int bb_chol_solve(double *x, const double *A, const double *b, int m, int nrhs);
+
+/* bridge_EM without the .C marshalling: returns the solve count (as bridge_EM's max_iter),
+ * the EM iteration count when every coefficient was dropped, or -1 (bb_last_error()). */
+int bb_bridge_em(double *beta, const double *y, const double *X, int n, int p, double ratio,
+                 double alpha, double lambda_max, double tol, int max_iter, int use_cg);
 
 #ifdef __cplusplus
 }

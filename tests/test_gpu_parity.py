@@ -406,3 +406,59 @@ def test_rccl_one_rank_communicator_is_identity(gpu_lib):
         e.close()
     for k in ("beta", "lambda", "sig2", "tau"):
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+# ---------------------------------------------------------------------------------------
+# Bridge EM (.C bridge_EM, BridgeRegression.cpp:600-708) against oracle/em.py
+# ---------------------------------------------------------------------------------------
+def _em_case(n, p, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, p))
+    b = np.zeros(p)
+    k = max(3, p // 10)
+    b[:k] = rng.choice([-1.0, 1.0], k) * rng.uniform(0.5, 3, k)
+    y = X @ b + rng.standard_normal(n)
+    return X, y
+
+
+@pytest.mark.parametrize("n,p,ratio", [(200, 12, 0.3), (300, 150, 0.05), (442, 10, 2.0)])
+def test_bridge_em_direct_matches_oracle(gpu_lib, n, p, ratio):
+    """Direct (Cholesky) maximisation steps: same active sets, same solve count, estimates
+    within 1e-9 relative (the device Cholesky's summation order differs from LAPACK's)."""
+    from oracle import em
+    bb = gpu_lib
+    X, y = _em_case(n, p, n + p)
+    tol = 1e-9
+    g = bb.bridge_em(y, X, alpha=0.5, ratio=ratio, lambda_max=ratio / tol, tol=tol,
+                     max_iter=30, ret_solves=True)
+    o, solves = em.bridge_em(y, X, ratio, 0.5, ratio / tol, tol, 30)
+    assert g["num.solves"] == solves
+    assert np.array_equal(g["beta"] == 0, o == 0)
+    scale = np.max(np.abs(o))
+    assert np.max(np.abs(g["beta"] - o)) <= 1e-9 * scale
+
+
+def test_bridge_em_cg_matches_oracle(gpu_lib):
+    """CG maximisation steps (parity unpinned: the reference's cg is un-vendored; both sides
+    run the textbook iteration), to the CG tolerance."""
+    from oracle import em
+    bb = gpu_lib
+    X, y = _em_case(250, 40, 3)
+    g = bb.bridge_em(y, X, alpha=0.5, ratio=0.2, lambda_max=0.2 / 1e-9, tol=1e-10,
+                     max_iter=60, use_cg=True, ret_solves=True)
+    o, solves = em.bridge_em(y, X, 0.2, 0.5, 0.2 / 1e-9, 1e-10, 60, use_cg=True)
+    assert np.array_equal(g["beta"] == 0, o == 0)
+    assert np.max(np.abs(g["beta"] - o)) <= 1e-6 * np.max(np.abs(o))
+    assert abs(g["num.solves"] - solves) <= 0.1 * solves + 5
+
+
+def test_bridge_em_all_dropped_and_trace(gpu_lib):
+    bb = gpu_lib
+    X, y = _em_case(120, 8, 5)
+    g = bb.bridge_em(y, X, alpha=0.5, ratio=1.0, lambda_max=1e-300, ret_solves=True)
+    assert g["num.solves"] == 0 and not g["beta"].any()
+    tr = bb.trace_beta(y, X, ratio_grid=np.exp(np.arange(-4.0, 4.01, 2.0)))
+    assert tr["beta"].shape == (5, 8)
+    # more shrinkage at smaller ratio: the L1 norm grows along the grid
+    l1 = np.abs(tr["beta"]).sum(axis=1)
+    assert np.all(np.diff(l1) >= -1e-9 * l1.max())

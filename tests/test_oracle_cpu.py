@@ -221,3 +221,64 @@ def test_ortho_chain_matches_dense_on_orthogonal_design():
     for j in range(4):
         se = math.hypot(_batch_means_se(o1["beta"][j]), _batch_means_se(o2["beta"][j]))
         assert abs(o1["beta"][j].mean() - o2["beta"][j].mean()) < 5 * se + 1e-3
+
+
+# ---------------------------------------------------------------------------------------
+# Bridge EM oracle (oracle/em.py, restating BridgeRegression.cpp:600-708)
+# ---------------------------------------------------------------------------------------
+def _em_problem(n=200, p=12, seed=11):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, p))
+    b = np.zeros(p)
+    b[:4] = [3.0, -2.0, 1.5, 0.02]
+    y = X @ b + rng.standard_normal(n)
+    return X, y
+
+
+def test_em_large_ratio_is_least_squares():
+    """tau large against O(1) coefficients: the penalty c2 lambda_j = alpha tau^-alpha
+    |beta_j|^(alpha-2) is ~5e-5 against X'X's ~200 diagonal, so EM stops next to OLS."""
+    from oracle import em
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((200, 12))
+    b = rng.choice([-1.0, 1.0], 12) * rng.uniform(1, 3, 12)
+    y = X @ b + rng.standard_normal(200)
+    beta, solves = em.bridge_em(y, X, ratio=1e8, alpha=0.5, lambda_max=1e300, tol=1e-12,
+                                max_iter=50)
+    ls = np.linalg.lstsq(X, y, rcond=None)[0]
+    assert np.allclose(beta, ls, rtol=1e-5, atol=0)
+    assert solves >= 2 * X.shape[1]
+
+
+def test_em_fixed_point_is_stationary():
+    """At convergence the active set satisfies (X'X + c2 diag(lambda(beta))) beta = X'y."""
+    from oracle import em
+    X, y = _em_problem()
+    ratio, alpha = 0.05, 0.5
+    beta, _ = em.bridge_em(y, X, ratio, alpha, lambda_max=ratio / 1e-9, tol=1e-13,
+                           max_iter=500)
+    act = beta != 0
+    assert 0 < act.sum() < X.shape[1]  # shrinkage drops the null coordinates
+    c1 = alpha * ratio ** (2 - alpha)
+    c2 = ratio ** -2
+    lam = c1 * np.abs(beta[act]) ** (alpha - 2)
+    Xa = X[:, act]
+    r = (Xa.T @ Xa + np.diag(c2 * lam)) @ beta[act] - Xa.T @ y
+    assert np.max(np.abs(r)) < 1e-6 * np.max(np.abs(Xa.T @ y))
+
+
+def test_em_cg_matches_direct():
+    from oracle import em
+    X, y = _em_problem()
+    bd, _ = em.bridge_em(y, X, 0.3, 0.5, 0.3 / 1e-9, 1e-10, 100)
+    bc, _ = em.bridge_em(y, X, 0.3, 0.5, 0.3 / 1e-9, 1e-10, 100, use_cg=True)
+    assert np.allclose(bc, bd, rtol=1e-6, atol=1e-8)
+
+
+def test_em_all_dropped_returns_iteration_count():
+    """lambda_max below every lambda: beta = 0 and the EM iteration count (0) is returned
+    (the reference's early `return iter`, BridgeRegression.cpp:654-657)."""
+    from oracle import em
+    X, y = _em_problem()
+    beta, it = em.bridge_em(y, X, 1.0, 0.5, lambda_max=1e-300, tol=1e-9, max_iter=30)
+    assert it == 0 and not beta.any()
