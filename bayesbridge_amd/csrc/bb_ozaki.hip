@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "bb_kernels.h"
 #include "bb_ozaki.h"
@@ -649,9 +650,148 @@ __global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restri
             }
 }
 
+// ---------------------------------------------------------------------------
+// Register-staged variant of k_oz_gemm16 (BB_OZ_SHAPE=16r): each wave moves its 8 KB of a
+// chunk with 8 plain global_load_dwordx4 into a 2-deep register ring and 8 ds_write_b128
+// into a 2-stage LDS ring (64 KB), instead of 8 LDS-DMA pieces (whose issue cost beside
+// MFMAs is 60-185 cycles each, MI355X_MICROARCH.md).  Step it: MFMAs on chunk it (frags in
+// registers), fragment reads of chunk it+1 (LDS stage (it+1)%2), ds_write of chunk it+2
+// (ring slot it%2, loaded two steps ago) into stage it%2, then the loads of chunk it+4 into
+// the slot just written.  Piece g's write waits for its load with 15 loads still in flight
+// (the rest of chunk it+2, all of chunk it+3, pieces < g of chunk it+4).
+// ---------------------------------------------------------------------------
+template <int dbg>
+__global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict__ R, int n_oz,
+                                                       int nkc, int nsplit,
+                                                       int8_t *__restrict__ P, OzConsts C) {
+    __shared__ __attribute__((aligned(1024))) int8_t smem[2 * kOzStageBytes];
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int u = xcd + 8 * (q / ntiles);
+    const int tile = q % ntiles;
+    const int mod = u % kOzMods;
+    const int split = u / kOzMods;
+    if (split >= nsplit) return;
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    I = __builtin_amdgcn_readfirstlane(I);
+    const int K = tile - I * (I + 1) / 2;
+    const int per = (nkc + nsplit - 1) / nsplit;
+    const int c0 = split * per;
+    const int nch = max(0, min(nkc, c0 + per) - c0);
+    const size_t kstride = (size_t)n_oz * kOzKC;
+    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
+    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid >> 1, wc = wid & 1;
+    const int voff = wid * 4096 + lane * 16;
+
+    // piece g: operand g >> 2, 16-row block 4 wid + (g & 3); chunk index clamped to the split
+    auto gload = [&](int it, int g) -> v4i {
+        const int kc = c0 + min(it, nch - 1);
+        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
+        return *(const v4i *)(src + voff);
+    };
+    auto lwrite = [&](int it, int g, v4i v) {
+        int8_t *dst = smem + (it & 1) * kOzStageBytes + (g >> 2) * kOzOpBytes + voff + (g & 3) * 1024;
+        *(v4i *)dst = v;
+    };
+
+    v4i acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+
+    auto frag_a = [&](int chunk, int i) {
+        const int8_t *A_ = smem + (chunk & 1) * kOzStageBytes;
+        return *(const v4i *)&A_[(wr * 8 + i) * 1024 + lane * 16];
+    };
+    auto frag_b = [&](int chunk, int j) {
+        const int8_t *B_ = smem + (chunk & 1) * kOzStageBytes + kOzOpBytes;
+        return *(const v4i *)&B_[(wc * 8 + j) * 1024 + lane * 16];
+    };
+    v4i ring0[8], ring1[8];
+    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[8], v4i (&fa_n)[8], v4i (&fb_n)[8],
+                    v4i (&rg)[8]) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            oz_mfma16(acc[g][0], fa_c[g], fb_c[0]);
+            if (!(dbg & 1)) lwrite(it + 2, g, rg[g]);
+            oz_mfma16(acc[g][1], fa_c[g], fb_c[1]);
+            if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
+            oz_mfma16(acc[g][2], fa_c[g], fb_c[2]);
+            if (!(dbg & 1)) rg[g] = gload(it + 4, g);
+            oz_mfma16(acc[g][3], fa_c[g], fb_c[3]);
+            if (!(dbg & 2)) fb_n[g] = frag_b(it + 1, g);
+            oz_mfma16(acc[g][4], fa_c[g], fb_c[4]);
+            oz_mfma16(acc[g][5], fa_c[g], fb_c[5]);
+            oz_mfma16(acc[g][6], fa_c[g], fb_c[6]);
+            oz_mfma16(acc[g][7], fa_c[g], fb_c[7]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    v4i fa0[8], fb0[8], fa1[8], fb1[8];
+    if (nch > 0) {
+        // chunks 0, 1 -> LDS stages 0, 1; chunks 2, 3 -> ring slots 0, 1
+#pragma unroll
+        for (int g = 0; g < 8; ++g) ring0[g] = gload(0, g);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) ring1[g] = gload(1, g);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) lwrite(0, g, ring0[g]);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) lwrite(1, g, ring1[g]);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) ring0[g] = gload(2, g);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) ring1[g] = gload(3, g);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fa0[i] = frag_a(0, i);
+            fb0[i] = frag_b(0, i);
+        }
+    }
+    int it = 0;
+    for (; it + 1 < nch; it += 2) {
+        step(it, fa0, fb0, fa1, fb1, ring0);
+        step(it + 1, fa1, fb1, fa0, fb0, ring1);
+    }
+    if (it < nch) step(it, fa0, fb0, fa1, fb1, ring0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
+    const int m = C.m[mod];
+    const double im = C.inv_m[mod];
+    const int hi = m / 2, lo = hi - m + 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rowl = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+                const int col = wc * 128 + j * 16 + (lane & 15);
+                const int cval = acc[i][j][r];
+                int rr = cval - (int)rint((double)cval * im) * m;
+                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
+                out[rowl * kOzT + col] = (int8_t)rr;
+            }
+}
+
 static int oz_shape() {
     static const int s = [] {
         const char *e = getenv("BB_OZ_SHAPE");
+        if (e && std::strcmp(e, "16r") == 0) return 17;  // register-staged 16x16x64
         return e ? atoi(e) : 16;
     }();
     return s;
@@ -666,6 +806,15 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
     const unsigned g = ntiles * kOzMods * nsplit;
     const OzConsts &C = oz_consts();
     const int shape = oz_shape();
+    if (shape == 17) {
+        switch (dbg) {
+            case 1: k_oz_gemm16r<1><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 2: k_oz_gemm16r<2><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 3: k_oz_gemm16r<3><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            default: k_oz_gemm16r<0><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
+        }
+        return;
+    }
     if (shape == 16 || shape == 8) {
         const int nw = shape == 8 ? 8 : 4;
 #define BB_OZ16(D, W) k_oz_gemm16<D, W, kOzStages16><<<g, W * 64, 0, s>>>(R, n_oz, nkc, nsplit, P, C)
