@@ -329,6 +329,38 @@ def test_teacher_forced_sweep_large(gpu_lib, n, p, gram_mode):
     e.close()
 
 
+def test_teacher_forced_bench_workload(gpu_lib):
+    """The benchmarked workload itself -- C3 (n = 2000, p = 50000) with bench.py's synthetic
+    X, y and sampler key, Ozaki-II Gram -- three sweeps, each teacher-forced from the oracle
+    state of the previous one (SURVEY 8(d) inputs; one oracle sweep is ~1 s of numpy)."""
+    import bench
+    bb = gpu_lib
+    n, p = 2000, 50000
+    X = bench.make_columns(n, 0, p)
+    y, btrue = bench.make_problem_y(n, p)
+    cfg = bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, trace_capacity=2,
+                          gram_mode=bb.GRAM_OZAKI)
+    e = bb.Engine(cfg, X, y)
+    assert e.method() == 2
+    e.init_state()
+    rng = np.random.default_rng(2)
+    beta, tau, sig2 = btrue + 0.01 * rng.standard_normal(p), 1.0, 1.0
+    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
+    for t in (101, 102, 103):
+        e.set_state(beta, tau, sig2, 0.5)
+        e.run(t, 1, first_slot=0, slot_step=0)
+        s = e.state()
+        b, lam, tau, sig2 = teacher_forced_sweep(X, y, beta, tau, sig2, 0.5, t, SEED, 0, hyper)
+        assert abs(s["tau"] - tau) / tau < 1e-12, t
+        assert abs(s["sig2"] - sig2) / sig2 < 1e-12, t
+        assert flips(s["lambda"], lam) == 0, t
+        assert np.max(np.abs(s["lambda"] - lam) / lam) < 1e-11, t
+        assert rel_err(s["beta"], b) < 1e-9, t
+        beta = b
+    assert e.error_flags() == 0
+    e.close()
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_shard_group_matches_single_engine(gpu_lib, world):
     """The column-sharded sweep (two exchanges per sweep) on one GPU vs the unsharded
