@@ -864,23 +864,23 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
                                                 const double *__restrict__ xu_part, int nxu,
                                                 double *__restrict__ red2, OzConsts C) {
     const int ntiles = nt * (nt + 1) / 2;
-    const long nquad = (long)ntiles * kOzT * kOzT / 4;
-    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= nquad) {
-        const long r = gid - nquad;
-        if (r < n_pad) {
-            // 8 interleaved partial sums (fixed order): 8 loads in flight per round trip
-            double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            int q = 0;
-            for (; q + 8 <= nxu; q += 8)
-#pragma unroll
-                for (int t = 0; t < 8; ++t) v[t] += xu_part[(size_t)(q + t) * n_pad + r];
-            for (int t = 0; q < nxu; ++q, ++t) v[t] += xu_part[(size_t)q * n_pad + r];
-            red2[tri_count(n_pad) + r] =
-                ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-        }
+    // the first blocks sum the X.u partials (a long dependent-load chain per row: started
+    // first, it overlaps the residue reconstruction instead of trailing it), 8 lanes per row
+    const int nxb = (n_pad * 8 + 255) / 256;
+    if ((int)blockIdx.x < nxb) {
+        const int t = threadIdx.x & 7;
+        const long r = ((long)blockIdx.x * 256 + threadIdx.x) >> 3;
+        double v = 0.0;
+        if (r < n_pad)
+            for (int q = t; q < nxu; q += 8) v += xu_part[(size_t)q * n_pad + r];
+        // fixed-order combine of the 8 lane sums
+        v += __shfl_xor(v, 4, 8);
+        v += __shfl_xor(v, 2, 8);
+        v += __shfl_xor(v, 1, 8);
+        if (t == 0 && r < n_pad) red2[tri_count(n_pad) + r] = v;
         return;
     }
+    const long gid = (long)(blockIdx.x - nxb) * 256 + threadIdx.x;
     const int tile = (int)(gid >> 14);
     const int e0 = (int)(gid & 16383) * 4;  // 4 consecutive columns of one tile row
     int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
@@ -938,31 +938,40 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
             if (k == 0) {
                 a[0] = r;
             } else {
+                // |a_j| <= 123, Pmod < 247, k <= 15 terms: |acc| < 2^19, so the 24-bit
+                // full-rate multiplies are exact
                 int acc = 0;
 #pragma unroll
-                for (int j = 0; j < k; ++j) acc += a[j] * kOzTab.Pmod[j][k];
+                for (int j = 0; j < k; ++j) acc += __mul24(a[j], kOzTab.Pmod[j][k]);
                 const int sk = oz_smod(acc, kOzTab.m[k], kOzTab.inv_mf[k]);
-                a[k] = oz_smod((r - sk) * kOzTab.invP[k], kOzTab.m[k], kOzTab.inv_mf[k]);
+                a[k] = oz_smod(__mul24(r - sk, kOzTab.invP[k]), kOzTab.m[k], kOzTab.inv_mf[k]);
             }
         }
-        __int128 X = a[kOzMods - 1];
+        // mixed-radix Horner C = a_0 + m_0 (a_1 + m_1 (a_2 + ...)) in double-double: hi m
+        // splits exactly into p + e (FMA), the rest is two-summed in, so (hi, lo) carries
+        // ~106 bits -- every step is exact while the partial value is an integer below 2^53,
+        // and C (< 2^124) comes out faithfully rounded
+        double hi = (double)a[kOzMods - 1], lo = 0.0;
 #pragma unroll
-        for (int k = kOzMods - 2; k >= 0; --k) X = X * (__int128)kOzTab.m[k] + (__int128)a[k];
-        const bool neg = X < 0;
-        if (neg) X = -X;
-        const unsigned long long hi = (unsigned long long)(X >> 64);
-        const unsigned long long lo = (unsigned long long)X;
-        double v = __builtin_fma((double)hi, 18446744073709551616.0, (double)lo);
-        v = neg ? -v : v;
-        red2[tri_index(gk, gi)] = ldexp(v, ei + escale[gk]);
+        for (int k = kOzMods - 2; k >= 0; --k) {
+            const double m = (double)kOzTab.m[k];
+            const double p = hi * m;
+            const double e = __builtin_fma(hi, m, -p);
+            const double t = __builtin_fma(lo, m, e + (double)a[k]);
+            const double s2 = p + t;
+            const double bp = s2 - p;
+            lo = (p - (s2 - bp)) + (t - bp);
+            hi = s2;
+        }
+        red2[tri_index(gk, gi)] = ldexp(hi + lo, ei + escale[gk]);
     }
 }
 
 void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
                    const int *escale, const double *xu_part, int nxu, double *red2) {
     const int nt = n_oz / kOzT;
-    const long ntot = (long)(nt * (nt + 1) / 2) * kOzT * kOzT / 4 + n_pad;
-    const unsigned g = (unsigned)((ntot + 255) / 256);
+    const long nquad = (long)(nt * (nt + 1) / 2) * kOzT * kOzT / 4;
+    const unsigned g = (unsigned)((nquad + 255) / 256 + (n_pad * 8 + 255) / 256);
     const OzConsts &C = oz_consts();
     switch (nsplit) {
         case 1: k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C); break;
