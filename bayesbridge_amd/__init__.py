@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = [
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
     "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode", "bb_bench_ozaki",
-    "bridge_EM", "bb_bridge_em",
+    "bridge_EM", "bb_bridge_em", "bb_bridge_em_batch",
 ]
 
 
@@ -129,6 +129,8 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bridge_EM.argtypes = [_dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _ip, _ip]
     L.bb_bridge_em.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int, c.c_double, c.c_double,
                                c.c_double, c.c_double, c.c_int, c.c_int]
+    L.bb_bridge_em_batch.argtypes = [_dp, _ip, _dp, _dp, c.c_int, c.c_int, _dp, _dp, c.c_int,
+                                     c.c_double, c.c_double, c.c_int]
     _lib = L
     return L
 
@@ -315,11 +317,39 @@ def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=F
         ratio_grid = np.exp(np.arange(-20.0, 20.0 + 1e-9, 0.1))
     ratio_grid = np.asarray(ratio_grid, dtype=np.float64)
     X = np.asarray(X, dtype=np.float64)
-    beta = np.zeros((ratio_grid.size, X.shape[1]))
-    for i, r in enumerate(ratio_grid):
-        beta[i] = bridge_em(y, X, alpha, ratio=r, lambda_max=r / tol, tol=tol,
-                            max_iter=max_iter, use_cg=use_cg)
+    if X.ndim == 1:
+        X = X[:, None]
+    P = X.shape[1]
+    if 1 <= P <= 64 and not use_cg:
+        # the whole grid in one device launch (a workgroup per ratio)
+        beta, _ = bridge_em_batch(y, X, ratio_grid, alpha=alpha,
+                                  lambda_max=ratio_grid / tol, tol=tol, max_iter=max_iter)
+    else:
+        beta = np.zeros((ratio_grid.size, P))
+        for i, r in enumerate(ratio_grid):
+            beta[i] = bridge_em(y, X, alpha, ratio=r, lambda_max=r / tol, tol=tol,
+                                max_iter=max_iter, use_cg=use_cg)
     return {"beta": beta, "grid": ratio_grid, "log.grid": np.log(ratio_grid)}
+
+
+def bridge_em_batch(y, X, ratios, alpha=0.5, lambda_max=None, tol=1e-9, max_iter=30):
+    """bridge.EM (direct solves) for every ratio in one device launch, p <= 64.
+    Returns (beta (len(ratios) x P), solves (len(ratios)))."""
+    L = library()
+    _require_gpu()
+    y = np.ascontiguousarray(np.asarray(y, dtype=np.float64).ravel())
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    ratios = np.ascontiguousarray(ratios, dtype=np.float64)
+    if lambda_max is None:
+        lambda_max = 1e9 * ratios
+    lmax = np.ascontiguousarray(np.broadcast_to(lambda_max, ratios.shape), dtype=np.float64)
+    N, P = X.shape
+    beta = np.zeros((ratios.size, P))
+    solves = np.zeros(ratios.size, dtype=np.int32)
+    _check(L.bb_bridge_em_batch(_p(beta), solves.ctypes.data_as(_ip), _p(y), _p(X), N, P,
+                                _p(ratios), _p(lmax), ratios.size, float(alpha), float(tol),
+                                int(max_iter)), "bb_bridge_em_batch")
+    return beta, solves
 
 
 def retstable_ld(num=1, alpha=1.0, V0=1.0, h=1.0):

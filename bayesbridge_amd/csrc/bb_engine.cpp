@@ -1391,6 +1391,57 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
     return ret;
 }
 
+// Batched EM over `count` ratios (trace.beta) for p <= 64, direct solves: X'X and X'y
+// once, then one launch in which a workgroup per ratio runs the whole EM (k_em_batch).
+// beta: count x p (row r = ratio r); solves: count (as bb_bridge_em returns, -1 on a
+// non positive-definite system).  Returns 0, or -1 with bb_last_error().
+int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double *Xh, int n,
+                       int p, const double *ratios, const double *lambda_max, int count,
+                       double alpha, double tol, int max_iter) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        if (p < 1 || p > 64) throw HipError("bb_bridge_em_batch: needs 1 <= p <= 64");
+        if (count < 1) throw HipError("bb_bridge_em_batch: empty ratio grid");
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile), p_pad = round_up(p, 256);
+        double *dX = dalloc<double>((size_t)n_pad * p_pad, owned);
+        double *dy = dalloc<double>(n_pad, owned);
+        HIPCHECK(hipMemcpy2D(dX, (size_t)n_pad * sizeof(double), Xh, (size_t)n * sizeof(double),
+                             (size_t)n * sizeof(double), (size_t)p, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dy, yh, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+        double *Xt = dalloc<double>((size_t)p_pad * n_pad, owned);
+        launch_transpose(0, dX, n_pad, n_pad, p_pad, Xt, p_pad);
+        double *ones = dalloc<double>(n_pad, owned);
+        {
+            std::vector<double> h1(n_pad, 1.0);
+            HIPCHECK(hipMemcpy(ones, h1.data(), n_pad * sizeof(double), hipMemcpyHostToDevice));
+        }
+        const int Sg = gram_splits_for(p_pad, n_pad);
+        const size_t gstride = (size_t)p_pad * p_pad;
+        double *sl = dalloc<double>(gstride * Sg, owned);
+        launch_gram(0, Xt, p_pad, ones, p_pad, n_pad, Sg, sl, p_pad, gstride);
+        double *G = dalloc<double>(gstride + p_pad, owned);
+        launch_slab_sum(0, sl, Sg, gstride, p_pad, nullptr, 0, G, 0);
+        double *bvec = dalloc<double>(p_pad, owned);
+        launch_coldot(0, dX, n_pad, n_pad, dy, p, bvec);
+        double *dr = dalloc<double>(count, owned), *dl = dalloc<double>(count, owned);
+        HIPCHECK(hipMemcpy(dr, ratios, count * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dl, lambda_max, count * sizeof(double), hipMemcpyHostToDevice));
+        double *db = dalloc<double>((size_t)count * p, owned);
+        int *ds = dalloc<int>(count, owned);
+        launch_em_batch(0, G, p_pad, bvec, p, dr, dl, count, alpha, tol, max_iter, db, ds);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(beta, db, (size_t)count * p * sizeof(double), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(solves, ds, count * sizeof(int), hipMemcpyDeviceToHost));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 // ---------------------------------------------------------------------------
 // Reference .C entry points
 // ---------------------------------------------------------------------------

@@ -667,6 +667,139 @@ void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *
     k_em_cg<<<1, kEmCgThreads, 0, s>>>(A, lda, n, b, x, tol, max_it, work, out_it);
 }
 
+// Batched bridge EM over a ratio grid (trace.beta, Code/R/bridge-trace.R): one 64-lane
+// workgroup per ratio runs the whole EM of BR::EM (BridgeRegression.cpp:600-708, direct
+// solves) for p <= 64 with the system in LDS -- lane i owns row i; right-looking Cholesky,
+// forward and backward substitution; dropped coordinates are identity rows with a zero
+// right-hand side, as in k_em_form.  No host round trip per iteration.
+constexpr int kEmBatchMaxP = 64;
+
+__device__ bool em_lds_solve(double (*A)[kEmBatchMaxP + 1], double *y, int p) {
+    const int lane = threadIdx.x;
+    bool ok = true;
+    for (int k = 0; k < p; ++k) {
+        __syncthreads();
+        const double akk = A[k][k];
+        if (!(akk > 0.0)) ok = false;
+        const double d = sqrt(akk);
+        __syncthreads();
+        if (lane > k && lane < p) A[lane][k] /= d;
+        if (lane == k) A[k][k] = d;
+        __syncthreads();
+        if (lane > k && lane < p) {
+            const double lik = A[lane][k];
+            for (int j = k + 1; j <= lane; ++j) A[lane][j] -= lik * A[j][k];
+        }
+    }
+    for (int k = 0; k < p; ++k) {  // L y' = y
+        __syncthreads();
+        const double yk = y[k] / A[k][k];
+        __syncthreads();
+        if (lane == k) y[k] = yk;
+        if (lane > k && lane < p) y[lane] -= A[lane][k] * yk;
+    }
+    for (int k = p - 1; k >= 0; --k) {  // L' x = y'
+        __syncthreads();
+        const double xk = y[k] / A[k][k];
+        __syncthreads();
+        if (lane == k) y[k] = xk;
+        if (lane < k) y[lane] -= A[k][lane] * xk;
+    }
+    __syncthreads();
+    return ok;
+}
+
+__global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const double *bvec,
+                                                 int p, const double *ratios,
+                                                 const double *lambda_max, double alpha,
+                                                 double tol, int max_iter, double *beta_out,
+                                                 int *solves_out) {
+    __shared__ double A[kEmBatchMaxP][kEmBatchMaxP + 1];
+    __shared__ double x[kEmBatchMaxP], old[kEmBatchMaxP], lam[kEmBatchMaxP];
+    __shared__ int mask[kEmBatchMaxP];
+    __shared__ double red[64];
+    const int lane = threadIdx.x, r = blockIdx.x;
+    const double tau = ratios[r], sig = 1.0, lmax = lambda_max[r];
+    const double c1 = alpha * exp((2 - alpha) * (log(tau) - log(sig)));
+    const double c2 = exp(-2 * (log(tau) - log(sig)));
+    double *out = beta_out + (size_t)r * p;
+    mask[lane] = lane < p;
+    lam[lane] = 0.0;
+    auto form = [&](bool with_lam) {
+        __syncthreads();
+        if (lane < p) {
+            const bool ai = mask[lane];
+            for (int j = 0; j < p; ++j) {
+                const int lo = lane < j ? lane : j, hi = lane < j ? j : lane;
+                double v;
+                if (ai && mask[j])
+                    v = G[(size_t)lo + (size_t)hi * ldg] + (with_lam && j == lane ? c2 * lam[lane] : 0.0);
+                else
+                    v = (j == lane) ? 1.0 : 0.0;
+                A[lane][j] = v;
+            }
+            x[lane] = ai ? bvec[lane] : 0.0;
+        }
+        __syncthreads();
+    };
+    form(false);
+    if (!em_lds_solve(A, x, p)) {
+        if (lane < p) out[lane] = 0.0;
+        if (lane == 0) solves_out[r] = -1;
+        return;
+    }
+    long total = p;
+    double dist = tol + 1.0;
+    int it = 0, pa = p;
+    while (dist > tol && it < max_iter) {
+        // expectation step: lambda_j, the active set (all lanes evaluate, lane j owns j)
+        int keep = 0;
+        if (lane < p && mask[lane]) {
+            const double l = c1 * exp((alpha - 2) * log(fabs(x[lane])));
+            if (l < lmax) {
+                lam[lane] = l;
+                old[lane] = x[lane];
+                keep = 1;
+            } else {
+                mask[lane] = 0;
+            }
+        }
+        __syncthreads();
+        const int num = __popcll(__ballot(keep));
+        if (num == 0) {
+            if (lane < p) out[lane] = 0.0;
+            if (lane == 0) solves_out[r] = it;
+            return;
+        }
+        pa = num;
+        form(true);
+        if (!em_lds_solve(A, x, p)) {
+            if (lane < p) out[lane] = 0.0;
+            if (lane == 0) solves_out[r] = -1;
+            return;
+        }
+        total += pa;
+        // distance over the active set, summed in coordinate order (as the host loop)
+        const double dv = (lane < p && mask[lane]) ? (x[lane] - old[lane]) : 0.0;
+        red[lane] = dv * dv;
+        __syncthreads();
+        double d2 = 0.0;
+        for (int j = 0; j < p; ++j) d2 += red[j];
+        dist = sqrt(d2);
+        ++it;
+        __syncthreads();
+    }
+    if (lane < p) out[lane] = mask[lane] ? x[lane] : 0.0;
+    if (lane == 0) solves_out[r] = (int)total;
+}
+
+void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, int p,
+                     const double *ratios, const double *lambda_max, int count, double alpha,
+                     double tol, int max_iter, double *beta_out, int *solves_out) {
+    k_em_batch<<<count, 64, 0, s>>>(G, ldg, b, p, ratios, lambda_max, alpha, tol, max_iter,
+                                    beta_out, solves_out);
+}
+
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
                    int rhs_col) {

@@ -494,3 +494,24 @@ def test_bridge_em_all_dropped_and_trace(gpu_lib):
     # more shrinkage at smaller ratio: the L1 norm grows along the grid
     l1 = np.abs(tr["beta"]).sum(axis=1)
     assert np.all(np.diff(l1) >= -1e-9 * l1.max())
+
+
+@pytest.mark.parametrize("n,p", [(442, 10), (300, 64)])
+def test_bridge_em_batch_matches_oracle(gpu_lib, n, p):
+    """trace.beta's grid in one launch (a workgroup per ratio, p <= 64) against the EM
+    oracle ratio by ratio: same active sets and solve counts, estimates to 1e-9."""
+    from oracle import em
+    bb = gpu_lib
+    X, y = _em_case(n, p, 7 * p)
+    tol = 1e-9
+    grid = np.exp(np.arange(-6.0, 6.01, 0.5))
+    beta, solves = bb.bridge_em_batch(y, X, grid, alpha=0.5, lambda_max=grid / tol, tol=tol,
+                                      max_iter=30)
+    for r, ratio in enumerate(grid):
+        o, s = em.bridge_em(y, X, ratio, 0.5, ratio / tol, tol, 30)
+        assert solves[r] == s, (ratio, solves[r], s)
+        assert np.array_equal(beta[r] == 0, o == 0), ratio
+        scale = max(np.max(np.abs(o)), 1e-300)
+        assert np.max(np.abs(beta[r] - o)) <= 1e-9 * scale, ratio
+    tr = bb.trace_beta(y, X, ratio_grid=grid)
+    assert np.array_equal(tr["beta"], beta)

@@ -1,0 +1,32 @@
+"""trace.beta timing: the default 401-ratio grid (bridge-trace.R) on a 442 x 10 design,
+one device launch (bb_bridge_em_batch) against the per-ratio bridge_EM loop, plus the
+numpy oracle loop (oracle/em.py) for scale."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bayesbridge_amd as bb  # noqa: E402
+from oracle import em  # noqa: E402
+
+rng = np.random.default_rng(4)
+n, p = 442, 10
+X = rng.standard_normal((n, p))
+y = X @ np.array([3, -2, 1.5, 0, 0, 0.5, 0, 0, -1, 0.0]) + rng.standard_normal(n)
+grid = np.exp(np.arange(-20.0, 20.0 + 1e-9, 0.1))
+tol = 1e-9
+bb.set_verbose(0)
+bb.trace_beta(y, X, ratio_grid=grid[:3])  # warm
+t0 = time.perf_counter()
+tb = bb.trace_beta(y, X, ratio_grid=grid)
+t1 = time.perf_counter()
+loop = np.array([bb.bridge_em(y, X, 0.5, ratio=r, lambda_max=r / tol, tol=tol) for r in grid])
+t2 = time.perf_counter()
+orc = np.array([em.bridge_em(y, X, r, 0.5, r / tol, tol, 30)[0] for r in grid])
+t3 = time.perf_counter()
+print(f"trace.beta {grid.size} ratios, p={p}: batched {1e3 * (t1 - t0):.1f} ms, "
+      f"per-ratio bridge_EM loop {1e3 * (t2 - t1):.1f} ms, numpy oracle loop "
+      f"{1e3 * (t3 - t2):.1f} ms; max |batched - loop| {np.max(np.abs(tb['beta'] - loop)):.2e}, "
+      f"max |batched - oracle| {np.max(np.abs(tb['beta'] - orc)):.2e}")
