@@ -29,6 +29,8 @@ struct OzTab {
     int invP[kOzMods];
     int Pmod[kOzMods][kOzMods];
     float inv_mf[kOzMods];
+    double inv_md[kOzMods];
+    double Wh[kOzMods], Wl[kOzMods];  // mixed-radix weights prod_{i<k} m_i = Wh + Wl
 };
 
 constexpr long long cx_inv_mod(long long a, long long m) {
@@ -55,6 +57,13 @@ constexpr OzTab oz_make_tab() {
             P = (P * kMods[j]) % kMods[k];
         }
         t.invP[k] = k ? (int)cx_inv_mod(P, kMods[k]) : 1;
+        t.inv_md[k] = 1.0 / (double)kMods[k];
+    }
+    __int128 W = 1;  // < 2^125: exact in 128 bits
+    for (int k = 0; k < kOzMods; ++k) {
+        t.Wh[k] = (double)W;
+        t.Wl[k] = (double)(W - (__int128)t.Wh[k]);
+        W *= kMods[k];
     }
     return t;
 }
@@ -931,38 +940,56 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
     for (int q = 0; q < 4; ++q) {
         const int gk = gk0 + q;
         if (gk > gi) break;
+        // Garner digits a_k (balanced): a_k = ((r_k - sum_{j<k} a_j P_jk) invP_k) mod m_k.
+        // The sums are pushed forward as each digit appears (independent 24-bit mads, |acc|
+        // < 2^19), so the serial chain per digit is one subtraction, one multiply and one
+        // fp64 reduction (|v| < 2^27: exact quotient within one, corrected).
         int a[kOzMods];
+        int acc[kOzMods];
+#pragma unroll
+        for (int k = 0; k < kOzMods; ++k) acc[k] = 0;
 #pragma unroll
         for (int k = 0; k < kOzMods; ++k) {
-            const int r = oz_smod(rs[k][q], kOzTab.m[k], kOzTab.inv_mf[k]);
+            const int m = kOzTab.m[k];
+            int d;
             if (k == 0) {
-                a[0] = r;
+                d = oz_smod(rs[0][q], m, kOzTab.inv_mf[0]);
             } else {
-                // |a_j| <= 123, Pmod < 247, k <= 15 terms: |acc| < 2^19, so the 24-bit
-                // full-rate multiplies are exact
-                int acc = 0;
+                const double v = (double)(rs[k][q] - acc[k]) * (double)kOzTab.invP[k];
+                const double qd = rint(v * kOzTab.inv_md[k]);
+                int t = (int)__builtin_fma(-qd, (double)m, v);
+                const int hi = m / 2, lo = hi - m + 1;
+                t = t > hi ? t - m : t;
+                d = t < lo ? t + m : t;
+            }
+            a[k] = d;
 #pragma unroll
-                for (int j = 0; j < k; ++j) acc += __mul24(a[j], kOzTab.Pmod[j][k]);
-                const int sk = oz_smod(acc, kOzTab.m[k], kOzTab.inv_mf[k]);
-                a[k] = oz_smod(__mul24(r - sk, kOzTab.invP[k]), kOzTab.m[k], kOzTab.inv_mf[k]);
+            for (int j = k + 1; j < kOzMods; ++j) acc[j] += __mul24(d, kOzTab.Pmod[k][j]);
+        }
+        // C = sum_k a_k W_k with W_k = Wh_k + Wl_k (106 bits): every term as an exact
+        // double-double (FMA split), then a pairwise tree of double-double additions (depth 4
+        // instead of a 15-step Horner chain).  Balanced digits vanish above C's size, so the
+        // sum is exact whenever C fits in ~106 bits and faithfully rounded beyond.
+        double th[kOzMods], tl[kOzMods];
+#pragma unroll
+        for (int k = 0; k < kOzMods; ++k) {
+            const double ad = (double)a[k];
+            th[k] = ad * kOzTab.Wh[k];
+            tl[k] = __builtin_fma(ad, kOzTab.Wh[k], -th[k]) + ad * kOzTab.Wl[k];
+        }
+#pragma unroll
+        for (int w = 1; w < kOzMods; w *= 2) {
+#pragma unroll
+            for (int k = 0; k + w < kOzMods; k += 2 * w) {
+                const double sh = th[k] + th[k + w];
+                const double bv = sh - th[k];
+                const double err = (th[k] - (sh - bv)) + (th[k + w] - bv);
+                const double sl = err + (tl[k] + tl[k + w]);
+                th[k] = sh + sl;
+                tl[k] = sl - (th[k] - sh);
             }
         }
-        // mixed-radix Horner C = a_0 + m_0 (a_1 + m_1 (a_2 + ...)) in double-double: hi m
-        // splits exactly into p + e (FMA), the rest is two-summed in, so (hi, lo) carries
-        // ~106 bits -- every step is exact while the partial value is an integer below 2^53,
-        // and C (< 2^124) comes out faithfully rounded
-        double hi = (double)a[kOzMods - 1], lo = 0.0;
-#pragma unroll
-        for (int k = kOzMods - 2; k >= 0; --k) {
-            const double m = (double)kOzTab.m[k];
-            const double p = hi * m;
-            const double e = __builtin_fma(hi, m, -p);
-            const double t = __builtin_fma(lo, m, e + (double)a[k]);
-            const double s2 = p + t;
-            const double bp = s2 - p;
-            lo = (p - (s2 - bp)) + (t - bp);
-            hi = s2;
-        }
+        const double hi = th[0], lo = tl[0];
         red2[tri_index(gk, gi)] = ldexp(hi + lo, ei + escale[gk]);
     }
 }
