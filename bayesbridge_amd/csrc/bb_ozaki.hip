@@ -511,8 +511,9 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R
 // The same tile, staging and schedule on v_mfma_i32_16x16x64_i8: one K step is a whole
 // 64-byte chunk, and a 16-row operand fragment (lane l: row l & 15, unit l >> 4) is exactly
 // one 1 KB block of the residue image, read lane-linearly.  Per wave 8 x 8 accumulator
-// blocks of 16 x 16 (256 registers), 64 MFMAs of 16 cycles per chunk.  C/D map: col =
-// l & 15, row = 4 (l >> 4) + reg.
+// blocks of 16 x 16 (256 registers), 64 MFMAs of 16 cycles per chunk.  The MFMA is issued
+// as B x A' (C/D map: col = l & 15 on the A side, row = 4 (l >> 4) + reg on the B side), so
+// each lane's 4 results are 4 consecutive output bytes.
 // ---------------------------------------------------------------------------
 // v_mfma_i32_16x16x64_i8 with the accumulator pinned to AGPRs (the builtin lets the register
 // allocator shuttle 64 four-register accumulators between the files every K step).  Every
@@ -610,15 +611,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restri
         const int st_next = (it + ST) % ST;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            oz_mfma16(acc[g][0], fa_c[g], fb_c[0]);
+            oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
             if (!(dbg & 1) && (PP == 8 || (g & 1))) glds_one(kc_next, st_next, PP == 8 ? g : g >> 1);
-            oz_mfma16(acc[g][1], fa_c[g], fb_c[1]);
+            oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
             if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
-            oz_mfma16(acc[g][2], fa_c[g], fb_c[2]);
+            oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
             if (!(dbg & 2) && (FJ == 8 || !(g & 1))) fb_n[g * FJ / 8] = frag_b(it + 1, g * FJ / 8);
-            oz_mfma16(acc[g][3], fa_c[g], fb_c[3]);
+            oz_mfma16(acc[g][3], fb_c[3], fa_c[g]);
 #pragma unroll
-            for (int j = 4; j < FJ; ++j) oz_mfma16(acc[g][j], fa_c[g], fb_c[j]);
+            for (int j = 4; j < FJ; ++j) oz_mfma16(acc[g][j], fb_c[j], fa_c[g]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -644,19 +645,25 @@ __global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restri
     const int m = C.m[mod];
     const double im = C.inv_m[mod];
     const int hi = m / 2, lo = hi - m + 1;
+    // acc[i][j] = (B block j)(A block i)': lane l, reg r holds row (I side) i*16 + (l & 15),
+    // column (K side) j*16 + 4 (l >> 4) + r, so a lane's four registers are four consecutive
+    // bytes of the tile row: one dword store per block
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < FJ; ++j)
+        for (int j = 0; j < FJ; ++j) {
+            const int rowl = wr * 128 + i * 16 + (lane & 15);
+            const int col = wc * FJ * 16 + j * 16 + 4 * (lane >> 4);
+            unsigned int wv = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int rowl = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
-                const int col = wc * FJ * 16 + j * 16 + (lane & 15);
                 const int cval = acc[i][j][r];
                 int rr = cval - (int)rint((double)cval * im) * m;
                 rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
-                out[rowl * kOzT + col] = (int8_t)rr;
+                wv |= ((unsigned int)rr & 0xffu) << (8 * r);
             }
+            *(unsigned int *)(out + rowl * kOzT + col) = wv;
+        }
 }
 
 // ---------------------------------------------------------------------------
@@ -731,18 +738,18 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict_
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            oz_mfma16(acc[g][0], fa_c[g], fb_c[0]);
+            oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
             if (!(dbg & 1)) lwrite(it + 2, g, rg[g]);
-            oz_mfma16(acc[g][1], fa_c[g], fb_c[1]);
+            oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
             if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
-            oz_mfma16(acc[g][2], fa_c[g], fb_c[2]);
+            oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
             if (!(dbg & 1)) rg[g] = gload(it + 4, g);
-            oz_mfma16(acc[g][3], fa_c[g], fb_c[3]);
+            oz_mfma16(acc[g][3], fb_c[3], fa_c[g]);
             if (!(dbg & 2)) fb_n[g] = frag_b(it + 1, g);
-            oz_mfma16(acc[g][4], fa_c[g], fb_c[4]);
-            oz_mfma16(acc[g][5], fa_c[g], fb_c[5]);
-            oz_mfma16(acc[g][6], fa_c[g], fb_c[6]);
-            oz_mfma16(acc[g][7], fa_c[g], fb_c[7]);
+            oz_mfma16(acc[g][4], fb_c[4], fa_c[g]);
+            oz_mfma16(acc[g][5], fb_c[5], fa_c[g]);
+            oz_mfma16(acc[g][6], fb_c[6], fa_c[g]);
+            oz_mfma16(acc[g][7], fb_c[7], fa_c[g]);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -785,16 +792,19 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict_
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j) {
+            const int rowl = wr * 128 + i * 16 + (lane & 15);
+            const int col = wc * 128 + j * 16 + 4 * (lane >> 4);
+            unsigned int wv = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int rowl = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
-                const int col = wc * 128 + j * 16 + (lane & 15);
                 const int cval = acc[i][j][r];
                 int rr = cval - (int)rint((double)cval * im) * m;
                 rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
-                out[rowl * kOzT + col] = (int8_t)rr;
+                wv |= ((unsigned int)rr & 0xffu) << (8 * r);
             }
+            *(unsigned int *)(out + rowl * kOzT + col) = wv;
+        }
 }
 
 static int oz_shape() {
