@@ -534,7 +534,9 @@ __device__ __forceinline__ void oz_wait_vm() {
     asm volatile("" ::: "memory");
 }
 
-template <int dbg, int NW, int ST>
+// TM = 0: every lower tile; TM = 1: only the off-diagonal tiles (I > K), the diagonal ones
+// then run paired in k_oz_gemm16d.  P keeps one slot per lower tile, t = I (I+1)/2 + K.
+template <int dbg, int NW, int ST, int TM = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restrict__ R, int n_oz,
                                                           int nkc, int nsplit,
                                                           int8_t *__restrict__ P, OzConsts C) {
@@ -545,17 +547,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restri
     __shared__ __attribute__((aligned(1024))) int8_t smem[ST * kOzStageBytes];
     const int nt = n_oz / kOzT;
     const int ntiles = nt * (nt + 1) / 2;
+    const int nenum = TM ? nt * (nt - 1) / 2 : ntiles;  // tiles this launch enumerates
     const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-    const int u = xcd + 8 * (q / ntiles);
-    const int tile = q % ntiles;
+    const int u = xcd + 8 * (q / nenum);
+    const int te = q % nenum;
     const int mod = u % kOzMods;
     const int split = u / kOzMods;
     if (split >= nsplit) return;
-    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-    while (I * (I + 1) / 2 > tile) --I;
+    // enumerated index -> (I, K): all lower tiles te = I (I+1)/2 + K, or the strictly
+    // lower ones te = I (I-1)/2 + K
+    const int sh = TM ? 1 : 0;
+    int I = (int)((sqrt(8.0 * te + 1.0) + (TM ? 1.0 : -1.0)) * 0.5);
+    while ((I + 1) * (I + 2 - 2 * sh) / 2 <= te) ++I;
+    while (I * (I + 1 - 2 * sh) / 2 > te) --I;
     I = __builtin_amdgcn_readfirstlane(I);
-    const int K = tile - I * (I + 1) / 2;
+    const int K = te - I * (I + 1 - 2 * sh) / 2;
+    const int tile = I * (I + 1) / 2 + K;
     const int per = (nkc + nsplit - 1) / nsplit;
     const int c0 = split * per;
     const int nch = max(0, min(nkc, c0 + per) - c0);
@@ -807,6 +814,323 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict_
         }
 }
 
+// ---------------------------------------------------------------------------
+// Diagonal tiles, two per workgroup.  A diagonal tile (I, I) needs only its lower half:
+// the off-diagonal quadrant (rows 128..255 x cols 0..127, 64 blocks) and the lower halves
+// of its two diagonal quadrants (36 + 36 blocks, the diagonal blocks whole).  Its two
+// operands are the same 256-row block, so one 16 KB operand slot per stage feeds a tile:
+// slot 0 = tile (I1, I1), slot 1 = tile (I2, I2).  Waves 0, 1 take the off-diagonal
+// quadrant of tile wid (64 MFMAs per chunk), waves 2, 3 the diagonal quadrants of tile
+// wid - 2 (72 MFMAs: D1 lower blocks in acc[i][j], i >= j; D2 strictly lower in acc[j][i];
+// D2's diagonal blocks in 8 VGPR accumulators).  Every wave reads the same 16 fragments of
+// its slot per chunk (blocks 8..15 as the A side, 0..7 as the K side).  The DMA ring and
+// the per-chunk protocol are k_oz_gemm16's.  The grid is tiles / 2 instead of tiles
+// workgroups for the diagonal band.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void oz_mfma16v(v4i &acc, const v4i &a, const v4i &b) {
+    asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+
+// One wave's whole pass (ring prologue, chunk loop, epilogue) for a role fixed at compile
+// time: the two roles keep disjoint accumulator live ranges, and both execute the same
+// barrier sequence (one per chunk plus the prologue's).
+template <int dbg, bool DIAGQ>
+__device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
+                                             const int8_t *baseB, size_t kstride, int c0,
+                                             int nch, int wid, int slot, int8_t *out, int m,
+                                             double im) {
+    const int lane = threadIdx.x & 63;
+    const int voff = wid * 4096 + lane * 16;
+    auto glds_one = [&](int kc, int stage, int g) {
+        int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
+        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
+        oz_glds(src + voff, sb + (4 * wid + (g & 3)) * 1024);
+    };
+    auto issue = [&](int kc, int stage) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) glds_one(kc, stage, g);
+    };
+    v4i acc[8][8], accv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        accv[i] = (v4i){0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+    }
+    // fragment blk of this wave's slot: blocks 8..15 -> fa (A side), 0..7 -> fb (K side)
+    auto frag = [&](int chunk, int blk) {
+        const int8_t *S_ = smem + (chunk % kOzStages) * kOzStageBytes + slot * kOzOpBytes;
+        return *(const v4i *)&S_[blk * 1024 + lane * 16];
+    };
+    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[8], v4i (&fa_n)[8], v4i (&fb_n)[8]) {
+        if (!(dbg & 4)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            oz_wait_vm<16>();
+            __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        const int kc_next = c0 + min(it + kOzStages, nch - 1);
+        const int st_next = (it + kOzStages) % kOzStages;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            if constexpr (!DIAGQ) {
+                // off-diagonal quadrant: rows 128 + 16 g (fa), cols 16 j (fb)
+                oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
+                if (!(dbg & 1)) glds_one(kc_next, st_next, g);
+                oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
+                if (!(dbg & 2)) fa_n[g] = frag(it + 1, 8 + g);
+                oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
+                if (!(dbg & 2)) fb_n[g] = frag(it + 1, g);
+#pragma unroll
+                for (int j = 3; j < 8; ++j) oz_mfma16(acc[g][j], fb_c[j], fa_c[g]);
+            } else {
+                // D1 (fb x fb) block (g, j <= g); D2 (fa x fa) block (g, j < g) in acc[j][g]
+                // and its diagonal block in accv[g]
+                oz_mfma16(acc[g][0], fb_c[0], fb_c[g]);
+                if (!(dbg & 1)) glds_one(kc_next, st_next, g);
+#pragma unroll
+                for (int j = 1; j <= g; ++j) oz_mfma16(acc[g][j], fb_c[j], fb_c[g]);
+                if (!(dbg & 2)) fa_n[g] = frag(it + 1, 8 + g);
+#pragma unroll
+                for (int j = 0; j < g; ++j) oz_mfma16(acc[j][g], fa_c[j], fa_c[g]);
+                oz_mfma16v(accv[g], fa_c[g], fa_c[g]);
+                if (!(dbg & 2)) fb_n[g] = frag(it + 1, g);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    v4i fa0[8], fb0[8], fa1[8], fb1[8];
+    if (nch > 0) {
+#pragma unroll
+        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        oz_wait_vm<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fa0[i] = frag(0, 8 + i);
+            fb0[i] = frag(0, i);
+        }
+    }
+    int it = 0;
+    for (; it + 1 < nch; it += 2) {
+        step(it, fa0, fb0, fa1, fb1);
+        step(it + 1, fa1, fb1, fa0, fb0);
+    }
+    if (it < nch) step(it, fa0, fb0, fa1, fb1);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    const int hi = m / 2, lo = hi - m + 1;
+    auto store = [&](int rowl, int col, const v4i &v) {
+        unsigned int wv = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int cval = v[r];
+            int rr = cval - (int)rint((double)cval * im) * m;
+            rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
+            wv |= ((unsigned int)rr & 0xffu) << (8 * r);
+        }
+        *(unsigned int *)(out + rowl * kOzT + col) = wv;
+    };
+    // (lane l, reg r of block (i, j) = row 16 i + (l & 15), column 16 j + 4 (l >> 4) + r)
+    const int rl = lane & 15, cl = 4 * (lane >> 4);
+    if constexpr (!DIAGQ) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) store(128 + 16 * i + rl, 16 * j + cl, acc[i][j]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+            for (int j = 0; j <= i; ++j) store(16 * i + rl, 16 * j + cl, acc[i][j]);
+#pragma unroll
+            for (int j = 0; j < i; ++j) store(128 + 16 * i + rl, 128 + 16 * j + cl, acc[j][i]);
+            store(128 + 16 * i + rl, 128 + 16 * i + cl, accv[i]);
+        }
+    }
+}
+
+// A full 256 x 256 off-diagonal tile on 4 waves (2 x 2, 128 x 128 each): k_oz_gemm16's
+// body with NW = 4, as a device pass for the unified launch below.
+template <int dbg>
+__device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
+                                             const int8_t *baseB, size_t kstride, int c0,
+                                             int nch, int wid, int8_t *out, int m, double im) {
+    const int lane = threadIdx.x & 63;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int voff = wid * 4096 + lane * 16;
+    auto glds_one = [&](int kc, int stage, int g) {
+        int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
+        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
+        oz_glds(src + voff, sb + (4 * wid + (g & 3)) * 1024);
+    };
+    auto issue = [&](int kc, int stage) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) glds_one(kc, stage, g);
+    };
+    v4i acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+    auto frag_a = [&](int chunk, int i) {
+        const int8_t *A_ = smem + (chunk % kOzStages) * kOzStageBytes;
+        return *(const v4i *)&A_[(wr * 8 + i) * 1024 + lane * 16];
+    };
+    auto frag_b = [&](int chunk, int j) {
+        const int8_t *B_ = smem + (chunk % kOzStages) * kOzStageBytes + kOzOpBytes;
+        return *(const v4i *)&B_[(wc * 8 + j) * 1024 + lane * 16];
+    };
+    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[8], v4i (&fa_n)[8], v4i (&fb_n)[8]) {
+        if (!(dbg & 4)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            oz_wait_vm<16>();
+            __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("" ::: "memory");
+        const int kc_next = c0 + min(it + kOzStages, nch - 1);
+        const int st_next = (it + kOzStages) % kOzStages;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
+            if (!(dbg & 1)) glds_one(kc_next, st_next, g);
+            oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
+            if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
+            oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
+            if (!(dbg & 2)) fb_n[g] = frag_b(it + 1, g);
+#pragma unroll
+            for (int j = 3; j < 8; ++j) oz_mfma16(acc[g][j], fb_c[j], fa_c[g]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    v4i fa0[8], fb0[8], fa1[8], fb1[8];
+    if (nch > 0) {
+#pragma unroll
+        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        oz_wait_vm<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fa0[i] = frag_a(0, i);
+            fb0[i] = frag_b(0, i);
+        }
+    }
+    int it = 0;
+    for (; it + 1 < nch; it += 2) {
+        step(it, fa0, fb0, fa1, fb1);
+        step(it + 1, fa1, fb1, fa0, fb0);
+    }
+    if (it < nch) step(it, fa0, fb0, fa1, fb1);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    const int hi = m / 2, lo = hi - m + 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int rowl = wr * 128 + i * 16 + (lane & 15);
+            const int col = wc * 128 + j * 16 + 4 * (lane >> 4);
+            unsigned int wv = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int cval = acc[i][j][r];
+                int rr = cval - (int)rint((double)cval * im) * m;
+                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
+                wv |= ((unsigned int)rr & 0xffu) << (8 * r);
+            }
+            *(unsigned int *)(out + rowl * kOzT + col) = wv;
+        }
+}
+
+// Unified launch: per (modulus, split) unit, nt (nt-1)/2 off-diagonal tiles and
+// ceil(nt/2) diagonal pairs, all of one unit on one XCD (block b -> XCD b % 8) so that the
+// pairs share their row blocks in L2 with the unit's off-diagonal tiles running beside them
+// (launched alone, the pairs stream their rows from HBM).
+template <int dbg>
+__global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict__ R, int n_oz,
+                                                       int nkc, int nsplit,
+                                                       int8_t *__restrict__ P, OzConsts C) {
+    __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int noff = nt * (nt - 1) / 2, npair = (nt + 1) / 2;
+    const int nper = noff + npair;
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int u = xcd + 8 * (q / nper);
+    const int local = q % nper;
+    const int mod = u % kOzMods;
+    const int split = u / kOzMods;
+    if (split >= nsplit) return;
+    const int per = (nkc + nsplit - 1) / nsplit;
+    const int c0 = split * per;
+    const int nch = max(0, min(nkc, c0 + per) - c0);
+    const size_t kstride = (size_t)n_oz * kOzKC;
+    const int8_t *plane = R + (size_t)mod * nkc * kstride;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int8_t *P0 = P + ((size_t)split * kOzMods + mod) * ntiles * (size_t)(kOzT * kOzT);
+    if (local < noff) {
+        // strictly lower tile te = I (I-1)/2 + K
+        int I = (int)((sqrt(8.0 * local + 1.0) + 1.0) * 0.5);
+        while ((I + 1) * I / 2 <= local) ++I;
+        while (I * (I - 1) / 2 > local) --I;
+        I = __builtin_amdgcn_readfirstlane(I);
+        const int K = local - I * (I - 1) / 2;
+        const int tile = I * (I + 1) / 2 + K;
+        oz_full_pass<dbg>(smem, plane + (size_t)I * kOzT * kOzKC, plane + (size_t)K * kOzT * kOzKC,
+                          kstride, c0, nch, wid, P0 + (size_t)tile * (kOzT * kOzT), C.m[mod],
+                          C.inv_m[mod]);
+    } else {
+        const int pr = local - noff;
+        const int I1 = 2 * pr, I2 = min(2 * pr + 1, nt - 1);  // odd nt: the last tile twice
+        const int slot = wid & 1;
+        const int Iw = slot ? I2 : I1;
+        int8_t *out = P0 + (size_t)(Iw * (Iw + 1) / 2 + Iw) * (kOzT * kOzT);
+        const int8_t *bA = plane + (size_t)I1 * kOzT * kOzKC;
+        const int8_t *bB = plane + (size_t)I2 * kOzT * kOzKC;
+        if (wid < 2)
+            oz_diag_pass<dbg, false>(smem, bA, bB, kstride, c0, nch, wid, slot, out, C.m[mod],
+                                     C.inv_m[mod]);
+        else
+            oz_diag_pass<dbg, true>(smem, bA, bB, kstride, c0, nch, wid, slot, out, C.m[mod],
+                                    C.inv_m[mod]);
+    }
+}
+
+template <int dbg>
+__global__ __launch_bounds__(256, 1) void k_oz_gemm16d(const int8_t *__restrict__ R, int n_oz,
+                                                       int nkc, int nsplit,
+                                                       int8_t *__restrict__ P, OzConsts C) {
+    __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
+    const int nt = n_oz / kOzT;
+    const int ntiles = nt * (nt + 1) / 2;
+    const int npair = (nt + 1) / 2;
+    const int b = blockIdx.x;
+    const int u = b / npair, pr = b % npair;
+    const int mod = u % kOzMods;
+    const int split = u / kOzMods;
+    if (split >= nsplit) return;
+    const int I1 = 2 * pr, I2 = min(2 * pr + 1, nt - 1);  // odd nt: the last tile twice
+    const int per = (nkc + nsplit - 1) / nsplit;
+    const int c0 = split * per;
+    const int nch = max(0, min(nkc, c0 + per) - c0);
+    const size_t kstride = (size_t)n_oz * kOzKC;
+    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I1 * kOzT * kOzKC;
+    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)I2 * kOzT * kOzKC;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int slot = wid & 1;
+    const int Iw = slot ? I2 : I1;
+    const int tile = Iw * (Iw + 1) / 2 + Iw;
+    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
+    if (wid < 2)
+        oz_diag_pass<dbg, false>(smem, baseA, baseB, kstride, c0, nch, wid, slot, out, C.m[mod],
+                                 C.inv_m[mod]);
+    else
+        oz_diag_pass<dbg, true>(smem, baseA, baseB, kstride, c0, nch, wid, slot, out, C.m[mod],
+                                C.inv_m[mod]);
+}
+
 static int oz_shape() {
     static const int s = [] {
         const char *e = getenv("BB_OZ_SHAPE");
@@ -831,6 +1155,23 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
             case 2: k_oz_gemm16r<2><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
             case 3: k_oz_gemm16r<3><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
             default: k_oz_gemm16r<0><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
+        }
+        return;
+    }
+    static const bool diag_pairs = [] {
+        const char *e = getenv("BB_OZ_DIAG");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (shape == 16 && diag_pairs) {
+        // off-diagonal tiles and diagonal pairs in one launch (k_oz_gemm16u)
+        const unsigned gu = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
+        switch (dbg) {
+            case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+            default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
         }
         return;
     }
