@@ -240,7 +240,7 @@ def main():
     gram_flops = float(n) * (n + 1) * p_loc
     if gram_mode == bb.GRAM_OZAKI:
         kernel_ops = 16.0 * n * (n + 1) * p_loc
-        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm16 (v_mfma_i32_16x16x64_i8)"
+        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm16u (v_mfma_i32_16x16x64_i8)"
     else:
         kernel_ops = gram_flops
         peak, unit, kname = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", "k_gram (v_mfma_f64_16x16x4_f64)"
@@ -248,7 +248,7 @@ def main():
     gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
     fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
 
-    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16" if gram_mode == bb.GRAM_OZAKI
+    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u" if gram_mode == bb.GRAM_OZAKI
                           else "bb::k_gram")
 
     cpu = None
