@@ -41,7 +41,7 @@ class bb_config(ctypes.Structure):
                 ("true_alpha", ctypes.c_double), ("ortho", ctypes.c_int),
                 ("method", ctypes.c_int), ("trace_capacity", ctypes.c_int),
                 ("seed", ctypes.c_uint64), ("stream", ctypes.c_uint64), ("device", ctypes.c_int),
-                ("gram_mode", ctypes.c_int)]
+                ("gram_mode", ctypes.c_int), ("betaburn", ctypes.c_int)]
 
 GRAM_FP64, GRAM_OZAKI = 0, 1
 
@@ -58,7 +58,8 @@ EXPORTED_SYMBOLS = [
     "bb_engine_phase_times", "bb_phase_count", "bb_phase_name", "bb_bench_lambda",
     "bb_group_create", "bb_group_destroy", "bb_group_init_state", "bb_group_run",
     "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode", "bb_bench_ozaki",
-    "bridge_EM", "bb_bridge_em", "bb_bridge_em_batch",
+    "bridge_EM", "bb_bridge_em", "bb_bridge_em_batch", "bridge_regression",
+    "bb_engine_get_tri_trace", "bb_engine_get_tri_basis", "bb_engine_set_tri_state",
 ]
 
 
@@ -126,6 +127,10 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_phase_name.restype = c.c_char_p
     L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
     L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
+    L.bridge_regression.argtypes = [_dp] * 9 + [_dp] * 9 + [_ip] * 4 + [_dp] + [_ip] * 3
+    L.bb_engine_get_tri_trace.argtypes = [c.c_void_p, c.c_int, c.c_int, _dp, _dp]
+    L.bb_engine_get_tri_basis.argtypes = [c.c_void_p, _dp, _dp, _dp]
+    L.bb_engine_set_tri_state.argtypes = [c.c_void_p, _dp]
     L.bridge_EM.argtypes = [_dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _ip, _ip]
     L.bb_bridge_em.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int, c.c_double, c.c_double,
                                c.c_double, c.c_double, c.c_int, c.c_int]
@@ -245,21 +250,63 @@ def bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_sh
     return out
 
 
+def bridge_reg_tri(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,
+                   nu_rate=2.0, alpha_a=1.0, alpha_b=1.0, sig2_true=0.0, tau_true=0.0,
+                   burn=500, ortho=False, betaburn=0, extras=False):
+    """bridge.reg.tri (BridgeWrapper.R:139-186) through ``.C("bridge_regression", ...)``.
+
+    Returns a dict: beta, u, w (omega), shape (M x P), sig2, tau, alpha (M), runtime.
+    Needs P <= N (the reference's svd-based rtnorm_gibbs indexes d[0..P-1]).
+    """
+    L = library()
+    _require_gpu()
+    y = np.asarray(y, dtype=np.float64).ravel()
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    N = y.shape[0]
+    R, P = X.shape
+    M = int(nsamp)
+    if not check_parameters(N, R, M, sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
+                            alpha_b):
+        raise ValueError("bridge_reg_tri: invalid parameters")
+    if not extras:
+        print("Variable extras only for Package testing.")
+    tr = {k: np.zeros((P, M), order="F") for k in ("beta", "u", "w", "shape")}
+    sig2 = np.zeros(M)
+    tau = np.zeros(M)
+    alph = np.zeros(M)
+    Xf = np.asfortranarray(X)
+    d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
+    i = lambda v: ctypes.byref(ctypes.c_int(int(v)))  # noqa: E731
+    rt = ctypes.c_double(0.0)
+    L.bridge_regression(_p(tr["beta"]), _p(tr["u"]), _p(tr["w"]), _p(tr["shape"]), _p(sig2),
+                        _p(tau), _p(alph), _p(y), _p(Xf), d(sig2_shape), d(sig2_scale),
+                        d(nu_shape), d(nu_rate), d(alpha_a), d(alpha_b), d(sig2_true),
+                        d(tau_true), d(alpha), i(P), i(N), i(M), i(burn), ctypes.byref(rt),
+                        i(1 if ortho else 0), i(betaburn), i(0))
+    out = {k: v.T.copy() for k, v in tr.items()}
+    out.update(sig2=sig2, tau=tau, alpha=alph, runtime=rt.value)
+    return out
+
+
 def bridge_reg(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,
                nu_rate=2.0, alpha_a=1.0, alpha_b=1.0, sig2_true=0.0, tau_true=0.0, burn=500,
                method="triangle", ortho=False):
     """bridge.reg (BridgeWrapper.R:240-276).
 
     Like the reference, the "stable" branch IGNORES the caller's hyper-parameters and
-    calls bridge.reg.stb with alpha=0.5, nu.shape = nu.rate = 0.5, burn=500.  The
-    triangle method is outside this build's scope.
+    calls bridge.reg.stb with alpha=0.5, nu.shape = nu.rate = 0.5, burn=500; the
+    "triangle" branch likewise calls bridge.reg.tri with those constants.
     """
     if method == "stable":
         return bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0,
                               nu_shape=0.5, nu_rate=0.5, alpha_a=1.0, alpha_b=1.0,
                               sig2_true=0.0, tau_true=0.0, burn=500, ortho=ortho)
     if method == "triangle":
-        raise NotImplementedError("bridge.reg(method='triangle') is not part of this build")
+        return bridge_reg_tri(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0,
+                              nu_shape=0.5, nu_rate=0.5, alpha_a=1.0, alpha_b=1.0,
+                              sig2_true=0.0, tau_true=0.0, burn=500, ortho=ortho)
     print('Unrecognized method.  Use "triangles" or "stable".')
     return None
 
@@ -499,6 +546,7 @@ class EngineConfig:
     stream: int = 0
     device: int = 0
     gram_mode: Optional[int] = None  # None: library default (env BB_GRAM_MODE)
+    betaburn: int = 0
 
     def to_c(self) -> bb_config:
         c = bb_config()
@@ -566,6 +614,28 @@ class Engine:
         _check(library().bb_engine_get_trace(self._h, slot0, count, _p(beta), _p(lam), _p(sig2),
                                              _p(tau), _p(alpha)), "bb_engine_get_trace")
         return dict(beta=beta, **{"lambda": lam}, sig2=sig2, tau=tau, alpha=alpha)
+
+    def tri_trace(self, slot0: int, count: int):
+        """Triangle method: u and shape traces (omega is ``trace()['lambda']``)."""
+        pl = self.p_local
+        u = np.zeros((pl, count), order="F")
+        shape = np.zeros((pl, count), order="F")
+        _check(library().bb_engine_get_tri_trace(self._h, slot0, count, _p(u), _p(shape)),
+               "bb_engine_get_tri_trace")
+        return dict(u=u, shape=shape)
+
+    def set_tri_state(self, u):
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        _check(library().bb_engine_set_tri_state(self._h, _p(u)), "bb_engine_set_tri_state")
+
+    def tri_basis(self):
+        """Triangle method: (tV, a, d) with X = U diag(d) V', tV = V' (P x P), a = V'X'y."""
+        p = self.p_local
+        tV = np.zeros((p, p), order="F")
+        a, d = np.zeros(p), np.zeros(p)
+        _check(library().bb_engine_get_tri_basis(self._h, _p(tV), _p(a), _p(d)),
+               "bb_engine_get_tri_basis")
+        return tV, a, d
 
     def state(self):
         pl = self.p_local

@@ -134,7 +134,7 @@ static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "ozprep"
 struct bb_engine {
     bb_config cfg{};
     int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
-    int method = 0;  // 1 chol, 2 woodbury, 3 ortho
+    int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture
     int group = 1;
     Hyper hy{};
     hipStream_t stream = nullptr;
@@ -161,6 +161,10 @@ struct bb_engine {
     // chol / ortho
     double *G = nullptr, *cvec = nullptr, *A = nullptr, *Y2 = nullptr, *W2 = nullptr,
            *gdiag = nullptr;
+    // triangle mixture: design basis (bb_tri.hip), omega in lam, shape in D, u in u
+    double *tVc = nullptr, *tVr = nullptr, *tri_a = nullptr, *tri_d = nullptr;
+    double *tr_u = nullptr, *tr_shape = nullptr;
+    std::vector<double> h_tV, h_a, h_d;
     // traces
     double *tr_beta = nullptr, *tr_lam = nullptr, *tr_sig2 = nullptr, *tr_tau = nullptr,
            *tr_alpha = nullptr;
@@ -267,6 +271,13 @@ struct bb_engine {
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
                                 red2, 1);
+        } else if (method == 4) {
+            // BridgeWrapper.cpp:166-168: omega, u, then the rtnorm_gibbs beta passes
+            mark(PH_BETA);
+            launch_tri_update(stream, beta, u, lam, D, p, tVc, tVr, tri_a, tri_d, sc,
+                              cfg.betaburn, cfg.seed, cfg.stream, t,
+                              slot_ptr(tr_beta, slot, p_loc), slot_ptr(tr_u, slot, p_loc), trl,
+                              slot_ptr(tr_shape, slot, p_loc), err);
         } else {
             launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
                           group, lam, nullptr, nullptr, trl, err);
@@ -303,7 +314,7 @@ struct bb_engine {
             chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2, flags, err);
             mark(PH_BETA);
             launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
-        } else {
+        } else if (method == 3) {
             mark(PH_BETA);
             launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta, trb);
         }
@@ -316,7 +327,8 @@ struct bb_engine {
             // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
             // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
             mark(PH_ALPHA);
-            const double pr_a = (method != 3 && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
+            // triangle driver: (alpha_a, alpha_b) in both loops (BridgeWrapper.cpp:146,173)
+            const double pr_a = (method <= 2 && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
             launch_alpha_mh(stream, beta, p, sc, pr_a, hy.alpha_b, cfg.seed, cfg.stream, t,
                             slot_ptr(tr_alpha, slot, 1));
         }
@@ -345,6 +357,105 @@ struct bb_engine {
 
 namespace {
 
+// Symmetric eigendecomposition G = V diag(ev) V' by cyclic Jacobi rotations (host, one-time
+// setup of the triangle method; O(p^3) per sweep of rotations, practical for p up to a few
+// hundred).  Column-major p x p; on return V's columns are eigenvectors.
+void jacobi_eigen(std::vector<double> A, int p, std::vector<double> &V, std::vector<double> &ev) {
+    V.assign((size_t)p * p, 0.0);
+    for (int i = 0; i < p; ++i) V[(size_t)i * p + i] = 1.0;
+    auto at = [&](int i, int j) -> double & { return A[(size_t)j * p + i]; };
+    double fro = 0.0;
+    for (double x : A) fro += x * x;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0;
+        for (int j = 0; j < p; ++j)
+            for (int i = 0; i < j; ++i) off += at(i, j) * at(i, j);
+        if (off <= 1e-32 * fro || off == 0.0) break;
+        for (int q = 1; q < p; ++q) {
+            for (int r = 0; r < q; ++r) {
+                const double arq = at(r, q);
+                if (arq == 0.0) continue;
+                const double theta = (at(q, q) - at(r, r)) / (2.0 * arq);
+                const double tt = (theta >= 0 ? 1.0 : -1.0) /
+                                  (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double cs = 1.0 / sqrt(tt * tt + 1.0), sn = tt * cs;
+                for (int k = 0; k < p; ++k) {  // columns r, q
+                    const double akr = at(k, r), akq = at(k, q);
+                    at(k, r) = cs * akr - sn * akq;
+                    at(k, q) = sn * akr + cs * akq;
+                }
+                for (int k = 0; k < p; ++k) {  // rows r, q
+                    const double ark = at(r, k), aqk = at(q, k);
+                    at(r, k) = cs * ark - sn * aqk;
+                    at(q, k) = sn * ark + cs * aqk;
+                }
+                for (int k = 0; k < p; ++k) {
+                    double &vr = V[(size_t)r * p + k], &vq = V[(size_t)q * p + k];
+                    const double a0 = vr, b0 = vq;
+                    vr = cs * a0 - sn * b0;
+                    vq = sn * a0 + cs * b0;
+                }
+            }
+        }
+    }
+    ev.resize(p);
+    for (int i = 0; i < p; ++i) ev[i] = at(i, i);
+}
+
+// X = U diag(d) V' from G = X'X (BridgeRegression.cpp:47-57, svd 'S' for n > p): tV = V'
+// with singular values in decreasing order, each right singular vector signed so its
+// largest-magnitude entry is positive; a = d * U'y = V' X'y.
+void tri_setup(bb_engine *e) {
+    const int p = e->p, pp = e->p_pad;
+    std::vector<double> Gp((size_t)pp * pp), c(pp);
+    HIPCHECK(hipStreamSynchronize(e->stream));
+    HIPCHECK(hipMemcpy(Gp.data(), e->G, Gp.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(c.data(), e->cvec, (size_t)pp * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> G((size_t)p * p);
+    for (int j = 0; j < p; ++j)
+        for (int i = 0; i < p; ++i) {  // the device Gram holds the upper triangle
+            const int r = i < j ? i : j, q = i < j ? j : i;
+            G[(size_t)j * p + i] = Gp[(size_t)q * pp + r];
+        }
+    std::vector<double> V, ev;
+    jacobi_eigen(G, p, V, ev);
+    std::vector<int> ord(p);
+    for (int i = 0; i < p; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ev[x] > ev[y]; });
+    e->h_tV.assign((size_t)p * p, 0.0);
+    e->h_a.assign(p, 0.0);
+    e->h_d.assign(p, 0.0);
+    std::vector<double> tVr((size_t)p * p);
+    for (int i = 0; i < p; ++i) {
+        const double *v = &V[(size_t)ord[i] * p];
+        int jm = 0;
+        for (int j = 1; j < p; ++j)
+            if (fabs(v[j]) > fabs(v[jm])) jm = j;
+        const double sg = v[jm] < 0 ? -1.0 : 1.0;
+        double a = 0.0;
+        for (int j = 0; j < p; ++j) {
+            const double x = sg * v[j];
+            e->h_tV[i + (size_t)j * p] = x;
+            tVr[(size_t)i * p + j] = x;
+            a += x * c[j];
+        }
+        e->h_a[i] = a;
+        e->h_d[i] = sqrt(ev[ord[i]] > 0 ? ev[ord[i]] : 0.0);
+    }
+    auto &o = e->owned;
+    e->tVc = dalloc<double>((size_t)p * p, o);
+    e->tVr = dalloc<double>((size_t)p * p, o);
+    e->tri_a = dalloc<double>(p, o);
+    e->tri_d = dalloc<double>(p, o);
+    HIPCHECK(hipMemcpy(e->tVc, e->h_tV.data(), (size_t)p * p * sizeof(double),
+                       hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(e->tVr, tVr.data(), (size_t)p * p * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(e->tri_a, e->h_a.data(), (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(e->tri_d, e->h_d.data(), (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+    e->tr_u = dalloc<double>((size_t)p * e->cap, o);
+    e->tr_shape = dalloc<double>((size_t)p * e->cap, o);
+}
+
 void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     const bb_config &c = e->cfg;
     e->n = c.n;
@@ -355,13 +466,18 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     e->cap = c.trace_capacity < 1 ? 1 : c.trace_capacity;
     e->hy = Hyper{c.sig2_shape, c.sig2_scale, c.nu_shape, c.nu_rate, c.alpha_a, c.alpha_b,
                   c.true_tau > 0, c.true_sig2 > 0, c.true_alpha > 0};
-    if (c.ortho) e->method = 3;
+    if (c.method == 4) e->method = 4;
+    else if (c.ortho) e->method = 3;
     else if (c.method == 1 || (c.method == 0 && c.p <= c.n)) e->method = 1;
     else e->method = 2;
     if (c.world > 1 && e->method != 2)
         throw HipError("column sharding (world > 1) is implemented for the Woodbury path only");
     if (c.world > 1 && !e->hy.know_alpha)
         throw HipError("unknown alpha with world > 1 is not supported");
+    if (e->method == 4 && c.ortho)
+        throw HipError("the orthogonal-design triangle sampler is not in this build");
+    if (e->method == 4 && (c.p > c.n || c.p > kTriMaxP))
+        throw HipError("triangle sampler needs p <= n and p <= 2048");
     if (e->method == 1 && c.p > 16384) throw HipError("p x p Cholesky path limited to p <= 16384");
     if (e->method == 2 && e->n_pad > 8192)
         throw HipError("Woodbury path limited to n <= 8192 in this build");
@@ -459,6 +575,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
             launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->gdiag);
         }
     }
+    if (e->method == 4) tri_setup(e);
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -494,6 +611,19 @@ void engine_init_state_local(bb_engine *e) {
     s.sig2 = c.true_sig2 > 0 ? c.true_sig2 : 0.0;
     s.tau = c.true_tau > 0 ? c.true_tau : 0.0;
     HIPCHECK(hipMemcpyAsync(e->sc, &s, sizeof(s), hipMemcpyHostToDevice, e->stream));
+    if (e->method == 4) {  // BridgeWrapper.cpp:123 u[0].fill(0.5); omega starts at 1.0 (:604)
+        std::vector<double> h(e->p_pad, 0.5);
+        HIPCHECK(hipMemcpyAsync(e->u, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice,
+                                e->stream));
+        std::vector<double> h1(e->p_pad, 1.0);
+        HIPCHECK(hipMemcpyAsync(e->lam, h1.data(), h1.size() * sizeof(double),
+                                hipMemcpyHostToDevice, e->stream));
+        HIPCHECK(hipMemcpyAsync(e->tr_u, h.data(), (size_t)e->p_loc * sizeof(double),
+                                hipMemcpyHostToDevice, e->stream));
+        HIPCHECK(hipMemcpyAsync(e->tr_lam, h1.data(), (size_t)e->p_loc * sizeof(double),
+                                hipMemcpyHostToDevice, e->stream));
+        HIPCHECK(hipStreamSynchronize(e->stream));
+    }
     // trace slot 0 holds the starting values (as the reference's slot 0 before burn-in)
     HIPCHECK(hipMemcpyAsync(e->tr_beta, e->beta, (size_t)e->p_loc * sizeof(double),
                             hipMemcpyDeviceToDevice, e->stream));
@@ -721,6 +851,50 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
 }
 
 int bb_engine_method(const bb_engine *e) { return e->method; }
+
+int bb_engine_get_tri_trace(bb_engine *e, int slot0, int count, double *u, double *shape) {
+    try {
+        if (e->method != 4) throw HipError("not a triangle-method engine");
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        const size_t pl = (size_t)e->p_loc;
+        for (int k = 0; k < count; ++k) {
+            const int s = (slot0 + k) % e->cap;
+            if (u)
+                HIPCHECK(hipMemcpy(u + k * pl, e->tr_u + s * pl, pl * sizeof(double),
+                                   hipMemcpyDeviceToHost));
+            if (shape)
+                HIPCHECK(hipMemcpy(shape + k * pl, e->tr_shape + s * pl, pl * sizeof(double),
+                                   hipMemcpyDeviceToHost));
+        }
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_set_tri_state(bb_engine *e, const double *u) {
+    try {
+        if (e->method != 4) throw HipError("not a triangle-method engine");
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        HIPCHECK(hipMemcpy(e->u, u, (size_t)e->p_loc * sizeof(double), hipMemcpyHostToDevice));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_get_tri_basis(bb_engine *e, double *tV, double *a, double *d) {
+    if (e->method != 4) {
+        set_error("not a triangle-method engine");
+        return -1;
+    }
+    if (tV) memcpy(tV, e->h_tV.data(), e->h_tV.size() * sizeof(double));
+    if (a) memcpy(a, e->h_a.data(), e->h_a.size() * sizeof(double));
+    if (d) memcpy(d, e->h_d.data(), e->h_d.size() * sizeof(double));
+    return 0;
+}
 int bb_engine_gram_mode(const bb_engine *e) { return e->cfg.gram_mode; }
 
 int bb_engine_enable_timing(bb_engine *e, int enable) {
@@ -1537,6 +1711,81 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
         printf("Aborting Gibbs sampler.\n");
     }
     bb_engine_get_trace(e, 0, m, betap, lambdap, sig2p, taup, alphap);
+    if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
+    *runtime = rt;
+    bb_engine_destroy(e);
+}
+
+void bridge_regression(double *betap, double *up, double *omegap, double *shapep,
+                       double *sig2p, double *taup, double *alphap, const double *yp,
+                       const double *Xp, const double *sig2_shape, const double *sig2_scale,
+                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                       const double *alpha_b, const double *true_sig2, const double *true_tau,
+                       const double *true_alpha, const int *P, const int *N, const int *M,
+                       const int *burn, double *runtime, const int *ortho,
+                       const int *betaburn, const int *use_hmc) {
+    const int p = *P, n = *N, m = *M, b = *burn;
+    *runtime = 0.0;
+    if (*ortho) {  // BridgeWrapper.cpp:624-633 (bridge_regression_ortho)
+        printf("Error: the orthogonal-design triangle sampler is not in this build.\n");
+        printf("Aborting Gibbs sampler.\n");
+        return;
+    }
+    (void)use_hmc;  // BridgeRegression.cpp:418 forces use_hmc = false
+    bb_config c;
+    bb_config_default(&c);
+    c.n = n;
+    c.p = p;
+    c.p_local = p;
+    c.sig2_shape = *sig2_shape;
+    c.sig2_scale = *sig2_scale;
+    c.nu_shape = *nu_shape;
+    c.nu_rate = *nu_rate;
+    c.alpha_a = *alpha_a;
+    c.alpha_b = *alpha_b;
+    c.true_sig2 = *true_sig2;
+    c.true_tau = *true_tau;
+    c.true_alpha = *true_alpha;
+    c.method = 4;
+    c.betaburn = *betaburn > 0 ? *betaburn : 0;  // BridgeRegression.cpp:407
+    c.trace_capacity = m < 1 ? 1 : m;
+    c.device = g_device;
+    next_call_key(&c.seed, &c.stream);
+    if (g_verbose) {  // BridgeWrapper.cpp:112-117
+        printf("Bridge Regression (mix. of triangles):");
+        if (c.true_alpha > 0) printf(" known alpha=%g", c.true_alpha);
+        if (c.true_sig2 > 0) printf(", sig2=%g", c.true_sig2);
+        if (c.true_tau > 0) printf(", tau=%g", c.true_tau);
+        printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
+    }
+    bb_engine *e = nullptr;
+    if (bb_engine_create(&c, Xp, yp, &e) != 0) {
+        printf("Error: %s\n", g_last_error.c_str());
+        printf("Aborting Gibbs sampler.\n");
+        return;
+    }
+    double rt = 0.0;
+    bool ok = bb_engine_init_state(e) == 0;
+    if (ok) {
+        // burn-in: `burn` sweeps in slot 0 (:141), MCMC slots 1..M-1 (:160)
+        ok = bb_engine_run(e, 1, b, 0, 0, 0) == 0 && bb_engine_sync(e) == 0;
+        auto t2 = std::chrono::steady_clock::now();
+        if (ok && m > 1) ok = bb_engine_run(e, (uint64_t)b + 1, m - 1, 1, 1, 1) == 0;
+        ok = (bb_engine_sync(e) == 0) && ok;
+        auto t3 = std::chrono::steady_clock::now();
+        rt = std::chrono::duration<double>(t3 - t2).count();
+        uint32_t f = 0;
+        if (ok && bb_engine_error_flags(e, &f) == 0 && (f & ~4u)) {
+            printf("Error: numerical failure in the device sampler (flags %u)\n", f);
+            printf("Aborting Gibbs sampler.\n");
+        }
+    }
+    if (!ok) {
+        printf("Error: %s\n", g_last_error.c_str());
+        printf("Aborting Gibbs sampler.\n");
+    }
+    bb_engine_get_trace(e, 0, m, betap, omegap, sig2p, taup, alphap);
+    bb_engine_get_tri_trace(e, 0, m, up, shapep);
     if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
     *runtime = rt;
     bb_engine_destroy(e);

@@ -27,6 +27,7 @@ constexpr int kGramBK = 16;     // Gram K step
 constexpr int kNB = 64;         // Cholesky block
 constexpr int kXvCols = 256;    // columns per block of the X.v partial-sum kernel
 constexpr int kXvRows = 512;    // rows per block of the X.v partial-sum kernel
+constexpr int kTriMaxP = 2048;  // triangle-mixture sampler: coefficients in one workgroup
 
 // Packed upper triangle, column-major: element (r, c), r <= c, at c (c + 1) / 2 + r.  The
 // Woodbury Gram travels in this form (red2), so its all-reduce moves n(n+1)/2 doubles.
@@ -151,6 +152,15 @@ void launch_beta_ortho(hipStream_t s, const double *gdiag, const double *c, cons
 // alpha | beta, tau random-walk MH (world == 1).
 void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, double pr_a,
                      double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr);
+
+// Triangle-mixture update (bb_tri.hip): omega, u and the rtnorm_gibbs beta passes of one
+// sweep of bridge.reg.tri, given sc->tau, sig2, alpha.  p <= kTriMaxP.  err bits: 64 a
+// truncated draw exhausted its attempts, 128 an empty truncation interval.
+void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, double *shape,
+                       int p, const double *tVc, const double *tVr, const double *a,
+                       const double *d, const DevScalars *sc, int betaburn, uint64_t k0,
+                       uint64_t k1, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega,
+                       double *tr_shape, uint32_t *err);
 
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,

@@ -1,0 +1,255 @@
+// bb_tri.hip -- triangle-mixture Gibbs update for bridge.reg.tri (gfx950).
+//
+// Reference: Code/C/BridgeRegression.cpp:97-147 (sample_u, sample_omega with shape),
+// :405-433 (sample_beta), :235-286 (rtnorm_gibbs); driver BridgeWrapper.cpp:80-204.
+//
+// rtnorm_gibbs is a sequential coordinate sweep over the p coordinates z = V'beta; each
+// step needs the tightest bounds over all p box constraints |beta_j| <= b_j.  One
+// workgroup of 256 threads runs the whole update: thread j owns coefficients
+// j + 256 k (b_j and beta_cur_j = (tV' z)_j stay in registers), the row v_i. of tV is
+// prefetched one coordinate ahead, the bounds are wave-reduced (max/min are exact, so any
+// tree gives the CPU checker's value) and lane 0 of wave 0 draws the truncated normal.
+// Two barriers per coordinate.  beta_cur is kept up to date incrementally
+// (beta_cur_j += v_ij dz_i) instead of recomputing dot(v_j, z) per coordinate as :254-258
+// does: the same quantity in O(p^2) instead of O(p^3) per pass (oracle/bb_oracle.c
+// bbo_tri_update uses the identical update order).
+//
+// r.tnorm comes from the un-vendored RNG library; it is restated from Robert (1995):
+// normal or uniform rejection when the standardised interval holds 0, else Robert's
+// uniform / translated-exponential proposal.  Counter kinds 8 (omega), 9 (u), 10 (z_i).
+#include <hip/hip_runtime.h>
+
+#include "bb_kernels.h"
+#include "bb_sampler.h"
+
+namespace bb {
+
+namespace {
+
+constexpr int kTriNT = 256;
+constexpr int kTriE = kTriMaxP / kTriNT;  // coefficients per thread
+constexpr long kTnMaxAttempts = 1l << 22;
+constexpr unsigned KIND_TRI_OMEGA = 8, KIND_TRI_U = 9, KIND_TRI_Z = 10;
+
+__device__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
+                         uint32_t *err) {
+    const double sq = sqrt(a * a + 4.0);
+    const double as = 0.5 * (a + sq);
+    const double thr = a + 2.0 / (a + sq) * exp(0.5 + 0.25 * (a * a - a * sq));
+    for (long k = 0; k < kTnMaxAttempts; ++k) {
+        U4 r = uniforms(key, t, KIND_TRI_Z, i, it, (uint64_t)k);
+        if (b <= thr) {
+            const double x = a + (b - a) * r.r[0];
+            if (r.r[1] <= exp(0.5 * (a * a - x * x))) return x;
+        } else {
+            const double x = a - log(r.r[0]) / as;
+            const double e = x - as;
+            if (x <= b && r.r[1] <= exp(-0.5 * e * e)) return x;
+        }
+    }
+    atomicOr(err, 64u);
+    return a;
+}
+
+__device__ double tnorm(double lo, double hi, double mu, double sd, Key key, uint64_t t,
+                        uint64_t i, uint64_t it, uint32_t *err) {
+    const double a = (lo - mu) / sd, b = (hi - mu) / sd;
+    if (!(a < b)) {
+        atomicOr(err, 128u);
+        return lo;
+    }
+    if (a <= 0.0 && b >= 0.0) {
+        const bool wide = (b - a) >= 2.5066282746310002;  // sqrt(2 pi)
+        for (long k = 0; k < kTnMaxAttempts; ++k) {
+            U4 r = uniforms(key, t, KIND_TRI_Z, i, it, (uint64_t)k);
+            if (wide) {
+                const double x = bm_normal(r.r[0], r.r[1]);
+                if (x >= a && x <= b) return mu + sd * x;
+            } else {
+                const double x = a + (b - a) * r.r[0];
+                if (r.r[1] <= exp(-0.5 * x * x)) return mu + sd * x;
+            }
+        }
+        atomicOr(err, 64u);
+        return lo;
+    }
+    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, err);
+    return mu - sd * tn_pos(-b, -a, key, t, i, it, err);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// tVc: tV column-major (tVc[i + j p] = tV(i, j)); tVr: its transpose (tVr[i p + j] =
+// tV(i, j)), so row i of tV is contiguous for the coordinate loop.
+__global__ __launch_bounds__(kTriNT) void k_tri_update(
+    double *beta, double *u, double *omega, double *shape, int p, const double *tVc,
+    const double *tVr, const double *av, const double *dv, const DevScalars *sc, int betaburn,
+    Key key, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega, double *tr_shape,
+    uint32_t *err) {
+    __shared__ double sz[kTriMaxP];
+    __shared__ double sb[kTriMaxP];
+    __shared__ double shmax[kTriNT / 64], shmin[kTriNT / 64];
+    __shared__ double sdz;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double tau = sc->tau, sig2 = sc->sig2, alpha = sc->alpha;
+
+    double bj[kTriE], bcur[kTriE];
+#pragma unroll
+    for (int e = 0; e < kTriE; ++e) {
+        const int j = tid + e * kTriNT;
+        bj[e] = 0.0;
+        if (j < p) {
+            const double betaj = beta[j];
+            // sample_omega (BridgeRegression.cpp:130-146)
+            const double aj = exp(alpha * log(fabs(betaj) / ((1.0 - u[j]) * tau)));
+            const double prob = alpha / (1.0 + alpha * aj);
+            U4 r = uniforms(key, t, KIND_TRI_OMEGA, (uint64_t)j, 0, 0);
+            double w, sh;
+            if (r.r[0] > prob) {
+                sh = 1.0;
+                w = -log(r.r[1]);  // Ga(1, 1)
+            } else {
+                sh = 2.0;
+                w = -log(r.r[1]) - log(r.r[2]);  // Ga(2, 1)
+            }
+            const double om = w + aj;
+            // sample_u (:97-111): flat(0, right)
+            const double right = 1.0 - fabs(betaj) / tau * exp(-1.0 * log(om) / alpha);
+            U4 r2 = uniforms(key, t, KIND_TRI_U, (uint64_t)j, 0, 0);
+            const double uj = right * r2.r[0];
+            bj[e] = (1.0 - uj) * exp(log(om) / alpha) * tau;  // sample_beta :410-412
+            omega[j] = om;
+            shape[j] = sh;
+            u[j] = uj;
+            if (tr_omega) tr_omega[j] = om;
+            if (tr_shape) tr_shape[j] = sh;
+            if (tr_u) tr_u[j] = uj;
+            sb[j] = betaj;
+        }
+    }
+    __syncthreads();
+    const double sig = sqrt(sig2);
+    for (int it = 0; it <= betaburn; ++it) {
+        // z = tV beta (:246)
+        for (int i = tid; i < p; i += kTriNT) {
+            double s = 0.0;
+            for (int j = 0; j < p; ++j) s += tVc[i + (size_t)j * p] * sb[j];
+            sz[i] = s;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kTriE; ++e) {
+            const int j = tid + e * kTriNT;
+            double s = 0.0;
+            if (j < p)
+                for (int k = 0; k < p; ++k) s += tVr[(size_t)k * p + j] * sz[k];
+            bcur[e] = s;
+        }
+        double vn[kTriE];
+#pragma unroll
+        for (int e = 0; e < kTriE; ++e) {
+            const int j = tid + e * kTriNT;
+            vn[e] = j < p ? tVr[j] : 0.0;
+        }
+        for (int i = 0; i < p; ++i) {  // :250-283
+            double v[kTriE];
+#pragma unroll
+            for (int e = 0; e < kTriE; ++e) v[e] = vn[e];
+            if (i + 1 < p) {
+#pragma unroll
+                for (int e = 0; e < kTriE; ++e) {
+                    const int j = tid + e * kTriNT;
+                    vn[e] = j < p ? tVr[(size_t)(i + 1) * p + j] : 0.0;
+                }
+            }
+            const double zi = sz[i];
+            double lmax = -1.0 * 1.7976931348623157e308, rmin = 1.7976931348623157e308;
+#pragma unroll
+            for (int e = 0; e < kTriE; ++e) {
+                const int j = tid + e * kTriNT;
+                if (j < p) {
+                    const double vji = v[e];
+                    const double rji = bcur[e] - vji * zi;
+                    const double dif = bj[e] - rji, sum = bj[e] + rji;
+                    const double left = (vji > 0 ? -sum : -dif) / fabs(vji);
+                    const double right = (vji > 0 ? dif : sum) / fabs(vji);
+                    lmax = lmax > left ? lmax : left;
+                    rmin = rmin < right ? rmin : right;
+                }
+            }
+            lmax = wave_max(lmax);
+            rmin = wave_min(rmin);
+            if (lane == 0) {
+                shmax[wv] = lmax;
+                shmin[wv] = rmin;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                double L = shmax[0], R = shmin[0];
+#pragma unroll
+                for (int w = 1; w < kTriNT / 64; ++w) {
+                    L = L > shmax[w] ? L : shmax[w];
+                    R = R < shmin[w] ? R : shmin[w];
+                }
+                const double di = dv[i];
+                double zn;
+                if (di > 1e-16) {
+                    zn = tnorm(L, R, av[i] / (di * di), sig / di, key, t, (uint64_t)i,
+                               (uint64_t)it, err);
+                } else {
+                    U4 r = uniforms(key, t, KIND_TRI_Z, (uint64_t)i, (uint64_t)it, 0);
+                    zn = L + (R - L) * r.r[0];
+                }
+                sdz = zn - zi;
+                sz[i] = zn;
+            }
+            __syncthreads();
+            const double dz = sdz;
+#pragma unroll
+            for (int e = 0; e < kTriE; ++e) bcur[e] += v[e] * dz;
+        }
+        // beta = tV' z (:285)
+#pragma unroll
+        for (int e = 0; e < kTriE; ++e) {
+            const int j = tid + e * kTriNT;
+            if (j < p) {
+                double s = 0.0;
+                for (int k = 0; k < p; ++k) s += tVr[(size_t)k * p + j] * sz[k];
+                sb[j] = s;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int e = 0; e < kTriE; ++e) {
+        const int j = tid + e * kTriNT;
+        if (j < p) {
+            beta[j] = sb[j];
+            if (tr_beta) tr_beta[j] = sb[j];
+        }
+    }
+}
+
+}  // namespace
+
+void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, double *shape,
+                       int p, const double *tVc, const double *tVr, const double *a,
+                       const double *d, const DevScalars *sc, int betaburn, uint64_t k0,
+                       uint64_t k1, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega,
+                       double *tr_shape, uint32_t *err) {
+    if (p < 1 || p > kTriMaxP) return;  // the engine checks p at setup
+    hipLaunchKernelGGL(k_tri_update, dim3(1), dim3(kTriNT), 0, s, beta, u, omega, shape, p, tVc,
+                       tVr, a, d, sc, betaburn, Key{k0, k1}, t, tr_beta, tr_u, tr_omega,
+                       tr_shape, err);
+}
+
+}  // namespace bb

@@ -72,6 +72,25 @@ void bridge_EM(double *betap, const double *yp, const double *Xp, const double *
                const double *alpha, const int *P, const int *N, const double *lambda_max,
                const double *tol, int *max_iter, const int *use_cg);
 
+/*
+ * Triangle-mixture Gibbs sampler: replaces Code/C/BridgeWrapper.cpp:572-657 (decl.
+ * BridgeWrapper.h:178-203; driver :80-204; conditionals BridgeRegression.cpp:97-147,
+ * 235-286, 405-465), called by bridge.reg.tri (BridgeWrapper.R:139-186) with 26 args.
+ * betap, up, omegap, shapep are P x M column-major traces; sig2p, taup, alphap are M.
+ * Requires P <= N and P <= 2048 (the reference's svd(X, 'A') indexing breaks for P > N).
+ * `ortho` and `use_hmc` are declared `const bool*` but R passes integers; both are read
+ * as ints.  The orthogonal-design triangle variant (ortho != 0) and HMC (dead code in the
+ * reference, :418) are not in this build: ortho prints an error and returns.
+ */
+void bridge_regression(double *betap, double *up, double *omegap, double *shapep,
+                       double *sig2p, double *taup, double *alphap, const double *yp,
+                       const double *Xp, const double *sig2_shape, const double *sig2_scale,
+                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                       const double *alpha_b, const double *true_sig2, const double *true_tau,
+                       const double *true_alpha, const int *P, const int *N, const int *M,
+                       const int *burn, double *runtime, const int *ortho,
+                       const int *betaburn, const int *use_hmc);
+
 /* ------------------------------------------------------------------------ */
 /* Part 2: extensions                                                        */
 /* ------------------------------------------------------------------------ */
@@ -115,12 +134,14 @@ typedef struct bb_config {
     double sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a, alpha_b;
     double true_sig2, true_tau, true_alpha;
     int ortho;          /* orthogonal-design variant (sample_beta_stable_ortho) */
-    int method;         /* 0 auto (chol if p <= n else woodbury), 1 chol, 2 woodbury */
+    int method;         /* 0 auto (chol if p <= n else woodbury), 1 chol, 2 woodbury,
+                           4 triangle mixture (bridge.reg.tri; p <= n, p <= 2048) */
     int trace_capacity; /* number of trace slots kept on device (>= 1) */
     uint64_t seed, stream;
     int device;
     int gram_mode;      /* Woodbury Gram: 0 fp64 MFMA, 1 Ozaki-II on int8 MFMA (fp64-accurate);
                            default 1, or 0 when env BB_GRAM_MODE=fp64 */
+    int betaburn;       /* triangle method: rtnorm_gibbs passes per sweep - 1 */
 } bb_config;
 
 void bb_config_default(bb_config *cfg);
@@ -177,6 +198,14 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
  * single GPU (RCCL cannot place two ranks on one device).  p > n path only.
  */
 typedef struct bb_group bb_group;
+/* Triangle method (cfg.method == 4): u and shape traces (omega comes back as `lambda`
+ * from bb_engine_get_trace), and the design basis X = U diag(d) V' the engine computed
+ * at setup: tV (P x P column-major, row i = i-th right singular vector), a = V'X'y, d. */
+int bb_engine_get_tri_trace(bb_engine *e, int slot0, int count, double *u, double *shape);
+int bb_engine_get_tri_basis(bb_engine *e, double *tV, double *a, double *d);
+/* Triangle method: overwrite the latent u (P) -- teacher-forced tests. */
+int bb_engine_set_tri_state(bb_engine *e, const double *u);
+
 int bb_group_create(bb_engine **engines, int count, bb_group **out);
 void bb_group_destroy(bb_group *g);
 int bb_group_init_state(bb_group *g);

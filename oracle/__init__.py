@@ -28,6 +28,9 @@ KIND_SIG2 = 4
 KIND_BETA_Z = 5
 KIND_DELTA = 6
 KIND_ALPHA = 7
+KIND_TRI_OMEGA = 8
+KIND_TRI_U = 9
+KIND_TRI_Z = 10
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -73,6 +76,14 @@ def lib():
                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, _dp,
                                    _u64p, ctypes.c_uint64]
         L.bbo_alpha_mh.restype = ctypes.c_double
+        L.bbo_tnorm.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, _u64p, ctypes.c_uint64, ctypes.c_uint64,
+                                ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]
+        L.bbo_tnorm.restype = ctypes.c_double
+        L.bbo_tri_update.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_long, _dp, _dp, _dp,
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_int, _u64p, ctypes.c_uint64, _dp, _dp, _dp]
+        L.bbo_tri_update.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -156,3 +167,29 @@ def alpha_mh(a_old, beta, tau, pr_a, pr_b, seed, stream, t, ep=0.1):
     s = np.empty_like(beta)
     return lib().bbo_alpha_mh(a_old, _ptr(beta), beta.shape[0], tau, pr_a, pr_b, ep, _ptr(s),
                               _key(seed, stream), t)
+
+
+def tnorm(lo, hi, mu, sd, seed, stream, t, i, it=0):
+    """r.tnorm(lo, hi, mu, sd) restated (Robert 1995); see bb_oracle.c bbo_tnorm."""
+    f = ctypes.c_int(0)
+    x = lib().bbo_tnorm(lo, hi, mu, sd, _key(seed, stream), t, i, it, ctypes.byref(f))
+    if f.value:
+        raise ValueError(f"tnorm failed (code {f.value})")
+    return x
+
+
+def tri_update(beta, u, tV, a, d, tau, sig2, alpha, betaburn, seed, stream, t):
+    """One sweep's omega, u, beta updates of the triangle sampler (bb_oracle.c
+    bbo_tri_update).  beta and u are updated in place; returns (omega, shape)."""
+    p = beta.shape[0]
+    tV = np.asfortranarray(tV, dtype=np.float64)
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    d = np.ascontiguousarray(d, dtype=np.float64)
+    omega, shape = np.empty(p), np.empty(p)
+    z, bcur, b = np.empty(p), np.empty(p), np.empty(p)
+    fails = lib().bbo_tri_update(_ptr(beta), _ptr(u), _ptr(omega), _ptr(shape), p, _ptr(tV),
+                                 _ptr(a), _ptr(d), tau, sig2, alpha, betaburn,
+                                 _key(seed, stream), t, _ptr(z), _ptr(bcur), _ptr(b))
+    if fails:
+        raise ValueError(f"tri_update: {fails} failed truncated-normal draws")
+    return omega, shape

@@ -346,3 +346,150 @@ double bbo_alpha_mh(double a_old, const double *beta, long p, double tau, double
     if (u[1] > exp(log_accept)) return a_old;
     return a_new;
 }
+
+/* ----------------------------------------------------------------------- */
+/* Triangle-mixture sampler (bridge.reg.tri): BridgeRegression.cpp:97-147    */
+/* (sample_u, sample_omega with shape), :405-433 (sample_beta), :235-286     */
+/* (rtnorm_gibbs).  The truncated normal r.tnorm comes from the un-vendored  */
+/* RNG library, so it is restated from Robert (1995): normal or uniform      */
+/* rejection when the interval holds 0, else Robert's uniform / translated-  */
+/* exponential choice.  Counter kinds 8 (omega), 9 (u), 10 (z_i attempts).   */
+/* ----------------------------------------------------------------------- */
+enum { BBO_KIND_TRI_OMEGA = 8, BBO_KIND_TRI_U = 9, BBO_KIND_TRI_Z = 10 };
+#define BBO_TN_MAX_ATTEMPTS (1L << 22)
+
+/* one-sided standard truncated normal on [a, b], 0 <= a < b (Robert 1995, prop. 2.3) */
+static double tn_pos(double a, double b, const uint64_t key[2], uint64_t t, uint64_t i,
+                     uint64_t it, int *fail)
+{
+    const double sq = sqrt(a * a + 4.0);
+    const double as = 0.5 * (a + sq);
+    const double thr = a + 2.0 / (a + sq) * exp(0.5 + 0.25 * (a * a - a * sq));
+    for (long k = 0; k < BBO_TN_MAX_ATTEMPTS; ++k) {
+        double r[4];
+        draw4(key, t, BBO_KIND_TRI_Z, i, it, (uint64_t)k, r);
+        if (b <= thr) {
+            const double x = a + (b - a) * r[0];
+            if (r[1] <= exp(0.5 * (a * a - x * x))) return x;
+        } else {
+            const double x = a - log(r[0]) / as;
+            const double e = x - as;
+            if (x <= b && r[1] <= exp(-0.5 * e * e)) return x;
+        }
+    }
+    *fail = 1;
+    return a;
+}
+
+/* r.tnorm(lo, hi, mu, sd) restated; attempts use counters (t, 10<<56 | i, it, k). */
+double bbo_tnorm(double lo, double hi, double mu, double sd, const uint64_t key[2], uint64_t t,
+                 uint64_t i, uint64_t it, int *fail)
+{
+    const double a = (lo - mu) / sd, b = (hi - mu) / sd;
+    if (!(a < b)) {
+        *fail = 2;
+        return lo;
+    }
+    if (a <= 0.0 && b >= 0.0) {
+        const int wide = (b - a) >= 2.5066282746310002; /* sqrt(2 pi) */
+        for (long k = 0; k < BBO_TN_MAX_ATTEMPTS; ++k) {
+            double r[4];
+            draw4(key, t, BBO_KIND_TRI_Z, i, it, (uint64_t)k, r);
+            if (wide) {
+                const double x = bm_normal(r[0], r[1]);
+                if (x >= a && x <= b) return mu + sd * x;
+            } else {
+                const double x = a + (b - a) * r[0];
+                if (r[1] <= exp(-0.5 * x * x)) return mu + sd * x;
+            }
+        }
+        *fail = 1;
+        return lo;
+    }
+    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, fail);
+    return mu - sd * tn_pos(-b, -a, key, t, i, it, fail);
+}
+
+/*
+ * One sweep's omega, u and beta updates of the triangle sampler, given tau, sig2,
+ * alpha.  tV is the p x p matrix V' of X = U diag(d) V' (column-major, tV[i + j p]),
+ * a = d * U'y (BridgeRegression.cpp:47-57).  u holds the previous sweep's u on entry.
+ * rtnorm_gibbs keeps beta_cur = tV' z up to date incrementally (beta_cur_j += v_ji dz_i)
+ * instead of recomputing dot(v_j, z) for every i (:254-258): the same quantity, O(p^2)
+ * instead of O(p^3) per pass.  Returns the number of failed truncated draws.
+ */
+long bbo_tri_update(double *beta, double *u, double *omega, double *shape, long p,
+                    const double *tV, const double *a, const double *d, double tau, double sig2,
+                    double alpha, int betaburn, const uint64_t key[2], uint64_t t, double *z,
+                    double *bcur, double *b)
+{
+    long fails = 0;
+    for (long j = 0; j < p; ++j) {
+        double r[4];
+        /* sample_omega :130-146 */
+        const double aj = exp(alpha * log(fabs(beta[j]) / ((1.0 - u[j]) * tau)));
+        const double prob = alpha / (1.0 + alpha * aj);
+        draw4(key, t, BBO_KIND_TRI_OMEGA, (uint64_t)j, 0, 0, r);
+        double w;
+        if (r[0] > prob) {
+            shape[j] = 1.0;
+            w = -log(r[1]); /* Ga(1, 1) */
+        } else {
+            shape[j] = 2.0;
+            w = -log(r[1]) - log(r[2]); /* Ga(2, 1) */
+        }
+        omega[j] = w + aj;
+        /* sample_u :97-111: flat(0, right) */
+        const double right = 1.0 - fabs(beta[j]) / tau * exp(-1.0 * log(omega[j]) / alpha);
+        draw4(key, t, BBO_KIND_TRI_U, (uint64_t)j, 0, 0, r);
+        u[j] = right * r[0];
+        /* sample_beta :410-412 */
+        b[j] = (1.0 - u[j]) * exp(log(omega[j]) / alpha) * tau;
+    }
+    const double sig = sqrt(sig2);
+    for (int it = 0; it <= betaburn; ++it) {
+        for (long i = 0; i < p; ++i) { /* z = tV beta (:246) */
+            double s = 0.0;
+            for (long j = 0; j < p; ++j) s += tV[i + j * p] * beta[j];
+            z[i] = s;
+        }
+        for (long j = 0; j < p; ++j) {
+            double s = 0.0;
+            for (long k = 0; k < p; ++k) s += tV[k + j * p] * z[k];
+            bcur[j] = s;
+        }
+        for (long i = 0; i < p; ++i) { /* :250-283 */
+            double lmax = -1.0 * 1.7976931348623157e308, rmin = 1.7976931348623157e308;
+            const double zi = z[i];
+            for (long j = 0; j < p; ++j) {
+                const double vji = tV[i + j * p];
+                const double rji = bcur[j] - vji * zi;
+                const double dif = b[j] - rji, sum = b[j] + rji;
+                const double left = (vji > 0 ? -sum : -dif) / fabs(vji);
+                const double right = (vji > 0 ? dif : sum) / fabs(vji);
+                lmax = lmax > left ? lmax : left;
+                rmin = rmin < right ? rmin : right;
+            }
+            double zn;
+            if (d[i] > 1e-16) {
+                int f = 0;
+                zn = bbo_tnorm(lmax, rmin, a[i] / (d[i] * d[i]), sig / d[i], key, t,
+                               (uint64_t)i, (uint64_t)it, &f);
+                fails += f != 0;
+            } else {
+                double r[4];
+                draw4(key, t, BBO_KIND_TRI_Z, (uint64_t)i, (uint64_t)it, 0, r);
+                zn = lmax + (rmin - lmax) * r[0];
+            }
+            const double dz = zn - zi;
+            z[i] = zn;
+            for (long j = 0; j < p; ++j) bcur[j] += tV[i + j * p] * dz;
+        }
+        for (long j = 0; j < p; ++j) { /* beta = tV' z (:285) */
+            double s = 0.0;
+            for (long k = 0; k < p; ++k) s += tV[k + j * p] * z[k];
+            beta[j] = s;
+        }
+    }
+    return fails;
+}

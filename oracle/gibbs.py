@@ -221,3 +221,75 @@ def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stre
     w = sla.solve_triangular(Lm, y / sig - v, lower=True)
     w = sla.solve_triangular(Lm.T, w, lower=False)
     return u + D * (Xk.T @ w) / sig, lam, tau, sig2
+
+
+def bridge_regression_tri(y, X, nsamp, basis, burn=500, alpha=0.5, sig2_shape=0.0,
+                          sig2_scale=0.0, nu_shape=2.0, nu_rate=2.0, alpha_a=1.0, alpha_b=1.0,
+                          true_sig2=0.0, true_tau=0.0, true_alpha=None, betaburn=0, seed=0,
+                          stream=0):
+    """Restatement of bridge_regression (triangle mixture), BridgeWrapper.cpp:80-204.
+
+    ``basis`` = (tV, a, d) with X = U diag(d) V', tV = V', a = V'X'y
+    (BridgeRegression.cpp:47-57).  Sweep order per :136-168: tau, sig2, omega, u,
+    beta (rtnorm_gibbs x (betaburn + 1)), alpha.  Burn-in runs ``burn`` sweeps in slot 0
+    (:141); the MCMC loop fills slots 1..M-1.  Sweep counters: t = 0 extra tau draw,
+    1..burn burn-in, burn + i MCMC slot i.
+    """
+    from . import tri_update
+
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, p = X.shape
+    M = int(nsamp)
+    tV, av, dv = basis
+    if true_alpha is None:
+        true_alpha = alpha
+    know_sig2, know_tau, know_alpha = true_sig2 > 0, true_tau > 0, true_alpha > 0
+    G = X.T @ X
+    c = X.T @ y
+    b0, _ = least_squares(G, c, n)
+    tr = {k: np.zeros((p, M)) for k in ("beta", "u", "w", "shape")}
+    tr["w"][:] = 1.0  # BridgeWrapper.cpp:604
+    sig2, tau, alph = np.zeros(M), np.zeros(M), np.zeros(M)
+    beta = b0.copy()
+    u = np.full(p, 0.5)  # :123
+    tr["beta"][:, 0] = beta
+    tr["u"][:, 0] = u
+    alph[0] = 0.5
+    if know_sig2:
+        sig2[:] = true_sig2
+    if know_tau:
+        tau[:] = true_tau
+    if know_alpha:
+        alph[:] = true_alpha
+
+    def draw_tau(b, a, t):
+        return tau_from_sum(sum_abs_pow(b, a), p, a, nu_shape, nu_rate, seed, stream, t)
+
+    def draw_sig2(b, t):
+        r = y - X @ b
+        return sig2_from_rss(float(r @ r), n, sig2_shape, sig2_scale, seed, stream, t)
+
+    def sweep(slot, prev, t):
+        nonlocal beta
+        if not know_tau:
+            tau[slot] = draw_tau(beta, alph[prev], t)
+        if not know_sig2:
+            sig2[slot] = draw_sig2(beta, t)
+        om, sh = tri_update(beta, u, tV, av, dv, tau[slot], sig2[slot], alph[prev], betaburn,
+                            seed, stream, t)
+        tr["w"][:, slot], tr["shape"][:, slot] = om, sh
+        tr["u"][:, slot], tr["beta"][:, slot] = u, beta
+        if not know_alpha:
+            alph[slot] = alpha_mh(alph[prev], beta, tau[slot], alpha_a, alpha_b, seed, stream, t)
+
+    if not know_tau:
+        tau[0] = draw_tau(beta, alph[0], 0)  # :139
+    for i in range(burn):
+        sweep(0, 0, 1 + i)
+    t0 = time.perf_counter()
+    for i in range(1, M):
+        sweep(i, i - 1, burn + i)
+    out = {k: v.T.copy() for k, v in tr.items()}
+    out.update(sig2=sig2, tau=tau, alpha=alph, runtime=time.perf_counter() - t0)
+    return out
