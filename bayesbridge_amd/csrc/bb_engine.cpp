@@ -162,7 +162,8 @@ struct bb_engine {
     double *G = nullptr, *cvec = nullptr, *A = nullptr, *Y2 = nullptr, *W2 = nullptr,
            *gdiag = nullptr;
     // triangle mixture: design basis (bb_tri.hip), omega in lam, shape in D, u in u
-    double *tVc = nullptr, *tVr = nullptr, *tri_a = nullptr, *tri_d = nullptr;
+    double *tVc = nullptr, *tVr = nullptr, *tri_a = nullptr, *tri_d = nullptr,
+           *tri_G = nullptr;
     double *tr_u = nullptr, *tr_shape = nullptr;
     std::vector<double> h_tV, h_a, h_d;
     // traces
@@ -274,8 +275,8 @@ struct bb_engine {
         } else if (method == 4) {
             // BridgeWrapper.cpp:166-168: omega, u, then the rtnorm_gibbs beta passes
             mark(PH_BETA);
-            launch_tri_update(stream, beta, u, lam, D, p, tVc, tVr, tri_a, tri_d, sc,
-                              cfg.betaburn, cfg.seed, cfg.stream, t,
+            launch_tri_update(stream, beta, u, lam, D, p, tVc, tVr, tri_a, tri_d, tri_G, cvec,
+                              cfg.ortho, sc, cfg.betaburn, cfg.seed, cfg.stream, t,
                               slot_ptr(tr_beta, slot, p_loc), slot_ptr(tr_u, slot, p_loc), trl,
                               slot_ptr(tr_shape, slot, p_loc), err);
         } else {
@@ -452,6 +453,8 @@ void tri_setup(bb_engine *e) {
     HIPCHECK(hipMemcpy(e->tVr, tVr.data(), (size_t)p * p * sizeof(double), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(e->tri_a, e->h_a.data(), (size_t)p * sizeof(double), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(e->tri_d, e->h_d.data(), (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+    e->tri_G = dalloc<double>((size_t)p * p, o);  // full symmetric X'X (ortho variant)
+    HIPCHECK(hipMemcpy(e->tri_G, G.data(), (size_t)p * p * sizeof(double), hipMemcpyHostToDevice));
     e->tr_u = dalloc<double>((size_t)p * e->cap, o);
     e->tr_shape = dalloc<double>((size_t)p * e->cap, o);
 }
@@ -474,8 +477,6 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
         throw HipError("column sharding (world > 1) is implemented for the Woodbury path only");
     if (c.world > 1 && !e->hy.know_alpha)
         throw HipError("unknown alpha with world > 1 is not supported");
-    if (e->method == 4 && c.ortho)
-        throw HipError("the orthogonal-design triangle sampler is not in this build");
     if (e->method == 4 && (c.p > c.n || c.p > kTriMaxP))
         throw HipError("triangle sampler needs p <= n and p <= 2048");
     if (e->method == 1 && c.p > 16384) throw HipError("p x p Cholesky path limited to p <= 16384");
@@ -634,7 +635,12 @@ void engine_init_state_local(bb_engine *e) {
 
 void engine_init_state(bb_engine *e) {
     engine_init_state_local(e);
-    if (e->method != 3 && !e->hy.know_tau) e->pre_and_scalars(0, 0, 1);  // :262
+    if (e->method == 4 && e->cfg.ortho) {
+        // triangle ortho driver draws sig2 then tau before burn-in (BridgeWrapper.cpp:374-375)
+        if (!e->hy.know_tau || !e->hy.know_sig2) e->pre_and_scalars(0, 0, 0);
+    } else if (e->method != 3 && !e->hy.know_tau) {
+        e->pre_and_scalars(0, 0, 1);  // :262
+    }
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -1726,11 +1732,6 @@ void bridge_regression(double *betap, double *up, double *omegap, double *shapep
                        const int *betaburn, const int *use_hmc) {
     const int p = *P, n = *N, m = *M, b = *burn;
     *runtime = 0.0;
-    if (*ortho) {  // BridgeWrapper.cpp:624-633 (bridge_regression_ortho)
-        printf("Error: the orthogonal-design triangle sampler is not in this build.\n");
-        printf("Aborting Gibbs sampler.\n");
-        return;
-    }
     (void)use_hmc;  // BridgeRegression.cpp:418 forces use_hmc = false
     bb_config c;
     bb_config_default(&c);
@@ -1747,6 +1748,7 @@ void bridge_regression(double *betap, double *up, double *omegap, double *shapep
     c.true_tau = *true_tau;
     c.true_alpha = *true_alpha;
     c.method = 4;
+    c.ortho = *ortho != 0;  // bridge_regression_ortho, BridgeWrapper.cpp:320-432
     c.betaburn = *betaburn > 0 ? *betaburn : 0;  // BridgeRegression.cpp:407
     c.trace_capacity = m < 1 ? 1 : m;
     c.device = g_device;
@@ -1756,6 +1758,7 @@ void bridge_regression(double *betap, double *up, double *omegap, double *shapep
         if (c.true_alpha > 0) printf(" known alpha=%g", c.true_alpha);
         if (c.true_sig2 > 0) printf(", sig2=%g", c.true_sig2);
         if (c.true_tau > 0) printf(", tau=%g", c.true_tau);
+        if (c.ortho) printf("\nAssuming orthogonal design matrix!");
         printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
     }
     bb_engine *e = nullptr;

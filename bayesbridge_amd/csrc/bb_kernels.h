@@ -154,13 +154,15 @@ void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, d
                      double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr);
 
 // Triangle-mixture update (bb_tri.hip): omega, u and the rtnorm_gibbs beta passes of one
-// sweep of bridge.reg.tri, given sc->tau, sig2, alpha.  p <= kTriMaxP.  err bits: 64 a
+// sweep of bridge.reg.tri, given sc->tau, sig2, alpha; ortho != 0: the orthogonal-design
+// variant's coordinate Gibbs on beta (full Gram Gf, c = X'y).  p <= kTriMaxP.  err bits: 64 a
 // truncated draw exhausted its attempts, 128 an empty truncation interval.
 void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, double *shape,
                        int p, const double *tVc, const double *tVr, const double *a,
-                       const double *d, const DevScalars *sc, int betaburn, uint64_t k0,
-                       uint64_t k1, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega,
-                       double *tr_shape, uint32_t *err);
+                       const double *d, const double *Gf, const double *c, int ortho,
+                       const DevScalars *sc, int betaburn, uint64_t k0, uint64_t k1, uint64_t t,
+                       double *tr_beta, double *tr_u, double *tr_omega, double *tr_shape,
+                       uint32_t *err);
 
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,

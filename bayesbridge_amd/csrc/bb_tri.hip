@@ -92,11 +92,12 @@ __device__ __forceinline__ double wave_min(double v) {
 // tV(i, j)), so row i of tV is contiguous for the coordinate loop.
 __global__ __launch_bounds__(kTriNT) void k_tri_update(
     double *beta, double *u, double *omega, double *shape, int p, const double *tVc,
-    const double *tVr, const double *av, const double *dv, const DevScalars *sc, int betaburn,
-    Key key, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega, double *tr_shape,
-    uint32_t *err) {
+    const double *tVr, const double *av, const double *dv, const double *Gf, const double *cv,
+    int ortho, const DevScalars *sc, int betaburn, Key key, uint64_t t, double *tr_beta,
+    double *tr_u, double *tr_omega, double *tr_shape, uint32_t *err) {
     __shared__ double sz[kTriMaxP];
     __shared__ double sb[kTriMaxP];
+    __shared__ double sbnd[kTriMaxP];
     __shared__ double shmax[kTriNT / 64], shmin[kTriNT / 64];
     __shared__ double sdz;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -127,6 +128,7 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
             U4 r2 = uniforms(key, t, KIND_TRI_U, (uint64_t)j, 0, 0);
             const double uj = right * r2.r[0];
             bj[e] = (1.0 - uj) * exp(log(om) / alpha) * tau;  // sample_beta :410-412
+            sbnd[j] = bj[e];
             omega[j] = om;
             shape[j] = sh;
             u[j] = uj;
@@ -138,7 +140,35 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     }
     __syncthreads();
     const double sig = sqrt(sig2);
-    for (int it = 0; it <= betaburn; ++it) {
+    if (ortho) {
+        // sample_beta_ortho (BridgeRegression.cpp:362-403): coordinate Gibbs on beta itself,
+        // m_j = (c_j - sum_{k != j} G_jk beta_k) / G_jj, one pass (its burn defaults to 0).
+        // Gf is the full symmetric Gram, row j contiguous.
+        for (int j = 0; j < p; ++j) {
+            double part = 0.0;
+#pragma unroll
+            for (int e = 0; e < kTriE; ++e) {
+                const int k = tid + e * kTriNT;
+                if (k < p && k != j) part += Gf[(size_t)j * p + k] * sb[k];
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            if (lane == 0) shmax[wv] = part;
+            __syncthreads();
+            if (tid == 0) {
+                double xb = 0.0;
+#pragma unroll
+                for (int w = 0; w < kTriNT / 64; ++w) xb += shmax[w];
+                const double gjj = Gf[(size_t)j * p + j];
+                const double m = (cv[j] - xb) / gjj;
+                const double v = sig2 / gjj;
+                const double bnd = sbnd[j];
+                sb[j] = tnorm(-1.0 * bnd, bnd, m, sqrt(v), key, t, (uint64_t)j, 0, err);
+            }
+            __syncthreads();
+        }
+    }
+    for (int it = 0; it <= (ortho ? -1 : betaburn); ++it) {
         // z = tV beta (:246)
         for (int i = tid; i < p; i += kTriNT) {
             double s = 0.0;
@@ -243,13 +273,14 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
 
 void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, double *shape,
                        int p, const double *tVc, const double *tVr, const double *a,
-                       const double *d, const DevScalars *sc, int betaburn, uint64_t k0,
-                       uint64_t k1, uint64_t t, double *tr_beta, double *tr_u, double *tr_omega,
-                       double *tr_shape, uint32_t *err) {
+                       const double *d, const double *Gf, const double *c, int ortho,
+                       const DevScalars *sc, int betaburn, uint64_t k0, uint64_t k1, uint64_t t,
+                       double *tr_beta, double *tr_u, double *tr_omega, double *tr_shape,
+                       uint32_t *err) {
     if (p < 1 || p > kTriMaxP) return;  // the engine checks p at setup
     hipLaunchKernelGGL(k_tri_update, dim3(1), dim3(kTriNT), 0, s, beta, u, omega, shape, p, tVc,
-                       tVr, a, d, sc, betaburn, Key{k0, k1}, t, tr_beta, tr_u, tr_omega,
-                       tr_shape, err);
+                       tVr, a, d, Gf, c, ortho, sc, betaburn, Key{k0, k1}, t, tr_beta, tr_u,
+                       tr_omega, tr_shape, err);
 }
 
 }  // namespace bb

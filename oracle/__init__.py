@@ -80,8 +80,8 @@ def lib():
                                 ctypes.c_double, _u64p, ctypes.c_uint64, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]
         L.bbo_tnorm.restype = ctypes.c_double
-        L.bbo_tri_update.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_long, _dp, _dp, _dp,
-                                     ctypes.c_double, ctypes.c_double, ctypes.c_double,
+        L.bbo_tri_update.argtypes = [_dp, _dp, _dp, _dp, ctypes.c_long, _dp, _dp, _dp, _dp,
+                                     _dp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_int, _u64p, ctypes.c_uint64, _dp, _dp, _dp]
         L.bbo_tri_update.restype = ctypes.c_long
         _lib = L
@@ -178,17 +178,22 @@ def tnorm(lo, hi, mu, sd, seed, stream, t, i, it=0):
     return x
 
 
-def tri_update(beta, u, tV, a, d, tau, sig2, alpha, betaburn, seed, stream, t):
+def tri_update(beta, u, tV, a, d, tau, sig2, alpha, betaburn, seed, stream, t, G=None, c=None):
     """One sweep's omega, u, beta updates of the triangle sampler (bb_oracle.c
-    bbo_tri_update).  beta and u are updated in place; returns (omega, shape)."""
+    bbo_tri_update).  beta and u are updated in place; returns (omega, shape).
+    With G = X'X and c = X'y given, beta is drawn by the orthogonal-design variant."""
     p = beta.shape[0]
+    ortho = G is not None
+    G = np.ascontiguousarray(G if ortho else np.zeros((1, 1)), dtype=np.float64)
+    c = np.ascontiguousarray(c if ortho else np.zeros(1), dtype=np.float64)
     tV = np.asfortranarray(tV, dtype=np.float64)
     a = np.ascontiguousarray(a, dtype=np.float64)
     d = np.ascontiguousarray(d, dtype=np.float64)
     omega, shape = np.empty(p), np.empty(p)
     z, bcur, b = np.empty(p), np.empty(p), np.empty(p)
     fails = lib().bbo_tri_update(_ptr(beta), _ptr(u), _ptr(omega), _ptr(shape), p, _ptr(tV),
-                                 _ptr(a), _ptr(d), tau, sig2, alpha, betaburn,
+                                 _ptr(a), _ptr(d), _ptr(G), _ptr(c), int(ortho), tau, sig2,
+                                 alpha, betaburn,
                                  _key(seed, stream), t, _ptr(z), _ptr(bcur), _ptr(b))
     if fails:
         raise ValueError(f"tri_update: {fails} failed truncated-normal draws")

@@ -419,9 +419,10 @@ double bbo_tnorm(double lo, double hi, double mu, double sd, const uint64_t key[
  * instead of O(p^3) per pass.  Returns the number of failed truncated draws.
  */
 long bbo_tri_update(double *beta, double *u, double *omega, double *shape, long p,
-                    const double *tV, const double *a, const double *d, double tau, double sig2,
-                    double alpha, int betaburn, const uint64_t key[2], uint64_t t, double *z,
-                    double *bcur, double *b)
+                    const double *tV, const double *a, const double *d, const double *G,
+                    const double *c, int ortho, double tau, double sig2, double alpha,
+                    int betaburn, const uint64_t key[2], uint64_t t, double *z, double *bcur,
+                    double *b)
 {
     long fails = 0;
     for (long j = 0; j < p; ++j) {
@@ -447,6 +448,21 @@ long bbo_tri_update(double *beta, double *u, double *omega, double *shape, long 
         b[j] = (1.0 - u[j]) * exp(log(omega[j]) / alpha) * tau;
     }
     const double sig = sqrt(sig2);
+    if (ortho) {
+        /* sample_beta_ortho (BridgeRegression.cpp:362-403), one pass: G is the full
+         * p x p X'X, c = X'y. */
+        for (long j = 0; j < p; ++j) {
+            double xb = 0.0;
+            for (long k = 0; k < p; ++k)
+                if (k != j) xb += G[j * p + k] * beta[k];
+            const double gjj = G[j * p + j];
+            const double m = (c[j] - xb) / gjj, v = sig2 / gjj;
+            int f = 0;
+            beta[j] = bbo_tnorm(-1.0 * b[j], b[j], m, sqrt(v), key, t, (uint64_t)j, 0, &f);
+            fails += f != 0;
+        }
+        return fails;
+    }
     for (int it = 0; it <= betaburn; ++it) {
         for (long i = 0; i < p; ++i) { /* z = tV beta (:246) */
             double s = 0.0;

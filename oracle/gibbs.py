@@ -226,14 +226,17 @@ def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stre
 def bridge_regression_tri(y, X, nsamp, basis, burn=500, alpha=0.5, sig2_shape=0.0,
                           sig2_scale=0.0, nu_shape=2.0, nu_rate=2.0, alpha_a=1.0, alpha_b=1.0,
                           true_sig2=0.0, true_tau=0.0, true_alpha=None, betaburn=0, seed=0,
-                          stream=0):
+                          stream=0, ortho=False):
     """Restatement of bridge_regression (triangle mixture), BridgeWrapper.cpp:80-204.
 
     ``basis`` = (tV, a, d) with X = U diag(d) V', tV = V', a = V'X'y
     (BridgeRegression.cpp:47-57).  Sweep order per :136-168: tau, sig2, omega, u,
     beta (rtnorm_gibbs x (betaburn + 1)), alpha.  Burn-in runs ``burn`` sweeps in slot 0
     (:141); the MCMC loop fills slots 1..M-1.  Sweep counters: t = 0 extra tau draw,
-    1..burn burn-in, burn + i MCMC slot i.
+    1..burn burn-in, burn + i MCMC slot i.  ``ortho``: bridge_regression_ortho
+    (:320-432): beta by sample_beta_ortho, and sig2 is also drawn before burn-in (:374).
+    The ortho driver draws sig2 after omega and u, which does not change any variate here
+    (sig2 depends on beta only and every draw has its own counter).
     """
     from . import tri_update
 
@@ -277,14 +280,16 @@ def bridge_regression_tri(y, X, nsamp, basis, burn=500, alpha=0.5, sig2_shape=0.
         if not know_sig2:
             sig2[slot] = draw_sig2(beta, t)
         om, sh = tri_update(beta, u, tV, av, dv, tau[slot], sig2[slot], alph[prev], betaburn,
-                            seed, stream, t)
+                            seed, stream, t, *((G, c) if ortho else ()))
         tr["w"][:, slot], tr["shape"][:, slot] = om, sh
         tr["u"][:, slot], tr["beta"][:, slot] = u, beta
         if not know_alpha:
             alph[slot] = alpha_mh(alph[prev], beta, tau[slot], alpha_a, alpha_b, seed, stream, t)
 
+    if ortho and not know_sig2:
+        sig2[0] = draw_sig2(beta, 0)  # :374
     if not know_tau:
-        tau[0] = draw_tau(beta, alph[0], 0)  # :139
+        tau[0] = draw_tau(beta, alph[0], 0)  # :139, ortho :375
     for i in range(burn):
         sweep(0, 0, 1 + i)
     t0 = time.perf_counter()

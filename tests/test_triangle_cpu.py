@@ -60,8 +60,8 @@ def test_tri_update_respects_box_and_is_deterministic():
         assert np.array_equal(beta, beta2) and np.array_equal(u, u2)
 
 
-@pytest.mark.parametrize("know_tau", [True, False])
-def test_tri_chain_matches_exact_posterior(know_tau):
+@pytest.mark.parametrize("know_tau,ortho", [(True, False), (False, False), (False, True)])
+def test_tri_chain_matches_exact_posterior(know_tau, ortho):
     rng = np.random.default_rng(42)
     n = 6
     x = rng.standard_normal(n)
@@ -71,7 +71,7 @@ def test_tri_chain_matches_exact_posterior(know_tau):
     out = gibbs.bridge_regression_tri(y, X, nsamp=20000, basis=_basis(X, y), burn=200,
                                       alpha=alpha, true_sig2=sig2,
                                       true_tau=tau if know_tau else 0.0, nu_shape=2.0,
-                                      nu_rate=2.0, seed=99, stream=0)
+                                      nu_rate=2.0, seed=99, stream=0, ortho=ortho)
     draws = out["beta"][:, 0]
     exact = _posterior_mean_1d(x, y, sig2, tau, alpha, None if know_tau else (2.0, 2.0))
     se = _batch_means_se(draws)
@@ -106,3 +106,19 @@ def test_tri_driver_slot_semantics():
     assert np.all(out["u"][0] == 0.5) and np.all(out["w"][0] == 1.0)
     assert np.all(out["shape"][0] == 0.0) and np.all(out["sig2"] == 2.0)
     assert set(np.unique(out["shape"][1:])) <= {1.0, 2.0}
+
+
+def test_tri_ortho_chain_matches_dense_on_orthogonal_design():
+    """On an orthogonal design the coordinate-wise beta update (sample_beta_ortho) and
+    the svd-basis rtnorm_gibbs target the same posterior."""
+    rng = np.random.default_rng(8)
+    n, p = 40, 3
+    Q, _ = np.linalg.qr(rng.standard_normal((n, p)))
+    X = Q * np.array([3.0, 2.0, 1.5])
+    y = X @ np.array([0.8, 0.0, -0.6]) + rng.standard_normal(n)
+    kw = dict(nsamp=6000, basis=_basis(X, y), burn=200, alpha=0.5, seed=12)
+    a = gibbs.bridge_regression_tri(y, X, ortho=True, **kw)
+    b = gibbs.bridge_regression_tri(y, X, ortho=False, **kw)
+    for j in range(p):
+        se = math.hypot(_batch_means_se(a["beta"][:, j]), _batch_means_se(b["beta"][:, j]))
+        assert abs(a["beta"][:, j].mean() - b["beta"][:, j].mean()) < 6 * se + 2e-3, j
