@@ -8,8 +8,8 @@
 // workgroup of 256 threads runs the whole update: thread j owns coefficients
 // j + 256 k (b_j and beta_cur_j = (tV' z)_j stay in registers), the row v_i. of tV is
 // prefetched one coordinate ahead, the bounds are wave-reduced (max/min are exact, so any
-// tree gives the CPU checker's value) and lane 0 of wave 0 draws the truncated normal.
-// Two barriers per coordinate.  beta_cur is kept up to date incrementally
+// tree gives the CPU checker's value) and every lane evaluates the same truncated-normal
+// draw redundantly: one barrier per coordinate.  beta_cur is kept up to date incrementally
 // (beta_cur_j += v_ij dz_i) instead of recomputing dot(v_j, z) per coordinate as :254-258
 // does: the same quantity in O(p^2) instead of O(p^3) per pass (oracle/bb_oracle.c
 // bbo_tri_update uses the identical update order).
@@ -31,20 +31,43 @@ constexpr int kTriE = kTriMaxP / kTriNT;  // coefficients per thread
 constexpr long kTnMaxAttempts = 1l << 22;
 constexpr unsigned KIND_TRI_OMEGA = 8, KIND_TRI_U = 9, KIND_TRI_Z = 10;
 
+// Attempt 0 of every coordinate's draw is precomputed in parallel before the coordinate
+// loop (pre = {r0, r1, Box-Muller normal of (r0, r1)}), so the serial chain only runs
+// Philox on a rejection.  Bit-identical to drawing it in place.
+struct Pre {
+    double r0, r1, x0;
+};
+
+__device__ __forceinline__ void attempt(Key key, uint64_t t, uint64_t i, uint64_t it, long k,
+                                        const Pre &pre, double &r0, double &r1, double &x0,
+                                        bool need_x) {
+    if (k == 0) {
+        r0 = pre.r0;
+        r1 = pre.r1;
+        x0 = pre.x0;
+    } else {
+        U4 r = uniforms(key, t, KIND_TRI_Z, i, it, (uint64_t)k);
+        r0 = r.r[0];
+        r1 = r.r[1];
+        x0 = need_x ? bm_normal(r0, r1) : 0.0;
+    }
+}
+
 __device__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
-                         uint32_t *err) {
+                         const Pre &pre, uint32_t *err) {
     const double sq = sqrt(a * a + 4.0);
     const double as = 0.5 * (a + sq);
     const double thr = a + 2.0 / (a + sq) * exp(0.5 + 0.25 * (a * a - a * sq));
     for (long k = 0; k < kTnMaxAttempts; ++k) {
-        U4 r = uniforms(key, t, KIND_TRI_Z, i, it, (uint64_t)k);
+        double r0, r1, x0;
+        attempt(key, t, i, it, k, pre, r0, r1, x0, false);
         if (b <= thr) {
-            const double x = a + (b - a) * r.r[0];
-            if (r.r[1] <= exp(0.5 * (a * a - x * x))) return x;
+            const double x = a + (b - a) * r0;
+            if (r1 <= exp(0.5 * (a * a - x * x))) return x;
         } else {
-            const double x = a - log(r.r[0]) / as;
+            const double x = a - log(r0) / as;
             const double e = x - as;
-            if (x <= b && r.r[1] <= exp(-0.5 * e * e)) return x;
+            if (x <= b && r1 <= exp(-0.5 * e * e)) return x;
         }
     }
     atomicOr(err, 64u);
@@ -52,7 +75,7 @@ __device__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, ui
 }
 
 __device__ double tnorm(double lo, double hi, double mu, double sd, Key key, uint64_t t,
-                        uint64_t i, uint64_t it, uint32_t *err) {
+                        uint64_t i, uint64_t it, const Pre &pre, uint32_t *err) {
     const double a = (lo - mu) / sd, b = (hi - mu) / sd;
     if (!(a < b)) {
         atomicOr(err, 128u);
@@ -61,20 +84,20 @@ __device__ double tnorm(double lo, double hi, double mu, double sd, Key key, uin
     if (a <= 0.0 && b >= 0.0) {
         const bool wide = (b - a) >= 2.5066282746310002;  // sqrt(2 pi)
         for (long k = 0; k < kTnMaxAttempts; ++k) {
-            U4 r = uniforms(key, t, KIND_TRI_Z, i, it, (uint64_t)k);
+            double r0, r1, x0;
+            attempt(key, t, i, it, k, pre, r0, r1, x0, wide);
             if (wide) {
-                const double x = bm_normal(r.r[0], r.r[1]);
-                if (x >= a && x <= b) return mu + sd * x;
+                if (x0 >= a && x0 <= b) return mu + sd * x0;
             } else {
-                const double x = a + (b - a) * r.r[0];
-                if (r.r[1] <= exp(-0.5 * x * x)) return mu + sd * x;
+                const double x = a + (b - a) * r0;
+                if (r1 <= exp(-0.5 * x * x)) return mu + sd * x;
             }
         }
         atomicOr(err, 64u);
         return lo;
     }
-    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, err);
-    return mu - sd * tn_pos(-b, -a, key, t, i, it, err);
+    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, pre, err);
+    return mu - sd * tn_pos(-b, -a, key, t, i, it, pre, err);
 }
 
 __device__ __forceinline__ double wave_max(double v) {
@@ -98,8 +121,9 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     __shared__ double sz[kTriMaxP];
     __shared__ double sb[kTriMaxP];
     __shared__ double sbnd[kTriMaxP];
-    __shared__ double shmax[kTriNT / 64], shmin[kTriNT / 64];
-    __shared__ double sdz;
+    __shared__ Pre spre[kTriMaxP];
+    // per-wave partials, double-buffered by coordinate parity: one barrier per coordinate
+    __shared__ double shmax[2][kTriNT / 64], shmin[2][kTriNT / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const double tau = sc->tau, sig2 = sc->sig2, alpha = sc->alpha;
 
@@ -140,10 +164,21 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     }
     __syncthreads();
     const double sig = sqrt(sig2);
+    // Every thread reduces the per-wave partials in the same order and evaluates the same
+    // draw (uniform control flow, no divergence), so no broadcast barrier is needed; the
+    // owner of a coefficient keeps the state it alone reads later.
+    auto precompute = [&](int it) {
+        for (int i = tid; i < p; i += kTriNT) {
+            U4 r = uniforms(key, t, KIND_TRI_Z, (uint64_t)i, (uint64_t)it, 0);
+            spre[i] = Pre{r.r[0], r.r[1], bm_normal(r.r[0], r.r[1])};
+        }
+    };
     if (ortho) {
         // sample_beta_ortho (BridgeRegression.cpp:362-403): coordinate Gibbs on beta itself,
         // m_j = (c_j - sum_{k != j} G_jk beta_k) / G_jj, one pass (its burn defaults to 0).
         // Gf is the full symmetric Gram, row j contiguous.
+        precompute(0);
+        __syncthreads();
         for (int j = 0; j < p; ++j) {
             double part = 0.0;
 #pragma unroll
@@ -153,22 +188,23 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-            if (lane == 0) shmax[wv] = part;
+            if (lane == 0) shmax[j & 1][wv] = part;
             __syncthreads();
-            if (tid == 0) {
-                double xb = 0.0;
+            double xb = 0.0;
 #pragma unroll
-                for (int w = 0; w < kTriNT / 64; ++w) xb += shmax[w];
+            for (int w = 0; w < kTriNT / 64; ++w) xb += shmax[j & 1][w];
+            if (tid == (j % kTriNT)) {  // the owner draws and keeps beta_j
                 const double gjj = Gf[(size_t)j * p + j];
                 const double m = (cv[j] - xb) / gjj;
                 const double v = sig2 / gjj;
                 const double bnd = sbnd[j];
-                sb[j] = tnorm(-1.0 * bnd, bnd, m, sqrt(v), key, t, (uint64_t)j, 0, err);
+                sb[j] = tnorm(-1.0 * bnd, bnd, m, sqrt(v), key, t, (uint64_t)j, 0, spre[j], err);
             }
-            __syncthreads();
         }
+        __syncthreads();
     }
     for (int it = 0; it <= (ortho ? -1 : betaburn); ++it) {
+        precompute(it);
         // z = tV beta (:246)
         for (int i = tid; i < p; i += kTriNT) {
             double s = 0.0;
@@ -219,34 +255,32 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
             lmax = wave_max(lmax);
             rmin = wave_min(rmin);
             if (lane == 0) {
-                shmax[wv] = lmax;
-                shmin[wv] = rmin;
+                shmax[i & 1][wv] = lmax;
+                shmin[i & 1][wv] = rmin;
             }
-            __syncthreads();
-            if (tid == 0) {
-                double L = shmax[0], R = shmin[0];
+            // LDS-only barrier: __syncthreads() would also drain the row prefetch (vmcnt(0))
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            double L = shmax[i & 1][0], R = shmin[i & 1][0];
 #pragma unroll
-                for (int w = 1; w < kTriNT / 64; ++w) {
-                    L = L > shmax[w] ? L : shmax[w];
-                    R = R < shmin[w] ? R : shmin[w];
-                }
-                const double di = dv[i];
-                double zn;
-                if (di > 1e-16) {
-                    zn = tnorm(L, R, av[i] / (di * di), sig / di, key, t, (uint64_t)i,
-                               (uint64_t)it, err);
-                } else {
-                    U4 r = uniforms(key, t, KIND_TRI_Z, (uint64_t)i, (uint64_t)it, 0);
-                    zn = L + (R - L) * r.r[0];
-                }
-                sdz = zn - zi;
-                sz[i] = zn;
+            for (int w = 1; w < kTriNT / 64; ++w) {
+                L = L > shmax[i & 1][w] ? L : shmax[i & 1][w];
+                R = R < shmin[i & 1][w] ? R : shmin[i & 1][w];
             }
-            __syncthreads();
-            const double dz = sdz;
+            const double di = dv[i];
+            double zn;
+            if (di > 1e-16) {
+                zn = tnorm(L, R, av[i] / (di * di), sig / di, key, t, (uint64_t)i, (uint64_t)it,
+                           spre[i], err);
+            } else {
+                zn = L + (R - L) * spre[i].r0;
+            }
+            const double dz = zn - zi;
+            if (tid == 0) sz[i] = zn;  // read again only after the loop's closing barrier
 #pragma unroll
             for (int e = 0; e < kTriE; ++e) bcur[e] += v[e] * dz;
         }
+        __syncthreads();
         // beta = tV' z (:285)
 #pragma unroll
         for (int e = 0; e < kTriE; ++e) {
