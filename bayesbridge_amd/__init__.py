@@ -60,6 +60,8 @@ EXPORTED_SYMBOLS = [
     "bb_bench_chol", "bb_gram_ozaki", "bb_engine_gram_mode", "bb_bench_ozaki",
     "bridge_EM", "bb_bridge_em", "bb_bridge_em_batch", "bridge_regression",
     "bb_engine_get_tri_trace", "bb_engine_get_tri_basis", "bb_engine_set_tri_state",
+    "rtnorm_left", "rtnorm_both", "rtnorm", "rtexpon_rate_left", "rtexpon_rate_both",
+    "rtexpon_rate", "mytest", "bb_trunc_batch",
 ]
 
 
@@ -128,6 +130,12 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
     L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
     L.bridge_regression.argtypes = [_dp] * 9 + [_dp] * 9 + [_ip] * 4 + [_dp] + [_ip] * 3
+    for name, npar in (("rtnorm_left", 3), ("rtnorm_both", 4), ("rtnorm", 4),
+                       ("rtexpon_rate_left", 2), ("rtexpon_rate_both", 3), ("rtexpon_rate", 3)):
+        getattr(L, name).argtypes = [_dp] * (1 + npar) + [_ip]
+    L.mytest.argtypes = [_ip, _dp]
+    L.bb_trunc_batch.argtypes = [c.c_int, c.c_int, _dp, _dp, _dp, _dp, _dp, c.c_uint64,
+                                 c.c_uint64]
     L.bb_engine_get_tri_trace.argtypes = [c.c_void_p, c.c_int, c.c_int, _dp, _dp]
     L.bb_engine_get_tri_basis.argtypes = [c.c_void_p, _dp, _dp, _dp]
     L.bb_engine_set_tri_state.argtypes = [c.c_void_p, _dp]
@@ -288,6 +296,119 @@ def bridge_reg_tri(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_sh
     out = {k: v.T.copy() for k, v in tr.items()}
     out.update(sig2=sig2, tau=tau, alpha=alph, runtime=rt.value)
     return out
+
+
+def _dotC(name, num, *params):
+    """``.C(name, x, params..., as.integer(num))`` with R's recycling (array(v, num))."""
+    L = library()
+    _require_gpu()
+    ps = [np.ascontiguousarray(np.resize(np.asarray(v, dtype=np.float64), num)) for v in params]
+    x = np.zeros(num)
+    getattr(L, name)(_p(x), *[_p(q) for q in ps], ctypes.byref(ctypes.c_int(num)))
+    return x
+
+
+def rtexp_left(num=1, left=0.0, rate=1.0):
+    """rtexp.left (BridgeWrapper.R:295-315)."""
+    if np.any(np.asarray(rate) <= 0):
+        print("rate must be >= 0.")
+        return None
+    if not num > 0:
+        print("num must be greater than zero.")
+        return None
+    return _dotC("rtexpon_rate_left", num, left, rate)
+
+
+def rtexp_both(num=1, left=0.0, right=1.0, rate=1.0):
+    """rtexp.both (BridgeWrapper.R:317-344); like R it only warns on bad bounds."""
+    if np.any(np.asarray(rate) <= 0):
+        print("rate must be >= 0.")
+        return None
+    if not num > 0:
+        print("num must be greater than zero.")
+        return None
+    if np.any(np.asarray(left) > np.asarray(right)):
+        print("left must be <= right.")
+    if np.any(np.asarray(right) == np.inf):
+        print("right must be < infinity.")
+    return _dotC("rtexpon_rate_both", num, left, right, rate)
+
+
+def rtexp(num=1, left=0.0, right=np.inf, rate=1.0):
+    """rtexp (BridgeWrapper.R:346-375)."""
+    if np.any(np.asarray(rate) <= 0):
+        print("rate must be > 0.")
+        return None
+    if not num > 0:
+        print("num must be greater than zero.")
+        return None
+    if np.any(np.asarray(left) > np.asarray(right)):
+        print("left must be <= right.")
+        return None
+    return _dotC("rtexpon_rate", num, left, right, rate)
+
+
+def rtnorm_left(num=1, left=0.0, mu=0.0, sig=1.0):
+    """rtnorm.left (BridgeWrapper.R:380-402)."""
+    if np.any(np.asarray(sig) <= 0):
+        print("sig must be greater than zero.")
+        return None
+    if not num > 0:
+        print("num must be greater than zero.")
+        return None
+    return _dotC("rtnorm_left", num, left, mu, sig)
+
+
+def rtnorm_right(num=1, right=0.0, mu=0.0, sig=1.0):
+    """rtnorm.right (BridgeWrapper.R:404-407)."""
+    x = rtnorm_left(num=num, left=-1.0 * np.asarray(right), mu=-1.0 * np.asarray(mu), sig=sig)
+    return None if x is None else -1.0 * x
+
+
+def rtnorm_both(num=1, left=-1.0, right=1.0, mu=0.0, sig=1.0):
+    """rtnorm.both (BridgeWrapper.R:409-437)."""
+    if np.any(np.asarray(sig) <= 0):
+        print("sig must be greater than zero.")
+        return None
+    if np.any(np.asarray(left) >= np.asarray(right)):
+        print("rtnorm: left must be less than right.")
+        return None
+    if not num > 0:
+        print("rtnorm: num must be greater than zero.")
+        return None
+    return _dotC("rtnorm_both", num, left, right, mu, sig)
+
+
+def rtruncated_norm(num=1, left=-np.inf, right=np.inf, mu=0.0, sig=1.0):
+    """rtruncated.norm (BridgeWrapper.R:439-474); rtnorm (:477-480) calls it."""
+    if np.any(np.asarray(sig) <= 0):
+        print("sig must be greater than zero.")
+        return None
+    if np.any(np.asarray(left) > np.asarray(right)):
+        print("left must be less than or equal to right.")
+        return None
+    if not num > 0:
+        print("num must be greater than zero.")
+        return None
+    return _dotC("rtnorm", num, left, right, mu, sig)
+
+
+def rtnorm(num=1, mu=0.0, sig=1.0, left=-np.inf, right=np.inf):
+    return rtruncated_norm(num=num, left=left, right=right, mu=mu, sig=sig)
+
+
+def trunc_batch(name, params, seed, stream=0):
+    """Device batch behind the truncated .C utilities under an explicit key (tests)."""
+    modes = {"rtnorm_left": 0, "rtnorm_both": 1, "rtnorm": 2, "rtexpon_rate_left": 3,
+             "rtexpon_rate_both": 4, "rtexpon_rate": 5}
+    L = library()
+    _require_gpu()
+    ps = [np.ascontiguousarray(q, dtype=np.float64) for q in params]
+    num = ps[0].shape[0]
+    ptrs = [_p(q) for q in ps] + [None] * (4 - len(ps))
+    x = np.zeros(num)
+    _check(L.bb_trunc_batch(modes[name], num, _p(x), *ptrs, seed, stream), "bb_trunc_batch")
+    return x
 
 
 def bridge_reg(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,

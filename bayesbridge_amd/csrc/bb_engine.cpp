@@ -1144,6 +1144,49 @@ int bb_retstable_batch(double *x, const double *alpha, const double *V0, const d
     return rc;
 }
 
+int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double *p1,
+                   const double *p2, const double *p3, uint64_t seed, uint64_t stream) {
+    if (num <= 0) return 0;
+    if (mode < 0 || mode > 5) {
+        set_error("bb_trunc_batch: invalid mode %d", mode);
+        return -1;
+    }
+    static const int nparams[6] = {3, 4, 4, 2, 3, 3};
+    const double *src[4] = {p0, p1, p2, p3};
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        double *dp[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; k < nparams[mode]; ++k) {
+            dp[k] = dalloc<double>(num, owned);
+            HIPCHECK(hipMemcpy(dp[k], src[k], num * sizeof(double), hipMemcpyHostToDevice));
+        }
+        double *dx = dalloc<double>(num, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        launch_trunc_batch(0, mode, num, dx, dp[0], dp[1], dp[2], dp[3], seed, stream, de);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(x, dx, num * sizeof(double), hipMemcpyDeviceToHost));
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+        if (f & 256u) {  // BridgeWrapper.cpp:815-822
+            for (int i = 0; i < num; ++i)
+                if (std::isnan(p0[i]) || std::isnan(p1[i]) || std::isnan(p2[i]) ||
+                    std::isinf(p0[i]))
+                    fprintf(stderr, "rtexpon_rate: caught non finite left value: %g; x[i] = %g.\n",
+                            p0[i], x[i]);
+        }
+        rc = (f & (64u | 128u)) ? -2 : 0;
+        if (rc) set_error("truncated draw: %s (flags %u)",
+                          (f & 128u) ? "empty truncation interval" : "rejection cap reached", f);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, double tau,
                      uint64_t seed, uint64_t stream, uint64_t t, uint64_t j0, int group) {
     if (p <= 0) return 0;
@@ -1625,6 +1668,49 @@ int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double
 // ---------------------------------------------------------------------------
 // Reference .C entry points
 // ---------------------------------------------------------------------------
+// BridgeWrapper.cpp:738-756: flags NaN / +Inf / -Inf / NA in x[0] and sets x[0] = NA when
+// it is 0 (a marshalling test of R's special values; host only).
+void mytest(int *out, double *x) {
+    const uint64_t na_bits = 0x7FF00000000007A2ull;  // R's NA_REAL
+    uint64_t bits;
+    memcpy(&bits, x, sizeof(bits));
+    out[0] = 0;
+    if (std::isnan(x[0])) out[0] = 1;
+    if (x[0] == HUGE_VAL) out[0] = 2;
+    if (x[0] == -HUGE_VAL) out[0] = 3;
+    if (std::isnan(x[0]) && (uint32_t)bits == 1954u) out[0] = 4;
+    if (x[0] == 0.0) memcpy(x, &na_bits, sizeof(na_bits));
+}
+
+static void trunc_call(int mode, int num, double *x, const double *p0, const double *p1,
+                       const double *p2, const double *p3, const char *name) {
+    uint64_t k0, k1;
+    next_call_key(&k0, &k1);
+    if (bb_trunc_batch(mode, num, x, p0, p1, p2, p3, k0, k1) != 0)
+        fprintf(stderr, "Error: %s: %s\n", name, g_last_error.c_str());
+}
+
+// BridgeWrapper.cpp:843-935 (decl. BridgeWrapper.h:236-242)
+void rtnorm_left(double *x, double *left, double *mu, double *sig, int *num) {
+    trunc_call(0, *num, x, left, mu, sig, nullptr, "rtnorm_left");
+}
+void rtnorm_both(double *x, double *left, double *right, double *mu, double *sig, int *num) {
+    trunc_call(1, *num, x, left, right, mu, sig, "rtnorm_both");
+}
+void rtnorm(double *x, double *left, double *right, double *mu, double *sig, int *num) {
+    trunc_call(2, *num, x, left, right, mu, sig, "rtnorm");
+}
+// BridgeWrapper.cpp:762-830 (decl. BridgeWrapper.h:230-234)
+void rtexpon_rate_left(double *x, double *left, double *rate, int *num) {
+    trunc_call(3, *num, x, left, rate, nullptr, nullptr, "rtexpon_rate_left");
+}
+void rtexpon_rate_both(double *x, double *left, double *right, double *rate, int *num) {
+    trunc_call(4, *num, x, left, right, rate, nullptr, "rtexpon_rate_both");
+}
+void rtexpon_rate(double *x, double *left, double *right, double *rate, int *num) {
+    trunc_call(5, *num, x, left, right, rate, nullptr, "rtexpon_rate");
+}
+
 void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num) {
     uint64_t k0, k1;
     next_call_key(&k0, &k1);

@@ -164,6 +164,14 @@ void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, do
                        double *tr_beta, double *tr_u, double *tr_omega, double *tr_shape,
                        uint32_t *err);
 
+// Truncated normal / exponential batches (bb_tri.hip) for the .C utilities: mode 0
+// rtnorm_left(l, mu, sig), 1 rtnorm_both(l, r, mu, sig), 2 rtnorm(l, r, mu, sig), 3
+// rtexpon_rate_left(l, rate), 4 rtexpon_rate_both(l, r, rate), 5 rtexpon_rate(l, r, rate).
+// err bits: 64 rejection cap, 128 empty interval, 256 non-finite rtexpon_rate input.
+void launch_trunc_batch(hipStream_t s, int mode, int num, double *x, const double *p0,
+                        const double *p1, const double *p2, const double *p3, uint64_t k0,
+                        uint64_t k1, uint32_t *err);
+
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
                            double *sig2_tr, double *alpha_tr);

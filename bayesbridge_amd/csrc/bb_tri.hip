@@ -303,7 +303,81 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     }
 }
 
+// Truncated normal / exponential batches behind the .C utilities rtnorm_left, rtnorm_both,
+// rtnorm, rtexpon_rate_left, rtexpon_rate_both, rtexpon_rate (BridgeWrapper.cpp:762-935):
+// one lane per draw; draw i uses counters (0, 10 << 56 | i, 0, k) for truncated-normal
+// attempts and (0, 12 << 56 | i, 0, 0) for the exponential / untruncated normal.
+constexpr unsigned KIND_TRUNC = 12;
+
+__device__ double texpon(double left, double right, double rate, double u) {
+    if (isinf(right)) return left - log(u) / rate;  // memoryless left truncation
+    return left - log1p(u * expm1(-rate * (right - left))) / rate;  // inversion on [l, r]
+}
+
+__global__ __launch_bounds__(256) void k_trunc_batch(int mode, int num, double *x,
+                                                     const double *p0, const double *p1,
+                                                     const double *p2, const double *p3, Key key,
+                                                     uint32_t *err) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= num) return;
+    const double inf = __builtin_inf();
+    U4 r = uniforms(key, 0, KIND_TRI_Z, (uint64_t)i, 0, 0);
+    const Pre pre{r.r[0], r.r[1], bm_normal(r.r[0], r.r[1])};
+    const U4 e = uniforms(key, 0, KIND_TRUNC, (uint64_t)i, 0, 0);
+    double out;
+    switch (mode) {
+        case 0:  // rtnorm_left(left, mu, sig)
+            out = tnorm(p0[i], inf, p1[i], p2[i], key, 0, i, 0, pre, err);
+            break;
+        case 1:  // rtnorm_both(left, right, mu, sig)
+            out = tnorm(p0[i], p1[i], p2[i], p3[i], key, 0, i, 0, pre, err);
+            break;
+        case 2: {  // rtnorm(left, right, mu, sig), USE_R branch (:904-919)
+            const double l = p0[i], rt = p1[i], mu = p2[i], sg = p3[i];
+            if (isnan(l) || isnan(rt) || isnan(mu) || isnan(sg)) {
+                out = __builtin_nan("");
+            } else if (!isinf(l) && !isinf(rt)) {
+                out = tnorm(l, rt, mu, sg, key, 0, i, 0, pre, err);
+            } else if (!isinf(l) && rt == inf) {
+                out = tnorm(l, inf, mu, sg, key, 0, i, 0, pre, err);
+            } else if (l == -inf && !isinf(rt)) {
+                out = -1.0 * tnorm(-1.0 * rt, inf, -1.0 * mu, sg, key, 0, i, 0, pre, err);
+            } else if (l == -inf && rt == inf) {
+                out = mu + sg * bm_normal(e.r[0], e.r[1]);
+            } else {
+                out = __builtin_nan("");
+            }
+            break;
+        }
+        case 3:  // rtexpon_rate_left(left, rate)
+            out = texpon(p0[i], inf, p1[i], e.r[0]);
+            break;
+        case 4:  // rtexpon_rate_both(left, right, rate)
+            out = texpon(p0[i], p1[i], p2[i], e.r[0]);
+            break;
+        default: {  // rtexpon_rate(left, right, rate) (:805-830)
+            const double l = p0[i], rt = p1[i], rate = p2[i];
+            if (isnan(l) || isnan(rt) || isnan(rate) || isinf(l)) {
+                out = __builtin_nan("");
+                atomicOr(err, 256u);  // the host prints the reference's stderr line
+            } else {
+                out = texpon(l, isinf(rt) ? inf : rt, rate, e.r[0]);
+            }
+            break;
+        }
+    }
+    x[i] = out;
+}
+
 }  // namespace
+
+void launch_trunc_batch(hipStream_t s, int mode, int num, double *x, const double *p0,
+                        const double *p1, const double *p2, const double *p3, uint64_t k0,
+                        uint64_t k1, uint32_t *err) {
+    if (num <= 0) return;
+    hipLaunchKernelGGL(k_trunc_batch, dim3((num + 255) / 256), dim3(256), 0, s, mode, num, x, p0,
+                       p1, p2, p3, Key{k0, k1}, err);
+}
 
 void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, double *shape,
                        int p, const double *tVc, const double *tVr, const double *a,

@@ -91,6 +91,24 @@ void bridge_regression(double *betap, double *up, double *omegap, double *shapep
                        const int *burn, double *runtime, const int *ortho,
                        const int *betaburn, const int *use_hmc);
 
+/*
+ * Truncated-distribution utilities: replace Code/C/BridgeWrapper.cpp:762-935 (decl.
+ * BridgeWrapper.h:230-242), called by rtexp.left / rtexp.both / rtexp and rtnorm.left /
+ * rtnorm.both / rtruncated.norm (BridgeWrapper.R:290-474).  x[i] gets one draw per
+ * parameter set i; draws run on the device, one lane each.  r.tnorm / r.texpon_rate come
+ * from the un-vendored RNG library and are restated.  rtnorm and
+ * rtexpon_rate follow the reference's USE_R special-value handling (NaN in, NaN out;
+ * rtexpon_rate prints its "caught non finite left value" line to stderr).
+ */
+void rtnorm_left(double *x, double *left, double *mu, double *sig, int *num);
+void rtnorm_both(double *x, double *left, double *right, double *mu, double *sig, int *num);
+void rtnorm(double *x, double *left, double *right, double *mu, double *sig, int *num);
+void rtexpon_rate_left(double *x, double *left, double *rate, int *num);
+void rtexpon_rate_both(double *x, double *left, double *right, double *rate, int *num);
+void rtexpon_rate(double *x, double *left, double *right, double *rate, int *num);
+/* BridgeWrapper.cpp:738-756: R special-value marshalling test (host only). */
+void mytest(int *out, double *x);
+
 /* ------------------------------------------------------------------------ */
 /* Part 2: extensions                                                        */
 /* ------------------------------------------------------------------------ */
@@ -198,6 +216,12 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
  * single GPU (RCCL cannot place two ranks on one device).  p > n path only.
  */
 typedef struct bb_group bb_group;
+/* Batch of truncated draws (mode 0..5 = rtnorm_left, rtnorm_both, rtnorm,
+ * rtexpon_rate_left, rtexpon_rate_both, rtexpon_rate; parameters in the .C order, unused
+ * ones NULL) under key (seed, stream).  Returns 0, or -2 if a draw failed. */
+int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double *p1,
+                   const double *p2, const double *p3, uint64_t seed, uint64_t stream);
+
 /* Triangle method (cfg.method == 4): u and shape traces (omega comes back as `lambda`
  * from bb_engine_get_trace), and the design basis X = U diag(d) V' the engine computed
  * at setup: tV (P x P column-major, row i = i-th right singular vector), a = V'X'y, d. */

@@ -84,6 +84,9 @@ def lib():
                                      _dp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_int, _u64p, ctypes.c_uint64, _dp, _dp, _dp]
         L.bbo_tri_update.restype = ctypes.c_long
+        L.bbo_trunc_batch.argtypes = [ctypes.c_int, ctypes.c_long, _dp, _dp, _dp, _dp, _dp,
+                                      _u64p]
+        L.bbo_trunc_batch.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -198,3 +201,23 @@ def tri_update(beta, u, tV, a, d, tau, sig2, alpha, betaburn, seed, stream, t, G
     if fails:
         raise ValueError(f"tri_update: {fails} failed truncated-normal draws")
     return omega, shape
+
+
+TRUNC_MODES = {"rtnorm_left": (0, 3), "rtnorm_both": (1, 4), "rtnorm": (2, 4),
+               "rtexpon_rate_left": (3, 2), "rtexpon_rate_both": (4, 3), "rtexpon_rate": (5, 3)}
+
+
+def trunc_batch(name, params, seed, stream=0):
+    """Oracle of the truncated-distribution .C utilities (bb_oracle.c bbo_trunc_batch);
+    ``params`` are the .C arguments after x, as equal-length arrays."""
+    mode, npar = TRUNC_MODES[name]
+    assert len(params) == npar
+    ps = [np.ascontiguousarray(q, dtype=np.float64) for q in params]
+    num = ps[0].shape[0]
+    ps += [np.zeros(1)] * (4 - npar)
+    x = np.zeros(num)
+    fails = lib().bbo_trunc_batch(mode, num, _ptr(x), *[_ptr(q) for q in ps],
+                                  _key(seed, stream))
+    if fails:
+        raise ValueError(f"{name}: {fails} failed draws")
+    return x

@@ -509,3 +509,50 @@ long bbo_tri_update(double *beta, double *u, double *omega, double *shape, long 
     }
     return fails;
 }
+
+/* ----------------------------------------------------------------------- */
+/* Truncated-distribution .C utilities, BridgeWrapper.cpp:762-935.          */
+/* Draw i: truncated-normal attempts on (0, 10<<56 | i, 0, k) (bbo_tnorm     */
+/* with t = 0, it = 0), exponential / plain normal on (0, 12<<56 | i, 0, 0). */
+/* ----------------------------------------------------------------------- */
+static double bbo_texpon(double left, double right, double rate, double u)
+{
+    if (isinf(right)) return left - log(u) / rate;
+    return left - log1p(u * expm1(-rate * (right - left))) / rate;
+}
+
+long bbo_trunc_batch(int mode, long num, double *x, const double *p0, const double *p1,
+                     const double *p2, const double *p3, const uint64_t key[2])
+{
+    long fails = 0;
+    const double inf = INFINITY;
+    for (long i = 0; i < num; ++i) {
+        double e[4];
+        int f = 0;
+        draw4(key, 0, 12, (uint64_t)i, 0, 0, e);
+        switch (mode) {
+        case 0: x[i] = bbo_tnorm(p0[i], inf, p1[i], p2[i], key, 0, i, 0, &f); break;
+        case 1: x[i] = bbo_tnorm(p0[i], p1[i], p2[i], p3[i], key, 0, i, 0, &f); break;
+        case 2: {
+            const double l = p0[i], r = p1[i], mu = p2[i], sg = p3[i];
+            if (isnan(l) || isnan(r) || isnan(mu) || isnan(sg)) x[i] = NAN;
+            else if (!isinf(l) && !isinf(r)) x[i] = bbo_tnorm(l, r, mu, sg, key, 0, i, 0, &f);
+            else if (!isinf(l) && r == inf) x[i] = bbo_tnorm(l, inf, mu, sg, key, 0, i, 0, &f);
+            else if (l == -inf && !isinf(r))
+                x[i] = -1.0 * bbo_tnorm(-1.0 * r, inf, -1.0 * mu, sg, key, 0, i, 0, &f);
+            else if (l == -inf && r == inf) x[i] = mu + sg * bm_normal(e[0], e[1]);
+            else x[i] = NAN;
+            break;
+        }
+        case 3: x[i] = bbo_texpon(p0[i], inf, p1[i], e[0]); break;
+        case 4: x[i] = bbo_texpon(p0[i], p1[i], p2[i], e[0]); break;
+        default: {
+            const double l = p0[i], r = p1[i], rate = p2[i];
+            if (isnan(l) || isnan(r) || isnan(rate) || isinf(l)) x[i] = NAN;
+            else x[i] = bbo_texpon(l, isinf(r) ? inf : r, rate, e[0]);
+        }
+        }
+        fails += f != 0;
+    }
+    return fails;
+}
