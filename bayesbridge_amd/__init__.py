@@ -61,7 +61,7 @@ EXPORTED_SYMBOLS = [
     "bridge_EM", "bb_bridge_em", "bb_bridge_em_batch", "bridge_regression",
     "bb_engine_get_tri_trace", "bb_engine_get_tri_basis", "bb_engine_set_tri_state",
     "rtnorm_left", "rtnorm_both", "rtnorm", "rtexpon_rate_left", "rtexpon_rate_both",
-    "rtexpon_rate", "mytest", "bb_trunc_batch",
+    "rtexpon_rate", "mytest", "bb_trunc_batch", "rrtgamma_rate", "bb_rrtgamma_batch",
 ]
 
 
@@ -134,6 +134,8 @@ def library(build: bool = True) -> ctypes.CDLL:
                        ("rtexpon_rate_left", 2), ("rtexpon_rate_both", 3), ("rtexpon_rate", 3)):
         getattr(L, name).argtypes = [_dp] * (1 + npar) + [_ip]
     L.mytest.argtypes = [_ip, _dp]
+    L.rrtgamma_rate.argtypes = [_dp] * 4 + [_ip]
+    L.bb_rrtgamma_batch.argtypes = [c.c_int, _dp, _dp, _dp, _dp, c.c_uint64, c.c_uint64]
     L.bb_trunc_batch.argtypes = [c.c_int, c.c_int, _dp, _dp, _dp, _dp, _dp, c.c_uint64,
                                  c.c_uint64]
     L.bb_engine_get_tri_trace.argtypes = [c.c_void_p, c.c_int, c.c_int, _dp, _dp]
@@ -395,6 +397,32 @@ def rtruncated_norm(num=1, left=-np.inf, right=np.inf, mu=0.0, sig=1.0):
 
 def rtnorm(num=1, mu=0.0, sig=1.0, left=-np.inf, right=np.inf):
     return rtruncated_norm(num=num, left=left, right=right, mu=mu, sig=sig)
+
+
+def rrtgamma(num=1, shape=1.0, rate=1.0, rtrunc=1.0, scale=None):
+    """rrtgamma (BridgeWrapper.R:482-509): Ga(shape, rate) right-truncated at rtrunc."""
+    rate = 1.0 / np.asarray(scale if scale is not None else 1.0 / np.asarray(rate, float), float)
+    if not np.all(np.asarray(shape) > 0):
+        print("shape must be greater than zero.")
+        return None
+    if not np.all(rate > 0):
+        print("scale/rate must be greater than zero.")
+        return None
+    if not np.all(np.asarray(rtrunc) > 0):
+        print("rtrunc must be greater than zero.")
+        return None
+    return _dotC("rrtgamma_rate", num, shape, rate, rtrunc)
+
+
+def rrtgamma_batch(shape, rate, right_t, seed, stream=0):
+    """Device batch behind rrtgamma_rate under an explicit key (tests)."""
+    L = library()
+    _require_gpu()
+    ps = [np.ascontiguousarray(q, dtype=np.float64) for q in (shape, rate, right_t)]
+    x = np.zeros(ps[0].shape[0])
+    _check(L.bb_rrtgamma_batch(x.shape[0], _p(x), *[_p(q) for q in ps], seed, stream),
+           "bb_rrtgamma_batch")
+    return x
 
 
 def trunc_batch(name, params, seed, stream=0):

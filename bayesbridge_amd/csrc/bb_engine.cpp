@@ -1187,6 +1187,36 @@ int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double 
     return rc;
 }
 
+int bb_rrtgamma_batch(int num, double *x, const double *shape, const double *rate,
+                      const double *right_t, uint64_t seed, uint64_t stream) {
+    if (num <= 0) return 0;
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const double *src[3] = {shape, rate, right_t};
+        double *dp[3];
+        for (int k = 0; k < 3; ++k) {
+            dp[k] = dalloc<double>(num, owned);
+            HIPCHECK(hipMemcpy(dp[k], src[k], num * sizeof(double), hipMemcpyHostToDevice));
+        }
+        double *dx = dalloc<double>(num, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        launch_rrtgamma_batch(0, num, dx, dp[0], dp[1], dp[2], seed, stream, de);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(x, dx, num * sizeof(double), hipMemcpyDeviceToHost));
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+        rc = f ? -2 : 0;
+        if (rc) set_error("rrtgamma: rejection cap reached (flags %u)", f);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
 int bb_sample_lambda(double *lambda, const double *beta, int p, double alpha, double tau,
                      uint64_t seed, uint64_t stream, uint64_t t, uint64_t j0, int group) {
     if (p <= 0) return 0;
@@ -1709,6 +1739,15 @@ void rtexpon_rate_both(double *x, double *left, double *right, double *rate, int
 }
 void rtexpon_rate(double *x, double *left, double *right, double *rate, int *num) {
     trunc_call(5, *num, x, left, right, rate, nullptr, "rtexpon_rate");
+}
+
+// BridgeWrapper.cpp:944-962 (decl. BridgeWrapper.h:242); `scale` carries the shape, as
+// rrtgamma (BridgeWrapper.R:482-509) passes it.
+void rrtgamma_rate(double *x, double *scale, double *rate, double *right_t, int *num) {
+    uint64_t k0, k1;
+    next_call_key(&k0, &k1);
+    if (bb_rrtgamma_batch(*num, x, scale, rate, right_t, k0, k1) != 0)
+        fprintf(stderr, "Error: rrtgamma_rate: %s\n", g_last_error.c_str());
 }
 
 void retstable_LD(double *x, double *alpha, double *V0, double *h, int *num) {

@@ -172,6 +172,11 @@ void launch_trunc_batch(hipStream_t s, int mode, int num, double *x, const doubl
                         const double *p1, const double *p2, const double *p3, uint64_t k0,
                         uint64_t k1, uint32_t *err);
 
+// Right-truncated gamma batch (rrtgamma_rate): x_i ~ Ga(shape_i, rate_i) on (0, right_t_i].
+void launch_rrtgamma_batch(hipStream_t s, int num, double *x, const double *shape,
+                           const double *rate, const double *right_t, uint64_t k0, uint64_t k1,
+                           uint32_t *err);
+
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
                            double *sig2_tr, double *alpha_tr);

@@ -369,7 +369,64 @@ __global__ __launch_bounds__(256) void k_trunc_batch(int mode, int num, double *
     x[i] = out;
 }
 
+// Right-truncated gamma (rrtgamma_rate, BridgeWrapper.cpp:944-962): Y = rate x ~ Ga(a, 1)
+// restricted to (0, T], T = rate right_t; the four exact rejection regimes of
+// oracle/bb_oracle.c bbo_rtgamma_std, attempt k on counters (0, 13 << 56 | i, k, 0).
+constexpr unsigned KIND_RTGAMMA = 13;
+
+__device__ double rtgamma_std(double a, double T, Key key, uint64_t i, uint32_t *err) {
+    for (long k = 0; k < kTnMaxAttempts; ++k) {
+        const U4 r = uniforms(key, 0, KIND_RTGAMMA, i, (uint64_t)k, 0);
+        if (T >= a) {  // Marsaglia-Tsang draw, accept if it lands below T
+            const double ap = a < 1.0 ? a + 1.0 : a;
+            const double d = ap - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * d);
+            const double x = bm_normal(r.r[0], r.r[1]);
+            double v = 1.0 + cc * x;
+            if (v <= 0.0) continue;
+            v = v * v * v;
+            const double x2 = x * x;
+            if (!(r.r[2] < 1.0 - 0.0331 * x2 * x2) &&
+                !(log(r.r[2]) < 0.5 * x2 + d * (1.0 - v + log(v))))
+                continue;
+            double y = d * v;
+            if (a < 1.0) y *= pow(r.r[3], 1.0 / a);
+            if (y <= T) return y;
+        } else if (a <= 1.0) {  // power proposal, accept w.p. e^-y
+            const double y = T * pow(r.r[0], 1.0 / a);
+            if (r.r[1] <= exp(-y)) return y;
+        } else if (T <= a - 1.0) {  // increasing log-concave: tangent envelope at T
+            const double c = (a - 1.0) / T - 1.0;
+            const double z = c > 0.0 ? -log1p(r.r[0] * expm1(-c * T)) / c : T * r.r[0];
+            const double y = T - z;
+            if (y > 0.0 && log(r.r[1]) <= (a - 1.0) * log(y / T) + z + c * z) return y;
+        } else {  // mode inside (0, T): uniform proposal bounded at the mode
+            const double m = a - 1.0;
+            const double y = T * r.r[0];
+            if (log(r.r[1]) <= (a - 1.0) * log(y / m) - (y - m)) return y;
+        }
+    }
+    atomicOr(err, 64u);
+    return T;
+}
+
+__global__ __launch_bounds__(256) void k_rrtgamma_batch(int num, double *x, const double *shape,
+                                                        const double *rate,
+                                                        const double *right_t, Key key,
+                                                        uint32_t *err) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= num) return;
+    x[i] = rtgamma_std(shape[i], rate[i] * right_t[i], key, (uint64_t)i, err) / rate[i];
+}
+
 }  // namespace
+
+void launch_rrtgamma_batch(hipStream_t s, int num, double *x, const double *shape,
+                           const double *rate, const double *right_t, uint64_t k0, uint64_t k1,
+                           uint32_t *err) {
+    if (num <= 0) return;
+    hipLaunchKernelGGL(k_rrtgamma_batch, dim3((num + 255) / 256), dim3(256), 0, s, num, x, shape,
+                       rate, right_t, Key{k0, k1}, err);
+}
 
 void launch_trunc_batch(hipStream_t s, int mode, int num, double *x, const double *p0,
                         const double *p1, const double *p2, const double *p3, uint64_t k0,

@@ -106,6 +106,10 @@ void rtnorm(double *x, double *left, double *right, double *mu, double *sig, int
 void rtexpon_rate_left(double *x, double *left, double *rate, int *num);
 void rtexpon_rate_both(double *x, double *left, double *right, double *rate, int *num);
 void rtexpon_rate(double *x, double *left, double *right, double *rate, int *num);
+/* Right-truncated gamma: replaces BridgeWrapper.cpp:944-962 (decl. BridgeWrapper.h:242),
+ * called by rrtgamma (BridgeWrapper.R:482-509); `scale` is the shape (the reference's
+ * parameter name).  x[i] ~ Ga(scale[i], rate[i]) restricted to (0, right_t[i]]. */
+void rrtgamma_rate(double *x, double *scale, double *rate, double *right_t, int *num);
 /* BridgeWrapper.cpp:738-756: R special-value marshalling test (host only). */
 void mytest(int *out, double *x);
 
@@ -221,6 +225,10 @@ typedef struct bb_group bb_group;
  * ones NULL) under key (seed, stream).  Returns 0, or -2 if a draw failed. */
 int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double *p1,
                    const double *p2, const double *p3, uint64_t seed, uint64_t stream);
+
+/* rrtgamma_rate under an explicit key (seed, stream). */
+int bb_rrtgamma_batch(int num, double *x, const double *shape, const double *rate,
+                      const double *right_t, uint64_t seed, uint64_t stream);
 
 /* Triangle method (cfg.method == 4): u and shape traces (omega comes back as `lambda`
  * from bb_engine_get_trace), and the design basis X = U diag(d) V' the engine computed

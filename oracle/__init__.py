@@ -87,6 +87,8 @@ def lib():
         L.bbo_trunc_batch.argtypes = [ctypes.c_int, ctypes.c_long, _dp, _dp, _dp, _dp, _dp,
                                       _u64p]
         L.bbo_trunc_batch.restype = ctypes.c_long
+        L.bbo_rrtgamma_batch.argtypes = [ctypes.c_long, _dp, _dp, _dp, _dp, _u64p]
+        L.bbo_rrtgamma_batch.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -205,6 +207,17 @@ def tri_update(beta, u, tV, a, d, tau, sig2, alpha, betaburn, seed, stream, t, G
 
 TRUNC_MODES = {"rtnorm_left": (0, 3), "rtnorm_both": (1, 4), "rtnorm": (2, 4),
                "rtexpon_rate_left": (3, 2), "rtexpon_rate_both": (4, 3), "rtexpon_rate": (5, 3)}
+
+
+def rrtgamma_batch(shape, rate, right_t, seed, stream=0):
+    """Oracle of .C("rrtgamma_rate"): Ga(shape, rate) truncated to (0, right_t]."""
+    ps = [np.ascontiguousarray(q, dtype=np.float64) for q in (shape, rate, right_t)]
+    x = np.zeros(ps[0].shape[0])
+    fails = lib().bbo_rrtgamma_batch(x.shape[0], _ptr(x), *[_ptr(q) for q in ps],
+                                     _key(seed, stream))
+    if fails:
+        raise ValueError(f"rrtgamma: {fails} failed draws")
+    return x
 
 
 def trunc_batch(name, params, seed, stream=0):

@@ -556,3 +556,63 @@ long bbo_trunc_batch(int mode, long num, double *x, const double *p0, const doub
     }
     return fails;
 }
+
+/* ----------------------------------------------------------------------- */
+/* Right-truncated gamma for rrtgamma_rate, BridgeWrapper.cpp:944-962:      */
+/* x ~ Ga(shape, rate) restricted to (0, right_t].  r.rtgamma_rate comes from */
+/* the un-vendored RNG library; restated as an exact rejection sampler on    */
+/* Y = rate * x ~ Ga(a, 1) | Y <= T, T = rate * right_t, attempt k on        */
+/* (0, 13<<56 | i, k, 0):                                                    */
+/*   T >= a      : Marsaglia-Tsang draw (one block), accept if Y <= T        */
+/*   a <= 1      : Y = T U^(1/a), accept w.p. e^-Y                            */
+/*   T <= a - 1  : increasing log-concave density: Y = T - Z, Z ~ Exp(c) on   */
+/*                 [0, T], c = (a-1)/T - 1 (tangent envelope at T)          */
+/*   otherwise   : uniform on (0, T], bound at the mode a - 1                 */
+/* ----------------------------------------------------------------------- */
+double bbo_rtgamma_std(double a, double T, const uint64_t key[2], uint64_t i, int *fail)
+{
+    for (long k = 0; k < BBO_TN_MAX_ATTEMPTS; ++k) {
+        double r[4];
+        draw4(key, 0, 13, i, (uint64_t)k, 0, r);
+        if (T >= a) {
+            const double ap = a < 1.0 ? a + 1.0 : a;
+            const double d = ap - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * d);
+            const double x = bm_normal(r[0], r[1]);
+            double v = 1.0 + cc * x;
+            if (v <= 0.0) continue;
+            v = v * v * v;
+            const double x2 = x * x;
+            if (!(r[2] < 1.0 - 0.0331 * x2 * x2) && !(log(r[2]) < 0.5 * x2 + d * (1.0 - v + log(v))))
+                continue;
+            double y = d * v;
+            if (a < 1.0) y *= pow(r[3], 1.0 / a);
+            if (y <= T) return y;
+        } else if (a <= 1.0) {
+            const double y = T * pow(r[0], 1.0 / a);
+            if (r[1] <= exp(-y)) return y;
+        } else if (T <= a - 1.0) {
+            const double c = (a - 1.0) / T - 1.0;
+            const double z = c > 0.0 ? -log1p(r[0] * expm1(-c * T)) / c : T * r[0];
+            const double y = T - z;
+            if (y > 0.0 && log(r[1]) <= (a - 1.0) * log(y / T) + z + c * z) return y;
+        } else {
+            const double m = a - 1.0;
+            const double y = T * r[0];
+            if (log(r[1]) <= (a - 1.0) * log(y / m) - (y - m)) return y;
+        }
+    }
+    *fail = 1;
+    return T;
+}
+
+long bbo_rrtgamma_batch(long num, double *x, const double *shape, const double *rate,
+                        const double *right_t, const uint64_t key[2])
+{
+    long fails = 0;
+    for (long i = 0; i < num; ++i) {
+        int f = 0;
+        x[i] = bbo_rtgamma_std(shape[i], rate[i] * right_t[i], key, (uint64_t)i, &f) / rate[i];
+        fails += f;
+    }
+    return fails;
+}

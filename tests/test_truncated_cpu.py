@@ -64,3 +64,14 @@ def test_mytest_flags_r_special_values():
     L.mytest(ctypes.byref(out), ctypes.byref(x))
     assert out.value == 0
     assert struct.unpack("<Q", struct.pack("<d", x.value))[0] == 0x7FF00000000007A2
+
+
+@pytest.mark.parametrize("a,b,t", [(0.5, 1.0, 0.3), (0.5, 1.0, 5.0), (3.0, 2.0, 0.2),
+                                   (3.0, 1.0, 2.5), (50.0, 1.0, 40.0), (50.0, 1.0, 49.5),
+                                   (2.0, 0.5, 100.0), (1.0, 1.0, 0.001), (1.5, 3.0, 0.2)])
+def test_rrtgamma_matches_truncated_gamma(a, b, t):
+    """All four rejection regimes of the restated r.rtgamma_rate (bbo_rtgamma_std)."""
+    x = oracle.rrtgamma_batch(np.full(N, a), np.full(N, b), np.full(N, t), seed=5)
+    assert np.all((x > 0) & (x <= t))
+    g = ss.gamma(a, scale=1.0 / b)
+    assert ss.kstest(x, lambda v: g.cdf(v) / g.cdf(t)).pvalue > 1e-3

@@ -45,3 +45,15 @@ def test_dotC_wrappers_respect_bounds(gpu_lib):
     x = bb.rtexp(2000, left=1.0, right=2.0, rate=3.0)
     assert np.all((x >= 1.0) & (x <= 2.0))
     assert bb.rtnorm_both(10, left=1.0, right=0.0) is None
+
+
+def test_rrtgamma_matches_oracle(gpu_lib):
+    shape = rng.uniform(0.2, 60, M)
+    rate = rng.uniform(0.1, 4, M)
+    right_t = shape / rate * rng.uniform(0.01, 2.0, M)  # below and above the mean
+    g = bb.rrtgamma_batch(shape, rate, right_t, seed=9, stream=2)
+    o = oracle.rrtgamma_batch(shape, rate, right_t, seed=9, stream=2)
+    assert np.all((g > 0) & (g <= right_t))
+    assert np.allclose(g, o, rtol=1e-12, atol=0)
+    x = bb.rrtgamma(1000, shape=2.0, rate=1.0, rtrunc=0.5)
+    assert np.all((x > 0) & (x <= 0.5))
