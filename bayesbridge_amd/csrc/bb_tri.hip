@@ -7,9 +7,9 @@
 // step needs the tightest bounds over all p box constraints |beta_j| <= b_j.  One
 // workgroup of 256 threads runs the whole update: thread j owns coefficients
 // j + 256 k (b_j and beta_cur_j = (tV' z)_j stay in registers), the row v_i. of tV is
-// prefetched one coordinate ahead, the bounds are wave-reduced (max/min are exact, so any
-// tree gives the CPU checker's value) and every lane evaluates the same truncated-normal
-// draw redundantly: one barrier per coordinate.  beta_cur is kept up to date incrementally
+// prefetched one coordinate ahead, the bounds are DPP-reduced per 16-lane row (max/min are
+// exact, so any tree gives the CPU checker's value) and every lane evaluates the same
+// truncated-normal draw redundantly: one barrier per coordinate.  beta_cur is kept up to date incrementally
 // (beta_cur_j += v_ij dz_i) instead of recomputing dot(v_j, z) per coordinate as :254-258
 // does: the same quantity in O(p^2) instead of O(p^3) per pass (oracle/bb_oracle.c
 // bbo_tri_update uses the identical update order).
@@ -53,7 +53,10 @@ __device__ __forceinline__ void attempt(Key key, uint64_t t, uint64_t i, uint64_
     }
 }
 
-__device__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
+// Force-inlined: an out-of-line call inside the coordinate loop costs its prologue's
+// s_waitcnt vmcnt(0), which drains the row prefetch and exposes a full memory latency
+// on every coordinate (measured ≈3.4 µs per coordinate with the call).
+__device__ __forceinline__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
                          const Pre &pre, uint32_t *err) {
     const double sq = sqrt(a * a + 4.0);
     const double as = 0.5 * (a + sq);
@@ -74,7 +77,7 @@ __device__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, ui
     return a;
 }
 
-__device__ double tnorm(double lo, double hi, double mu, double sd, Key key, uint64_t t,
+__device__ __forceinline__ double tnorm(double lo, double hi, double mu, double sd, Key key, uint64_t t,
                         uint64_t i, uint64_t it, const Pre &pre, uint32_t *err) {
     const double a = (lo - mu) / sd, b = (hi - mu) / sd;
     if (!(a < b)) {
@@ -100,15 +103,28 @@ __device__ double tnorm(double lo, double hi, double mu, double sd, Key key, uin
     return mu - sd * tn_pos(-b, -a, key, t, i, it, pre, err);
 }
 
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+// Row-of-16 max / min through DPP (quad xor 1, quad xor 2, half-row mirror, row mirror):
+// every lane of a 16-lane row ends with the row's extreme.  v_max_f64 takes no DPP operand
+// on gfx9, so each step moves the two halves with v_mov_b32_dpp.  Replaces a 6-step
+// ds_bpermute butterfly per value (an LDS round trip per step).
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+__device__ __forceinline__ double row16_max(double v) {
+    v = fmax(v, dpp_d<0xB1>(v));
+    v = fmax(v, dpp_d<0x4E>(v));
+    v = fmax(v, dpp_d<0x141>(v));
+    return fmax(v, dpp_d<0x140>(v));
+}
+__device__ __forceinline__ double row16_min(double v) {
+    v = fmin(v, dpp_d<0xB1>(v));
+    v = fmin(v, dpp_d<0x4E>(v));
+    v = fmin(v, dpp_d<0x141>(v));
+    return fmin(v, dpp_d<0x140>(v));
 }
 
 // tVc: tV column-major (tVc[i + j p] = tV(i, j)); tVr: its transpose (tVr[i p + j] =
@@ -122,8 +138,11 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     __shared__ double sb[kTriMaxP];
     __shared__ double sbnd[kTriMaxP];
     __shared__ Pre spre[kTriMaxP];
+    // per-coordinate constants staged once: a global load inside the serial loop would put
+    // a full memory latency on every coordinate's critical path
+    __shared__ double sav[kTriMaxP], sdv[kTriMaxP];
     // per-wave partials, double-buffered by coordinate parity: one barrier per coordinate
-    __shared__ double shmax[2][kTriNT / 64], shmin[2][kTriNT / 64];
+    __shared__ double shmax[2][kTriNT / 16], shmin[2][kTriNT / 16];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const double tau = sc->tau, sig2 = sc->sig2, alpha = sc->alpha;
 
@@ -160,6 +179,8 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
             if (tr_shape) tr_shape[j] = sh;
             if (tr_u) tr_u[j] = uj;
             sb[j] = betaj;
+            sav[j] = ortho ? cv[j] : av[j];
+            sdv[j] = ortho ? Gf[(size_t)j * p + j] : dv[j];
         }
     }
     __syncthreads();
@@ -179,12 +200,25 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
         // Gf is the full symmetric Gram, row j contiguous.
         precompute(0);
         __syncthreads();
+        double gn[kTriE];
+#pragma unroll
+        for (int e = 0; e < kTriE; ++e) gn[e] = tid + e * kTriNT < p ? Gf[tid + e * kTriNT] : 0.0;
         for (int j = 0; j < p; ++j) {
+            double g[kTriE];
+#pragma unroll
+            for (int e = 0; e < kTriE; ++e) g[e] = gn[e];
+            if (j + 1 < p) {
+#pragma unroll
+                for (int e = 0; e < kTriE; ++e) {
+                    const int k = tid + e * kTriNT;
+                    gn[e] = k < p ? Gf[(size_t)(j + 1) * p + k] : 0.0;
+                }
+            }
             double part = 0.0;
 #pragma unroll
             for (int e = 0; e < kTriE; ++e) {
                 const int k = tid + e * kTriNT;
-                if (k < p && k != j) part += Gf[(size_t)j * p + k] * sb[k];
+                if (k < p && k != j) part += g[e] * sb[k];
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
@@ -194,8 +228,8 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
 #pragma unroll
             for (int w = 0; w < kTriNT / 64; ++w) xb += shmax[j & 1][w];
             if (tid == (j % kTriNT)) {  // the owner draws and keeps beta_j
-                const double gjj = Gf[(size_t)j * p + j];
-                const double m = (cv[j] - xb) / gjj;
+                const double gjj = sdv[j];
+                const double m = (sav[j] - xb) / gjj;
                 const double v = sig2 / gjj;
                 const double bnd = sbnd[j];
                 sb[j] = tnorm(-1.0 * bnd, bnd, m, sqrt(v), key, t, (uint64_t)j, 0, spre[j], err);
@@ -252,25 +286,25 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
                     rmin = rmin < right ? rmin : right;
                 }
             }
-            lmax = wave_max(lmax);
-            rmin = wave_min(rmin);
-            if (lane == 0) {
-                shmax[i & 1][wv] = lmax;
-                shmin[i & 1][wv] = rmin;
+            lmax = row16_max(lmax);
+            rmin = row16_min(rmin);
+            if ((lane & 15) == 0) {  // one partial per 16-lane row
+                shmax[i & 1][tid >> 4] = lmax;
+                shmin[i & 1][tid >> 4] = rmin;
             }
             // LDS-only barrier: __syncthreads() would also drain the row prefetch (vmcnt(0))
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             double L = shmax[i & 1][0], R = shmin[i & 1][0];
 #pragma unroll
-            for (int w = 1; w < kTriNT / 64; ++w) {
+            for (int w = 1; w < kTriNT / 16; ++w) {
                 L = L > shmax[i & 1][w] ? L : shmax[i & 1][w];
                 R = R < shmin[i & 1][w] ? R : shmin[i & 1][w];
             }
-            const double di = dv[i];
+            const double di = sdv[i];
             double zn;
             if (di > 1e-16) {
-                zn = tnorm(L, R, av[i] / (di * di), sig / di, key, t, (uint64_t)i, (uint64_t)it,
+                zn = tnorm(L, R, sav[i] / (di * di), sig / di, key, t, (uint64_t)i, (uint64_t)it,
                            spre[i], err);
             } else {
                 zn = L + (R - L) * spre[i].r0;
