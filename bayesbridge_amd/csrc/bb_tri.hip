@@ -7,9 +7,10 @@
 // step needs the tightest bounds over all p box constraints |beta_j| <= b_j.  One
 // workgroup of 256 threads runs the whole update: thread j owns coefficients
 // j + 256 k (b_j and beta_cur_j = (tV' z)_j stay in registers), the row v_i. of tV is
-// prefetched one coordinate ahead, the bounds are DPP-reduced per 16-lane row (max/min are
-// exact, so any tree gives the CPU checker's value) and every lane evaluates the same
-// truncated-normal draw redundantly: one barrier per coordinate.  beta_cur is kept up to date incrementally
+// prefetched one coordinate ahead, the bounds are DPP-reduced per 16-lane row, then per
+// wave (max/min are exact, so any tree gives the CPU checker's value) and every lane
+// evaluates the same truncated-normal draw redundantly: one barrier per coordinate.
+// beta_cur is kept up to date incrementally
 // (beta_cur_j += v_ij dz_i) instead of recomputing dot(v_j, z) per coordinate as :254-258
 // does: the same quantity in O(p^2) instead of O(p^3) per pass (oracle/bb_oracle.c
 // bbo_tri_update uses the identical update order).
@@ -53,9 +54,9 @@ __device__ __forceinline__ void attempt(Key key, uint64_t t, uint64_t i, uint64_
     }
 }
 
-// Force-inlined: an out-of-line call inside the coordinate loop costs its prologue's
-// s_waitcnt vmcnt(0), which drains the row prefetch and exposes a full memory latency
-// on every coordinate (measured ≈3.4 µs per coordinate with the call).
+// Force-inlined: the compiler outlined tnorm, and an out-of-line call inside the
+// coordinate loop costs its prologue's s_waitcnt vmcnt(0), which drains the row prefetch
+// on every coordinate.
 __device__ __forceinline__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
                          const Pre &pre, uint32_t *err) {
     const double sq = sqrt(a * a + 4.0);
@@ -127,6 +128,23 @@ __device__ __forceinline__ double row16_min(double v) {
     return fmin(v, dpp_d<0x140>(v));
 }
 
+// Combine the four row extremes of a wave (every lane holds its row's value) through
+// scalar reads of lanes 0, 16, 32, 48: the wave's extreme, uniform in every lane.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double rows_max(double v) {
+    return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)),
+                fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
+__device__ __forceinline__ double rows_min(double v) {
+    return fmin(fmin(readlane_d(v, 0), readlane_d(v, 16)),
+                fmin(readlane_d(v, 32), readlane_d(v, 48)));
+}
+
 // tVc: tV column-major (tVc[i + j p] = tV(i, j)); tVr: its transpose (tVr[i p + j] =
 // tV(i, j)), so row i of tV is contiguous for the coordinate loop.
 __global__ __launch_bounds__(kTriNT) void k_tri_update(
@@ -142,7 +160,7 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     // a full memory latency on every coordinate's critical path
     __shared__ double sav[kTriMaxP], sdv[kTriMaxP];
     // per-wave partials, double-buffered by coordinate parity: one barrier per coordinate
-    __shared__ double shmax[2][kTriNT / 16], shmin[2][kTriNT / 16];
+    __shared__ double shmax[2][kTriNT / 64], shmin[2][kTriNT / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const double tau = sc->tau, sig2 = sc->sig2, alpha = sc->alpha;
 
@@ -286,18 +304,18 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
                     rmin = rmin < right ? rmin : right;
                 }
             }
-            lmax = row16_max(lmax);
-            rmin = row16_min(rmin);
-            if ((lane & 15) == 0) {  // one partial per 16-lane row
-                shmax[i & 1][tid >> 4] = lmax;
-                shmin[i & 1][tid >> 4] = rmin;
+            lmax = rows_max(row16_max(lmax));
+            rmin = rows_min(row16_min(rmin));
+            if (lane == 0) {  // one partial per wave
+                shmax[i & 1][wv] = lmax;
+                shmin[i & 1][wv] = rmin;
             }
             // LDS-only barrier: __syncthreads() would also drain the row prefetch (vmcnt(0))
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             double L = shmax[i & 1][0], R = shmin[i & 1][0];
 #pragma unroll
-            for (int w = 1; w < kTriNT / 16; ++w) {
+            for (int w = 1; w < kTriNT / 64; ++w) {
                 L = L > shmax[i & 1][w] ? L : shmax[i & 1][w];
                 R = R < shmin[i & 1][w] ? R : shmin[i & 1][w];
             }
