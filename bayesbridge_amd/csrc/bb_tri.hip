@@ -254,6 +254,16 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
             }
         }
         __syncthreads();
+    } else {
+        // the conditional mean a_i / d_i^2 and sd sigma / d_i of every coordinate, off the
+        // serial chain (same expressions, so the same bits); sd < 0 flags d_i <= 1e-16
+        for (int i = tid; i < p; i += kTriNT) {
+            const double di = sdv[i];
+            const bool ok = di > 1e-16;
+            sav[i] = ok ? sav[i] / (di * di) : 0.0;
+            sdv[i] = ok ? sig / di : -1.0;
+        }
+        __syncthreads();
     }
     for (int it = 0; it <= (ortho ? -1 : betaburn); ++it) {
         precompute(it);
@@ -319,11 +329,10 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
                 L = L > shmax[i & 1][w] ? L : shmax[i & 1][w];
                 R = R < shmin[i & 1][w] ? R : shmin[i & 1][w];
             }
-            const double di = sdv[i];
+            const double sdi = sdv[i];
             double zn;
-            if (di > 1e-16) {
-                zn = tnorm(L, R, sav[i] / (di * di), sig / di, key, t, (uint64_t)i, (uint64_t)it,
-                           spre[i], err);
+            if (sdi > 0.0) {
+                zn = tnorm(L, R, sav[i], sdi, key, t, (uint64_t)i, (uint64_t)it, spre[i], err);
             } else {
                 zn = L + (R - L) * spre[i].r0;
             }
