@@ -18,6 +18,14 @@
  *   - closed-form Gaussian conditional moments of beta | rest, and
  *   - 1-D quadrature of the exact bridge posterior (known sig2, tau).
  *
+ * Also restated here, same status: the triangle-mixture update (bbo_tri_update,
+ * BridgeRegression.cpp:97-147, 235-286, 362-433) and the truncated-distribution .C
+ * utilities (bbo_tnorm, bbo_trunc_batch, bbo_rrtgamma_batch, BridgeWrapper.cpp:762-962).
+ * Their truncated normal / exponential / gamma draws come from the un-vendored RNG
+ * library and are pinned distributionally (KS tests against scipy's truncnorm,
+ * truncexpon and the truncated gamma CDF; exact 1-D bridge posterior for the triangle
+ * chain: tests/test_triangle_cpu.py, tests/test_truncated_cpu.py).
+ *
  * The reference draws its variates from R's RNG (absent).  Here every variate
  * is a pure function of a Philox counter (DESIGN.md "RNG counter layout"), the
  * same layout the HIP kernels use, so the GPU path and this oracle consume
