@@ -52,6 +52,33 @@ def vectors():
     d = oracle.normals(12, SEED, 0, 7, oracle.KIND_DELTA)
     out["wb_X"], out["wb_y"], out["wb_lambda"] = Xw, yw, lam
     out["wb_beta"] = gibbs.beta_step_woodbury(Xw, yw, lam, 0.8, 1.3, z, d)
+    # truncated-distribution .C utilities (restated r.tnorm / texpon / rtgamma)
+    lo = np.array([-np.inf, -1.0, 0.5, 2.0, 4.0, -7.0, -0.3, 1.0])
+    hi = np.array([np.inf, 1.0, np.inf, 2.5, np.inf, -5.0, 0.2, 1.5])
+    mu = np.array([0.0, 0.5, 1.0, 0.0, 0.0, 1.0, 0.0, 3.0])
+    sg = np.array([1.0, 2.0, 2.0, 1.0, 1.0, 1.0, 0.1, 0.5])
+    out["tn_lo"], out["tn_hi"], out["tn_mu"], out["tn_sig"] = lo, hi, mu, sg
+    out["tn_rtnorm"] = oracle.trunc_batch("rtnorm", [lo, hi, mu, sg], SEED, 1)
+    le, re_, rate = np.array([0.0, 1.0, -2.0, 3.0]), np.array([1.0, np.inf, 10.0, 3.5]), \
+        np.array([2.0, 0.5, 5.0, 0.1])
+    out["te_left"], out["te_right"], out["te_rate"] = le, re_, rate
+    out["te_rtexpon"] = oracle.trunc_batch("rtexpon_rate", [le, re_, rate], SEED, 2)
+    ga, gb, gt = np.array([0.5, 0.5, 3.0, 50.0, 1.5]), np.array([1.0, 1.0, 2.0, 1.0, 3.0]), \
+        np.array([0.3, 5.0, 0.2, 40.0, 0.2])
+    out["rg_shape"], out["rg_rate"], out["rg_right"] = ga, gb, gt
+    out["rg_x"] = oracle.rrtgamma_batch(ga, gb, gt, SEED, 3)
+    # one triangle-mixture update (omega, u, rtnorm_gibbs) from a fixed state
+    Xt = rng.standard_normal((25, 4))
+    yt = Xt @ np.array([1.0, 0.0, -1.0, 0.2]) + rng.standard_normal(25)
+    G = Xt.T @ Xt
+    ev, V = np.linalg.eigh(G)
+    o = np.argsort(ev)[::-1]
+    tV = np.asfortranarray(V[:, o].T)
+    at, dt = tV @ (Xt.T @ yt), np.sqrt(ev[o])
+    bt, ut = np.linalg.solve(G, Xt.T @ yt), np.full(4, 0.5)
+    out["tri_tV"], out["tri_a"], out["tri_d"], out["tri_beta0"] = tV, at, dt, bt.copy()
+    om, sh = oracle.tri_update(bt, ut, tV, at, dt, 1.1, 0.9, 0.5, 1, SEED, 0, 4)
+    out["tri_beta"], out["tri_u"], out["tri_omega"], out["tri_shape"] = bt, ut, om, sh
     return out
 
 

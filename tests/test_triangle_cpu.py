@@ -122,3 +122,14 @@ def test_tri_ortho_chain_matches_dense_on_orthogonal_design():
     for j in range(p):
         se = math.hypot(_batch_means_se(a["beta"][:, j]), _batch_means_se(b["beta"][:, j]))
         assert abs(a["beta"][:, j].mean() - b["beta"][:, j].mean()) < 6 * se + 2e-3, j
+
+
+def test_tri_golden_fixture_invariants():
+    """The committed triangle fixture (tests/golden) respects the box constraint it was
+    drawn under (b = (1 - u) omega^(1/alpha) tau, tau = 1.1, alpha = 0.5)."""
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_vectors.npz"))
+    b = (1 - g["tri_u"]) * g["tri_omega"] ** 2.0 * 1.1
+    assert np.all(np.abs(g["tri_beta"]) <= b * (1 + 1e-12))
+    assert np.allclose(g["tri_tV"] @ g["tri_tV"].T, np.eye(4), atol=1e-12)
