@@ -62,6 +62,8 @@ EXPORTED_SYMBOLS = [
     "bb_engine_get_tri_trace", "bb_engine_get_tri_basis", "bb_engine_set_tri_state",
     "rtnorm_left", "rtnorm_both", "rtnorm", "rtexpon_rate_left", "rtexpon_rate_both",
     "rtexpon_rate", "mytest", "bb_trunc_batch", "rrtgamma_rate", "bb_rrtgamma_batch",
+    "bridge_reg_stable_csc", "bb_engine_create_csc", "bb_engine_sparse_pairs", "bb_sparse_gram",
+    "bb_bench_sparse_gram",
 ]
 
 
@@ -129,6 +131,15 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_phase_name.restype = c.c_char_p
     L.retstable_LD.argtypes = [_dp, _dp, _dp, _dp, _ip]
     L.bridge_reg_stable.argtypes = [_dp] * 7 + [_dp] * 9 + [_ip] * 4 + [_dp, _ip]
+    L.bridge_reg_stable_csc.argtypes = ([_dp] * 6 + [_ip, _ip, _dp] + [_dp] * 9 + [_ip] * 4 +
+                                        [_dp, _ip])
+    L.bb_engine_create_csc.argtypes = [c.POINTER(bb_config), _ip, _ip, _dp, _dp,
+                                       c.POINTER(c.c_void_p)]
+    L.bb_engine_sparse_pairs.argtypes = [c.c_void_p]
+    L.bb_engine_sparse_pairs.restype = c.c_longlong
+    L.bb_sparse_gram.argtypes = [_dp, _dp, _ip, _ip, _dp, _dp, _dp, c.c_int, c.c_int]
+    L.bb_bench_sparse_gram.argtypes = [_ip, _ip, _dp, _dp, c.c_int, c.c_int, c.c_int, _dp, _dp,
+                                       c.POINTER(c.c_longlong)]
     L.bridge_regression.argtypes = [_dp] * 9 + [_dp] * 9 + [_ip] * 4 + [_dp] + [_ip] * 3
     for name, npar in (("rtnorm_left", 3), ("rtnorm_both", 4), ("rtnorm", 4),
                        ("rtexpon_rate_left", 2), ("rtexpon_rate_both", 3), ("rtexpon_rate", 3)):
@@ -219,22 +230,54 @@ def check_parameters(N, R, M, sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a
     return ok and all(checks)
 
 
+def _is_sparse(X) -> bool:
+    try:
+        import scipy.sparse as sp
+    except ImportError:  # pragma: no cover
+        return False
+    return sp.issparse(X)
+
+
+def csc_arrays(X):
+    """(colptr, rowidx, val, shape) of a scipy.sparse matrix in canonical CSC form -- the
+    layout of R's dgCMatrix (X@p, X@i, X@x): int32 indices, rows sorted and unique within
+    each column."""
+    import scipy.sparse as sp
+
+    Xc = sp.csc_matrix(X, dtype=np.float64, copy=True)
+    Xc.sum_duplicates()
+    Xc.sort_indices()
+    colptr = np.ascontiguousarray(Xc.indptr, dtype=np.int32)
+    rowidx = np.ascontiguousarray(Xc.indices, dtype=np.int32)
+    val = np.ascontiguousarray(Xc.data, dtype=np.float64)
+    if rowidx.size == 0:  # keep valid pointers for the C ABI
+        rowidx = np.zeros(1, dtype=np.int32)
+        val = np.zeros(1)
+    return colptr, rowidx, val, Xc.shape
+
+
 def bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_shape=2.0,
                    nu_rate=2.0, alpha_a=1.0, alpha_b=1.0, sig2_true=0.0, tau_true=0.0,
                    burn=500, ortho=False, colnames=None):
     """bridge.reg.stb (BridgeWrapper.R:194-234) through ``.C("bridge_reg_stable", ...)``.
 
     Returns a dict: beta (M x P), lambda (M x P), sig2, tau, alpha (M), runtime.
-    ``alpha`` is alpha.true (> 0 fixes alpha; <= 0 samples it by MH).
+    ``alpha`` is alpha.true (> 0 fixes alpha; <= 0 samples it by MH).  A scipy.sparse X
+    goes through ``.C("bridge_reg_stable_csc", ...)`` (the dgCMatrix layout; the sparse
+    Woodbury draw for P > N).
     """
     L = library()
     _require_gpu()
     y = np.asarray(y, dtype=np.float64).ravel()
-    X = np.asarray(X, dtype=np.float64)
-    if X.ndim == 1:
-        X = X[:, None]
+    sparse = _is_sparse(X)
+    if sparse:
+        colptr, rowidx, val, (R, P) = csc_arrays(X)
+    else:
+        X = np.asarray(X, dtype=np.float64)
+        if X.ndim == 1:
+            X = X[:, None]
+        R, P = X.shape
     N = y.shape[0]
-    R, P = X.shape
     M = int(nsamp)
     if not check_parameters(N, R, M, sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
                             alpha_b):
@@ -245,14 +288,21 @@ def bridge_reg_stb(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_sh
     sig2 = np.zeros(M)
     tau = np.zeros(M)
     alph = np.zeros(M)
-    Xf = np.asfortranarray(X)
     d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
     i = lambda v: ctypes.byref(ctypes.c_int(int(v)))  # noqa: E731
     rt = ctypes.c_double(0.0)
-    L.bridge_reg_stable(_p(beta), _p(lam), _p(sig2), _p(tau), _p(alph), _p(y), _p(Xf),
-                        d(sig2_shape), d(sig2_scale), d(nu_shape), d(nu_rate), d(alpha_a),
-                        d(alpha_b), d(sig2_true), d(tau_true), d(alpha), i(P), i(N), i(M),
-                        i(burn), ctypes.byref(rt), i(1 if ortho else 0))
+    hyper = (d(sig2_shape), d(sig2_scale), d(nu_shape), d(nu_rate), d(alpha_a), d(alpha_b),
+             d(sig2_true), d(tau_true), d(alpha), i(P), i(N), i(M), i(burn), ctypes.byref(rt),
+             i(1 if ortho else 0))
+    if sparse:
+        # .C("bridge_reg_stable_csc", ..., X@p, X@i, X@x, ...) for a dgCMatrix
+        L.bridge_reg_stable_csc(_p(beta), _p(lam), _p(sig2), _p(tau), _p(alph), _p(y),
+                                colptr.ctypes.data_as(_ip), rowidx.ctypes.data_as(_ip), _p(val),
+                                *hyper)
+    else:
+        Xf = np.asfortranarray(X)
+        L.bridge_reg_stable(_p(beta), _p(lam), _p(sig2), _p(tau), _p(alph), _p(y), _p(Xf),
+                            *hyper)
     out = {"beta": beta.T.copy(), "lambda": lam.T.copy(), "sig2": sig2, "tau": tau,
            "alpha": alph, "runtime": rt.value}
     if colnames is not None:
@@ -656,6 +706,34 @@ def gram(Y, w, mode=GRAM_FP64):
     return C
 
 
+def sparse_gram(X, D, u=None):
+    """(X diag(D) X', X u) for a sparse X through the pair-list kernels (full n x n)."""
+    L = library()
+    _require_gpu()
+    colptr, rowidx, val, (n, p) = csc_arrays(X)
+    D = np.ascontiguousarray(D, dtype=np.float64)
+    C = np.zeros((n, n), order="F")
+    xu = np.zeros(n)
+    uu = None if u is None else np.ascontiguousarray(u, dtype=np.float64)
+    _check(L.bb_sparse_gram(_p(C), _p(xu), colptr.ctypes.data_as(_ip), rowidx.ctypes.data_as(_ip),
+                            _p(val), _p(D), None if uu is None else _p(uu), n, p),
+           "bb_sparse_gram")
+    return C, xu
+
+
+def bench_sparse_gram(X, D, reps=10):
+    """(pair-list Gram ms, CSR row pass ms, pair count) for a sparse X."""
+    L = library()
+    _require_gpu()
+    colptr, rowidx, val, (n, p) = csc_arrays(X)
+    D = np.ascontiguousarray(D, dtype=np.float64)
+    g, r, k = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
+    _check(L.bb_bench_sparse_gram(colptr.ctypes.data_as(_ip), rowidx.ctypes.data_as(_ip), _p(val),
+                                  _p(D), n, p, reps, ctypes.byref(g), ctypes.byref(r),
+                                  ctypes.byref(k)), "bb_bench_sparse_gram")
+    return g.value, r.value, k.value
+
+
 def chol_solve(A, b):
     L = library()
     _require_gpu()
@@ -714,18 +792,29 @@ class Engine:
     """One Gibbs chain (or one column shard of it) resident on one GPU."""
 
     def __init__(self, cfg: EngineConfig, X_local, y):
+        """X_local: dense (n x p_local) or scipy.sparse (-> the sparse Woodbury engine)."""
         L = library()
         _require_gpu()
         self.cfg = cfg
         self._c = cfg.to_c()
-        X_local = np.asfortranarray(X_local, dtype=np.float64)
         y = np.ascontiguousarray(y, dtype=np.float64)
-        assert X_local.shape == (cfg.n, self._c.p_local), X_local.shape
         self.p_local = self._c.p_local
         h = ctypes.c_void_p()
-        _check(L.bb_engine_create(ctypes.byref(self._c), _p(X_local), _p(y), ctypes.byref(h)),
-               "bb_engine_create")
+        if _is_sparse(X_local):
+            colptr, rowidx, val, shape = csc_arrays(X_local)
+            assert shape == (cfg.n, self._c.p_local), shape
+            _check(L.bb_engine_create_csc(ctypes.byref(self._c), colptr.ctypes.data_as(_ip),
+                                          rowidx.ctypes.data_as(_ip), _p(val), _p(y),
+                                          ctypes.byref(h)), "bb_engine_create_csc")
+        else:
+            X_local = np.asfortranarray(X_local, dtype=np.float64)
+            assert X_local.shape == (cfg.n, self._c.p_local), X_local.shape
+            _check(L.bb_engine_create(ctypes.byref(self._c), _p(X_local), _p(y),
+                                      ctypes.byref(h)), "bb_engine_create")
         self._h = h
+
+    def sparse_pairs(self) -> int:
+        return int(library().bb_engine_sparse_pairs(self._h))
 
     def comm_init(self, id_bytes: bytes):
         _check(library().bb_engine_comm_init(self._h, ctypes.c_char_p(id_bytes)),

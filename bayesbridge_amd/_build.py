@@ -14,8 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SO_PATH = os.path.join(HERE, "BayesBridge.so")
-SOURCES = ["bb_kernels.hip", "bb_ozaki.hip", "bb_tri.hip", "bb_engine.cpp"]
-HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h"]
+SOURCES = ["bb_kernels.hip", "bb_ozaki.hip", "bb_tri.hip", "bb_sparse.hip", "bb_engine.cpp"]
+HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h", "bb_sparse.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 
 
@@ -42,13 +42,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}"]
-    for src in SOURCES:
+    procs = []
+    for src in SOURCES:  # translation units compile in parallel
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
         cmd = [hipcc(), *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        procs.append((cmd, subprocess.Popen(cmd)))
         objs.append(obj)
+    failed = [cmd for cmd, pr in procs if pr.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     tmp = SO_PATH + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-ldl"]

@@ -20,6 +20,7 @@
 #include "../../include/bayesbridge.h"
 #include "bb_kernels.h"
 #include "bb_ozaki.h"
+#include "bb_sparse.h"
 
 using namespace bb;
 
@@ -116,6 +117,117 @@ void next_call_key(uint64_t *k0, uint64_t *k1) {
     *k1 = g_stream++;
 }
 
+// ---------------------------------------------------------------------------
+// Sparse design (CSC input): CSC + CSR copies on the device and the Gram pair list
+// (bb_sparse.h).  Built once at setup; X is constant over a chain.
+// ---------------------------------------------------------------------------
+struct SparseDesign {
+    int n = 0, n_pad = 0, p = 0;
+    long nnz = 0;
+    size_t pairs = 0;
+    int *colptr = nullptr, *rowidx = nullptr, *rowptr = nullptr, *colidx = nullptr,
+        *cpos = nullptr, *pj = nullptr;
+    double *cval = nullptr, *rval = nullptr, *prod = nullptr;
+    unsigned *estart = nullptr;
+
+    // Validates the CSC (colptr[0] = 0, non-decreasing, rows in [0, n), strictly increasing
+    // within a column -- R's dgCMatrix is in this canonical form), transposes it on the host
+    // into a CSR with each entry's CSC position, uploads both and builds the pair list.
+    void build(hipStream_t s, int n_, int n_pad_, int p_, const int *cp, const int *ri,
+               const double *cv, std::vector<void *> &owned) {
+        n = n_;
+        n_pad = n_pad_;
+        p = p_;
+        if (cp[0] != 0) throw HipError("CSC: colptr[0] must be 0");
+        for (int j = 0; j < p; ++j) {
+            if (cp[j + 1] < cp[j]) throw HipError("CSC: colptr must be non-decreasing");
+            for (int q = cp[j]; q < cp[j + 1]; ++q) {
+                if (ri[q] < 0 || ri[q] >= n) throw HipError("CSC: row index out of range");
+                if (q > cp[j] && ri[q] <= ri[q - 1])
+                    throw HipError("CSC: row indices must be strictly increasing within a "
+                                   "column (canonical dgCMatrix form)");
+            }
+        }
+        nnz = cp[p];
+        std::vector<int> rp(n_pad + 1, 0), ci(nnz > 0 ? nnz : 1), pos(nnz > 0 ? nnz : 1);
+        std::vector<double> rv(nnz > 0 ? nnz : 1);
+        for (long q = 0; q < nnz; ++q) ++rp[ri[q] + 1];
+        for (int r = 0; r < n_pad; ++r) rp[r + 1] += rp[r];
+        std::vector<int> next(rp.begin(), rp.end() - 1);
+        for (int j = 0; j < p; ++j)
+            for (int q = cp[j]; q < cp[j + 1]; ++q) {
+                const int k = next[ri[q]]++;
+                ci[k] = j;
+                rv[k] = cv[q];
+                pos[k] = q;
+            }
+        colptr = dalloc<int>(p + 1, owned);
+        rowidx = dalloc<int>(nnz, owned);
+        cval = dalloc<double>(nnz, owned);
+        rowptr = dalloc<int>(n_pad + 1, owned);
+        colidx = dalloc<int>(nnz, owned);
+        rval = dalloc<double>(nnz, owned);
+        cpos = dalloc<int>(nnz, owned);
+        HIPCHECK(hipMemcpy(colptr, cp, (size_t)(p + 1) * sizeof(int), hipMemcpyHostToDevice));
+        if (nnz > 0) {
+            HIPCHECK(hipMemcpy(rowidx, ri, (size_t)nnz * sizeof(int), hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(cval, cv, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(colidx, ci.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(rval, rv.data(), (size_t)nnz * sizeof(double), hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(cpos, pos.data(), (size_t)nnz * sizeof(int), hipMemcpyHostToDevice));
+        }
+        HIPCHECK(hipMemcpy(rowptr, rp.data(), (size_t)(n_pad + 1) * sizeof(int),
+                           hipMemcpyHostToDevice));
+        // pair counts per output column, host scan, then the pair list itself
+        unsigned long long *dcnt = nullptr, *dbase = nullptr;
+        HIPCHECK(hipMalloc(&dcnt, (size_t)n_pad * sizeof(unsigned long long)));
+        launch_sp_count(s, rowptr, colidx, cpos, colptr, n_pad, dcnt);
+        std::vector<unsigned long long> cnt(n_pad), base(n_pad);
+        HIPCHECK(hipMemcpyAsync(cnt.data(), dcnt, cnt.size() * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        (void)hipFree(dcnt);
+        unsigned long long tot = 0;
+        for (int c = 0; c < n_pad; ++c) {
+            base[c] = tot;
+            tot += cnt[c];
+        }
+        if (tot > 0xFFFFFF00ull)
+            throw HipError("sparse Gram: more than 2^32 - 1 column pairs (X too dense for the "
+                           "pair-list Gram; use the dense entry point)");
+        pairs = (size_t)tot;
+        size_t fr = 0, total_mem = 0;
+        HIPCHECK(hipMemGetInfo(&fr, &total_mem));
+        const size_t need = pairs * (sizeof(double) + sizeof(int)) +
+                            (tri_count(n_pad) + 1) * sizeof(unsigned);
+        if (need + (size_t(1) << 28) > fr) {
+            char b[256];
+            snprintf(b, sizeof(b), "sparse Gram: pair list needs %.2f GB, %.2f GB free", need / 1e9,
+                     fr / 1e9);
+            throw HipError(b);
+        }
+        estart = dalloc<unsigned>(tri_count(n_pad) + 1, owned);
+        prod = dalloc<double>(pairs, owned);
+        pj = dalloc<int>(pairs, owned);
+        HIPCHECK(hipMalloc(&dbase, (size_t)n_pad * sizeof(unsigned long long)));
+        HIPCHECK(hipMemcpyAsync(dbase, base.data(), base.size() * sizeof(unsigned long long),
+                                hipMemcpyHostToDevice, s));
+        launch_sp_build(s, rowptr, colidx, cpos, rval, colptr, rowidx, cval, n_pad, dbase, estart,
+                        prod, pj);
+        const unsigned last = (unsigned)tot;
+        HIPCHECK(hipMemcpyAsync(estart + tri_count(n_pad), &last, sizeof(unsigned),
+                                hipMemcpyHostToDevice, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        (void)hipFree(dbase);
+    }
+
+    // tri (packed upper triangle of X diag(D) X', n_pad wide) and xu = X u
+    void gram(hipStream_t s, const double *D, const double *u, double *tri, double *xu) const {
+        launch_sp_gram(s, estart, prod, pj, D, n_pad, tri);
+        launch_sp_rows(s, rowptr, colidx, rval, n_pad, u, D, xu, tri);
+    }
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -134,8 +246,9 @@ static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "ozprep"
 struct bb_engine {
     bb_config cfg{};
     int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
-    int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture
+    int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture, 5 sparse woodbury
     int group = 1;
+    SparseDesign spd;  // method 5: CSC/CSR design and the Gram pair list
     Hyper hy{};
     hipStream_t stream = nullptr;
     std::vector<void *> owned;
@@ -221,6 +334,20 @@ struct bb_engine {
         return base + (size_t)(slot % cap) * stride;
     }
 
+    bool woodbury() const { return method == 2 || method == 5; }
+
+    // X beta of the current beta into the partials k_pre sums next
+    void xbeta() {
+        if (method == 5) {
+            launch_sp_rows(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, beta, nullptr,
+                           xb_part, nullptr);
+            nparts = 1;
+        } else {
+            launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
+            nparts = xv_chunks(p_loc);
+        }
+    }
+
     void pre_and_scalars(uint64_t t, int slot, int tau_only) {
         launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
         allreduce(red1, (size_t)nbS + n_pad);
@@ -247,7 +374,16 @@ struct bb_engine {
                        slot_ptr(tr_alpha, slot, 1), 0, err);
         double *trl = slot_ptr(tr_lam, slot, p_loc);
         mark(PH_LAMBDA);
-        if (method == 2) {
+        if (method == 5) {
+            launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
+                          t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            mark(PH_GRAM);
+            launch_sp_gram(stream, spd.estart, spd.prod, spd.pj, D, n_pad, red2);
+            mark(PH_XU);
+            // Gram diagonal and X u from one pass over the CSR rows
+            launch_sp_rows(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, D,
+                           red2 + tri_count(n_pad), red2);
+        } else if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
             if (cfg.gram_mode == 1) {
@@ -288,7 +424,16 @@ struct bb_engine {
     void phase_c(uint64_t t, int slot, int mcmc_phase) {
         double *trb = slot_ptr(tr_beta, slot, p_loc);
         bool xb_fused = false;
-        if (method == 2) {
+        if (method == 5) {
+            mark(PH_FORM);
+            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
+            mark(PH_CHOL);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd, flags);
+            mark(PH_SOLVE);
+            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
+            mark(PH_BETA);
+            launch_sp_beta(stream, spd.colptr, spd.rowidx, spd.cval, p_loc, w, u, D, sc, beta, trb);
+        } else if (method == 2) {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
             mark(PH_CHOL);
@@ -321,8 +466,7 @@ struct bb_engine {
         }
         if (!xb_fused) {
             mark(PH_XB);
-            launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
-            nparts = xv_chunks(p_loc);
+            xbeta();
         }
         if (!hy.know_alpha) {
             // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
@@ -343,7 +487,7 @@ struct bb_engine {
         phase_a(t);
         allreduce(red1, red1_count());
         phase_b(t, slot);
-        if (method == 2) allreduce(red2, red2_count());
+        if (woodbury()) allreduce(red2, red2_count());
         phase_c(t, slot, mcmc_phase);
     }
 
@@ -459,7 +603,12 @@ void tri_setup(bb_engine *e) {
     e->tr_shape = dalloc<double>((size_t)p * e->cap, o);
 }
 
-void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
+struct SparseIn {
+    const int *colptr, *rowidx;
+    const double *val;
+};
+
+void engine_setup(bb_engine *e, const double *Xh, const double *yh, const SparseIn *spin) {
     const bb_config &c = e->cfg;
     e->n = c.n;
     e->p = c.p;
@@ -469,27 +618,36 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
     e->cap = c.trace_capacity < 1 ? 1 : c.trace_capacity;
     e->hy = Hyper{c.sig2_shape, c.sig2_scale, c.nu_shape, c.nu_rate, c.alpha_a, c.alpha_b,
                   c.true_tau > 0, c.true_sig2 > 0, c.true_alpha > 0};
-    if (c.method == 4) e->method = 4;
+    if (spin) {
+        if (c.ortho || c.method == 1 || c.method == 3 || c.method == 4)
+            throw HipError("a CSC design runs the Woodbury (p > n) draw only");
+        e->method = 5;
+    } else if (c.method == 4) e->method = 4;
     else if (c.ortho) e->method = 3;
     else if (c.method == 1 || (c.method == 0 && c.p <= c.n)) e->method = 1;
     else e->method = 2;
-    if (c.world > 1 && e->method != 2)
+    if (c.world > 1 && !e->woodbury())
         throw HipError("column sharding (world > 1) is implemented for the Woodbury path only");
     if (c.world > 1 && !e->hy.know_alpha)
         throw HipError("unknown alpha with world > 1 is not supported");
     if (e->method == 4 && (c.p > c.n || c.p > kTriMaxP))
         throw HipError("triangle sampler needs p <= n and p <= 2048");
     if (e->method == 1 && c.p > 16384) throw HipError("p x p Cholesky path limited to p <= 16384");
-    if (e->method == 2 && e->n_pad > 8192)
+    if (e->woodbury() && e->n_pad > 8192)
         throw HipError("Woodbury path limited to n <= 8192 in this build");
 
     HIPCHECK(hipSetDevice(c.device));
     HIPCHECK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     auto &o = e->owned;
     const int n_pad = e->n_pad, p_pad = e->p_pad;
-    e->X = dalloc<double>((size_t)n_pad * p_pad, o);
-    HIPCHECK(hipMemcpy2D(e->X, (size_t)n_pad * sizeof(double), Xh, (size_t)c.n * sizeof(double),
-                         (size_t)c.n * sizeof(double), (size_t)c.p_local, hipMemcpyHostToDevice));
+    if (spin) {
+        e->spd.build(e->stream, c.n, n_pad, c.p_local, spin->colptr, spin->rowidx, spin->val, o);
+    } else {
+        e->X = dalloc<double>((size_t)n_pad * p_pad, o);
+        HIPCHECK(hipMemcpy2D(e->X, (size_t)n_pad * sizeof(double), Xh,
+                             (size_t)c.n * sizeof(double), (size_t)c.n * sizeof(double),
+                             (size_t)c.p_local, hipMemcpyHostToDevice));
+    }
     e->y = dalloc<double>(n_pad, o);
     HIPCHECK(hipMemcpy(e->y, yh, (size_t)c.n * sizeof(double), hipMemcpyHostToDevice));
     e->beta = dalloc<double>(p_pad, o);
@@ -529,16 +687,20 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh) {
             e->slabs = dalloc<double>(e->slab_stride * e->S, o);
         }
         e->xu_part = dalloc<double>((size_t)xv_chunks(p_pad) * n_pad, o);
+    }
+    if (e->woodbury()) {
         e->red2 = dalloc<double>(tri_count(n_pad) + n_pad, o);
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
         e->w = dalloc<double>(n_pad, o);
     }
-    e->PT = dalloc<double>((size_t)2 * kNB * ((n_pad > p_pad ? n_pad : p_pad) + kNB), o);
-    e->Wd = dalloc<double>((size_t)kNB * (n_pad > p_pad ? n_pad : p_pad), o);
-    e->flags = dalloc<unsigned int>(chol_flag_words(n_pad > p_pad ? n_pad : p_pad, 1), o);
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
-    const bool small = c.p <= c.n && c.world == 1;
-    if (e->method != 2 || small) {
+    const bool small = c.p <= c.n && c.world == 1 && e->method != 5;
+    // the Cholesky scratch covers the n x n (Woodbury) and any p x p (chol, LS start) system
+    const int m_sys = (e->woodbury() && !small) ? n_pad : (n_pad > p_pad ? n_pad : p_pad);
+    e->PT = dalloc<double>((size_t)2 * kNB * (m_sys + kNB), o);
+    e->Wd = dalloc<double>((size_t)kNB * m_sys, o);
+    e->flags = dalloc<unsigned int>(chol_flag_words(m_sys, 1), o);
+    if ((e->method != 2 && e->method != 5) || small) {
         e->cvec = dalloc<double>(p_pad, o);
         launch_coldot(e->stream, e->X, n_pad, n_pad, e->y, c.p_local, e->cvec);
         e->gdiag = dalloc<double>(p_pad, o);
@@ -628,8 +790,7 @@ void engine_init_state_local(bb_engine *e) {
     // trace slot 0 holds the starting values (as the reference's slot 0 before burn-in)
     HIPCHECK(hipMemcpyAsync(e->tr_beta, e->beta, (size_t)e->p_loc * sizeof(double),
                             hipMemcpyDeviceToDevice, e->stream));
-    launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
-    e->nparts = xv_chunks(e->p_loc);
+    e->xbeta();
     launch_record_scalars(e->stream, e->sc, e->tr_tau, e->tr_sig2, e->tr_alpha);
 }
 
@@ -712,7 +873,7 @@ int bb_engine_create(const bb_config *cfg, const double *X_local, const double *
         if (e->cfg.p_local <= 0) e->cfg.p_local = e->cfg.p;
         if (e->cfg.world < 1) e->cfg.world = 1;
         if (cfg->n <= 0 || cfg->p <= 0) throw HipError("n and p must be positive");
-        engine_setup(e, X_local, y);
+        engine_setup(e, X_local, y, nullptr);
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         delete e;
@@ -720,6 +881,30 @@ int bb_engine_create(const bb_config *cfg, const double *X_local, const double *
     }
     *out = e;
     return 0;
+}
+
+int bb_engine_create_csc(const bb_config *cfg, const int *colptr, const int *rowidx,
+                         const double *val, const double *y, bb_engine **out) {
+    *out = nullptr;
+    bb_engine *e = new bb_engine();
+    try {
+        e->cfg = *cfg;
+        if (e->cfg.p_local <= 0) e->cfg.p_local = e->cfg.p;
+        if (e->cfg.world < 1) e->cfg.world = 1;
+        if (cfg->n <= 0 || cfg->p <= 0) throw HipError("n and p must be positive");
+        SparseIn sp{colptr, rowidx, val};
+        engine_setup(e, nullptr, y, &sp);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        delete e;
+        return -1;
+    }
+    *out = e;
+    return 0;
+}
+
+long long bb_engine_sparse_pairs(const bb_engine *e) {
+    return e->method == 5 ? (long long)e->spd.pairs : -1;
 }
 
 void bb_engine_destroy(bb_engine *e) { delete e; }
@@ -846,8 +1031,7 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
         s.sig2 = sig2;
         s.alpha = alpha;
         HIPCHECK(hipMemcpy(e->sc, &s, sizeof(s), hipMemcpyHostToDevice));
-        launch_xv(e->stream, e->X, e->n_pad, e->beta, e->p_loc, e->n_pad, e->xb_part);
-        e->nparts = xv_chunks(e->p_loc);
+        e->xbeta();
         HIPCHECK(hipStreamSynchronize(e->stream));
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -1044,7 +1228,7 @@ int bb_group_create(bb_engine **engines, int count, bb_group **out) {
         size_t c = 0;
         for (auto *m : g->members) {
             c = std::max(c, m->red1_count());
-            if (m->method == 2) c = std::max(c, m->red2_count());
+            if (m->woodbury()) c = std::max(c, m->red2_count());
         }
         g->tmp_count = c;
         HIPCHECK(hipMalloc(&g->tmp, c * sizeof(double)));
@@ -1069,7 +1253,7 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
             for (auto *m : g->members) m->phase_a(t);
             g->reduce(&bb_engine::red1, g->members[0]->red1_count());
             for (auto *m : g->members) m->phase_b(t, slot);
-            if (g->members[0]->method == 2)
+            if (g->members[0]->woodbury())
                 g->reduce(&bb_engine::red2, g->members[0]->red2_count());
             for (auto *m : g->members) m->phase_c(t, slot, mcmc_phase);
         }
@@ -1414,6 +1598,83 @@ int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
         for (int c = 0; c < n; ++c)
             for (int r = 0; r < n; ++r)
                 C[(size_t)r + (size_t)c * n] = r <= c ? h[tri_index(r, c)] : h[tri_index(c, r)];
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_sparse_gram(double *C, double *xu, const int *colptr, const int *rowidx, const double *val,
+                   const double *D, const double *u, int n, int p) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile);
+        SparseDesign sd;
+        sd.build(0, n, n_pad, p, colptr, rowidx, val, owned);
+        double *dD = dalloc<double>(p, owned), *du = dalloc<double>(p, owned);
+        HIPCHECK(hipMemcpy(dD, D, (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+        if (u) HIPCHECK(hipMemcpy(du, u, (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+        double *tri = dalloc<double>(tri_count(n_pad), owned);
+        double *dxu = dalloc<double>(n_pad, owned);
+        sd.gram(0, dD, du, tri, dxu);
+        HIPCHECK(hipGetLastError());
+        std::vector<double> h(tri_count(n_pad));
+        HIPCHECK(hipMemcpy(h.data(), tri, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int c = 0; c < n; ++c)
+            for (int r = 0; r < n; ++r)
+                C[(size_t)r + (size_t)c * n] = r <= c ? h[tri_index(r, c)] : h[tri_index(c, r)];
+        if (xu) HIPCHECK(hipMemcpy(xu, dxu, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_bench_sparse_gram(const int *colptr, const int *rowidx, const double *val, const double *D,
+                         int n, int p, int reps, double *ms_gram, double *ms_rows,
+                         long long *pairs) {
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        const int n_pad = round_up(n, kGramTile);
+        SparseDesign sd;
+        sd.build(0, n, n_pad, p, colptr, rowidx, val, owned);
+        double *dD = dalloc<double>(p, owned), *du = dalloc<double>(p, owned);
+        HIPCHECK(hipMemcpy(dD, D, (size_t)p * sizeof(double), hipMemcpyHostToDevice));
+        double *tri = dalloc<double>(tri_count(n_pad), owned);
+        double *dxu = dalloc<double>(n_pad, owned);
+        hipEvent_t e0, e1, e2;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        HIPCHECK(hipEventCreate(&e2));
+        sd.gram(0, dD, du, tri, dxu);  // warm
+        float tg = 0, tr = 0;
+        for (int r = 0; r < reps; ++r) {
+            HIPCHECK(hipEventRecord(e0, 0));
+            launch_sp_gram(0, sd.estart, sd.prod, sd.pj, dD, n_pad, tri);
+            HIPCHECK(hipEventRecord(e1, 0));
+            launch_sp_rows(0, sd.rowptr, sd.colidx, sd.rval, n_pad, du, dD, dxu, tri);
+            HIPCHECK(hipEventRecord(e2, 0));
+            HIPCHECK(hipEventSynchronize(e2));
+            float a = 0, b = 0;
+            HIPCHECK(hipEventElapsedTime(&a, e0, e1));
+            HIPCHECK(hipEventElapsedTime(&b, e1, e2));
+            tg += a;
+            tr += b;
+        }
+        *ms_gram = tg / reps;
+        *ms_rows = tr / reps;
+        if (pairs) *pairs = (long long)sd.pairs;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         rc = -1;
@@ -1773,14 +2034,16 @@ void bridge_EM(double *betap, const double *yp, const double *Xp, const double *
     *max_iter = it;
 }
 
-void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,
-                       double *alphap, const double *yp, const double *Xp,
-                       const double *sig2_shape, const double *sig2_scale,
-                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
-                       const double *alpha_b, const double *true_sig2, const double *true_tau,
-                       const double *true_alpha, const int *P, const int *N, const int *M,
-                       const int *burn, double *runtime, const int *ortho) {
-    const int p = *P, n = *N, m = *M, b = *burn;
+}  // extern "C"
+
+namespace {
+
+// bb_config of a .C bridge_reg_stable call (BridgeWrapper.cpp:659-693)
+bb_config stable_call_config(const double *sig2_shape, const double *sig2_scale,
+                             const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                             const double *alpha_b, const double *true_sig2,
+                             const double *true_tau, const double *true_alpha, int p, int n,
+                             int m, const int *ortho) {
     bb_config c;
     bb_config_default(&c);
     c.n = n;
@@ -1799,6 +2062,16 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
     c.trace_capacity = m < 1 ? 1 : m;
     c.device = g_device;
     next_call_key(&c.seed, &c.stream);
+    return c;
+}
+
+// The stable driver around an engine (BridgeWrapper.cpp:207-313 / :434-537): banner, state
+// initialisation, B + 1 burn-in sweeps in slot 0, M - 1 MCMC sweeps into slots 1.., copy-out.
+// `create` builds the engine (dense or CSC design); errors print and return partial traces.
+template <class Create>
+void run_stable_chain(const bb_config &c, Create create, int b, double *betap, double *lambdap,
+                      double *sig2p, double *taup, double *alphap, double *runtime) {
+    const int m = c.trace_capacity;
     const bool know_sig2 = c.true_sig2 > 0, know_tau = c.true_tau > 0, know_alpha = c.true_alpha > 0;
     if (g_verbose) {  // BridgeWrapper.cpp:235-240
         printf("Bridge Regression (mix. of normals):");
@@ -1809,7 +2082,7 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
         printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
     }
     bb_engine *e = nullptr;
-    if (bb_engine_create(&c, Xp, yp, &e) != 0) {
+    if (create(&c, &e) != 0) {
         printf("Error: %s\n", g_last_error.c_str());
         printf("Aborting Gibbs sampler.\n");
         *runtime = 0.0;
@@ -1845,6 +2118,57 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
     if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
     *runtime = rt;
     bb_engine_destroy(e);
+}
+
+}  // namespace
+
+extern "C" {
+
+void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,
+                       double *alphap, const double *yp, const double *Xp,
+                       const double *sig2_shape, const double *sig2_scale,
+                       const double *nu_shape, const double *nu_rate, const double *alpha_a,
+                       const double *alpha_b, const double *true_sig2, const double *true_tau,
+                       const double *true_alpha, const int *P, const int *N, const int *M,
+                       const int *burn, double *runtime, const int *ortho) {
+    const bb_config c = stable_call_config(sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
+                                           alpha_b, true_sig2, true_tau, true_alpha, *P, *N, *M,
+                                           ortho);
+    run_stable_chain(
+        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xp, yp, e); },
+        *burn, betap, lambdap, sig2p, taup, alphap, runtime);
+}
+
+void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double *taup,
+                           double *alphap, const double *yp, const int *Xcolptr,
+                           const int *Xrowidx, const double *Xval, const double *sig2_shape,
+                           const double *sig2_scale, const double *nu_shape,
+                           const double *nu_rate, const double *alpha_a, const double *alpha_b,
+                           const double *true_sig2, const double *true_tau,
+                           const double *true_alpha, const int *P, const int *N, const int *M,
+                           const int *burn, double *runtime, const int *ortho) {
+    const int p = *P, n = *N;
+    const bb_config c = stable_call_config(sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
+                                           alpha_b, true_sig2, true_tau, true_alpha, p, n, *M,
+                                           ortho);
+    if (p > n && !c.ortho) {
+        run_stable_chain(
+            c,
+            [&](const bb_config *cc, bb_engine **e) {
+                return bb_engine_create_csc(cc, Xcolptr, Xrowidx, Xval, yp, e);
+            },
+            *burn, betap, lambdap, sig2p, taup, alphap, runtime);
+        return;
+    }
+    // p <= n or the orthogonal design: the dense paths of bridge_reg_stable (least-squares
+    // start, p x p Cholesky or ortho draw) on the densified X
+    std::vector<double> Xd((size_t)n * p, 0.0);
+    for (int j = 0; j < p; ++j)
+        for (int q = Xcolptr[j]; q < Xcolptr[j + 1]; ++q)
+            if (Xrowidx[q] >= 0 && Xrowidx[q] < n) Xd[(size_t)j * n + Xrowidx[q]] = Xval[q];
+    run_stable_chain(
+        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xd.data(), yp, e); },
+        *burn, betap, lambdap, sig2p, taup, alphap, runtime);
 }
 
 void bridge_regression(double *betap, double *up, double *omegap, double *shapep,

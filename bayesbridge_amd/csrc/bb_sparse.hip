@@ -1,0 +1,255 @@
+// bb_sparse.hip -- gfx950 kernels of the sparse-design Woodbury sweep (bb_sparse.h).
+//
+// Replaces, for a CSC design, the three passes over X of the beta | rest draw
+// (Code/C/BridgeRegression.cpp:552-575 in its Woodbury form):
+//   Gram     X diag(D) X'  -> k_sp_gram (off-diagonal) + k_sp_rows<true> (diagonal)
+//   X u, X b               -> k_sp_rows
+//   X' w                   -> k_sp_beta (fused into the beta update)
+// and, once at setup, the pair list the Gram streams (k_sp_count, k_sp_build).
+//
+// Every sum has a fixed order (lane-strided partial sums, then a fixed xor tree), so a
+// sweep is bitwise reproducible.  No atomics touch floating-point data.
+#include <hip/hip_runtime.h>
+
+#include "bb_sparse.h"
+
+namespace bb {
+
+namespace {
+
+__device__ __forceinline__ double readlane_dbl(double v, int lane) {
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffu), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+template <int W>
+__device__ __forceinline__ double group_sum(double v) {
+    // xor tree inside aligned groups of W lanes; every lane of the group gets the sum
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// setup: pair list
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sp_count(const int *__restrict__ rowptr,
+                                                  const int *__restrict__ colidx,
+                                                  const int *__restrict__ cpos,
+                                                  const int *__restrict__ colptr, int n_pad,
+                                                  unsigned long long *__restrict__ cnt) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= n_pad) return;
+    unsigned long long s = 0;
+    for (int k = rowptr[c] + lane; k < rowptr[c + 1]; k += 64)
+        s += (unsigned long long)(cpos[k] - colptr[colidx[k]]);  // entries of column j above c
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) cnt[c] = s;
+}
+
+void launch_sp_count(hipStream_t s, const int *rowptr, const int *colidx, const int *cpos,
+                     const int *colptr, int n_pad, unsigned long long *cnt) {
+    k_sp_count<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, cpos, colptr, n_pad, cnt);
+}
+
+// One workgroup per output column c (= row c of X).  The per-row counts of the pairs
+// (r, c), r < c, are formed in LDS, scanned into segment starts, and wave 0 then places
+// the pairs walking row c's CSR entries in column order: a column's rows are distinct, so
+// the LDS cursor updates of one instruction never collide, and within an entry's segment
+// the pairs end up sorted by j.
+__global__ __launch_bounds__(256) void k_sp_build(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx, const int *__restrict__ cpos,
+    const double *__restrict__ rval, const int *__restrict__ colptr,
+    const int *__restrict__ rowidx, const double *__restrict__ cval,
+    const unsigned long long *__restrict__ base, unsigned *__restrict__ estart,
+    double *__restrict__ prod, int *__restrict__ pj) {
+    extern __shared__ unsigned cur[];  // c words: count, then cursor, per row r < c
+    __shared__ unsigned part[257];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c = blockIdx.x;
+    for (int r = tid; r < c; r += 256) cur[r] = 0u;
+    __syncthreads();
+    const int k0 = rowptr[c], k1 = rowptr[c + 1];
+    for (int k = k0 + tid; k < k1; k += 256) {
+        const int j = colidx[k];
+        for (int q = colptr[j]; q < cpos[k]; ++q) atomicAdd(&cur[rowidx[q]], 1u);
+    }
+    __syncthreads();
+    // exclusive scan over r in [0, c): one contiguous chunk per thread
+    const int chunk = (c + 255) / 256;
+    const int r0 = min(c, tid * chunk), r1 = min(c, r0 + chunk);
+    unsigned s = 0;
+    for (int r = r0; r < r1; ++r) s += cur[r];
+    part[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned run = 0;
+        for (int i = 0; i < 256; ++i) {
+            const unsigned v = part[i];
+            part[i] = run;
+            run += v;
+        }
+        part[256] = run;
+    }
+    __syncthreads();
+    const unsigned long long b = base[c];
+    const size_t e0 = tri_index(0, c);
+    unsigned run = part[tid];
+    for (int r = r0; r < r1; ++r) {
+        const unsigned v = cur[r];
+        cur[r] = run;
+        estart[e0 + r] = (unsigned)(b + run);
+        run += v;
+    }
+    if (tid == 0) estart[e0 + c] = (unsigned)(b + part[256]);  // empty diagonal segment
+    __syncthreads();
+    if (tid >= 64) return;
+    for (int kb = k0; kb < k1; kb += 64) {
+        const int k = kb + lane;
+        const bool ok = k < k1;
+        const int jl = ok ? colidx[k] : 0;
+        const int q0l = ok ? colptr[jl] : 0;
+        const int q1l = ok ? cpos[k] : 0;
+        const double xl = ok ? rval[k] : 0.0;
+        const int nb = min(64, k1 - kb);
+        for (int l = 0; l < nb; ++l) {
+            const int j = __builtin_amdgcn_readlane(jl, l);
+            const int q0 = __builtin_amdgcn_readlane(q0l, l);
+            const int q1 = __builtin_amdgcn_readlane(q1l, l);
+            const double xc = readlane_dbl(xl, l);
+            for (int q = q0 + lane; q < q1; q += 64) {
+                const int r = rowidx[q];
+                const unsigned pos = cur[r];
+                cur[r] = pos + 1u;
+                const size_t o = (size_t)(b + pos);
+                prod[o] = cval[q] * xc;
+                pj[o] = j;
+            }
+        }
+    }
+}
+
+void launch_sp_build(hipStream_t s, const int *rowptr, const int *colidx, const int *cpos,
+                     const double *rval, const int *colptr, const int *rowidx,
+                     const double *cval, int n_pad, const unsigned long long *base,
+                     unsigned *estart, double *prod, int *pj) {
+    k_sp_build<<<n_pad, 256, (size_t)n_pad * sizeof(unsigned), s>>>(
+        rowptr, colidx, cpos, rval, colptr, rowidx, cval, base, estart, prod, pj);
+}
+
+// ---------------------------------------------------------------------------
+// per sweep
+// ---------------------------------------------------------------------------
+// Gram off-diagonal: kSpLpe lanes per packed entry; lane q sums the entry's pairs
+// q, q + kSpLpe, ... in order (two in flight), then a fixed xor tree.  A wave covers
+// 64 / kSpLpe consecutive entries, i.e. one contiguous stretch of the pair arrays.
+constexpr int kSpLpe = 4;
+
+__global__ __launch_bounds__(256) void k_sp_gram(const unsigned *__restrict__ estart,
+                                                 const double *__restrict__ prod,
+                                                 const int *__restrict__ pj,
+                                                 const double *__restrict__ D, size_t nent,
+                                                 double *__restrict__ out) {
+    const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t e = gid / kSpLpe;
+    const unsigned q = (unsigned)(gid % kSpLpe);
+    double s = 0.0;
+    if (e < nent) {
+        const unsigned en = estart[e + 1];
+        unsigned k = estart[e] + q;
+        for (; k + kSpLpe < en; k += 2 * kSpLpe) {
+            const double p0 = prod[k], p1 = prod[k + kSpLpe];
+            const int j0 = pj[k], j1 = pj[k + kSpLpe];
+            s += p0 * D[j0];
+            s += p1 * D[j1];
+        }
+        if (k < en) s += prod[k] * D[pj[k]];
+    }
+    s = group_sum<kSpLpe>(s);
+    if (q == 0 && e < nent) out[e] = s;
+}
+
+void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, const int *pj,
+                    const double *D, int n_pad, double *out) {
+    const size_t nent = tri_count(n_pad);
+    const size_t threads = nent * kSpLpe;
+    k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out);
+}
+
+// One wave per row c of X (CSR), lanes strided over the row's entries, fixed tree.
+template <bool DIAG>
+__global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
+                                                 const int *__restrict__ colidx,
+                                                 const double *__restrict__ rval, int n_pad,
+                                                 const double *__restrict__ v,
+                                                 const double *__restrict__ D,
+                                                 double *__restrict__ xv,
+                                                 double *__restrict__ tri) {
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= n_pad) return;
+    double s = 0.0, d = 0.0;
+    for (int k = rowptr[c] + lane; k < rowptr[c + 1]; k += 64) {
+        const int j = colidx[k];
+        const double x = rval[k];
+        s += x * v[j];
+        if (DIAG) d += x * x * D[j];
+    }
+    s = group_sum<64>(s);
+    if (DIAG) d = group_sum<64>(d);
+    if (lane == 0) {
+        xv[c] = s;
+        if (DIAG) tri[tri_index(c, c)] = d;
+    }
+}
+
+void launch_sp_rows(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
+                    int n_pad, const double *v, const double *D, double *xv, double *tri) {
+    const int blocks = (n_pad + 3) / 4;
+    if (D)
+        k_sp_rows<true><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri);
+    else
+        k_sp_rows<false><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri);
+}
+
+// 16 lanes per column of the CSC: s = X_j . w, beta_j = u_j + D_j s / sig.
+constexpr int kSpBetaLanes = 16;
+
+__global__ __launch_bounds__(256) void k_sp_beta(const int *__restrict__ colptr,
+                                                 const int *__restrict__ rowidx,
+                                                 const double *__restrict__ cval, int p_loc,
+                                                 const double *__restrict__ w,
+                                                 const double *__restrict__ u,
+                                                 const double *__restrict__ D,
+                                                 const DevScalars *sc, double *__restrict__ beta,
+                                                 double *__restrict__ trace) {
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const int j = (int)(gid / kSpBetaLanes);
+    const int q = (int)(gid % kSpBetaLanes);
+    double s = 0.0;
+    if (j < p_loc)
+        for (int k = colptr[j] + q; k < colptr[j + 1]; k += kSpBetaLanes) s += cval[k] * w[rowidx[k]];
+    s = group_sum<kSpBetaLanes>(s);
+    if (q == 0 && j < p_loc) {
+        const double sig = sqrt(sc->sig2);
+        const double b = u[j] + D[j] * s / sig;
+        beta[j] = b;
+        if (trace) trace[j] = b;
+    }
+}
+
+void launch_sp_beta(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,
+                    int p_loc, const double *w, const double *u, const double *D,
+                    const DevScalars *sc, double *beta, double *beta_trace) {
+    const long threads = (long)p_loc * kSpBetaLanes;
+    k_sp_beta<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(colptr, rowidx, cval, p_loc, w, u,
+                                                                D, sc, beta, beta_trace);
+}
+
+}  // namespace bb

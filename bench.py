@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: Gibbs sweeps/s of the BayesBridge stable sampler on MI355X.
 
-Workload (BASELINE.json metric): Gaussian bridge regression, n=2000, p=50000, alpha=0.5
-(SURVEY.md C3), synthetic design of SURVEY.md s8(d).  One step = one full Gibbs sweep
-(tau, sig2, all p lambda_j, beta | rest) with X resident in HBM.  At N GPUs the p columns
-are sharded across one process per GPU with one RCCL all-reduce per exchange step
+Default workload (BASELINE.json metric): Gaussian bridge regression, n=2000, p=50000,
+alpha=0.5, synthetic design of SURVEY.md s8(d).  One step = one full Gibbs
+sweep (tau, sig2, all p lambda_j, beta | rest) with X resident in HBM.  At N GPUs the p
+columns are sharded across one process per GPU with one RCCL all-reduce per exchange step
 (strong scaling: the total problem is fixed).
+
+Other BASELINE configs, one JSON line each (``--workload``):
+  c2  n=1000, p=5000, alpha=0.5, dense Woodbury
+  c5  n=5000, p=200000, alpha=0.3, sparse CSC design at 1 % density (pair-list sparse Gram,
+      the HBM-bound path)
 
 Defaults follow SURVEY.md 8(d): M = 1000 timed sweeps after B = 100 burn-in sweeps, every
 timed sweep recording beta / lambda / sig2 / tau into the device-resident trace.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
-  roofline     -- the fp64 MFMA Gram kernel (dominant kernel): algorithmic flops per
-                  launch / average launch duration from HIP events on the engine stream
-  cpu_baseline -- the oracle's Woodbury sweep (numpy/OpenBLAS + C latent sampler) timed
-                  on this host on a bounded number of sweeps (rank 0, N=1 only).
+  roofline     -- the dominant kernel: algorithmic work per launch / average launch duration
+                  from HIP events on the engine stream
+  cpu_baseline -- the oracle's sweep (numpy/scipy OpenBLAS + C latent sampler) timed on this
+                  host on a bounded number of sweeps (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -63,6 +68,80 @@ def make_problem_y(n, p, seed=DATA_SEED):
     Xs = make_columns(n, 0, s, seed)
     y = Xs @ b[:s] + rng.standard_normal(n)
     return y - y.mean(), b
+
+
+SPARSE_DENSITY = 0.01  # C5: each X_ij non-zero independently with this probability
+
+WORKLOADS = {
+    # name: (n, p, alpha, sparse)
+    "c2": (1000, 5000, 0.5, False),
+    "c3": (2000, 50000, 0.5, False),
+    "c5": (5000, 200000, 0.3, True),
+}
+
+
+def make_sparse_columns(n, j0, j1, density=SPARSE_DENSITY, seed=DATA_SEED, block=1000):
+    """Columns [j0, j1) of the synthetic sparse X of C5 as a scipy CSC matrix: every entry
+    is non-zero independently with probability `density` (positions by geometric gaps over
+    a column block, column-major), values N(0,1), columns NOT centred (centring would fill
+    them in).  Column blocks are seeded independently, so any shard can be generated alone."""
+    import scipy.sparse as sps
+
+    rows, cols, vals = [], [], []
+    for b in range(j0 // block, (j1 + block - 1) // block):
+        rng = np.random.default_rng([seed, 7, b])
+        N = n * block
+        m = int(N * density + 12 * math.sqrt(N * density) + 64)
+        pos = np.cumsum(rng.geometric(density, size=m)) - 1
+        while pos[-1] < N:  # practically never: extend the gap sequence
+            pos = np.concatenate([pos, pos[-1] + np.cumsum(rng.geometric(density, size=m))])
+        pos = pos[pos < N]
+        v = rng.standard_normal(pos.size)
+        c = pos // n + b * block
+        keep = (c >= j0) & (c < j1)
+        rows.append(pos[keep] % n)
+        cols.append(c[keep] - j0)
+        vals.append(v[keep])
+    r, c, v = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    return sps.csc_matrix((v, (r, c)), shape=(n, j1 - j0))
+
+
+def make_sparse_problem_y(n, p, density=SPARSE_DENSITY, seed=DATA_SEED):
+    """y = X b + e for the sparse design: b's first max(5, p/100) entries +-U(1,3), the rest
+    0; e ~ N(0,1); y centred."""
+    s = max(5, p // 100)
+    rng = np.random.default_rng([seed, 999998])
+    b = np.zeros(p)
+    b[:s] = rng.uniform(1, 3, size=s) * rng.choice([-1.0, 1.0], size=s)
+    Xs = make_sparse_columns(n, 0, s, density, seed)
+    y = Xs @ b[:s] + rng.standard_normal(n)
+    return y - y.mean(), b
+
+
+def cpu_baseline_sparse(n, p, alpha, sweeps, log_every=True):
+    """Oracle Woodbury sweeps on the sparse design (scipy SpGEMM X diag(D) X', LAPACK
+    Cholesky, the C tilted-stable sampler).  Returns (median s per sweep, threads)."""
+    import oracle
+    from oracle import gibbs
+
+    X = make_sparse_columns(n, 0, p)
+    y, _ = make_sparse_problem_y(n, p)
+    beta = np.zeros(p)
+    times = []
+    for t in range(1, sweeps + 1):
+        t0 = time.perf_counter()
+        tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, 2.0, 2.0, 1, 0, t)
+        r = y - X @ beta
+        sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, 1, 0, t)
+        lam = oracle.sample_lambda(beta, alpha, tau, 1, 0, t)
+        z = oracle.normals(p, 1, 0, t, oracle.KIND_BETA_Z)
+        d = oracle.normals(n, 1, 0, t, oracle.KIND_DELTA)
+        beta = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
+        times.append(time.perf_counter() - t0)
+        if log_every:
+            log(f"[cpu_baseline] sparse sweep {t}: {times[-1]:.3f} s")
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return float(np.median(times)), threads
 
 
 def cpu_baseline(n, p, alpha, sweeps, log_every=True):
@@ -126,15 +205,22 @@ def main():
     # M = 1000 timed sweeps after B = 100 burn-in sweeps
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--rows", type=int, default=2000)
-    ap.add_argument("--cols", type=int, default=50000)
-    ap.add_argument("--alpha", type=float, default=0.5)
-    ap.add_argument("--cpu-sweeps", type=int, default=5)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="BASELINE config (default c3, the headline metric)")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--alpha", type=float, default=None)
+    ap.add_argument("--cpu-sweeps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
-                    help="Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
+                    help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
                          "BB_GRAM_MODE, else the library default)")
     args = ap.parse_args()
+    wn, wp, walpha, sparse = WORKLOADS[args.workload]
+    n = args.rows or wn
+    p = args.cols or wp
+    alpha = args.alpha or walpha
+    cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else (2 if sparse else 5)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -159,14 +245,19 @@ def main():
     torch.cuda.set_device(device)
 
     bb.set_verbose(0)
-    n, p, alpha = args.rows, args.cols, args.alpha
     per = (p + world - 1) // world
     j0 = min(p, rank * per)
     j1 = min(p, j0 + per)
     p_loc = j1 - j0
     t_setup0 = time.perf_counter()
-    X = make_columns(n, j0, j1)
-    y, _ = make_problem_y(n, p)
+    if sparse:
+        X = make_sparse_columns(n, j0, j1)
+        y, _ = make_sparse_problem_y(n, p)
+        nnz_loc = int(X.nnz)
+    else:
+        X = make_columns(n, j0, j1)
+        y, _ = make_problem_y(n, p)
+        nnz_loc = n * p_loc
     cfg = bb.EngineConfig(n=n, p=p, p_local=p_loc, j0=j0, rank=rank, world=world,
                           true_alpha=alpha, method=2,
                           trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
@@ -189,8 +280,8 @@ def main():
         eng.comm_init(bb.Engine.comm_unique_id())
     eng.init_state()
     setup_s = time.perf_counter() - t_setup0
-    log(f"[rank {rank}] setup {setup_s:.2f} s  (n={n}, p={p}, p_local={p_loc}, "
-        f"method={eng.method()})")
+    log(f"[rank {rank}] setup {setup_s:.2f} s  (workload={args.workload}, n={n}, p={p}, "
+        f"p_local={p_loc}, method={eng.method()})")
 
     t = 1
     eng.run(t, args.warmup, first_slot=-1)
@@ -233,34 +324,72 @@ def main():
 
     value = args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-    # Dominant kernel = the Gram GEMM.  fp64 path: algorithmic fp64 flops of one k_gram
-    # launch on this rank, n(n+1) p_local.  Ozaki path: algorithmic int8 ops of
-    # one k_oz_gemm launch, kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
     gram_mode = eng.gram_mode()
     gram_flops = float(n) * (n + 1) * p_loc
-    if gram_mode == bb.GRAM_OZAKI:
+    n_pad = -(-n // 128) * 128
+    ntri = n_pad * (n_pad + 1) // 2
+    if sparse:
+        # Dominant kernel = the pair-list sparse Gram, HBM-bound: per launch it streams the
+        # pair list (8 B product + 4 B column index per pair), the segment starts (4 B per
+        # packed entry), writes the packed triangle (8 B per entry) and reads D (8 B per
+        # column, L2-resident after the first touch) -- DESIGN.md s6.2.
+        pairs = eng.sparse_pairs()
+        kernel_bytes = 12.0 * pairs + 12.0 * ntri + 8.0 * p_loc
+        achieved = kernel_bytes / (gram_ms * 1e-3) / 1e9 if gram_ms > 0 else 0.0
+        peak, unit, kname, bound = 8000.0, "GB/s", "k_sp_gram (pair-list SpMV)", "hbm"
+        kernel_ops = kernel_bytes
+        alg_bytes = kernel_bytes
+        traffic = pmc_traffic(n, p, world, "bb::k_sp_gram")
+    elif gram_mode == bb.GRAM_OZAKI:
+        # Dominant kernel = the Gram GEMM: algorithmic int8 ops of one k_oz_gemm launch,
+        # kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
         kernel_ops = 16.0 * n * (n + 1) * p_loc
-        peak, unit, kname = INT8_MFMA_PEAK_TOPS, "TOP/s", "k_oz_gemm16u (v_mfma_i32_16x16x64_i8)"
+        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+        peak, unit, kname, bound = (INT8_MFMA_PEAK_TOPS, "TOP/s",
+                                    "k_oz_gemm16u (v_mfma_i32_16x16x64_i8)", "mfma")
+        alg_bytes = 16.0 * n * p_loc
+        traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u")
     else:
+        # fp64 path: algorithmic fp64 flops of one k_gram launch, n(n+1) p_local
         kernel_ops = gram_flops
-        peak, unit, kname = FP64_MFMA_PEAK_TFLOPS, "TFLOP/s", "k_gram (v_mfma_f64_16x16x4_f64)"
-    achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
+        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+        peak, unit, kname, bound = (FP64_MFMA_PEAK_TFLOPS, "TFLOP/s",
+                                    "k_gram (v_mfma_f64_16x16x4_f64)", "mfma")
+        alg_bytes = 8.0 * n * p_loc
+        traffic = pmc_traffic(n, p, world, "bb::k_gram")
+    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0) + \
+        (phases.get("xu", 0.0) if sparse else 0.0)
     fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
 
-    traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u" if gram_mode == bb.GRAM_OZAKI
-                          else "bb::k_gram")
-
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sweeps > 0:
-        log(f"[cpu_baseline] timing {args.cpu_sweeps} oracle sweeps at n={n}, p={p} ...")
-        per_sweep, threads = cpu_baseline(n, p, alpha, args.cpu_sweeps)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sweeps > 0:
+        log(f"[cpu_baseline] timing {cpu_sweeps} oracle sweeps at n={n}, p={p} ...")
+        if sparse:
+            per_sweep, threads = cpu_baseline_sparse(n, p, alpha, cpu_sweeps)
+            what = "scipy SpGEMM + LAPACK"
+        else:
+            per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps)
+            what = "numpy/OpenBLAS"
         cpu = {"value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads, "kind": "port",
-               "sample": f"{args.cpu_sweeps} Woodbury sweeps of the oracle (numpy/OpenBLAS "
-                         f"{threads} threads + C tilted-stable sampler) at n={n}, p={p}; "
+               "sample": f"{cpu_sweeps} Woodbury sweeps of the oracle ({what}, "
+                         f"{threads} threads, + C tilted-stable sampler) at n={n}, p={p}; "
                          f"median sweep {per_sweep:.3f} s"}
 
     if rank == 0:
+        wl = {"c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
+              "c5": f"C5 sparse CSC Gaussian bridge (density {SPARSE_DENSITY})"}[args.workload]
+        config = {"workload": f"{wl} n={n} p={p} alpha={alpha}",
+                  "rccl": bool(world > 1 or force_rccl),
+                  "n": n, "p": p, "alpha": alpha,
+                  "beta_step": "woodbury (exact, p > n)",
+                  "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
+                                                             if world > 1 else "")}
+        if sparse:
+            config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
+                          nnz=nnz_loc * world if world == 1 else None, pairs=eng.sparse_pairs())
+        else:
+            config["gram"] = ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
+                              else "fp64 mfma")
         rec = {
             "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
             "value": value,
@@ -273,23 +402,16 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md 8(d) Gaussian design, seed 20240501)",
-            "config": {"workload": f"C3 Gaussian bridge n={n} p={p} alpha={alpha}",
-                       "rccl": bool(world > 1 or force_rccl),
-                       "n": n, "p": p, "alpha": alpha,
-                       "beta_step": "woodbury (exact, p > n)",
-                       "gram": ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
-                                else "fp64 mfma"),
-                       "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
-                                                                  if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": kname,
+            "data": ("synthetic (SURVEY.md 8(d) design, seed 20240501"
+                     + (f", Bernoulli({SPARSE_DENSITY}) sparsity)" if sparse else ")")),
+            "config": config,
+            "roofline": {"bound": bound, "kernel": kname,
                          "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak,
                          "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
                          "traffic_source": traffic[1] if traffic else None,
-                         "algorithmic_bytes_per_launch": (16.0 * n * p_loc if gram_mode == bb.GRAM_OZAKI
-                                                          else 8.0 * n * p_loc),
+                         "algorithmic_bytes_per_launch": alg_bytes,
                          "gram_ms_avg": gram_ms,
                          "sweep_ms_avg_events": sweep_ms,
                          "ops_per_launch": kernel_ops,

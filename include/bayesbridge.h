@@ -79,8 +79,9 @@ void bridge_EM(double *betap, const double *yp, const double *Xp, const double *
  * betap, up, omegap, shapep are P x M column-major traces; sig2p, taup, alphap are M.
  * Requires P <= N and P <= 2048 (the reference's svd(X, 'A') indexing breaks for P > N).
  * `ortho` and `use_hmc` are declared `const bool*` but R passes integers; both are read
- * as ints.  The orthogonal-design triangle variant (ortho != 0) and HMC (dead code in the
- * reference, :418) are not in this build: ortho prints an error and returns.
+ * as ints.  ortho != 0 runs the orthogonal-design triangle driver (bridge_regression_ortho,
+ * BridgeWrapper.cpp:320-432).  use_hmc is ignored: the reference forces it false
+ * (BridgeRegression.cpp:418).
  */
 void bridge_regression(double *betap, double *up, double *omegap, double *shapep,
                        double *sig2p, double *taup, double *alphap, const double *yp,
@@ -112,6 +113,24 @@ void rtexpon_rate(double *x, double *left, double *right, double *rate, int *num
 void rrtgamma_rate(double *x, double *scale, double *rate, double *right_t, int *num);
 /* BridgeWrapper.cpp:738-756: R special-value marshalling test (host only). */
 void mytest(int *out, double *x);
+
+/*
+ * bridge_reg_stable for a sparse design given in compressed-sparse-column form, the
+ * layout of R's Matrix::dgCMatrix (X@p = Xcolptr, P + 1 entries; X@i = Xrowidx, 0-based
+ * rows strictly increasing within a column; X@x = Xval).  Same outputs, hyper-parameters
+ * and semantics as bridge_reg_stable on the dense X (BridgeWrapper.cpp:659-732); there is
+ * no reference counterpart (BASELINE config C5).  For P > N (non-ortho) the Woodbury draw
+ * runs on the CSC/CSR design with a pair-list sparse Gram; otherwise X is
+ * densified and the dense path runs.
+ */
+void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double *taup,
+                           double *alphap, const double *yp, const int *Xcolptr,
+                           const int *Xrowidx, const double *Xval, const double *sig2_shape,
+                           const double *sig2_scale, const double *nu_shape,
+                           const double *nu_rate, const double *alpha_a, const double *alpha_b,
+                           const double *true_sig2, const double *true_tau,
+                           const double *true_alpha, const int *P, const int *N, const int *M,
+                           const int *burn, double *runtime, const int *ortho);
 
 /* ------------------------------------------------------------------------ */
 /* Part 2: extensions                                                        */
@@ -157,7 +176,8 @@ typedef struct bb_config {
     double true_sig2, true_tau, true_alpha;
     int ortho;          /* orthogonal-design variant (sample_beta_stable_ortho) */
     int method;         /* 0 auto (chol if p <= n else woodbury), 1 chol, 2 woodbury,
-                           4 triangle mixture (bridge.reg.tri; p <= n, p <= 2048) */
+                           4 triangle mixture (bridge.reg.tri; p <= n, p <= 2048);
+                           5 sparse Woodbury is selected by bb_engine_create_csc */
     int trace_capacity; /* number of trace slots kept on device (>= 1) */
     uint64_t seed, stream;
     int device;
@@ -172,6 +192,14 @@ void bb_config_default(bb_config *cfg);
 int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
                      bb_engine **out);
 void bb_engine_destroy(bb_engine *e);
+
+/* Create from a CSC design (the engine's p_local columns; colptr has p_local + 1 entries,
+ * canonical row order): the sparse Woodbury engine (method 5).  Builds the Gram pair list
+ * on the device at setup; fails (-1, bb_last_error) if it does not fit in HBM. */
+int bb_engine_create_csc(const bb_config *cfg, const int *colptr, const int *rowidx,
+                         const double *val, const double *y, bb_engine **out);
+/* Number of off-diagonal Gram pairs (X_rj X_cj != 0, r < c) of a sparse engine, else -1. */
+long long bb_engine_sparse_pairs(const bb_engine *e);
 
 /*
  * RCCL communicator for world > 1: rank 0 calls bb_comm_unique_id, the bytes are
@@ -302,6 +330,17 @@ int bb_bench_ozaki(int n, int k, int nsplit, int dbg, int reps, double *ms);
 /* The same Gram through the Ozaki-II int8 path (w >= 0): exact integer Gram of the
  * row-scaled, fp64-rounded Y diag(sqrt(w)), rounded once to fp64. */
 int bb_gram_ozaki(double *C, const double *Y, const double *w, int n, int k);
+
+/* Sparse Gram of a CSC design (n x p): C = X diag(D) X' (n x n column-major, full
+ * symmetric) and xu = X u (n; u and xu may be NULL), through the engine's pair-list
+ * kernels. */
+int bb_sparse_gram(double *C, double *xu, const int *colptr, const int *rowidx, const double *val,
+                   const double *D, const double *u, int n, int p);
+/* Microbenchmark of the sparse Gram: average ms of the pair-list kernel and of the CSR row
+ * pass (diagonal + X u) over `reps` launches; pairs receives the pair count. */
+int bb_bench_sparse_gram(const int *colptr, const int *rowidx, const double *val, const double *D,
+                         int n, int p, int reps, double *ms_gram, double *ms_rows,
+                         long long *pairs);
 
 /* SPD solve via the blocked device Cholesky: A (m x m, column-major, only the
  * upper triangle read) -> x = A^-1 b for nrhs right-hand sides (m x nrhs). */

@@ -21,6 +21,7 @@ import time
 
 import numpy as np
 import scipy.linalg as sla
+import scipy.sparse as sps
 
 from . import (KIND_BETA_Z, KIND_DELTA, alpha_mh, normals, sample_lambda, sig2_from_rss,
                sum_abs_pow, tau_from_sum)
@@ -63,7 +64,11 @@ def beta_step_woodbury(X, y, lam, sig2, tau, z, delta):
     D = (tau * tau) / lam
     u = np.sqrt(D) * z
     v = (X @ u) / sig + delta
-    M = (X * D) @ X.T / sig2
+    if sps.issparse(X):  # sparse design (BASELINE config C5): scipy SpGEMM
+        Xc = sps.csc_matrix(X)
+        M = np.asarray((Xc @ sps.diags(D) @ Xc.T).toarray()) / sig2
+    else:
+        M = (X * D) @ X.T / sig2
     M[np.diag_indices_from(M)] += 1.0
     Lm = np.linalg.cholesky(M)
     w = sla.solve_triangular(Lm, y / sig - v, lower=True)
@@ -91,7 +96,12 @@ def bridge_regression_stable(y, X, nsamp, burn=500, alpha=0.5, sig2_shape=0.0, s
     p <= n else woodbury -- the HIP path's choice).
     """
     y = np.ascontiguousarray(y, dtype=np.float64)
-    X = np.asfortranarray(X, dtype=np.float64)
+    if sps.issparse(X):
+        X = sps.csc_matrix(X, dtype=np.float64)
+        if method == "auto" and X.shape[1] <= X.shape[0]:
+            X = X.toarray()
+    if not sps.issparse(X):
+        X = np.asfortranarray(X, dtype=np.float64)
     n, p = X.shape
     M = int(nsamp)
     if true_alpha is None:
