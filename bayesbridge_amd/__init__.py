@@ -63,7 +63,7 @@ EXPORTED_SYMBOLS = [
     "rtnorm_left", "rtnorm_both", "rtnorm", "rtexpon_rate_left", "rtexpon_rate_both",
     "rtexpon_rate", "mytest", "bb_trunc_batch", "rrtgamma_rate", "bb_rrtgamma_batch",
     "bridge_reg_stable_csc", "bb_engine_create_csc", "bb_engine_sparse_pairs", "bb_sparse_gram",
-    "bb_bench_sparse_gram",
+    "bb_bench_sparse_gram", "bb_engine_sparse_info",
 ]
 
 
@@ -137,6 +137,8 @@ def library(build: bool = True) -> ctypes.CDLL:
                                        c.POINTER(c.c_void_p)]
     L.bb_engine_sparse_pairs.argtypes = [c.c_void_p]
     L.bb_engine_sparse_pairs.restype = c.c_longlong
+    L.bb_engine_sparse_info.argtypes = [c.c_void_p, c.POINTER(c.c_longlong),
+                                        c.POINTER(c.c_longlong), _ip, _ip]
     L.bb_sparse_gram.argtypes = [_dp, _dp, _ip, _ip, _dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_bench_sparse_gram.argtypes = [_ip, _ip, _dp, _dp, c.c_int, c.c_int, c.c_int, _dp, _dp,
                                        c.POINTER(c.c_longlong)]
@@ -815,6 +817,14 @@ class Engine:
 
     def sparse_pairs(self) -> int:
         return int(library().bb_engine_sparse_pairs(self._h))
+
+    def sparse_info(self):
+        """dict(pairs, nnz, max_row, col_mode) of a sparse-design engine."""
+        pr, nz, mr, cm = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_int(), ctypes.c_int()
+        _check(library().bb_engine_sparse_info(self._h, ctypes.byref(pr), ctypes.byref(nz),
+                                               ctypes.byref(mr), ctypes.byref(cm)),
+               "bb_engine_sparse_info")
+        return dict(pairs=pr.value, nnz=nz.value, max_row=mr.value, col_mode=bool(cm.value))
 
     def comm_init(self, id_bytes: bytes):
         _check(library().bb_engine_comm_init(self._h, ctypes.c_char_p(id_bytes)),

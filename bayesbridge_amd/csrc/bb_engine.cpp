@@ -129,6 +129,9 @@ struct SparseDesign {
         *cpos = nullptr, *pj = nullptr;
     double *cval = nullptr, *rval = nullptr, *prod = nullptr;
     unsigned *estart = nullptr;
+    unsigned short *pidx = nullptr;
+    int max_row = 0;        // largest row nnz
+    bool col_mode = false;  // by-column Gram kernel (max_row <= kSpColMaxRow)
 
     // Validates the CSC (colptr[0] = 0, non-decreasing, rows in [0, n), strictly increasing
     // within a column -- R's dgCMatrix is in this canonical form), transposes it on the host
@@ -152,6 +155,9 @@ struct SparseDesign {
         std::vector<int> rp(n_pad + 1, 0), ci(nnz > 0 ? nnz : 1), pos(nnz > 0 ? nnz : 1);
         std::vector<double> rv(nnz > 0 ? nnz : 1);
         for (long q = 0; q < nnz; ++q) ++rp[ri[q] + 1];
+        max_row = 0;
+        for (int r = 0; r < n_pad; ++r) max_row = std::max(max_row, rp[r + 1]);
+        col_mode = max_row <= kSpColMaxRow;
         for (int r = 0; r < n_pad; ++r) rp[r + 1] += rp[r];
         std::vector<int> next(rp.begin(), rp.end() - 1);
         for (int j = 0; j < p; ++j)
@@ -198,7 +204,7 @@ struct SparseDesign {
         pairs = (size_t)tot;
         size_t fr = 0, total_mem = 0;
         HIPCHECK(hipMemGetInfo(&fr, &total_mem));
-        const size_t need = pairs * (sizeof(double) + sizeof(int)) +
+        const size_t need = pairs * (sizeof(double) + (col_mode ? 2 : sizeof(int))) +
                             (tri_count(n_pad) + 1) * sizeof(unsigned);
         if (need + (size_t(1) << 28) > fr) {
             char b[256];
@@ -208,12 +214,15 @@ struct SparseDesign {
         }
         estart = dalloc<unsigned>(tri_count(n_pad) + 1, owned);
         prod = dalloc<double>(pairs, owned);
-        pj = dalloc<int>(pairs, owned);
+        if (col_mode)
+            pidx = dalloc<unsigned short>(pairs, owned);
+        else
+            pj = dalloc<int>(pairs, owned);
         HIPCHECK(hipMalloc(&dbase, (size_t)n_pad * sizeof(unsigned long long)));
         HIPCHECK(hipMemcpyAsync(dbase, base.data(), base.size() * sizeof(unsigned long long),
                                 hipMemcpyHostToDevice, s));
         launch_sp_build(s, rowptr, colidx, cpos, rval, colptr, rowidx, cval, n_pad, dbase, estart,
-                        prod, pj);
+                        prod, pj, pidx);
         const unsigned last = (unsigned)tot;
         HIPCHECK(hipMemcpyAsync(estart + tri_count(n_pad), &last, sizeof(unsigned),
                                 hipMemcpyHostToDevice, s));
@@ -223,8 +232,13 @@ struct SparseDesign {
 
     // tri (packed upper triangle of X diag(D) X', n_pad wide) and xu = X u
     void gram(hipStream_t s, const double *D, const double *u, double *tri, double *xu) const {
-        launch_sp_gram(s, estart, prod, pj, D, n_pad, tri);
-        launch_sp_rows(s, rowptr, colidx, rval, n_pad, u, D, xu, tri);
+        if (col_mode) {
+            launch_sp_gram_col(s, rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad, max_row,
+                               tri, xu);
+        } else {
+            launch_sp_gram(s, estart, prod, pj, D, n_pad, tri);
+            launch_sp_rows(s, rowptr, colidx, rval, n_pad, u, D, xu, tri);
+        }
     }
 };
 
@@ -378,11 +392,8 @@ struct bb_engine {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
             mark(PH_GRAM);
-            launch_sp_gram(stream, spd.estart, spd.prod, spd.pj, D, n_pad, red2);
-            mark(PH_XU);
-            // Gram diagonal and X u from one pass over the CSR rows
-            launch_sp_rows(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, D,
-                           red2 + tri_count(n_pad), red2);
+            // packed Gram (with its diagonal) and X u
+            spd.gram(stream, D, u, red2, red2 + tri_count(n_pad));
         } else if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
@@ -905,6 +916,19 @@ int bb_engine_create_csc(const bb_config *cfg, const int *colptr, const int *row
 
 long long bb_engine_sparse_pairs(const bb_engine *e) {
     return e->method == 5 ? (long long)e->spd.pairs : -1;
+}
+
+int bb_engine_sparse_info(const bb_engine *e, long long *pairs, long long *nnz, int *max_row,
+                          int *col_mode) {
+    if (e->method != 5) {
+        set_error("not a sparse-design engine");
+        return -1;
+    }
+    if (pairs) *pairs = (long long)e->spd.pairs;
+    if (nnz) *nnz = (long long)e->spd.nnz;
+    if (max_row) *max_row = e->spd.max_row;
+    if (col_mode) *col_mode = e->spd.col_mode ? 1 : 0;
+    return 0;
 }
 
 void bb_engine_destroy(bb_engine *e) { delete e; }
@@ -1658,9 +1682,13 @@ int bb_bench_sparse_gram(const int *colptr, const int *rowidx, const double *val
         float tg = 0, tr = 0;
         for (int r = 0; r < reps; ++r) {
             HIPCHECK(hipEventRecord(e0, 0));
-            launch_sp_gram(0, sd.estart, sd.prod, sd.pj, dD, n_pad, tri);
+            if (sd.col_mode)
+                sd.gram(0, dD, du, tri, dxu);
+            else
+                launch_sp_gram(0, sd.estart, sd.prod, sd.pj, dD, n_pad, tri);
             HIPCHECK(hipEventRecord(e1, 0));
-            launch_sp_rows(0, sd.rowptr, sd.colidx, sd.rval, n_pad, du, dD, dxu, tri);
+            if (!sd.col_mode)
+                launch_sp_rows(0, sd.rowptr, sd.colidx, sd.rval, n_pad, du, dD, dxu, tri);
             HIPCHECK(hipEventRecord(e2, 0));
             HIPCHECK(hipEventSynchronize(e2));
             float a = 0, b = 0;

@@ -9,9 +9,11 @@
 //   CSC   colptr[p_loc + 1], rowidx[nnz], cval[nnz]   (rows sorted within a column)
 //   CSR   rowptr[n_pad + 1], colidx[nnz], rval[nnz], cpos[nnz] = CSC position of entry k
 //   pairs for every off-diagonal Gram entry (r, c), r < c, in packed upper-triangle order
-//         e = tri_index(r, c): estart[e] .. estart[e + 1] index prod[] = X_rj X_cj and
-//         pj[] = j over the columns j where both are non-zero, j increasing.  Diagonal
-//         entries have empty segments (their sum comes from the CSR row pass).
+//         e = tri_index(r, c): estart[e] .. estart[e + 1] index prod[] = X_rj X_cj over the
+//         columns j where both are non-zero, j increasing, with either pidx[] = the
+//         position of j in row c's CSR list (16 bit; rows of <= kSpColMaxRow non-zeros,
+//         the by-column kernel) or pj[] = j (32 bit; the general kernel).  Diagonal
+//         entries have empty segments (their sum comes from the row pass).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -20,6 +22,11 @@
 #include "bb_kernels.h"
 
 namespace bb {
+
+// Rows of X with more non-zeros than this (64 KB of LDS for D over the row) use the
+// general pair-list kernel with 32-bit column indices.
+constexpr int kSpColMaxRow = 8192;
+int sp_col_max_row();
 
 // cnt[c] = number of (r, j) pairs with r < c and X_rj X_cj != 0  (c < n_pad).
 void launch_sp_count(hipStream_t s, const int *rowptr, const int *colidx, const int *cpos,
@@ -30,7 +37,14 @@ void launch_sp_count(hipStream_t s, const int *rowptr, const int *colidx, const 
 void launch_sp_build(hipStream_t s, const int *rowptr, const int *colidx, const int *cpos,
                      const double *rval, const int *colptr, const int *rowidx,
                      const double *cval, int n_pad, const unsigned long long *base,
-                     unsigned *estart, double *prod, int *pj);
+                     unsigned *estart, double *prod, int *pj, unsigned short *pidx);
+
+// By-column Gram (rows of <= kSpColMaxRow non-zeros): the packed triangle of X diag(D) X'
+// including its diagonal, and xu = X u (xu may be nullptr).  max_row = largest row nnz.
+void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
+                        const unsigned *estart, const double *prod, const unsigned short *pidx,
+                        const double *D, const double *u, int n_pad, int max_row, double *tri,
+                        double *xu);
 
 // out[e] = sum_k prod[k] D[pj[k]] over every packed entry e < tri_count(n_pad)
 // (diagonal entries come out 0; k_sp_rows fills them).

@@ -2,8 +2,9 @@
 //
 // Replaces, for a CSC design, the three passes over X of the beta | rest draw
 // (Code/C/BridgeRegression.cpp:552-575 in its Woodbury form):
-//   Gram     X diag(D) X'  -> k_sp_gram (off-diagonal) + k_sp_rows<true> (diagonal)
-//   X u, X b               -> k_sp_rows
+//   Gram     X diag(D) X'  -> k_sp_gram_col (with the diagonal and X u), or for rows
+//                             denser than kSpColMaxRow k_sp_gram + k_sp_rows<true>
+//   X u, X b               -> k_sp_rows (X u inside k_sp_gram_col)
 //   X' w                   -> k_sp_beta (fused into the beta update)
 // and, once at setup, the pair list the Gram streams (k_sp_count, k_sp_build).
 //
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void k_sp_build(
     const double *__restrict__ rval, const int *__restrict__ colptr,
     const int *__restrict__ rowidx, const double *__restrict__ cval,
     const unsigned long long *__restrict__ base, unsigned *__restrict__ estart,
-    double *__restrict__ prod, int *__restrict__ pj) {
+    double *__restrict__ prod, int *__restrict__ pj, unsigned short *__restrict__ pidx) {
     extern __shared__ unsigned cur[];  // c words: count, then cursor, per row r < c
     __shared__ unsigned part[257];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -129,7 +130,10 @@ __global__ __launch_bounds__(256) void k_sp_build(
                 cur[r] = pos + 1u;
                 const size_t o = (size_t)(b + pos);
                 prod[o] = cval[q] * xc;
-                pj[o] = j;
+                if (pidx)
+                    pidx[o] = (unsigned short)(kb + l - k0);  // position of j in row c
+                else
+                    pj[o] = j;
             }
         }
     }
@@ -138,9 +142,9 @@ __global__ __launch_bounds__(256) void k_sp_build(
 void launch_sp_build(hipStream_t s, const int *rowptr, const int *colidx, const int *cpos,
                      const double *rval, const int *colptr, const int *rowidx,
                      const double *cval, int n_pad, const unsigned long long *base,
-                     unsigned *estart, double *prod, int *pj) {
+                     unsigned *estart, double *prod, int *pj, unsigned short *pidx) {
     k_sp_build<<<n_pad, 256, (size_t)n_pad * sizeof(unsigned), s>>>(
-        rowptr, colidx, cpos, rval, colptr, rowidx, cval, base, estart, prod, pj);
+        rowptr, colidx, cpos, rval, colptr, rowidx, cval, base, estart, prod, pj, pidx);
 }
 
 // ---------------------------------------------------------------------------
@@ -180,6 +184,83 @@ void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, c
     const size_t nent = tri_count(n_pad);
     const size_t threads = nent * kSpLpe;
     k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out);
+}
+
+// Gram by output column (the production kernel when every row of X has at most
+// kSpColMaxRow non-zeros).  All pairs of the entries (r, c), r < c, share row c of X, so
+// their columns j lie in row c's support J_c: the workgroup stages D[J_c] in LDS once and
+// the pairs carry 16-bit positions into J_c instead of 32-bit column indices -- the
+// per-pair D gathers become LDS reads and the pair stream shrinks to 10 bytes.  The same
+// pass forms the diagonal sum_j X_cj^2 D_j and (X u)_c.  Entries keep k_sp_gram's lane
+// groups and per-lane order (kSpLpe lanes per entry, lane q sums pairs q, q + kSpLpe, ...),
+// with kSpDepth pairs per lane in flight.  Heaviest columns (largest c) launch first.
+constexpr int kSpDepth = 8;
+
+__global__ __launch_bounds__(256) void k_sp_gram_col(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx,
+    const double *__restrict__ rval, const unsigned *__restrict__ estart,
+    const double *__restrict__ prod, const unsigned short *__restrict__ pidx,
+    const double *__restrict__ D, const double *__restrict__ u, int n_pad,
+    double *__restrict__ tri, double *__restrict__ xu) {
+    extern __shared__ double Dl[];  // D over row c's support
+    __shared__ double red[2][4];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = n_pad - 1 - (int)blockIdx.x;
+    const int k0 = rowptr[c], nk = rowptr[c + 1] - k0;
+    double sd = 0.0, su = 0.0;
+    for (int l = tid; l < nk; l += 256) {
+        const int j = colidx[k0 + l];
+        const double x = rval[k0 + l], d = D[j];
+        Dl[l] = d;
+        sd += x * x * d;
+        if (u) su += x * u[j];
+    }
+    sd = group_sum<64>(sd);
+    su = group_sum<64>(su);
+    if (lane == 0) {
+        red[0][wid] = sd;
+        red[1][wid] = su;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        tri[tri_index(c, c)] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        if (xu) xu[c] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+    const size_t e0 = tri_index(0, c);
+    const int g = tid / kSpLpe, q = tid % kSpLpe;
+    for (int r0 = 0; r0 < c; r0 += 256 / kSpLpe) {
+        const int r = r0 + g;
+        double s = 0.0;
+        if (r < c) {
+            const unsigned en = estart[e0 + r + 1];
+            for (unsigned k = estart[e0 + r] + q; k < en; k += kSpDepth * kSpLpe) {
+                double pv[kSpDepth];
+                unsigned short iv[kSpDepth];
+#pragma unroll
+                for (int i = 0; i < kSpDepth; ++i) {
+                    const unsigned kk = k + i * kSpLpe;
+                    pv[i] = kk < en ? prod[kk] : 0.0;
+                    iv[i] = kk < en ? pidx[kk] : (unsigned short)0;
+                }
+#pragma unroll
+                for (int i = 0; i < kSpDepth; ++i)
+                    if (k + i * kSpLpe < en) s += pv[i] * Dl[iv[i]];
+            }
+        }
+        s = group_sum<kSpLpe>(s);
+        if (q == 0 && r < c) tri[e0 + r] = s;
+    }
+}
+
+int sp_col_max_row() { return kSpColMaxRow; }
+
+void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
+                        const unsigned *estart, const double *prod, const unsigned short *pidx,
+                        const double *D, const double *u, int n_pad, int max_row, double *tri,
+                        double *xu) {
+    const size_t lds = (size_t)(max_row > 0 ? max_row : 1) * sizeof(double);
+    k_sp_gram_col<<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad,
+                                          tri, xu);
 }
 
 // One wave per row c of X (CSR), lanes strided over the row's entries, fixed tree.

@@ -329,17 +329,26 @@ def main():
     n_pad = -(-n // 128) * 128
     ntri = n_pad * (n_pad + 1) // 2
     if sparse:
-        # Dominant kernel = the pair-list sparse Gram, HBM-bound: per launch it streams the
-        # pair list (8 B product + 4 B column index per pair), the segment starts (4 B per
-        # packed entry), writes the packed triangle (8 B per entry) and reads D (8 B per
-        # column, L2-resident after the first touch) -- DESIGN.md s6.2.
-        pairs = eng.sparse_pairs()
-        kernel_bytes = 12.0 * pairs + 12.0 * ntri + 8.0 * p_loc
+        # Dominant kernel = the pair-list sparse Gram, HBM-bound.  By-column
+        # kernel, per launch: the pair stream (8 B product + 2 B row position per pair), the
+        # segment starts (4 B per packed entry) and the packed triangle written (8 B per
+        # entry), the CSR rows (4 B index + 8 B value per non-zero) and D, u (8 B each per
+        # column).  The general kernel streams 4 B column indices instead and gathers D.
+        si = eng.sparse_info()
+        pairs = si["pairs"]
+        if si["col_mode"]:
+            kernel_bytes = 10.0 * pairs + 12.0 * ntri + 12.0 * si["nnz"] + 16.0 * p_loc
+            kname = "k_sp_gram_col (pair-list Gram by output column)"
+            kfull = "bb::k_sp_gram_col"
+        else:
+            kernel_bytes = 12.0 * pairs + 12.0 * ntri + 8.0 * p_loc
+            kname = "k_sp_gram (pair-list Gram)"
+            kfull = "bb::k_sp_gram"
         achieved = kernel_bytes / (gram_ms * 1e-3) / 1e9 if gram_ms > 0 else 0.0
-        peak, unit, kname, bound = 8000.0, "GB/s", "k_sp_gram (pair-list SpMV)", "hbm"
+        peak, unit, bound = 8000.0, "GB/s", "hbm"
         kernel_ops = kernel_bytes
         alg_bytes = kernel_bytes
-        traffic = pmc_traffic(n, p, world, "bb::k_sp_gram")
+        traffic = pmc_traffic(n, p, world, kfull)
     elif gram_mode == bb.GRAM_OZAKI:
         # Dominant kernel = the Gram GEMM: algorithmic int8 ops of one k_oz_gemm launch,
         # kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
@@ -357,9 +366,10 @@ def main():
                                     "k_gram (v_mfma_f64_16x16x4_f64)", "mfma")
         alg_bytes = 8.0 * n * p_loc
         traffic = pmc_traffic(n, p, world, "bb::k_gram")
-    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0) + \
-        (phases.get("xu", 0.0) if sparse else 0.0)
-    fp64_equiv = gram_flops / (gram_total_ms * 1e-3) / 1e12 if gram_total_ms > 0 else 0.0
+    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
+    # the dense Gram's fp64-equivalent rate (meaningless for the sparse design)
+    fp64_equiv = (gram_flops / (gram_total_ms * 1e-3) / 1e12
+                  if gram_total_ms > 0 and not sparse else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sweeps > 0:
@@ -385,8 +395,9 @@ def main():
                   "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
                                                              if world > 1 else "")}
         if sparse:
+            si = eng.sparse_info()
             config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
-                          nnz=nnz_loc * world if world == 1 else None, pairs=eng.sparse_pairs())
+                          nnz_local=si["nnz"], pairs_local=si["pairs"], max_row_nnz=si["max_row"])
         else:
             config["gram"] = ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
                               else "fp64 mfma")

@@ -200,6 +200,10 @@ int bb_engine_create_csc(const bb_config *cfg, const int *colptr, const int *row
                          const double *val, const double *y, bb_engine **out);
 /* Number of off-diagonal Gram pairs (X_rj X_cj != 0, r < c) of a sparse engine, else -1. */
 long long bb_engine_sparse_pairs(const bb_engine *e);
+/* Sparse engine layout: pair count, nnz of the shard, largest row nnz, and whether the
+ * by-column Gram kernel runs (1: every row has <= 8192 non-zeros) or the general one (0). */
+int bb_engine_sparse_info(const bb_engine *e, long long *pairs, long long *nnz, int *max_row,
+                          int *col_mode);
 
 /*
  * RCCL communicator for world > 1: rank 0 calls bb_comm_unique_id, the bytes are

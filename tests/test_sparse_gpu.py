@@ -56,6 +56,29 @@ def test_sparse_gram_matches_scipy(gpu_lib, n, p, density, extra):
     assert np.array_equal(C, C.T)
 
 
+def test_sparse_gram_general_kernel_dense_row(gpu_lib):
+    """A row with more than 8192 non-zeros sends the design to the general pair-list kernel
+    (32-bit column indices, D gathered from HBM/L2) instead of the by-column one."""
+    bb = gpu_lib
+    n, p = 90, 9000
+    X = rand_csc(n, p, 0.01, 61).tolil()
+    rng = np.random.default_rng(62)
+    X[7, :] = rng.standard_normal((1, p))
+    X = sps.csc_matrix(X)
+    D = 10.0 ** rng.uniform(-4, 1, p)
+    u = rng.standard_normal(p)
+    e = bb.Engine(bb.EngineConfig(n=n, p=p), X, np.zeros(n))
+    info = e.sparse_info()
+    e.close()
+    assert not info["col_mode"] and info["max_row"] == p
+    C, xu = bb.sparse_gram(X, D, u)
+    ref = (X.toarray() * D) @ X.toarray().T
+    scale = (np.abs(X.toarray()) * D) @ np.abs(X.toarray()).T
+    m = scale > 0
+    assert np.max(np.abs(C - ref)[m] / scale[m]) < 1e-14
+    assert np.allclose(xu, X @ u, rtol=1e-12, atol=1e-12)
+
+
 def test_sparse_gram_exact_on_integers(gpu_lib):
     """Integer X and D: every partial sum is an exact integer, so the pair-list Gram must
     equal the int64 product bit for bit (pins the pair placement and segment starts)."""
