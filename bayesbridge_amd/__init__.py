@@ -63,7 +63,8 @@ EXPORTED_SYMBOLS = [
     "rtnorm_left", "rtnorm_both", "rtnorm", "rtexpon_rate_left", "rtexpon_rate_both",
     "rtexpon_rate", "mytest", "bb_trunc_batch", "rrtgamma_rate", "bb_rrtgamma_batch",
     "bridge_reg_stable_csc", "bb_engine_create_csc", "bb_engine_sparse_pairs", "bb_sparse_gram",
-    "bb_bench_sparse_gram", "bb_engine_sparse_info",
+    "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
+    "bb_pg_batch",
 ]
 
 
@@ -137,6 +138,9 @@ def library(build: bool = True) -> ctypes.CDLL:
                                        c.POINTER(c.c_void_p)]
     L.bb_engine_sparse_pairs.argtypes = [c.c_void_p]
     L.bb_engine_sparse_pairs.restype = c.c_longlong
+    L.bridge_reg_logit.argtypes = [_dp] * 6 + [_dp] * 6 + [_ip] * 4 + [_dp]
+    L.bb_engine_get_omega.argtypes = [c.c_void_p, _dp]
+    L.bb_pg_batch.argtypes = [_dp, _dp, c.c_int, c.c_uint64, c.c_uint64, c.c_uint64]
     L.bb_engine_sparse_info.argtypes = [c.c_void_p, c.POINTER(c.c_longlong),
                                         c.POINTER(c.c_longlong), _ip, _ip]
     L.bb_sparse_gram.argtypes = [_dp, _dp, _ip, _ip, _dp, _dp, _dp, c.c_int, c.c_int]
@@ -350,6 +354,52 @@ def bridge_reg_tri(y, X, nsamp, alpha=0.5, sig2_shape=0.0, sig2_scale=0.0, nu_sh
     out = {k: v.T.copy() for k, v in tr.items()}
     out.update(sig2=sig2, tau=tau, alpha=alph, runtime=rt.value)
     return out
+
+
+def bridge_reg_logit(y, X, nsamp, alpha=0.5, nu_shape=2.0, nu_rate=2.0, alpha_a=1.0,
+                     alpha_b=1.0, tau_true=0.0, burn=500):
+    """Logistic bridge regression (Polya-Gamma Gibbs, BASELINE config C4) through
+    ``.C("bridge_reg_logit", ...)``; y in {0, 1}.  No reference counterpart: the R-style
+    front end mirrors bridge.reg.stb (same checks, same trace layout, no sig2).
+
+    Returns a dict: beta (M x P), lambda (M x P), tau, alpha (M), runtime.
+    """
+    L = library()
+    _require_gpu()
+    y = np.asarray(y, dtype=np.float64).ravel()
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    N = y.shape[0]
+    R, P = X.shape
+    M = int(nsamp)
+    if not check_parameters(N, R, M, 0.0, 0.0, nu_shape, nu_rate, alpha_a, alpha_b):
+        raise ValueError("bridge_reg_logit: invalid parameters")
+    if not np.all((y == 0) | (y == 1)):
+        raise ValueError("bridge_reg_logit: y must be 0/1")
+    beta = np.zeros((P, M), order="F")
+    lam = np.zeros((P, M), order="F")
+    tau = np.zeros(M)
+    alph = np.zeros(M)
+    Xf = np.asfortranarray(X)
+    d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
+    i = lambda v: ctypes.byref(ctypes.c_int(int(v)))  # noqa: E731
+    rt = ctypes.c_double(0.0)
+    L.bridge_reg_logit(_p(beta), _p(lam), _p(tau), _p(alph), _p(y), _p(Xf), d(nu_shape),
+                       d(nu_rate), d(alpha_a), d(alpha_b), d(tau_true), d(alpha), i(P), i(N),
+                       i(M), i(burn), ctypes.byref(rt))
+    return {"beta": beta.T.copy(), "lambda": lam.T.copy(), "tau": tau, "alpha": alph,
+            "runtime": rt.value}
+
+
+def pg_batch(psi, seed, stream=0, t=0):
+    """omega_i ~ PG(1, psi_i) on the device under an explicit key (tests)."""
+    L = library()
+    _require_gpu()
+    psi = np.ascontiguousarray(psi, dtype=np.float64)
+    om = np.zeros_like(psi)
+    _check(L.bb_pg_batch(_p(om), _p(psi), psi.shape[0], seed, stream, t), "bb_pg_batch")
+    return om
 
 
 def _dotC(name, num, *params):
@@ -862,6 +912,12 @@ class Engine:
         _check(library().bb_engine_get_trace(self._h, slot0, count, _p(beta), _p(lam), _p(sig2),
                                              _p(tau), _p(alpha)), "bb_engine_get_trace")
         return dict(beta=beta, **{"lambda": lam}, sig2=sig2, tau=tau, alpha=alpha)
+
+    def omega(self):
+        """Logistic engine: the current Polya-Gamma latents (n)."""
+        om = np.zeros(self.cfg.n)
+        _check(library().bb_engine_get_omega(self._h, _p(om)), "bb_engine_get_omega")
+        return om
 
     def tri_trace(self, slot0: int, count: int):
         """Triangle method: u and shape traces (omega is ``trace()['lambda']``)."""

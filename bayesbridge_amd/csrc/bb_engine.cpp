@@ -248,19 +248,20 @@ struct SparseDesign {
 // Engine
 // ---------------------------------------------------------------------------
 enum Phase {
-    PH_PRE, PH_SCALARS, PH_LAMBDA, PH_OZPREP, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL,
+    PH_PRE, PH_SCALARS, PH_LAMBDA, PH_PG, PH_OZPREP, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL,
     PH_SOLVE, PH_BETA, PH_XB, PH_ALPHA, PH_END, PH_COUNT
 };
 // "gram" times the Gram GEMM kernel alone (k_gram, or k_oz_gemm after "ozprep" = row scales
 // + residues); "reduce" is the split/slab combine (k_slab_sum or the CRT k_oz_crt).
-static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "ozprep", "gram", "xu",
-                                            "reduce", "form", "chol", "solve", "beta", "xb",
-                                            "alpha", "end"};
+static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
+                                            "xu", "reduce", "form", "chol", "solve", "beta",
+                                            "xb", "alpha", "end"};
 
 struct bb_engine {
     bb_config cfg{};
     int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
-    int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture, 5 sparse woodbury
+    int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture, 5 sparse woodbury,
+                     // 6 logistic (Polya-Gamma)
     int group = 1;
     SparseDesign spd;  // method 5: CSC/CSR design and the Gram pair list
     Hyper hy{};
@@ -285,6 +286,8 @@ struct bb_engine {
     unsigned long long *oz_rowbits = nullptr;
     int *oz_escale = nullptr;
     int8_t *oz_R = nullptr, *oz_P = nullptr;
+    // logistic: X' resident for X'Omega X, omega, kappa = y - 1/2, the per-sweep Gram
+    double *Xt = nullptr, *omega = nullptr, *kappa = nullptr, *Gw = nullptr;
     // chol / ortho
     double *G = nullptr, *cvec = nullptr, *A = nullptr, *Y2 = nullptr, *W2 = nullptr,
            *gdiag = nullptr;
@@ -419,6 +422,16 @@ struct bb_engine {
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
                                 red2, 1);
+        } else if (method == 6) {
+            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
+                          group, lam, nullptr, nullptr, trl, err);
+            mark(PH_PG);
+            // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums)
+            launch_pg(stream, red1 + nbS, n, n_pad, cfg.seed, cfg.stream, t, omega, err);
+            mark(PH_GRAM);
+            launch_gram(stream, Xt, p_pad, omega, p_pad, n_pad, S, slabs, p_pad, slab_stride);
+            mark(PH_REDUCE);
+            launch_slab_sum(stream, slabs, S, slab_stride, p_pad, nullptr, 0, Gw, 0);
         } else if (method == 4) {
             // BridgeWrapper.cpp:166-168: omega, u, then the rtnorm_gibbs beta passes
             mark(PH_BETA);
@@ -461,9 +474,11 @@ struct bb_engine {
             } else {
                 launch_beta_woodbury(stream, X, n_pad, n_pad, w, u, D, sc, p_loc, beta, trb);
             }
-        } else if (method == 1) {
+        } else if (method == 1 || method == 6) {
+            // logistic: A = X'Omega X + diag(lambda / tau^2) (sig2 = 1), c = X'kappa
             mark(PH_FORM);
-            launch_form_a(stream, G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad, p_pad);
+            launch_form_a(stream, method == 6 ? Gw : G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad,
+                          p_pad);
             mark(PH_CHOL);
             chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd, flags);
             mark(PH_SOLVE);
@@ -484,7 +499,8 @@ struct bb_engine {
             // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
             mark(PH_ALPHA);
             // triangle driver: (alpha_a, alpha_b) in both loops (BridgeWrapper.cpp:146,173)
-            const double pr_a = (method <= 2 && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
+            const double pr_a =
+                ((method <= 2 || method == 5) && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
             launch_alpha_mh(stream, beta, p, sc, pr_a, hy.alpha_b, cfg.seed, cfg.stream, t,
                             slot_ptr(tr_alpha, slot, 1));
         }
@@ -630,9 +646,17 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     e->hy = Hyper{c.sig2_shape, c.sig2_scale, c.nu_shape, c.nu_rate, c.alpha_a, c.alpha_b,
                   c.true_tau > 0, c.true_sig2 > 0, c.true_alpha > 0};
     if (spin) {
-        if (c.ortho || c.method == 1 || c.method == 3 || c.method == 4)
+        if (c.ortho || c.method == 1 || c.method == 3 || c.method == 4 || c.method == 6)
             throw HipError("a CSC design runs the Woodbury (p > n) draw only");
         e->method = 5;
+    } else if (c.method == 6) {
+        e->method = 6;
+        e->hy.know_sig2 = 1;  // the PG mixture has unit scale
+        // X'Omega X runs over K = n_pad rows: pad to 512 so the Gram can split K 16 ways
+        e->n_pad = round_up(c.n, 512);
+        if (c.world > 1) throw HipError("the logistic path runs on one device (world == 1)");
+        if (c.ortho) throw HipError("the logistic path has no orthogonal-design variant");
+        if (c.p > 16384) throw HipError("logistic path limited to p <= 16384");
     } else if (c.method == 4) e->method = 4;
     else if (c.ortho) e->method = 3;
     else if (c.method == 1 || (c.method == 0 && c.p <= c.n)) e->method = 1;
@@ -705,13 +729,29 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         e->w = dalloc<double>(n_pad, o);
     }
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
-    const bool small = c.p <= c.n && c.world == 1 && e->method != 5;
+    const bool small = c.p <= c.n && c.world == 1 && e->method != 5 && e->method != 6;
     // the Cholesky scratch covers the n x n (Woodbury) and any p x p (chol, LS start) system
     const int m_sys = (e->woodbury() && !small) ? n_pad : (n_pad > p_pad ? n_pad : p_pad);
     e->PT = dalloc<double>((size_t)2 * kNB * (m_sys + kNB), o);
     e->Wd = dalloc<double>((size_t)kNB * m_sys, o);
     e->flags = dalloc<unsigned int>(chol_flag_words(m_sys, 1), o);
-    if ((e->method != 2 && e->method != 5) || small) {
+    if (e->method == 6) {
+        // logistic: X' resident (p_pad x n_pad), K-split slabs of X'Omega X, c = X'kappa
+        e->Xt = dalloc<double>((size_t)p_pad * n_pad, o);
+        launch_transpose(e->stream, e->X, n_pad, n_pad, p_pad, e->Xt, p_pad);
+        e->S = gram_splits_for(p_pad, n_pad);
+        e->slab_stride = (size_t)p_pad * p_pad;
+        e->slabs = dalloc<double>(e->slab_stride * e->S, o);
+        e->Gw = dalloc<double>((size_t)p_pad * p_pad + p_pad, o);
+        e->omega = dalloc<double>(n_pad, o);
+        e->kappa = dalloc<double>(n_pad, o);
+        launch_kappa(e->stream, e->y, c.n, n_pad, e->kappa);
+        e->cvec = dalloc<double>(p_pad, o);
+        launch_coldot(e->stream, e->X, n_pad, n_pad, e->kappa, c.p_local, e->cvec);
+        e->A = dalloc<double>((size_t)p_pad * (p_pad + kNB), o);
+        e->Y2 = dalloc<double>((size_t)2 * p_pad, o);
+        e->W2 = dalloc<double>((size_t)2 * p_pad, o);
+    } else if ((e->method != 2 && e->method != 5) || small) {
         e->cvec = dalloc<double>(p_pad, o);
         launch_coldot(e->stream, e->X, n_pad, n_pad, e->y, c.p_local, e->cvec);
         e->gdiag = dalloc<double>(p_pad, o);
@@ -775,14 +815,14 @@ void engine_init_state_local(bb_engine *e) {
     }
     if (!ls_ok) {
         HIPCHECK(hipMemsetAsync(e->beta, 0, (size_t)e->p_pad * sizeof(double), e->stream));
-        if (g_verbose && c.rank == 0) {
+        if (g_verbose && c.rank == 0 && e->method != 6) {
             printf("Warning: cannot calculate least squares estimate; X'X is singular.\n");
             printf("Warning: setting least squares estimate to 0.0.\n");
         }
     }
     DevScalars s{};
     s.alpha = c.true_alpha > 0 ? c.true_alpha : 0.5;
-    s.sig2 = c.true_sig2 > 0 ? c.true_sig2 : 0.0;
+    s.sig2 = e->method == 6 ? 1.0 : (c.true_sig2 > 0 ? c.true_sig2 : 0.0);
     s.tau = c.true_tau > 0 ? c.true_tau : 0.0;
     HIPCHECK(hipMemcpyAsync(e->sc, &s, sizeof(s), hipMemcpyHostToDevice, e->stream));
     if (e->method == 4) {  // BridgeWrapper.cpp:123 u[0].fill(0.5); omega starts at 1.0 (:604)
@@ -1066,6 +1106,18 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
 
 int bb_engine_method(const bb_engine *e) { return e->method; }
 
+int bb_engine_get_omega(bb_engine *e, double *omega) {
+    try {
+        if (e->method != 6) throw HipError("not a logistic engine");
+        HIPCHECK(hipStreamSynchronize(e->stream));
+        HIPCHECK(hipMemcpy(omega, e->omega, (size_t)e->n * sizeof(double), hipMemcpyDeviceToHost));
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
 int bb_engine_get_tri_trace(bb_engine *e, int slot0, int count, double *u, double *shape) {
     try {
         if (e->method != 4) throw HipError("not a triangle-method engine");
@@ -1344,6 +1396,33 @@ int bb_retstable_batch(double *x, const double *alpha, const double *V0, const d
         }
         rc = (int)(f & ~4u) ? -2 : 0;
         if (rc) set_error("retstable: rejection cap reached (flags %u)", f);
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        rc = -1;
+    }
+    for (void *q : owned) (void)hipFree(q);
+    return rc;
+}
+
+int bb_pg_batch(double *omega, const double *psi, int n, uint64_t seed, uint64_t stream,
+                uint64_t t) {
+    if (n <= 0) return 0;
+    std::vector<void *> owned;
+    int rc = 0;
+    try {
+        HIPCHECK(hipSetDevice(g_device));
+        double *dp = dalloc<double>(n, owned), *dw = dalloc<double>(n, owned);
+        uint32_t *de = dalloc<uint32_t>(1, owned);
+        HIPCHECK(hipMemcpy(dp, psi, (size_t)n * sizeof(double), hipMemcpyHostToDevice));
+        launch_pg(0, dp, n, n, seed, stream, t, dw, de);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipMemcpy(omega, dw, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+        uint32_t f = 0;
+        HIPCHECK(hipMemcpy(&f, de, sizeof(f), hipMemcpyDeviceToHost));
+        if (f) {
+            set_error("pg: rejection cap reached (flags %u)", f);
+            rc = -2;
+        }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         rc = -1;
@@ -2098,11 +2177,12 @@ bb_config stable_call_config(const double *sig2_shape, const double *sig2_scale,
 // `create` builds the engine (dense or CSC design); errors print and return partial traces.
 template <class Create>
 void run_stable_chain(const bb_config &c, Create create, int b, double *betap, double *lambdap,
-                      double *sig2p, double *taup, double *alphap, double *runtime) {
+                      double *sig2p, double *taup, double *alphap, double *runtime,
+                      const char *title = "Bridge Regression (mix. of normals):") {
     const int m = c.trace_capacity;
     const bool know_sig2 = c.true_sig2 > 0, know_tau = c.true_tau > 0, know_alpha = c.true_alpha > 0;
     if (g_verbose) {  // BridgeWrapper.cpp:235-240
-        printf("Bridge Regression (mix. of normals):");
+        printf("%s", title);
         if (know_alpha) printf(" known alpha=%g", c.true_alpha);
         if (know_sig2) printf(", sig2=%g", c.true_sig2);
         if (know_tau) printf(", tau=%g", c.true_tau);
@@ -2197,6 +2277,30 @@ void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double
     run_stable_chain(
         c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xd.data(), yp, e); },
         *burn, betap, lambdap, sig2p, taup, alphap, runtime);
+}
+
+void bridge_reg_logit(double *betap, double *lambdap, double *taup, double *alphap,
+                      const double *yp, const double *Xp, const double *nu_shape,
+                      const double *nu_rate, const double *alpha_a, const double *alpha_b,
+                      const double *true_tau, const double *true_alpha, const int *P,
+                      const int *N, const int *M, const int *burn, double *runtime) {
+    const double zero = 0.0, one = 1.0;
+    const int no = 0;
+    bb_config c = stable_call_config(&zero, &zero, nu_shape, nu_rate, alpha_a, alpha_b, &one,
+                                     true_tau, true_alpha, *P, *N, *M, &no);
+    c.method = 6;
+    for (int i = 0; i < *N; ++i)
+        if (!(yp[i] == 0.0 || yp[i] == 1.0)) {
+            printf("Error: logistic bridge needs y in {0, 1} (y[%d] = %g)\n", i, yp[i]);
+            printf("Aborting Gibbs sampler.\n");
+            *runtime = 0.0;
+            return;
+        }
+    std::vector<double> sig2(c.trace_capacity);
+    run_stable_chain(
+        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xp, yp, e); },
+        *burn, betap, lambdap, sig2.data(), taup, alphap, runtime,
+        "Bridge Regression (logistic, Polya-Gamma mix. of normals):");
 }
 
 void bridge_regression(double *betap, double *up, double *omegap, double *shapep,

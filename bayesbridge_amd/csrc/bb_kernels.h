@@ -177,6 +177,12 @@ void launch_rrtgamma_batch(hipStream_t s, int num, double *x, const double *shap
                            const double *rate, const double *right_t, uint64_t k0, uint64_t k1,
                            uint32_t *err);
 
+// Logistic bridge (bb_logit.hip): omega_i ~ PG(1, psi_i) for i < n (0 on padding rows),
+// err bit 32 when a draw exhausted its attempts; kappa = y - 1/2.
+void launch_pg(hipStream_t s, const double *psi, int n, int n_pad, uint64_t k0, uint64_t k1,
+               uint64_t t, double *omega, uint32_t *err);
+void launch_kappa(hipStream_t s, const double *y, int n, int n_pad, double *kappa);
+
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
                            double *sig2_tr, double *alpha_tr);

@@ -73,11 +73,43 @@ def make_problem_y(n, p, seed=DATA_SEED):
 SPARSE_DENSITY = 0.01  # C5: each X_ij non-zero independently with this probability
 
 WORKLOADS = {
-    # name: (n, p, alpha, sparse)
-    "c2": (1000, 5000, 0.5, False),
-    "c3": (2000, 50000, 0.5, False),
-    "c5": (5000, 200000, 0.3, True),
+    # name: (n, p, alpha, kind)
+    "c2": (1000, 5000, 0.5, "dense"),
+    "c3": (2000, 50000, 0.5, "dense"),
+    "c4": (10000, 1000, 0.5, "logit"),
+    "c5": (5000, 200000, 0.3, "sparse"),
 }
+
+
+def make_logit_problem(n, p, seed=DATA_SEED):
+    """C4 synthetic logistic design: X_ij ~ N(0,1), beta's first max(5, p/100) entries
+    +-U(1,3) and the rest 0, y_i ~ Bernoulli(1/(1 + exp(-x_i'beta))).
+    Returns (X (F order), y in {0,1}, beta)."""
+    rng = np.random.default_rng([seed, 4])
+    X = np.asfortranarray(rng.standard_normal((n, p)))
+    s = max(5, p // 100)
+    b = np.zeros(p)
+    b[:s] = rng.uniform(1, 3, size=s) * rng.choice([-1.0, 1.0], size=s)
+    y = (rng.random(n) < 1.0 / (1.0 + np.exp(-(X @ b)))).astype(np.float64)
+    return X, y, b
+
+
+def cpu_baseline_logit(n, p, alpha, sweeps, log_every=True):
+    """Oracle logistic sweeps (numpy X'Omega X, LAPACK Cholesky, C PG and tilted-stable
+    samplers).  Returns (median s per sweep, threads)."""
+    from oracle import gibbs
+
+    X, y, _ = make_logit_problem(n, p)
+    beta, tau = np.zeros(p), 1.0
+    times = []
+    for t in range(1, sweeps + 1):
+        t0 = time.perf_counter()
+        beta, _, tau, _ = gibbs.logit_sweep(X, y, beta, tau, alpha, t, 1, 0)
+        times.append(time.perf_counter() - t0)
+        if log_every:
+            log(f"[cpu_baseline] logistic sweep {t}: {times[-1]:.3f} s")
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return float(np.median(times)), threads
 
 
 def make_sparse_columns(n, j0, j1, density=SPARSE_DENSITY, seed=DATA_SEED, block=1000):
@@ -216,11 +248,13 @@ def main():
                     help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
                          "BB_GRAM_MODE, else the library default)")
     args = ap.parse_args()
-    wn, wp, walpha, sparse = WORKLOADS[args.workload]
+    wn, wp, walpha, kind = WORKLOADS[args.workload]
+    sparse, logit = kind == "sparse", kind == "logit"
     n = args.rows or wn
     p = args.cols or wp
     alpha = args.alpha or walpha
-    cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else (2 if sparse else 5)
+    cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
+        (2 if sparse else 20 if logit else 5)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -250,16 +284,21 @@ def main():
     j1 = min(p, j0 + per)
     p_loc = j1 - j0
     t_setup0 = time.perf_counter()
+    if logit and world > 1:
+        raise SystemExit("the logistic workload runs on one GPU (replicas only)")
     if sparse:
         X = make_sparse_columns(n, j0, j1)
         y, _ = make_sparse_problem_y(n, p)
         nnz_loc = int(X.nnz)
+    elif logit:
+        X, y, _ = make_logit_problem(n, p)
+        nnz_loc = n * p
     else:
         X = make_columns(n, j0, j1)
         y, _ = make_problem_y(n, p)
         nnz_loc = n * p_loc
     cfg = bb.EngineConfig(n=n, p=p, p_local=p_loc, j0=j0, rank=rank, world=world,
-                          true_alpha=alpha, method=2,
+                          true_alpha=alpha, method=6 if logit else 2,
                           trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
                           stream=0, device=device,
                           gram_mode=None if args.gram is None else
@@ -349,6 +388,15 @@ def main():
         kernel_ops = kernel_bytes
         alg_bytes = kernel_bytes
         traffic = pmc_traffic(n, p, world, kfull)
+    elif logit:
+        # Dominant kernel = the per-sweep X'Omega X (fp64 MFMA k_gram over K = n rows):
+        # n p (p + 1) algorithmic flops per launch (path p <= n, C4)
+        kernel_ops = float(n) * p * (p + 1)
+        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+        peak, unit, kname, bound = (FP64_MFMA_PEAK_TFLOPS, "TFLOP/s",
+                                    "k_gram X'Omega X (v_mfma_f64_16x16x4_f64)", "mfma")
+        alg_bytes = 8.0 * n * p
+        traffic = pmc_traffic(n, p, world, "bb::k_gram")
     elif gram_mode == bb.GRAM_OZAKI:
         # Dominant kernel = the Gram GEMM: algorithmic int8 ops of one k_oz_gemm launch,
         # kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
@@ -369,7 +417,7 @@ def main():
     gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
     # the dense Gram's fp64-equivalent rate (meaningless for the sparse design)
     fp64_equiv = (gram_flops / (gram_total_ms * 1e-3) / 1e12
-                  if gram_total_ms > 0 and not sparse else None)
+                  if gram_total_ms > 0 and kind == "dense" else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sweeps > 0:
@@ -377,27 +425,35 @@ def main():
         if sparse:
             per_sweep, threads = cpu_baseline_sparse(n, p, alpha, cpu_sweeps)
             what = "scipy SpGEMM + LAPACK"
+        elif logit:
+            per_sweep, threads = cpu_baseline_logit(n, p, alpha, cpu_sweeps)
+            what = "numpy X'Omega X + LAPACK + C Polya-Gamma sampler"
         else:
             per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps)
             what = "numpy/OpenBLAS"
         cpu = {"value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads, "kind": "port",
-               "sample": f"{cpu_sweeps} Woodbury sweeps of the oracle ({what}, "
+               "sample": f"{cpu_sweeps} {'logistic' if logit else 'Woodbury'} sweeps of the "
+                         f"oracle ({what}, "
                          f"{threads} threads, + C tilted-stable sampler) at n={n}, p={p}; "
                          f"median sweep {per_sweep:.3f} s"}
 
     if rank == 0:
         wl = {"c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
+              "c4": "C4 logistic bridge (Polya-Gamma)",
               "c5": f"C5 sparse CSC Gaussian bridge (density {SPARSE_DENSITY})"}[args.workload]
         config = {"workload": f"{wl} n={n} p={p} alpha={alpha}",
                   "rccl": bool(world > 1 or force_rccl),
                   "n": n, "p": p, "alpha": alpha,
-                  "beta_step": "woodbury (exact, p > n)",
+                  "beta_step": ("p x p Cholesky of X'Omega X + diag(lambda/tau^2)" if logit
+                                else "woodbury (exact, p > n)"),
                   "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
                                                              if world > 1 else "")}
         if sparse:
             si = eng.sparse_info()
             config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
                           nnz_local=si["nnz"], pairs_local=si["pairs"], max_row_nnz=si["max_row"])
+        elif logit:
+            config["gram"] = "X'Omega X fp64 mfma"
         else:
             config["gram"] = ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
                               else "fp64 mfma")

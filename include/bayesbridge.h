@@ -132,6 +132,22 @@ void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double
                            const double *true_alpha, const int *P, const int *N, const int *M,
                            const int *burn, double *runtime, const int *ortho);
 
+/*
+ * Logistic bridge regression by Polya-Gamma augmentation (BASELINE config C4; no reference
+ * counterpart): y_i in {0, 1} ~ Bernoulli(1 / (1 + exp(-x_i'beta))), bridge prior
+ * exp(-sum |beta_j / tau|^alpha).  Per sweep: tau | beta and lambda | beta, tau as in
+ * bridge_reg_stable (BridgeRegression.cpp:453-465, 506-510), omega_i ~ PG(1, x_i'beta),
+ * beta ~ N(A^-1 X'(y - 1/2), A^-1) with A = X'Omega X + diag(lambda / tau^2) (the
+ * reference's sample_beta_stable with sig2 = 1).  Layout, trace slots, burn-in and
+ * error behaviour as bridge_reg_stable; there is no sig2.  Unknown alpha (true_alpha <= 0)
+ * runs the reference's MH step with the (alpha_a, alpha_b) prior.
+ */
+void bridge_reg_logit(double *betap, double *lambdap, double *taup, double *alphap,
+                      const double *yp, const double *Xp, const double *nu_shape,
+                      const double *nu_rate, const double *alpha_a, const double *alpha_b,
+                      const double *true_tau, const double *true_alpha, const int *P,
+                      const int *N, const int *M, const int *burn, double *runtime);
+
 /* ------------------------------------------------------------------------ */
 /* Part 2: extensions                                                        */
 /* ------------------------------------------------------------------------ */
@@ -177,7 +193,8 @@ typedef struct bb_config {
     int ortho;          /* orthogonal-design variant (sample_beta_stable_ortho) */
     int method;         /* 0 auto (chol if p <= n else woodbury), 1 chol, 2 woodbury,
                            4 triangle mixture (bridge.reg.tri; p <= n, p <= 2048);
-                           5 sparse Woodbury is selected by bb_engine_create_csc */
+                           5 sparse Woodbury is selected by bb_engine_create_csc;
+                           6 logistic bridge (Polya-Gamma; y in {0, 1}) */
     int trace_capacity; /* number of trace slots kept on device (>= 1) */
     uint64_t seed, stream;
     int device;
@@ -258,6 +275,11 @@ typedef struct bb_group bb_group;
 int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double *p1,
                    const double *p2, const double *p3, uint64_t seed, uint64_t stream);
 
+/* omega_i ~ PG(1, psi_i), i < n, under key (seed, stream) and sweep counter t -- the
+ * logistic path's Polya-Gamma kernel (tests).  Returns 0, or -2 if a draw failed. */
+int bb_pg_batch(double *omega, const double *psi, int n, uint64_t seed, uint64_t stream,
+                uint64_t t);
+
 /* rrtgamma_rate under an explicit key (seed, stream). */
 int bb_rrtgamma_batch(int num, double *x, const double *shape, const double *rate,
                       const double *right_t, uint64_t seed, uint64_t stream);
@@ -276,8 +298,11 @@ int bb_group_init_state(bb_group *g);
 int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
                  int mcmc_phase);
 
-/* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho. */
+/* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho, 4 triangle,
+ * 5 sparse woodbury, 6 logistic. */
 int bb_engine_method(const bb_engine *e);
+/* Logistic engine: the current Polya-Gamma latents omega (N). */
+int bb_engine_get_omega(bb_engine *e, double *omega);
 /* Gram implementation in use on the Woodbury path: 0 fp64 MFMA, 1 Ozaki-II int8. */
 int bb_engine_gram_mode(const bb_engine *e);
 

@@ -31,6 +31,8 @@ KIND_ALPHA = 7
 KIND_TRI_OMEGA = 8
 KIND_TRI_U = 9
 KIND_TRI_Z = 10
+KIND_PG = 11
+KIND_PG_IG = 12
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _dp = ctypes.POINTER(ctypes.c_double)
@@ -89,6 +91,8 @@ def lib():
         L.bbo_trunc_batch.restype = ctypes.c_long
         L.bbo_rrtgamma_batch.argtypes = [ctypes.c_long, _dp, _dp, _dp, _dp, _u64p]
         L.bbo_rrtgamma_batch.restype = ctypes.c_long
+        L.bbo_pg_batch.argtypes = [_dp, _dp, ctypes.c_long, _u64p, ctypes.c_uint64]
+        L.bbo_pg_batch.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -234,3 +238,14 @@ def trunc_batch(name, params, seed, stream=0):
     if fails:
         raise ValueError(f"{name}: {fails} failed draws")
     return x
+
+
+def pg_batch(psi, seed, stream, t):
+    """omega_i ~ PG(1, psi_i) (Polson, Scott & Windle 2013; bb_oracle.c bbo_pg1), counters
+    (t, kind 11/12, i, attempt, sub-attempt)."""
+    psi = np.ascontiguousarray(psi, dtype=np.float64)
+    om = np.empty_like(psi)
+    fails = lib().bbo_pg_batch(_ptr(om), _ptr(psi), psi.shape[0], _key(seed, stream), t)
+    if fails:
+        raise ValueError(f"pg_batch: {fails} failed draws")
+    return om

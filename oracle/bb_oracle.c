@@ -624,3 +624,127 @@ long bbo_rrtgamma_batch(long num, double *x, const double *shape, const double *
     }
     return fails;
 }
+
+/* ----------------------------------------------------------------------- */
+/* Polya-Gamma PG(1, z) draws for the logistic bridge (BASELINE config C4).  */
+/* ----------------------------------------------------------------------- */
+/*
+ * No reference counterpart (the reference has no logistic model).  This is
+ * the published exact sampler of Polson, Scott & Windle (2013, JASA 108:1339-1349,
+ * "Bayesian inference for logistic models using Polya-Gamma latent variables", Algorithms
+ * 1-2 and the appendix): PG(1, z) = J*(1, z/2) / 4, J* drawn by Devroye's alternating-series
+ * method with the truncation point t = 0.64 -- a proposal mixing an exponential tail on
+ * (t, inf) and an inverse-Gaussian body on (0, t), accepted by the alternating series of
+ * the J* density.  PARITY UNPINNED against any reference implementation; pinned by the
+ * exact moments E = tanh(z/2)/(2z), Var = (sinh z - z) / (4 z^3 cosh^2(z/2)), the Laplace
+ * transform cosh(z/2) / cosh(sqrt((z^2/2 + s)/2)) and a two-sample KS test against the
+ * infinite-convolution definition (tests/test_logit_cpu.py).
+ *
+ * Counter-based like every draw here: outer attempt o uses block (t, kind 11, i, o, 0) =
+ * {mixture choice, exponential, series uniform}; the inverse-Gaussian body's sub-attempt k
+ * uses block (t, kind 12, i, o, k).  The GPU kernel (bb_logit.hip) evaluates the same
+ * expressions in the same order.
+ */
+#define BBO_PG_T 0.64
+#define BBO_KIND_PG 11
+#define BBO_KIND_PG_IG 12
+#define BBO_PG_MAX_ATTEMPTS 1000
+#define BBO_PG_MAX_TERMS 1000
+
+static double pg_log_ncdf(double x) { return log(0.5 * erfc(-x * 0.70710678118654752440)); }
+
+/* n-th coefficient of the alternating series of the J*(1, 0) density at x */
+static double pg_a(int n, double x)
+{
+    const double K = (n + 0.5) * M_PI;
+    if (x > BBO_PG_T) return K * exp(-0.5 * K * K * x);
+    if (x > 0.0)
+        return exp(-1.5 * (log(0.5 * M_PI) + log(x)) + log(K) - 2.0 * (n + 0.5) * (n + 0.5) / x);
+    return 0.0;
+}
+
+/* probability of the exponential piece: p / (p + q) */
+static double pg_mass_texpon(double z)
+{
+    const double t = BBO_PG_T;
+    const double fz = 0.125 * M_PI * M_PI + 0.5 * z * z;
+    const double b = sqrt(1.0 / t) * (t * z - 1.0);
+    const double a = -sqrt(1.0 / t) * (t * z + 1.0);
+    const double x0 = log(fz) + fz * t;
+    const double xb = x0 - z + pg_log_ncdf(b);
+    const double xa = x0 + z + pg_log_ncdf(a);
+    const double qdivp = 4.0 / M_PI * (exp(xb) + exp(xa));
+    return 1.0 / (1.0 + qdivp);
+}
+
+/* inverse-Gaussian IG(1/z, 1) truncated to (0, t) */
+static double pg_rtigauss(double z, const uint64_t key[2], uint64_t t, uint64_t i, uint64_t o,
+                          int *fail)
+{
+    const double tr = BBO_PG_T;
+    for (uint64_t k = 0; k < BBO_PG_MAX_ATTEMPTS; ++k) {
+        double u[4];
+        draw4(key, t, BBO_KIND_PG_IG, i, o, k, u);
+        if (z < 1.0 / tr) {
+            /* mean above t: 1/X from a truncated chi-square(1) by rejection, then the
+             * exp(-z^2 X / 2) tilt */
+            const double E1 = -log(u[0]), E2 = -log(u[1]);
+            if (E1 * E1 > 2.0 * E2 / tr) continue;
+            const double d = 1.0 + E1 * tr;
+            const double X = tr / (d * d);
+            if (u[2] <= exp(-0.5 * z * z * X)) return X;
+        } else {
+            /* mean below t: Michael-Schucany-Haas inverse-Gaussian draw until X < t */
+            const double mu = 1.0 / z;
+            double Y = bm_normal(u[0], u[1]);
+            Y *= Y;
+            const double half_mu = 0.5 * mu, mu_Y = mu * Y;
+            double X = mu + half_mu * mu_Y - half_mu * sqrt(4.0 * mu_Y + mu_Y * mu_Y);
+            if (u[2] > mu / (mu + X)) X = mu * mu / X;
+            if (X <= tr) return X;
+        }
+    }
+    *fail = 1;
+    return tr;
+}
+
+double bbo_pg1(double psi, const uint64_t key[2], uint64_t t, uint64_t i, int *fail)
+{
+    const double z = fabs(psi) * 0.5;
+    const double fz = 0.125 * M_PI * M_PI + 0.5 * z * z;
+    const double mass = pg_mass_texpon(z);
+    for (uint64_t o = 0; o < BBO_PG_MAX_ATTEMPTS; ++o) {
+        double u[4];
+        draw4(key, t, BBO_KIND_PG, i, o, 0, u);
+        double X;
+        if (u[0] < mass)
+            X = BBO_PG_T + (-log(u[1])) / fz;
+        else
+            X = pg_rtigauss(z, key, t, i, o, fail);
+        double S = pg_a(0, X);
+        const double Y = u[2] * S;
+        for (int n = 1; n < BBO_PG_MAX_TERMS; ++n) {
+            if (n & 1) {
+                S -= pg_a(n, X);
+                if (Y <= S) return 0.25 * X;
+            } else {
+                S += pg_a(n, X);
+                if (Y > S) break;
+            }
+        }
+    }
+    *fail = 1;
+    return 0.25;
+}
+
+/* omega_i ~ PG(1, psi_i), i = 0 .. n-1; returns the number of failed draws */
+long bbo_pg_batch(double *omega, const double *psi, long n, const uint64_t key[2], uint64_t t)
+{
+    long fails = 0;
+    for (long i = 0; i < n; ++i) {
+        int f = 0;
+        omega[i] = bbo_pg1(psi[i], key, t, (uint64_t)i, &f);
+        fails += f;
+    }
+    return fails;
+}

@@ -308,3 +308,67 @@ def bridge_regression_tri(y, X, nsamp, basis, burn=500, alpha=0.5, sig2_shape=0.
     out = {k: v.T.copy() for k, v in tr.items()}
     out.update(sig2=sig2, tau=tau, alpha=alph, runtime=time.perf_counter() - t0)
     return out
+
+
+def logit_sweep(X, y, beta, tau, alpha, t, seed, stream, nu_shape=2.0, nu_rate=2.0,
+                know_tau=False):
+    """One logistic-bridge sweep (BASELINE config C4; no reference counterpart) in the
+    order tau | beta, lambda | beta, tau, omega | beta, beta | omega, lambda, tau.
+
+    tau and lambda are the reference's conditionals (BridgeRegression.cpp:453-465, 506-510);
+    omega_i ~ PG(1, x_i'beta) (Polson, Scott & Windle 2013; bb_oracle.c bbo_pg1); beta is
+    the reference's sample_beta_stable map (:552-575) with sig2 = 1, X'X -> X'Omega X and
+    X'y -> X'(y - 1/2).  Returns (beta, lambda, tau, omega)."""
+    from . import pg_batch
+
+    n, p = X.shape
+    if not know_tau:
+        tau = tau_from_sum(sum_abs_pow(beta, alpha), p, alpha, nu_shape, nu_rate, seed, stream, t)
+    lam = sample_lambda(beta, alpha, tau, seed, stream, t)
+    omega = pg_batch(X @ beta, seed, stream, t)
+    G = (X.T * omega) @ X
+    c = X.T @ (y - 0.5)
+    z = normals(p, seed, stream, t, KIND_BETA_Z)
+    return beta_step_chol(G, c, lam, 1.0, tau, z), lam, tau, omega
+
+
+def bridge_regression_logit(y, X, nsamp, burn=500, alpha=0.5, nu_shape=2.0, nu_rate=2.0,
+                            alpha_a=1.0, alpha_b=1.0, true_tau=0.0, seed=0, stream=0,
+                            record_state=False):
+    """Restatement of .C("bridge_reg_logit"): the stable driver's slots and counters
+    (pre-burn tau draw at t = 0, B + 1 burn-in sweeps in slot 0 at t = 1 + i, MCMC slot i at
+    t = B + 1 + i; BridgeWrapper.cpp:262-298), beta starting at 0, alpha MH (if alpha <= 0)
+    with the (alpha_a, alpha_b) prior.  Returns traces beta, lambda (P x M), tau, alpha (M)."""
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    X = np.asfortranarray(X, dtype=np.float64)
+    n, p = X.shape
+    M = int(nsamp)
+    know_tau, know_alpha = true_tau > 0, alpha > 0
+    beta = np.zeros((p, M))
+    lam = np.ones((p, M))
+    tau = np.full(M, true_tau if know_tau else 0.0)
+    alph = np.full(M, alpha if know_alpha else 0.5)
+    states = []
+    if not know_tau:
+        tau[0] = tau_from_sum(sum_abs_pow(beta[:, 0], alph[0]), p, alph[0], nu_shape, nu_rate,
+                              seed, stream, 0)
+
+    def step(slot, prev, t):
+        b, lam[:, slot], tau[slot], om = logit_sweep(X, y, beta[:, prev], tau[prev], alph[prev],
+                                                     t, seed, stream, nu_shape, nu_rate, know_tau)
+        beta[:, slot] = b
+        if not know_alpha:
+            alph[slot] = alpha_mh(alph[prev], b, tau[slot], alpha_a, alpha_b, seed, stream, t)
+        else:
+            alph[slot] = alph[prev]
+        if record_state:
+            states.append((t, tau[slot], lam[:, slot].copy(), om, b.copy(), alph[slot]))
+
+    for i in range(burn + 1):
+        step(0, 0, 1 + i)
+    for i in range(1, M):
+        step(i, i - 1, burn + 1 + i)
+    out = dict(beta=beta, **{"lambda": lam}, tau=tau, alpha=alph)
+    if record_state:
+        out["states"] = states
+    return out
