@@ -64,7 +64,8 @@ EXPORTED_SYMBOLS = [
     "rtexpon_rate", "mytest", "bb_trunc_batch", "rrtgamma_rate", "bb_rrtgamma_batch",
     "bridge_reg_stable_csc", "bb_engine_create_csc", "bb_engine_sparse_pairs", "bb_sparse_gram",
     "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
-    "bb_pg_batch",
+    "bb_pg_batch", "bb_group_create_rccl", "bb_group_sync", "bb_set_device_count",
+    "bb_set_trace_budget", "bb_debug_interrupt_after", "bb_last_call_info",
 ]
 
 
@@ -120,6 +121,12 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_bench_ozaki.argtypes = [c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, _dp]
     L.bb_chol_solve.argtypes = [_dp, _dp, _dp, c.c_int, c.c_int]
     L.bb_group_create.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
+    L.bb_group_create_rccl.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
+    L.bb_group_sync.argtypes = [c.c_void_p]
+    L.bb_set_device_count.argtypes = [c.c_int]
+    L.bb_set_trace_budget.argtypes = [c.c_longlong]
+    L.bb_debug_interrupt_after.argtypes = [c.c_int]
+    L.bb_last_call_info.argtypes = [_ip, _ip, _ip]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -206,6 +213,28 @@ def set_rng_state(seed: int, stream: int) -> None:
 
 def set_verbose(v: int) -> None:
     library().bb_set_verbose(int(v))
+
+
+def set_device_count(k: int) -> None:
+    """Cap the devices a .C sampler call may shard over (0: every visible device)."""
+    library().bb_set_device_count(int(k))
+
+
+def set_trace_budget(nbytes: int) -> None:
+    """Device bytes of the trace ring per engine (<= 0 restores the 1 GiB default)."""
+    library().bb_set_trace_budget(int(nbytes))
+
+
+def debug_interrupt_after(polls: int) -> None:
+    """Test hook: the polls-th interrupt poll from now reports an interrupt (-1 clears)."""
+    library().bb_debug_interrupt_after(int(polls))
+
+
+def last_call_info():
+    """dict(devices, trace_capacity, interrupted) of the last .C sampler call."""
+    d, c, i = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    library().bb_last_call_info(ctypes.byref(d), ctypes.byref(c), ctypes.byref(i))
+    return dict(devices=d.value, trace_capacity=c.value, interrupted=bool(i.value))
 
 
 # ---------------------------------------------------------------------------
@@ -998,15 +1027,18 @@ class Engine:
 
 
 class ShardGroup:
-    """Column shards of one chain as several engines on ONE device, exchanging through
-    on-device sums -- the sharded decomposition without RCCL (single-GPU testing)."""
+    """Column shards of one chain driven by one host thread.  rccl=False: engines on ONE
+    device exchanging through on-device sums (the sharded decomposition on a single GPU);
+    rccl=True: engines on distinct devices exchanging with RCCL (ncclCommInitAll) -- the
+    single-process multi-GPU path of the .C entry points."""
 
-    def __init__(self, engines):
+    def __init__(self, engines, rccl=False):
         L = library()
         self.engines = list(engines)
         arr = (ctypes.c_void_p * len(self.engines))(*[e._h.value for e in self.engines])
         h = ctypes.c_void_p()
-        _check(L.bb_group_create(arr, len(self.engines), ctypes.byref(h)), "bb_group_create")
+        fn = L.bb_group_create_rccl if rccl else L.bb_group_create
+        _check(fn(arr, len(self.engines), ctypes.byref(h)), "bb_group_create")
         self._h = h
 
     def init_state(self):
@@ -1017,8 +1049,7 @@ class ShardGroup:
                                       int(slot_step), int(mcmc_phase)), "bb_group_run")
 
     def sync(self):
-        for e in self.engines:
-            e.sync()
+        _check(library().bb_group_sync(self._h), "bb_group_sync")
 
     def close(self):
         if getattr(self, "_h", None):

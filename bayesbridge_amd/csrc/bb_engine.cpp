@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1243,18 +1244,32 @@ int bb_engine_error_flags(bb_engine *e, uint32_t *flags) {
 }
 
 // ---------------------------------------------------------------------------
-// Shard groups: several column-shard engines driven by one host thread, with the two
-// per-sweep exchanges done as on-device sums (members on one device) -- used to test the
-// sharded decomposition on a single GPU.
+// Shard groups: several column-shard engines driven by ONE host thread, interleaving their
+// phases around the two per-sweep exchanges.  Two exchange modes:
+//   - on-device sums: every member on one device (tests the sharded decomposition on one
+//     GPU -- RCCL cannot place two ranks on one device);
+//   - RCCL: members on distinct devices with communicators from ncclCommInitAll, each
+//     exchange one ncclGroupStart / ncclAllReduce per member / ncclGroupEnd on the members'
+//     streams.  This is the single-process multi-GPU path behind the .C entry points: R
+//     calls .C from one process (BridgeWrapper.R:220-228), SURVEY.md 5 "distributed comm
+//     backend".
 // ---------------------------------------------------------------------------
 struct bb_group {
     std::vector<bb_engine *> members;
+    bool rccl = false;
+    std::vector<ncclComm_t> comms;
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
     std::vector<hipEvent_t> mev;
     double *tmp = nullptr;
     size_t tmp_count = 0;
     ~bb_group() {
+        for (auto *m : members) {
+            (void)hipSetDevice(m->cfg.device);
+            (void)hipStreamSynchronize(m->stream);
+        }
+        for (auto c : comms) ncclCommDestroy(c);
+        if (!members.empty()) (void)hipSetDevice(members[0]->cfg.device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (tmp) (void)hipFree(tmp);
         if (ev) (void)hipEventDestroy(ev);
@@ -1263,6 +1278,15 @@ struct bb_group {
     }
     // sum buf(member) over members, result written back to every member's buf
     void reduce(double *bb_engine::*buf, size_t count) {
+        if (rccl) {
+            NCCLCHECK(ncclGroupStart());
+            for (size_t i = 0; i < members.size(); ++i)
+                NCCLCHECK(ncclAllReduce(members[i]->*buf, members[i]->*buf, count, ncclFloat64,
+                                        ncclSum, comms[i], members[i]->stream));
+            NCCLCHECK(ncclGroupEnd());
+            return;
+        }
+        HIPCHECK(hipSetDevice(members[0]->cfg.device));
         for (size_t i = 0; i < members.size(); ++i) {
             HIPCHECK(hipEventRecord(mev[i], members[i]->stream));
             HIPCHECK(hipStreamWaitEvent(stream, mev[i], 0));
@@ -1277,29 +1301,25 @@ struct bb_group {
         HIPCHECK(hipEventRecord(ev, stream));
         for (auto *m : members) HIPCHECK(hipStreamWaitEvent(m->stream, ev, 0));
     }
+    void on(bb_engine *m) { HIPCHECK(hipSetDevice(m->cfg.device)); }
 };
 
-extern "C" {
+namespace {
 
-int bb_group_create(bb_engine **engines, int count, bb_group **out) {
-    *out = nullptr;
+bb_group *group_create(bb_engine **engines, int count, bool rccl) {
     bb_group *g = new bb_group();
     try {
         if (count < 1) throw HipError("empty group");
         for (int i = 0; i < count; ++i) {
             if (engines[i]->cfg.world != count || engines[i]->cfg.rank != i)
                 throw HipError("group member rank/world mismatch");
-            if (engines[i]->cfg.device != engines[0]->cfg.device)
-                throw HipError("group members must share one device (use RCCL across devices)");
+            for (int k = 0; k < i; ++k)
+                if ((engines[k]->cfg.device == engines[i]->cfg.device) == rccl)
+                    throw HipError(rccl ? "an RCCL group needs its members on distinct devices"
+                                        : "an on-device group needs its members on one device "
+                                          "(use an RCCL group across devices)");
+            if (engines[i]->comm) throw HipError("group members must not own a communicator");
             g->members.push_back(engines[i]);
-        }
-        HIPCHECK(hipSetDevice(engines[0]->cfg.device));
-        HIPCHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
-        HIPCHECK(hipEventCreateWithFlags(&g->ev, hipEventDisableTiming));
-        for (int i = 0; i < count; ++i) {
-            hipEvent_t e;
-            HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            g->mev.push_back(e);
         }
         size_t c = 0;
         for (auto *m : g->members) {
@@ -1307,14 +1327,43 @@ int bb_group_create(bb_engine **engines, int count, bb_group **out) {
             if (m->woodbury()) c = std::max(c, m->red2_count());
         }
         g->tmp_count = c;
-        HIPCHECK(hipMalloc(&g->tmp, c * sizeof(double)));
+        if (rccl) {
+            g->rccl = true;
+            std::vector<int> devs(count);
+            for (int i = 0; i < count; ++i) devs[i] = engines[i]->cfg.device;
+            g->comms.assign(count, nullptr);
+            NCCLCHECK(ncclCommInitAll(g->comms.data(), count, devs.data()));
+        } else {
+            HIPCHECK(hipSetDevice(engines[0]->cfg.device));
+            HIPCHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+            HIPCHECK(hipEventCreateWithFlags(&g->ev, hipEventDisableTiming));
+            for (int i = 0; i < count; ++i) {
+                hipEvent_t e;
+                HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                g->mev.push_back(e);
+            }
+            HIPCHECK(hipMalloc(&g->tmp, c * sizeof(double)));
+        }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         delete g;
-        return -1;
+        return nullptr;
     }
-    *out = g;
-    return 0;
+    return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bb_group_create(bb_engine **engines, int count, bb_group **out) {
+    *out = group_create(engines, count, false);
+    return *out ? 0 : -1;
+}
+
+int bb_group_create_rccl(bb_engine **engines, int count, bb_group **out) {
+    *out = group_create(engines, count, true);
+    return *out ? 0 : -1;
 }
 
 void bb_group_destroy(bb_group *g) { delete g; }
@@ -1322,18 +1371,39 @@ void bb_group_destroy(bb_group *g) { delete g; }
 int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
                  int mcmc_phase) {
     try {
-        HIPCHECK(hipSetDevice(g->members[0]->cfg.device));
         for (int k = 0; k < count; ++k) {
             const uint64_t t = t0 + (uint64_t)k;
             const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
-            for (auto *m : g->members) m->phase_a(t);
+            for (auto *m : g->members) {
+                g->on(m);
+                m->phase_a(t);
+            }
             g->reduce(&bb_engine::red1, g->members[0]->red1_count());
-            for (auto *m : g->members) m->phase_b(t, slot);
+            for (auto *m : g->members) {
+                g->on(m);
+                m->phase_b(t, slot);
+            }
             if (g->members[0]->woodbury())
                 g->reduce(&bb_engine::red2, g->members[0]->red2_count());
-            for (auto *m : g->members) m->phase_c(t, slot, mcmc_phase);
+            for (auto *m : g->members) {
+                g->on(m);
+                m->phase_c(t, slot, mcmc_phase);
+            }
         }
         HIPCHECK(hipGetLastError());
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_group_sync(bb_group *g) {
+    try {
+        for (auto *m : g->members) {
+            g->on(m);
+            HIPCHECK(hipStreamSynchronize(m->stream));
+        }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;
@@ -1346,20 +1416,28 @@ int bb_group_init_state(bb_group *g) {
     try {
         for (auto *m : g->members) {
             if (m->G != nullptr) throw HipError("group init supports the p > n path only");
+            g->on(m);
             engine_init_state_local(m);
         }
         bool draw_tau = g->members[0]->method != 3 && !g->members[0]->hy.know_tau;
         if (draw_tau) {
-            for (auto *m : g->members)
+            for (auto *m : g->members) {
+                g->on(m);
                 launch_pre(m->stream, m->xb_part, m->nparts, m->n_pad, m->beta, m->p_loc, m->sc,
                            m->red1, m->nbS);
+            }
             g->reduce(&bb_engine::red1, g->members[0]->red1_count());
-            for (auto *m : g->members)
+            for (auto *m : g->members) {
+                g->on(m);
                 launch_scalars(m->stream, m->red1, m->nbS, m->y, m->n, m->p, m->sc, m->hy,
                                m->cfg.seed, m->cfg.stream, 0, m->tr_tau, m->tr_sig2,
                                m->tr_alpha, 1, m->err);
+            }
         }
-        for (auto *m : g->members) HIPCHECK(hipStreamSynchronize(m->stream));
+        for (auto *m : g->members) {
+            g->on(m);
+            HIPCHECK(hipStreamSynchronize(m->stream));
+        }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;
@@ -2145,6 +2223,54 @@ void bridge_EM(double *betap, const double *yp, const double *Xp, const double *
 
 namespace {
 
+// ---------------------------------------------------------------------------
+// .C drivers: device selection, trace ring with chunked copy-out, interrupt polling.
+// ---------------------------------------------------------------------------
+int g_max_devices = 0;                      // bb_set_device_count (0: every visible device)
+size_t g_trace_budget = size_t(1) << 30;   // device bytes of trace ring per engine
+std::atomic<int> g_debug_interrupt{-1};     // bb_debug_interrupt_after (test hook)
+int g_last_devices = 0, g_last_interrupted = 0, g_last_capacity = 0;
+
+// R's interrupt machinery, resolved at run time (absent outside R).  The reference polls
+// R_CheckUserInterrupt every 10 sweeps (BridgeWrapper.cpp:273-275, 295-297), which longjmps
+// out of the sampler; here the check runs under R_ToplevelExec, so a pending interrupt is
+// caught without unwinding through frames that own device memory or communicators, the
+// chain stops, the device is released, and the interrupt is re-raised from the .C frame.
+struct RInterrupt {
+    int (*toplevel)(void (*)(void *), void *) = nullptr;  // R_ToplevelExec (Rboolean)
+    void (*check)(void) = nullptr;                        // R_CheckUserInterrupt
+    void (*onintr)(void) = nullptr;                       // Rf_onintr
+    bool tried = false;
+    bool ok() {
+        if (!tried) {
+            tried = true;
+            toplevel = (int (*)(void (*)(void *), void *))dlsym(RTLD_DEFAULT, "R_ToplevelExec");
+            check = (void (*)(void))dlsym(RTLD_DEFAULT, "R_CheckUserInterrupt");
+            onintr = (void (*)(void))dlsym(RTLD_DEFAULT, "Rf_onintr");
+        }
+        return toplevel && check;
+    }
+} g_rint;
+
+void r_check_cb(void *) { g_rint.check(); }
+
+bool poll_interrupt() {
+    int d = g_debug_interrupt.load();
+    while (d >= 0) {  // test hook: the d-th poll from now reports an interrupt
+        if (g_debug_interrupt.compare_exchange_weak(d, d == 0 ? -1 : d - 1)) {
+            if (d == 0) return true;
+            break;
+        }
+    }
+    if (g_rint.ok()) return g_rint.toplevel(r_check_cb, nullptr) == 0;
+    return false;
+}
+
+// From a .C frame with no live C++ objects: hand the caught interrupt back to R.
+void reraise_interrupt() {
+    if (g_rint.ok() && g_rint.onintr) g_rint.onintr();
+}
+
 // bb_config of a .C bridge_reg_stable call (BridgeWrapper.cpp:659-693)
 bb_config stable_call_config(const double *sig2_shape, const double *sig2_scale,
                              const double *nu_shape, const double *nu_rate, const double *alpha_a,
@@ -2172,65 +2298,263 @@ bb_config stable_call_config(const double *sig2_shape, const double *sig2_scale,
     return c;
 }
 
-// The stable driver around an engine (BridgeWrapper.cpp:207-313 / :434-537): banner, state
-// initialisation, B + 1 burn-in sweeps in slot 0, M - 1 MCMC sweeps into slots 1.., copy-out.
-// `create` builds the engine (dense or CSC design); errors print and return partial traces.
+// Trace ring slots for M samples of p_local coefficients (`ntr` p-long traces per slot):
+// the whole run if it fits the per-engine budget, else a ring copied out in chunks.
+int ring_capacity(int m, int p_local, int ntr) {
+    const size_t per = (size_t)ntr * p_local * sizeof(double) + 3 * sizeof(double);
+    size_t cap = g_trace_budget / (per ? per : 1);
+    if (cap < 16) cap = 16;
+    return (int)std::min<size_t>(cap, (size_t)(m < 1 ? 1 : m));
+}
+
+// Devices for a column-sharded chain: 1 unless p > n on the Woodbury path with alpha known
+// and more than one device visible; at least 4096 columns per device.
+int chain_devices(const bb_config &c) {
+    const int nvis = bb_device_count();
+    int k = g_max_devices > 0 ? std::min(g_max_devices, nvis) : nvis;
+    if (c.p <= c.n || c.ortho || c.true_alpha <= 0 || (c.method != 0 && c.method != 2)) return 1;
+    k = std::min(k, std::max(1, c.p / 4096));
+    return std::max(1, k);
+}
+
+// One chain: a single engine, or the column shards of a multi-device RCCL group.
+struct Chain {
+    std::vector<bb_engine *> eng;
+    std::vector<int> j0s;
+    bb_group *grp = nullptr;
+    int p = 0, cap = 1;
+    hipEvent_t evring[3] = {nullptr, nullptr, nullptr};
+    long nmarks = 0;
+
+    ~Chain() {
+        for (auto e : evring)
+            if (e) (void)hipEventDestroy(e);
+        if (grp) bb_group_destroy(grp);
+        for (auto *e : eng) bb_engine_destroy(e);
+    }
+    int init() { return grp ? bb_group_init_state(grp) : bb_engine_init_state(eng[0]); }
+    int run(uint64_t t0, int count, int slot, int step, int mcmc) {
+        return grp ? bb_group_run(grp, t0, count, slot, step, mcmc)
+                   : bb_engine_run(eng[0], t0, count, slot, step, mcmc);
+    }
+    int sync() { return grp ? bb_group_sync(grp) : bb_engine_sync(eng[0]); }
+    uint32_t flags() {
+        uint32_t all = 0;
+        for (auto *e : eng) {
+            uint32_t f = 0;
+            (void)hipSetDevice(e->cfg.device);
+            if (bb_engine_error_flags(e, &f) == 0) all |= f;
+        }
+        return all;
+    }
+    // Marks the work enqueued so far (member 0's stream: members advance in lockstep through
+    // the exchanges) and waits until at most two marked blocks are ahead of the device.
+    void throttle() {
+        HIPCHECK(hipSetDevice(eng[0]->cfg.device));
+        hipEvent_t &e = evring[nmarks % 3];
+        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(e, eng[0]->stream));
+        if (nmarks >= 2) HIPCHECK(hipEventSynchronize(evring[(nmarks - 2) % 3]));
+        ++nmarks;
+    }
+    // trace slots [slot0, slot0 + count) -> samples [s0, s0 + count) of the P x M outputs
+    int copy_out(int slot0, int count, int s0, double *beta, double *lam, double *sig2,
+                 double *tau, double *alpha, double *u = nullptr, double *shape = nullptr) {
+        if (count <= 0) return 0;
+        const size_t P = (size_t)p;
+        if (eng.size() == 1) {
+            int rc = bb_engine_get_trace(eng[0], slot0, count, beta + s0 * P, lam + s0 * P,
+                                         sig2 ? sig2 + s0 : nullptr, tau + s0, alpha + s0);
+            if (rc == 0 && (u || shape))
+                rc = bb_engine_get_tri_trace(eng[0], slot0, count, u ? u + s0 * P : nullptr,
+                                             shape ? shape + s0 * P : nullptr);
+            return rc;
+        }
+        for (size_t r = 0; r < eng.size(); ++r) {
+            bb_engine *e = eng[r];
+            const size_t pl = (size_t)e->p_loc;
+            std::vector<double> b(pl * count), l(pl * count);
+            (void)hipSetDevice(e->cfg.device);
+            if (bb_engine_get_trace(e, slot0, count, b.data(), l.data(),
+                                    r == 0 && sig2 ? sig2 + s0 : nullptr,
+                                    r == 0 ? tau + s0 : nullptr, r == 0 ? alpha + s0 : nullptr))
+                return -1;
+            for (int k = 0; k < count; ++k) {
+                memcpy(beta + (s0 + k) * P + j0s[r], &b[k * pl], pl * sizeof(double));
+                memcpy(lam + (s0 + k) * P + j0s[r], &l[k * pl], pl * sizeof(double));
+            }
+        }
+        return 0;
+    }
+};
+
+// Builds the chain: `create(cfg, j0, j1, &engine)` makes the engine of columns [j0, j1).
 template <class Create>
-void run_stable_chain(const bb_config &c, Create create, int b, double *betap, double *lambdap,
-                      double *sig2p, double *taup, double *alphap, double *runtime,
-                      const char *title = "Bridge Regression (mix. of normals):") {
-    const int m = c.trace_capacity;
-    const bool know_sig2 = c.true_sig2 > 0, know_tau = c.true_tau > 0, know_alpha = c.true_alpha > 0;
-    if (g_verbose) {  // BridgeWrapper.cpp:235-240
-        printf("%s", title);
-        if (know_alpha) printf(" known alpha=%g", c.true_alpha);
-        if (know_sig2) printf(", sig2=%g", c.true_sig2);
-        if (know_tau) printf(", tau=%g", c.true_tau);
-        if (c.ortho) printf("\nAssuming orthogonal design matrix!");
-        printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
+int chain_build(Chain &ch, bb_config c, int ntr, Create create) {
+    const int ndev = chain_devices(c);
+    const int nvis = std::max(1, bb_device_count());
+    ch.p = c.p;
+    if (ndev <= 1) {
+        c.trace_capacity = ring_capacity(c.trace_capacity, c.p, ntr);
+        ch.cap = c.trace_capacity;
+        bb_engine *e = nullptr;
+        if (create(&c, 0, c.p, &e) != 0) return -1;
+        ch.eng.push_back(e);
+        ch.j0s.push_back(0);
+        return 0;
     }
-    bb_engine *e = nullptr;
-    if (create(&c, &e) != 0) {
-        printf("Error: %s\n", g_last_error.c_str());
-        printf("Aborting Gibbs sampler.\n");
-        *runtime = 0.0;
-        return;
+    const int per = (c.p + ndev - 1) / ndev;
+    const int cap = ring_capacity(c.trace_capacity, per, ntr);
+    ch.cap = cap;
+    for (int r = 0; r < ndev; ++r) {
+        bb_config cr = c;
+        const int j0 = r * per, j1 = std::min(c.p, j0 + per);
+        cr.p_local = j1 - j0;
+        cr.j0 = j0;
+        cr.rank = r;
+        cr.world = ndev;
+        cr.device = (g_device + r) % nvis;
+        cr.trace_capacity = cap;
+        bb_engine *e = nullptr;
+        if (create(&cr, j0, j1, &e) != 0) return -1;
+        ch.eng.push_back(e);
+        ch.j0s.push_back(j0);
     }
-    double rt = 0.0;
-    bool ok = bb_engine_init_state(e) == 0;
-    if (ok) {
+    ch.grp = group_create(ch.eng.data(), ndev, true);
+    return ch.grp ? 0 : -1;
+}
+
+enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_INTERRUPTED = 2 };
+
+// Burn-in then the MCMC samples, in blocks of 10 sweeps between interrupt polls (at most two
+// blocks queued ahead of the device), the trace ring copied out whenever it is full.
+// Sample s >= 1 runs at t = t_base + s; burn-in is `nburn` sweeps in slot 0 from t = 1.
+Outcome drive_chain(Chain &ch, int nburn, uint64_t t_base, int m, int b, double *betap,
+                    double *lambdap, double *sig2p, double *taup, double *alphap,
+                    double *runtime, double *up = nullptr, double *shapep = nullptr) {
+    constexpr int kBlock = 10;  // BridgeWrapper.cpp:273-275, 295-297: every 10 sweeps
+    *runtime = 0.0;
+    if (ch.init() != 0) return OUT_ERROR;
+    bool interrupted = false;
+    try {
         auto t0 = std::chrono::steady_clock::now();
-        ok = bb_engine_run(e, 1, b + 1, 0, 0, 0) == 0 && bb_engine_sync(e) == 0;
+        for (int k = 0; k < nburn && !interrupted; k += kBlock) {
+            if (ch.run(1 + (uint64_t)k, std::min(kBlock, nburn - k), 0, 0, 0) != 0)
+                return OUT_ERROR;
+            ch.throttle();
+            interrupted = poll_interrupt();
+        }
+        if (ch.sync() != 0) return OUT_ERROR;
         auto t1 = std::chrono::steady_clock::now();
-        if (g_verbose && ok) {
-            double bt = std::chrono::duration<double>(t1 - t0).count();
+        if (g_verbose && !interrupted) {
+            const double bt = std::chrono::duration<double>(t1 - t0).count();
             printf("Burn-in complete: %g sec. for %i iterations.\n", bt, b);
             if (b > 0) printf("Expect approx. %g sec. for %i samples.\n", bt * m / b, m);
         }
-        auto t2 = std::chrono::steady_clock::now();
-        if (ok && m > 1) ok = bb_engine_run(e, (uint64_t)b + 2, m - 1, 1, 1, 1) == 0;
-        ok = (bb_engine_sync(e) == 0) && ok;
-        auto t3 = std::chrono::steady_clock::now();
-        rt = std::chrono::duration<double>(t3 - t2).count();
-        uint32_t f = 0;
-        if (ok && bb_engine_error_flags(e, &f) == 0 && (f & ~4u)) {
+        int copied = 0, next = 1;  // samples copied out / next sample to compute
+        while (copied < m && !interrupted) {
+            const int hi = std::min(m, copied + ch.cap);
+            for (int s = next; s < hi && !interrupted; s += kBlock) {
+                const int cnt = std::min(kBlock, hi - s);
+                if (ch.run(t_base + (uint64_t)s, cnt, s % ch.cap, 1, 1) != 0) return OUT_ERROR;
+                ch.throttle();
+                interrupted = poll_interrupt();
+                next = s + cnt;
+            }
+            if (ch.sync() != 0) return OUT_ERROR;
+            if (ch.copy_out(copied % ch.cap, next - copied, copied, betap, lambdap, sig2p, taup,
+                            alphap, up, shapep) != 0)
+                return OUT_ERROR;
+            copied = next;
+        }
+        if (interrupted && copied == 0 && ch.sync() == 0)
+            (void)ch.copy_out(0, 1, 0, betap, lambdap, sig2p, taup, alphap, up, shapep);
+        *runtime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+        if (interrupted) {
+            printf("Interrupted: %i of %i samples returned.\n", std::max(copied, 1), m);
+            return OUT_INTERRUPTED;
+        }
+        const uint32_t f = ch.flags();
+        if (f & ~4u) {
             printf("Error: numerical failure in the device sampler (flags %u)\n", f);
             printf("Aborting Gibbs sampler.\n");
         }
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return OUT_ERROR;
     }
-    if (!ok) {
-        printf("Error: %s\n", g_last_error.c_str());
-        printf("Aborting Gibbs sampler.\n");
+    return OUT_OK;
+}
+
+void print_banner(const char *title, const bb_config &c, int b, int m) {
+    if (!g_verbose) return;  // BridgeWrapper.cpp:235-240 (stable), :112-117 (triangles)
+    printf("%s", title);
+    if (c.true_alpha > 0) printf(" known alpha=%g", c.true_alpha);
+    if (c.true_sig2 > 0 && c.method != 6) printf(", sig2=%g", c.true_sig2);
+    if (c.true_tau > 0) printf(", tau=%g", c.true_tau);
+    if (c.ortho) printf("\nAssuming orthogonal design matrix!");
+    printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
+}
+
+// The stable-family .C driver (BridgeWrapper.cpp:207-313 / :434-537): B + 1 burn-in sweeps
+// in slot 0, MCMC sample i at t = B + 1 + i.  Errors print and return partial traces.
+template <class Create>
+Outcome stable_call(const bb_config &c, Create create, int b, double *betap, double *lambdap,
+                    double *sig2p, double *taup, double *alphap, double *runtime,
+                    const char *title) {
+    const int m = c.trace_capacity;
+    print_banner(title, c, b, m);
+    g_last_interrupted = 0;
+    Outcome o;
+    {
+        Chain ch;
+        if (chain_build(ch, c, 2, create) != 0) {
+            printf("Error: %s\n", g_last_error.c_str());
+            printf("Aborting Gibbs sampler.\n");
+            *runtime = 0.0;
+            return OUT_ERROR;
+        }
+        g_last_devices = (int)ch.eng.size();
+        g_last_capacity = ch.cap;
+        o = drive_chain(ch, b + 1, (uint64_t)b + 1, m, b, betap, lambdap, sig2p, taup, alphap,
+                        runtime);
+        if (o == OUT_ERROR) {
+            printf("Error: %s\n", g_last_error.c_str());
+            printf("Aborting Gibbs sampler.\n");
+        }
     }
-    bb_engine_get_trace(e, 0, m, betap, lambdap, sig2p, taup, alphap);
-    if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
-    *runtime = rt;
-    bb_engine_destroy(e);
+    if (g_verbose && o == OUT_OK) printf("Sampling complete: %g sec. for %i iterations.\n", *runtime, m);
+    g_last_interrupted = o == OUT_INTERRUPTED;
+    return o;
+}
+
+Outcome stable_dense(const bb_config &c, const double *yp, const double *Xp, int b,
+                     double *betap, double *lambdap, double *sig2p, double *taup, double *alphap,
+                     double *runtime, const char *title) {
+    const int n = c.n;
+    return stable_call(
+        c,
+        [&](const bb_config *cc, int j0, int, bb_engine **e) {
+            return bb_engine_create(cc, Xp + (size_t)j0 * n, yp, e);
+        },
+        b, betap, lambdap, sig2p, taup, alphap, runtime, title);
 }
 
 }  // namespace
 
 extern "C" {
+
+void bb_set_device_count(int count) { g_max_devices = count < 0 ? 0 : count; }
+void bb_set_trace_budget(long long bytes) {
+    g_trace_budget = bytes > 0 ? (size_t)bytes : (size_t(1) << 30);
+}
+void bb_debug_interrupt_after(int polls) { g_debug_interrupt = polls; }
+int bb_last_call_info(int *devices, int *trace_capacity, int *interrupted) {
+    if (devices) *devices = g_last_devices;
+    if (trace_capacity) *trace_capacity = g_last_capacity;
+    if (interrupted) *interrupted = g_last_interrupted;
+    return 0;
+}
 
 void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *taup,
                        double *alphap, const double *yp, const double *Xp,
@@ -2242,10 +2566,92 @@ void bridge_reg_stable(double *betap, double *lambdap, double *sig2p, double *ta
     const bb_config c = stable_call_config(sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
                                            alpha_b, true_sig2, true_tau, true_alpha, *P, *N, *M,
                                            ortho);
-    run_stable_chain(
-        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xp, yp, e); },
-        *burn, betap, lambdap, sig2p, taup, alphap, runtime);
+    if (stable_dense(c, yp, Xp, *burn, betap, lambdap, sig2p, taup, alphap, runtime,
+                     "Bridge Regression (mix. of normals):") == OUT_INTERRUPTED)
+        reraise_interrupt();
 }
+
+}  // extern "C"
+
+namespace {
+
+Outcome stable_csc(const bb_config &c, const double *yp, const int *Xcolptr, const int *Xrowidx,
+                   const double *Xval, int b, double *betap, double *lambdap, double *sig2p,
+                   double *taup, double *alphap, double *runtime) {
+    const int p = c.p, n = c.n;
+    const char *title = "Bridge Regression (mix. of normals):";
+    if (p > n && !c.ortho) {
+        return stable_call(
+            c,
+            [&](const bb_config *cc, int j0, int j1, bb_engine **e) {
+                // the shard's columns: colptr rebased to its first entry
+                std::vector<int> cp(j1 - j0 + 1);
+                for (int j = j0; j <= j1; ++j) cp[j - j0] = Xcolptr[j] - Xcolptr[j0];
+                return bb_engine_create_csc(cc, cp.data(), Xrowidx + Xcolptr[j0],
+                                            Xval + Xcolptr[j0], yp, e);
+            },
+            b, betap, lambdap, sig2p, taup, alphap, runtime, title);
+    }
+    // p <= n or the orthogonal design: the dense paths of bridge_reg_stable (least-squares
+    // start, p x p Cholesky or ortho draw) on the densified X
+    std::vector<double> Xd((size_t)n * p, 0.0);
+    for (int j = 0; j < p; ++j)
+        for (int q = Xcolptr[j]; q < Xcolptr[j + 1]; ++q)
+            if (Xrowidx[q] >= 0 && Xrowidx[q] < n) Xd[(size_t)j * n + Xrowidx[q]] = Xval[q];
+    return stable_dense(c, yp, Xd.data(), b, betap, lambdap, sig2p, taup, alphap, runtime, title);
+}
+
+Outcome logit_call(bb_config c, const double *yp, const double *Xp, int b, double *betap,
+                   double *lambdap, double *taup, double *alphap, double *runtime) {
+    c.method = 6;
+    for (int i = 0; i < c.n; ++i)
+        if (!(yp[i] == 0.0 || yp[i] == 1.0)) {
+            printf("Error: logistic bridge needs y in {0, 1} (y[%d] = %g)\n", i, yp[i]);
+            printf("Aborting Gibbs sampler.\n");
+            *runtime = 0.0;
+            return OUT_ERROR;
+        }
+    std::vector<double> sig2(c.trace_capacity);
+    return stable_dense(c, yp, Xp, b, betap, lambdap, sig2.data(), taup, alphap, runtime,
+                        "Bridge Regression (logistic, Polya-Gamma mix. of normals):");
+}
+
+// The triangle-mixture driver (BridgeWrapper.cpp:80-204 / :320-432): `burn` sweeps in slot
+// 0, MCMC sample i at t = burn + i.
+Outcome tri_call(const bb_config &c, const double *yp, const double *Xp, int b, double *betap,
+                 double *up, double *omegap, double *shapep, double *sig2p, double *taup,
+                 double *alphap, double *runtime) {
+    const int m = c.trace_capacity;
+    print_banner("Bridge Regression (mix. of triangles):", c, b, m);
+    g_last_interrupted = 0;
+    Outcome o;
+    {
+        Chain ch;
+        if (chain_build(ch, c, 4, [&](const bb_config *cc, int, int, bb_engine **e) {
+                return bb_engine_create(cc, Xp, yp, e);
+            }) != 0) {
+            printf("Error: %s\n", g_last_error.c_str());
+            printf("Aborting Gibbs sampler.\n");
+            *runtime = 0.0;
+            return OUT_ERROR;
+        }
+        g_last_devices = 1;
+        g_last_capacity = ch.cap;
+        o = drive_chain(ch, b, (uint64_t)b, m, b, betap, omegap, sig2p, taup, alphap, runtime, up,
+                        shapep);
+        if (o == OUT_ERROR) {
+            printf("Error: %s\n", g_last_error.c_str());
+            printf("Aborting Gibbs sampler.\n");
+        }
+    }
+    if (g_verbose && o == OUT_OK) printf("Sampling complete: %g sec. for %i iterations.\n", *runtime, m);
+    g_last_interrupted = o == OUT_INTERRUPTED;
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
 
 void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double *taup,
                            double *alphap, const double *yp, const int *Xcolptr,
@@ -2255,28 +2661,12 @@ void bridge_reg_stable_csc(double *betap, double *lambdap, double *sig2p, double
                            const double *true_sig2, const double *true_tau,
                            const double *true_alpha, const int *P, const int *N, const int *M,
                            const int *burn, double *runtime, const int *ortho) {
-    const int p = *P, n = *N;
     const bb_config c = stable_call_config(sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a,
-                                           alpha_b, true_sig2, true_tau, true_alpha, p, n, *M,
+                                           alpha_b, true_sig2, true_tau, true_alpha, *P, *N, *M,
                                            ortho);
-    if (p > n && !c.ortho) {
-        run_stable_chain(
-            c,
-            [&](const bb_config *cc, bb_engine **e) {
-                return bb_engine_create_csc(cc, Xcolptr, Xrowidx, Xval, yp, e);
-            },
-            *burn, betap, lambdap, sig2p, taup, alphap, runtime);
-        return;
-    }
-    // p <= n or the orthogonal design: the dense paths of bridge_reg_stable (least-squares
-    // start, p x p Cholesky or ortho draw) on the densified X
-    std::vector<double> Xd((size_t)n * p, 0.0);
-    for (int j = 0; j < p; ++j)
-        for (int q = Xcolptr[j]; q < Xcolptr[j + 1]; ++q)
-            if (Xrowidx[q] >= 0 && Xrowidx[q] < n) Xd[(size_t)j * n + Xrowidx[q]] = Xval[q];
-    run_stable_chain(
-        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xd.data(), yp, e); },
-        *burn, betap, lambdap, sig2p, taup, alphap, runtime);
+    if (stable_csc(c, yp, Xcolptr, Xrowidx, Xval, *burn, betap, lambdap, sig2p, taup, alphap,
+                   runtime) == OUT_INTERRUPTED)
+        reraise_interrupt();
 }
 
 void bridge_reg_logit(double *betap, double *lambdap, double *taup, double *alphap,
@@ -2286,21 +2676,10 @@ void bridge_reg_logit(double *betap, double *lambdap, double *taup, double *alph
                       const int *N, const int *M, const int *burn, double *runtime) {
     const double zero = 0.0, one = 1.0;
     const int no = 0;
-    bb_config c = stable_call_config(&zero, &zero, nu_shape, nu_rate, alpha_a, alpha_b, &one,
-                                     true_tau, true_alpha, *P, *N, *M, &no);
-    c.method = 6;
-    for (int i = 0; i < *N; ++i)
-        if (!(yp[i] == 0.0 || yp[i] == 1.0)) {
-            printf("Error: logistic bridge needs y in {0, 1} (y[%d] = %g)\n", i, yp[i]);
-            printf("Aborting Gibbs sampler.\n");
-            *runtime = 0.0;
-            return;
-        }
-    std::vector<double> sig2(c.trace_capacity);
-    run_stable_chain(
-        c, [&](const bb_config *cc, bb_engine **e) { return bb_engine_create(cc, Xp, yp, e); },
-        *burn, betap, lambdap, sig2.data(), taup, alphap, runtime,
-        "Bridge Regression (logistic, Polya-Gamma mix. of normals):");
+    const bb_config c = stable_call_config(&zero, &zero, nu_shape, nu_rate, alpha_a, alpha_b,
+                                           &one, true_tau, true_alpha, *P, *N, *M, &no);
+    if (logit_call(c, yp, Xp, *burn, betap, lambdap, taup, alphap, runtime) == OUT_INTERRUPTED)
+        reraise_interrupt();
 }
 
 void bridge_regression(double *betap, double *up, double *omegap, double *shapep,
@@ -2311,68 +2690,16 @@ void bridge_regression(double *betap, double *up, double *omegap, double *shapep
                        const double *true_alpha, const int *P, const int *N, const int *M,
                        const int *burn, double *runtime, const int *ortho,
                        const int *betaburn, const int *use_hmc) {
-    const int p = *P, n = *N, m = *M, b = *burn;
-    *runtime = 0.0;
     (void)use_hmc;  // BridgeRegression.cpp:418 forces use_hmc = false
-    bb_config c;
-    bb_config_default(&c);
-    c.n = n;
-    c.p = p;
-    c.p_local = p;
-    c.sig2_shape = *sig2_shape;
-    c.sig2_scale = *sig2_scale;
-    c.nu_shape = *nu_shape;
-    c.nu_rate = *nu_rate;
-    c.alpha_a = *alpha_a;
-    c.alpha_b = *alpha_b;
-    c.true_sig2 = *true_sig2;
-    c.true_tau = *true_tau;
-    c.true_alpha = *true_alpha;
+    const int no = 0;
+    bb_config c = stable_call_config(sig2_shape, sig2_scale, nu_shape, nu_rate, alpha_a, alpha_b,
+                                     true_sig2, true_tau, true_alpha, *P, *N, *M, &no);
     c.method = 4;
-    c.ortho = *ortho != 0;  // bridge_regression_ortho, BridgeWrapper.cpp:320-432
+    c.ortho = *ortho != 0;                       // bridge_regression_ortho, :320-432
     c.betaburn = *betaburn > 0 ? *betaburn : 0;  // BridgeRegression.cpp:407
-    c.trace_capacity = m < 1 ? 1 : m;
-    c.device = g_device;
-    next_call_key(&c.seed, &c.stream);
-    if (g_verbose) {  // BridgeWrapper.cpp:112-117
-        printf("Bridge Regression (mix. of triangles):");
-        if (c.true_alpha > 0) printf(" known alpha=%g", c.true_alpha);
-        if (c.true_sig2 > 0) printf(", sig2=%g", c.true_sig2);
-        if (c.true_tau > 0) printf(", tau=%g", c.true_tau);
-        if (c.ortho) printf("\nAssuming orthogonal design matrix!");
-        printf("\nBurn-in: %i, Num. Samples: %i\n", b, m);
-    }
-    bb_engine *e = nullptr;
-    if (bb_engine_create(&c, Xp, yp, &e) != 0) {
-        printf("Error: %s\n", g_last_error.c_str());
-        printf("Aborting Gibbs sampler.\n");
-        return;
-    }
-    double rt = 0.0;
-    bool ok = bb_engine_init_state(e) == 0;
-    if (ok) {
-        // burn-in: `burn` sweeps in slot 0 (:141), MCMC slots 1..M-1 (:160)
-        ok = bb_engine_run(e, 1, b, 0, 0, 0) == 0 && bb_engine_sync(e) == 0;
-        auto t2 = std::chrono::steady_clock::now();
-        if (ok && m > 1) ok = bb_engine_run(e, (uint64_t)b + 1, m - 1, 1, 1, 1) == 0;
-        ok = (bb_engine_sync(e) == 0) && ok;
-        auto t3 = std::chrono::steady_clock::now();
-        rt = std::chrono::duration<double>(t3 - t2).count();
-        uint32_t f = 0;
-        if (ok && bb_engine_error_flags(e, &f) == 0 && (f & ~4u)) {
-            printf("Error: numerical failure in the device sampler (flags %u)\n", f);
-            printf("Aborting Gibbs sampler.\n");
-        }
-    }
-    if (!ok) {
-        printf("Error: %s\n", g_last_error.c_str());
-        printf("Aborting Gibbs sampler.\n");
-    }
-    bb_engine_get_trace(e, 0, m, betap, omegap, sig2p, taup, alphap);
-    bb_engine_get_tri_trace(e, 0, m, up, shapep);
-    if (g_verbose) printf("Sampling complete: %g sec. for %i iterations.\n", rt, m);
-    *runtime = rt;
-    bb_engine_destroy(e);
+    if (tri_call(c, yp, Xp, *burn, betap, up, omegap, shapep, sig2p, taup, alphap, runtime) ==
+        OUT_INTERRUPTED)
+        reraise_interrupt();
 }
 
 }  // extern "C"

@@ -244,6 +244,9 @@ def main():
     ap.add_argument("--alpha", type=float, default=None)
     ap.add_argument("--cpu-sweeps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-process", action="store_true",
+                    help="drive --gpus N devices from ONE process through an RCCL shard group "
+                         "(ncclCommInitAll) -- the path the .C entry points use under R")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
                     help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
                          "BB_GRAM_MODE, else the library default)")
@@ -256,6 +259,8 @@ def main():
     cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
         (2 if sparse else 20 if logit else 5)
 
+    if args.single_process:
+        return single_process(args, n, p, alpha, kind)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -492,6 +497,65 @@ def main():
     eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+def single_process(args, n, p, alpha, kind):
+    """--single-process: the .C entry points' multi-GPU path -- one host thread, one engine
+    per device holding a column shard, exchanges through an RCCL group (bb_group_create_rccl,
+    ncclCommInitAll).  Same workload, timing protocol and JSON line as the default mode."""
+    import torch
+
+    import bayesbridge_amd as bb
+
+    if kind == "logit":
+        raise SystemExit("the logistic workload runs on one GPU")
+    ndev = args.gpus
+    if ndev > max(1, torch.cuda.device_count()):
+        raise SystemExit(f"--single-process --gpus {ndev}: only {torch.cuda.device_count()} visible")
+    bb.set_verbose(0)
+    per = (p + ndev - 1) // ndev
+    y = make_sparse_problem_y(n, p)[0] if kind == "sparse" else make_problem_y(n, p)[0]
+    t_setup0 = time.perf_counter()
+    engines = []
+    for r in range(ndev):
+        j0, j1 = r * per, min(p, (r + 1) * per)
+        X = make_sparse_columns(n, j0, j1) if kind == "sparse" else make_columns(n, j0, j1)
+        cfg = bb.EngineConfig(n=n, p=p, p_local=j1 - j0, j0=j0, rank=r, world=ndev,
+                              true_alpha=alpha, method=2,
+                              trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
+                              stream=0, device=r)
+        engines.append(bb.Engine(cfg, X, y))
+        del X
+    grp = bb.ShardGroup(engines, rccl=ndev > 1) if ndev > 1 else None
+    (grp or engines[0]).init_state()
+    setup_s = time.perf_counter() - t_setup0
+    runner = grp or engines[0]
+    runner.run(1, args.warmup, first_slot=-1)
+    runner.sync()
+    engines[0].enable_timing(True, phases=False)
+    engines[0].reset_timing()
+    t0 = time.perf_counter()
+    runner.run(1 + args.warmup, args.steps, first_slot=0)
+    runner.sync()
+    elapsed = time.perf_counter() - t0
+    gram_ms, _, _ = engines[0].kernel_times()
+    rec = {
+        "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
+        "value": args.steps / elapsed, "unit": "sweeps/s", "n_gpus": ndev,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md 8(d) design, seed 20240501)",
+        "config": {"workload": f"{args.workload} n={n} p={p} alpha={alpha}", "n": n, "p": p,
+                   "alpha": alpha, "parallelism": f"column-shard x{ndev}, one process, "
+                                                  "RCCL group (ncclCommInitAll)"},
+        "roofline": None, "cpu_baseline": None, "gram_ms_rank0": gram_ms, "setup_s": setup_s,
+    }
+    print(json.dumps(rec), flush=True)
+    if grp:
+        grp.close()
+    for e in engines:
+        e.close()
 
 
 if __name__ == "__main__":

@@ -293,10 +293,33 @@ int bb_engine_get_tri_basis(bb_engine *e, double *tV, double *a, double *d);
 int bb_engine_set_tri_state(bb_engine *e, const double *u);
 
 int bb_group_create(bb_engine **engines, int count, bb_group **out);
+/* The same group over engines on DISTINCT devices, exchanging with RCCL: communicators from
+ * ncclCommInitAll, each exchange an ncclGroupStart / ncclAllReduce per member / ncclGroupEnd
+ * on the members' streams.  This is the single-process multi-GPU path the .C entry points
+ * use (R calls .C from one process). */
+int bb_group_create_rccl(bb_engine **engines, int count, bb_group **out);
 void bb_group_destroy(bb_group *g);
 int bb_group_init_state(bb_group *g);
 int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
                  int mcmc_phase);
+int bb_group_sync(bb_group *g);
+
+/*
+ * .C driver controls.  bridge_reg_stable / bridge_reg_stable_csc shard the columns of a
+ * p > n (Woodbury, alpha known, non-ortho) problem over the visible devices in one process
+ * (>= 4096 columns per device, an RCCL group); bb_set_device_count(k) caps that at k devices
+ * (0: all).  Traces live on the device in a ring of at most `bytes` per engine (default
+ * 1 GiB), copied out to the caller's P x M buffers whenever it fills, so M is not bounded by
+ * HBM.  Every 10 sweeps the driver polls R's interrupt (R_CheckUserInterrupt under
+ * R_ToplevelExec, as BridgeWrapper.cpp:273-275 polls), stops, releases the device, returns
+ * the samples drawn so far and re-raises the interrupt in R.
+ */
+void bb_set_device_count(int count);
+void bb_set_trace_budget(long long bytes);
+/* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
+void bb_debug_interrupt_after(int polls);
+/* Last .C sampler call: devices used, trace ring slots, whether it was interrupted. */
+int bb_last_call_info(int *devices, int *trace_capacity, int *interrupted);
 
 /* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho, 4 triangle,
  * 5 sparse woodbury, 6 logistic. */

@@ -1,0 +1,127 @@
+"""The .C drivers' host machinery on the GPU: the device trace ring with chunked copy-out,
+interrupt polling (simulated through bb_debug_interrupt_after), and the single-process
+RCCL shard group that bridge_reg_stable uses across devices (exercised at one device, the
+only count a one-GPU box can hold: RCCL cannot place two ranks on one device)."""
+import numpy as np
+import pytest
+
+from tests.conftest import synthetic_problem
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xB4E5B41D6E
+
+
+def _same(a, b, keys=("beta", "lambda", "sig2", "tau", "alpha")):
+    for k in keys:
+        assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("n,p", [(100, 20), (60, 700)])
+def test_trace_ring_copy_out_is_exact(gpu_lib, n, p):
+    """A 16-slot ring copied out every 16 samples gives the whole-run traces bit for bit."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(n, p, seed=3)
+    bb.set_seed(SEED)
+    full = bb.bridge_reg_stb(y, X, nsamp=100, burn=15)
+    assert bb.last_call_info()["trace_capacity"] == 100
+    bb.set_trace_budget(1)
+    try:
+        bb.set_seed(SEED)
+        ring = bb.bridge_reg_stb(y, X, nsamp=100, burn=15)
+        assert bb.last_call_info()["trace_capacity"] == 16
+    finally:
+        bb.set_trace_budget(0)
+    _same(full, ring)
+
+
+def test_trace_ring_triangle(gpu_lib):
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(80, 10, seed=4)
+    bb.set_seed(SEED + 1)
+    full = bb.bridge_reg_tri(y, X, nsamp=50, burn=5, extras=True)
+    bb.set_trace_budget(1)
+    try:
+        bb.set_seed(SEED + 1)
+        ring = bb.bridge_reg_tri(y, X, nsamp=50, burn=5, extras=True)
+    finally:
+        bb.set_trace_budget(0)
+    _same(full, ring, ("beta", "u", "w", "shape", "sig2", "tau"))
+
+
+def test_interrupt_returns_partial_traces_and_rerun_is_clean(gpu_lib):
+    """An interrupt at the 4th poll (burn-in is 2 blocks of 10 sweeps, so it lands after
+    20 MCMC sweeps) stops the chain, returns the samples drawn so far -- identical to the
+    same samples of an uninterrupted run -- and leaves the library ready for the next call."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(100, 20, seed=5)
+    bb.set_seed(SEED + 2)
+    full = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    bb.set_seed(SEED + 2)
+    bb.debug_interrupt_after(3)
+    part = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    info = bb.last_call_info()
+    assert info["interrupted"]
+    done = 21  # sample 0 (after burn-in) + two blocks of 10 MCMC sweeps
+    for k in ("beta", "lambda"):
+        assert np.array_equal(part[k][:done], full[k][:done]), k
+        assert not part[k][done:].any(), k
+    for k in ("sig2", "tau"):
+        assert np.array_equal(part[k][:done], full[k][:done]), k
+    bb.set_seed(SEED + 2)
+    again = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    assert not bb.last_call_info()["interrupted"]
+    _same(full, again)
+
+
+def test_interrupt_during_burn_in(gpu_lib):
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(60, 400, seed=6)
+    bb.debug_interrupt_after(0)
+    out = bb.bridge_reg_stb(y, X, nsamp=30, burn=50)
+    assert bb.last_call_info()["interrupted"]
+    assert np.all(np.isfinite(out["beta"][0])) and not out["beta"][1:].any()
+
+
+@pytest.mark.parametrize("mode", ["rccl", "ondevice"])
+def test_one_member_group_equals_single_engine(gpu_lib, mode):
+    """A one-member shard group (RCCL communicator from ncclCommInitAll, or the on-device
+    sums) reproduces the communicator-free engine bit for bit."""
+    bb = gpu_lib
+    n, p = 150, 2000
+    X, y, _ = synthetic_problem(n, p, seed=31)
+    outs = []
+    for grouped in (False, True):
+        e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=11, method=2,
+                                      trace_capacity=8), X, y)
+        if grouped:
+            g = bb.ShardGroup([e], rccl=(mode == "rccl"))
+            g.init_state()
+            g.run(1, 8, first_slot=0, slot_step=1)
+            g.sync()
+        else:
+            e.init_state()
+            e.run(1, 8, first_slot=0, slot_step=1)
+        outs.append(e.trace(0, 8))
+        if grouped:
+            g.close()
+        e.close()
+    for k in ("beta", "lambda", "sig2", "tau"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_c_entry_device_count_control(gpu_lib):
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(50, 9000, seed=7)
+    bb.set_device_count(1)
+    try:
+        bb.set_seed(SEED + 3)
+        a = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
+        assert bb.last_call_info()["devices"] == 1
+    finally:
+        bb.set_device_count(0)
+    bb.set_seed(SEED + 3)
+    b = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
+    assert bb.last_call_info()["devices"] == min(bb.device_count(), 9000 // 4096)
+    if bb.device_count() == 1:
+        _same(a, b)
