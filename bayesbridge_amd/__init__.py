@@ -853,7 +853,7 @@ class EngineConfig:
     seed: int = 0xB4E5B41D6E
     stream: int = 0
     device: int = 0
-    gram_mode: Optional[int] = None  # None: library default (env BB_GRAM_MODE)
+    gram_mode: Optional[int] = None  # None: library default (Ozaki-II)
     betaburn: int = 0
 
     def to_c(self) -> bb_config:

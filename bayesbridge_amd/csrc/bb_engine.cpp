@@ -276,8 +276,8 @@ struct bb_engine {
     double *xb_part = nullptr, *red1 = nullptr;
     int nparts = 0, nbS = 0;
     // woodbury
-    double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *PT = nullptr,
-           *w = nullptr, *Wd = nullptr;
+    double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *w = nullptr,
+           *Wd = nullptr;
     unsigned int *flags = nullptr;
     int S = 1;
     size_t slab_stride = 0;
@@ -453,7 +453,7 @@ struct bb_engine {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
             mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd, flags);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags);
             mark(PH_SOLVE);
             chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
             mark(PH_BETA);
@@ -462,7 +462,7 @@ struct bb_engine {
             mark(PH_FORM);
             launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
             mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, PT, Wd, flags);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags);
             mark(PH_SOLVE);
             chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
             mark(PH_BETA);
@@ -481,7 +481,7 @@ struct bb_engine {
             launch_form_a(stream, method == 6 ? Gw : G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad,
                           p_pad);
             mark(PH_CHOL);
-            chol_factor(stream, A, p_pad, p_pad, 1, err, PT, Wd, flags);
+            chol_factor(stream, A, p_pad, p_pad, 1, err, Wd, flags);
             mark(PH_SOLVE);
             launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
             chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2, flags, err);
@@ -733,7 +733,6 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     const bool small = c.p <= c.n && c.world == 1 && e->method != 5 && e->method != 6;
     // the Cholesky scratch covers the n x n (Woodbury) and any p x p (chol, LS start) system
     const int m_sys = (e->woodbury() && !small) ? n_pad : (n_pad > p_pad ? n_pad : p_pad);
-    e->PT = dalloc<double>((size_t)2 * kNB * (m_sys + kNB), o);
     e->Wd = dalloc<double>((size_t)kNB * m_sys, o);
     e->flags = dalloc<unsigned int>(chol_flag_words(m_sys, 1), o);
     if (e->method == 6) {
@@ -802,7 +801,7 @@ void engine_init_state_local(bb_engine *e) {
         e->clear_err();
         launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, e->p_pad, e->A,
                       e->p_pad, e->p_pad);
-        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->PT, e->Wd, e->flags);
+        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->Wd, e->flags);
         HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
                                 e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
         chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1, e->flags, e->err);
@@ -911,9 +910,9 @@ void bb_config_default(bb_config *c) {
     c->true_alpha = 0.5;
     c->trace_capacity = 1;
     c->seed = 0xB4E5B41D6EULL;
-    // Woodbury Gram: Ozaki-II int8 (fp64-accurate, ~2x faster at C3) unless BB_GRAM_MODE=fp64
-    const char *gm = getenv("BB_GRAM_MODE");
-    c->gram_mode = (gm && strcmp(gm, "fp64") == 0) ? 0 : 1;
+    // Woodbury Gram: Ozaki-II int8 (fp64-accurate, ~2x faster at C3); cfg.gram_mode = 0
+    // selects the fp64 MFMA Gram
+    c->gram_mode = 1;
 }
 
 int bb_engine_create(const bb_config *cfg, const double *X_local, const double *y,
@@ -1664,7 +1663,6 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
         for (int r = 0; r < m_pad; ++r) h[(size_t)r + (size_t)m_pad * m_pad] = 1.0;
         double *src = dalloc<double>(h.size(), owned), *dA = dalloc<double>(h.size(), owned);
         HIPCHECK(hipMemcpy(src, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad, owned);
@@ -1677,7 +1675,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
         for (int it = 0; it <= reps; ++it) {
             HIPCHECK(hipMemcpyAsync(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice, 0));
             HIPCHECK(hipEventRecord(e0, 0));
-            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
+            chol_factor(0, dA, m_pad, m_pad, 1, de, Wd, fl);
             HIPCHECK(hipEventRecord(e1, 0));
             chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, 1, fl, de);
             HIPCHECK(hipEventRecord(e2, 0));
@@ -1697,7 +1695,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
             unsigned long long *dt = dalloc<unsigned long long>(nts, owned);
             HIPCHECK(hipMemset(dt, 0, nts * sizeof(unsigned long long)));
             HIPCHECK(hipMemcpy(dA, src, h.size() * sizeof(double), hipMemcpyDeviceToDevice));
-            chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl, dt);
+            chol_factor(0, dA, m_pad, m_pad, 1, de, Wd, fl, dt);
             HIPCHECK(hipDeviceSynchronize());
             HIPCHECK(hipMemcpy(trace, dt, nts * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         }
@@ -1924,12 +1922,11 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         for (int q = 0; q < nrhs; ++q)
             for (int r = 0; r < m; ++r) h[(size_t)r + (size_t)(m_pad + q) * m_pad] = bh[r + (size_t)q * m];
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        double *PT = dalloc<double>((size_t)2 * kNB * (m_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
-        chol_factor(0, dA, m_pad, m_pad, 1, de, PT, Wd, fl);
+        chol_factor(0, dA, m_pad, m_pad, 1, de, Wd, fl);
         chol_bsolve(0, dA, m_pad, m_pad, Wd, dA + (size_t)m_pad * m_pad, W, nrhs, fl, de);
         HIPCHECK(hipGetLastError());
         std::vector<double> hw((size_t)m_pad * nrhs);
@@ -1990,7 +1987,6 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
         double *bvec = dalloc<double>(p_pad, owned);
         launch_coldot(0, dX, n_pad, n_pad, dy, p, bvec);
         double *A = dalloc<double>((size_t)p_pad * (p_pad + kNB), owned);
-        double *PT = dalloc<double>((size_t)2 * kNB * (p_pad + kNB), owned);
         double *Wd = dalloc<double>((size_t)kNB * p_pad, owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(p_pad, 1), owned);
         double *W = dalloc<double>(p_pad, owned);
@@ -2012,7 +2008,7 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
             launch_em_form(0, G, p_pad, with_lam ? dlam : nullptr, dmask, bvec, p, p_pad, A,
                            p_pad, p_pad);
             HIPCHECK(hipMemset(de, 0, sizeof(uint32_t)));
-            chol_factor(0, A, p_pad, p_pad, 1, de, PT, Wd, fl);
+            chol_factor(0, A, p_pad, p_pad, 1, de, Wd, fl);
             chol_bsolve(0, A, p_pad, p_pad, Wd, A + (size_t)p_pad * p_pad, W, 1, fl, de);
             HIPCHECK(hipGetLastError());
             uint32_t f = 0;

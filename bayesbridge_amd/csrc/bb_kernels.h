@@ -104,21 +104,20 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    int rhs_col);
 
 // In-place upper Cholesky A = U'U of the leading m_pad x m_pad block with the
-// forward solve U'^-1 folded into the nrhs_blocks column blocks that follow.
-// PT: scratch of 2 x kNB x (m_pad + nrhs_blocks * kNB) doubles; Wd: m_pad/kNB blocks of
-// kNB x kNB receiving U_kk^-T (used by chol_bsolve).
-// flags: chol_flag_words(m_pad, nrhs_blocks) unsigned ints of scratch (set-once flags
-// tagged with a per-buffer epoch; zeroed only when first seen).  Env BB_CHOL=steps selects the one-launch-per-block-step variant.
+// forward solve U'^-1 folded into the nrhs_blocks column blocks that follow (one persistent
+// launch, k_chol_persistent).  Wd: m_pad/kNB blocks of kNB x kNB receiving U_kk^-T (used by
+// chol_bsolve).  flags: chol_flag_words(m_pad, nrhs_blocks) unsigned ints of scratch (set-once
+// flags tagged with a per-buffer epoch; zeroed only when first seen).  trace: optional
+// timestamps (bb_bench_chol).
 size_t chol_flag_words(int m_pad, int nrhs_blocks);
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT, double *Wd, unsigned int *flags,
-                 unsigned long long *trace = nullptr);
+                 double *Wd, unsigned int *flags, unsigned long long *trace = nullptr);
 
 
 // Backward solve U W = Y (Y, W: m_pad x nrhs <= 2, ld = m_pad); Y may be overwritten.
-// With the flag buffer of the factorisation just run (chol_factor with nrhs_blocks = 1,
-// persistent mode) and an error word: one persistent launch; otherwise (or with env
-// BB_BSOLVE=multi) one launch per kBsNB blocks.
+// With the flag buffer of the factorisation just run (chol_factor with nrhs_blocks = 1) and
+// an error word: one persistent launch; otherwise (or beyond one workgroup per CU) one
+// launch per kBsNB blocks.
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
                  double *Y, double *W, int nrhs, unsigned int *flags = nullptr,
                  uint32_t *err = nullptr);

@@ -809,24 +809,13 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 }
 
 // ---------------------------------------------------------------------------
-// Blocked right-looking Cholesky A = U'U (upper, column-major, NB = 64) with the
-// forward solve folded into trailing right-hand-side column blocks.  ONE launch per block
-// step kp (panel PT_{kp-1} of the previous step is ready):
-//   workgroup 0      applies step kp-1's update to A_kp,kp and eliminates [A_kp,kp | I]
-//                    -> W_kp = U_kp,kp^-T, stores it and releases flags[kp];
-//   panel workgroups (j > kp, RHS blocks included) apply step kp-1's update to A_kp,j in
-//                    LDS, acquire flags[kp], then form U_kp,j = W_kp A_kp,j (MFMA) into A and
-//                    row-major into PT_kp (RHS blocks: the forward substitution);
-//   trailing workgroups apply step kp-1's update to every tile (i, j), kp < i <= j.
-// The flag hand-off follows the agent-scope release/acquire recipe (cdna_hip_programming
-// Guideline 16); flags are zeroed per factorisation; spins are bounded (error bit 16).
+// Blocked Cholesky A = U'U (upper, column-major, NB = 64) with the forward solve folded into
+// trailing right-hand-side column blocks: k_chol_persistent below.
 // Pivot chain (tools/diag_latency.hip: a dependent fp64 op ~48 cycles, an LDS
 // write/barrier/read round trip ~270): the wave owning rows 8b..8b+7 factors them with
-// v_readlane broadcasts (no barrier), publishes the 8 rows once, and the other waves apply a
-// rank-8 update -- valid because a symmetric elimination's multipliers depend only on the
-// final pivot rows.  Pivot rows are published with their strictly-lower part zeroed so every
-// value stays finite without per-element masks.  U_kp,kp itself is never stored: the
-// backward solve uses W_kp.
+// v_readlane broadcasts (no barrier) and publishes each pivot row as soon as it is final;
+// the other waves apply it -- valid because a symmetric elimination's multipliers depend
+// only on the final pivot rows.  U_kk itself is never stored: the backward solve uses W_k.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double fast_rcp(double p) {
     // v_rcp_f64 (~2^-26 accurate) + one Newton step in FMA form: ~1 ulp for the normal
@@ -842,278 +831,8 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Trailing update of one 64x64 tile in global memory: A_ij -= U_ki' U_kj (PT = U's block
-// row k, row-major), 8 waves x 2 MFMA blocks of 16x16.
-__device__ __forceinline__ void tile_update_global(double *A, int lda, int ib, int jb,
-                                                  const double *__restrict__ PT, int ldpt) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int blk = wid * 2 + h;
-        const int bx = blk >> 2, by = blk & 3;
-        v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int kk = 0; kk < 16; ++kk) {
-            const double *pr = PT + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
-            const double av = pr[jb + bx * 16 + (lane & 15)];
-            const double bv = pr[ib + by * 16 + (lane & 15)];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int x = bx * 16 + (lane >> 4) + 4 * rr;  // column within block j
-            const int y = by * 16 + (lane & 15);           // row within block i
-            A[(size_t)(ib + y) + (size_t)(jb + x) * lda] -= acc[rr];
-        }
-    }
-}
-
-// Same update applied to a 64x64 tile held in LDS as T[row][col] (pitch 65).
-__device__ __forceinline__ void tile_update_lds(double (*T)[65], int ib, int jb,
-                                               const double *__restrict__ PT, int ldpt,
-                                               bool upper_only) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int blk = wid * 2 + h;
-        const int bx = blk >> 2, by = blk & 3;
-        v4d acc = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int kk = 0; kk < 16; ++kk) {
-            const double *pr = PT + (size_t)(kk * 4 + (lane >> 4)) * ldpt;
-            const double av = pr[jb + bx * 16 + (lane & 15)];
-            const double bv = pr[ib + by * 16 + (lane & 15)];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            const int x = bx * 16 + (lane >> 4) + 4 * rr;
-            const int y = by * 16 + (lane & 15);
-            if (!upper_only || y <= x) T[y][x] -= acc[rr];
-        }
-    }
-}
-
-// Diagnostic timestamps of the step's critical path, written only when a trace buffer is
-// given (bb_bench_chol): [kp][0..7] s_memrealtime (100 MHz), [kp][8..15] the same points in
-// shader clocks (s_memtime).  Slots: [kp][0..4] workgroup 0 start / tile loaded /
-// updated / eliminated / flag released, [kp][5..7] panel workgroup 1 start / acquired / done.
-#define CHOL_TS(slot)                                                                      \
-    do {                                                                                    \
-        if (trace && threadIdx.x == 0) {                                                  \
-            trace[kp * 32 + (slot)] = __builtin_amdgcn_s_memrealtime();                     \
-            trace[kp * 32 + 8 + (slot)] = __builtin_amdgcn_s_memtime();                     \
-        }                                                                                   \
-    } while (0)
-
-__global__ __launch_bounds__(512) void k_chol_step(double *A, int lda, int kp, int nblk,
-                                                   int ncb, const double *__restrict__ PTin,
-                                                   double *PTout, int ldpt, double *Wd,
-                                                   unsigned int *flags, uint32_t *err,
-                                                   unsigned long long *trace) {
-    __shared__ double T[64][65];                                   // one 64x64 tile
-    __shared__ __attribute__((aligned(16))) double rows[2][8][128];  // published pivot rows
-    __shared__ double rinv[2][8];
-    __shared__ double piv[64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int npanel = ncb - kp - 1;
-    const int ib = kp * kNB;
-    if ((int)blockIdx.x > npanel) {
-        // ---- trailing update of tile (i, j), kp < i <= j (RHS blocks included) ----
-        const int a = nblk - kp - 1;
-        const int tri = a * (a + 1) / 2;
-        const int t = blockIdx.x - npanel - 1;
-        int i, j;
-        if (t < tri) {
-            int jj = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-            while ((jj + 1) * (jj + 2) / 2 <= t) ++jj;
-            while (jj * (jj + 1) / 2 > t) --jj;
-            j = kp + 1 + jj;
-            i = kp + 1 + (t - jj * (jj + 1) / 2);
-        } else {
-            const int t2 = t - tri;
-            j = nblk + t2 / a;
-            i = kp + 1 + t2 % a;
-        }
-        tile_update_global(A, lda, i * kNB, j * kNB, PTin, ldpt);
-        return;
-    }
-    if (blockIdx.x > 0) {
-        // ---- panel workgroup: U_kp,j = W_kp (A_kp,j - step kp-1 update) ----
-        const int j = kp + blockIdx.x;
-        const int jb = j * kNB;
-        if (blockIdx.x != 1) trace = nullptr;
-        CHOL_TS(5);
-        for (int e = tid; e < 64 * 64; e += 512) {
-            const int y = e & 63, x = e >> 6;
-            T[y][x] = A[(size_t)(ib + y) + (size_t)(jb + x) * lda];
-        }
-        __syncthreads();
-        if (kp > 0) {
-            tile_update_lds(T, ib, jb, PTin, ldpt, false);
-            __syncthreads();
-        }
-        if (tid == 0) {
-            unsigned spins = 0;
-            while (__hip_atomic_load(&flags[kp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                   0u) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) {
-                    atomicOr(err, 16u);
-                    break;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        CHOL_TS(6);
-        __syncthreads();
-        // D'[x][r] = sum_s T[s][x] W[r][s]: 8 waves x 2 blocks of 16x16 over the 64x64 result
-        const double *W = Wd + (size_t)kp * kNB * kNB;
-        v4d acc[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
-        const int bxx = (wid >> 1) * 16;      // x block (0..48)
-        const int brr = (wid & 1) * 32;       // r base (0 / 32), two 16-wide blocks
-#pragma unroll 4
-        for (int kk = 0; kk < 16; ++kk) {
-            const int sr = kk * 4 + (lane >> 4);
-            const double av = T[sr][bxx + (lane & 15)];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const double bv = W[(size_t)sr * kNB + brr + h * 16 + (lane & 15)];
-                acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[h], 0, 0, 0);
-            }
-        }
-        __syncthreads();  // T is overwritten with U below
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {
-                const int x = bxx + (lane >> 4) + 4 * rr;
-                const int rw = brr + h * 16 + (lane & 15);
-                const double v = acc[h][rr];
-                A[(size_t)(ib + rw) + (size_t)(jb + x) * lda] = v;
-                T[rw][x] = v;
-            }
-        __syncthreads();
-        for (int e = tid; e < 64 * 64; e += 512) {
-            const int x = e & 63, rw = e >> 6;
-            PTout[(size_t)rw * ldpt + jb + x] = T[rw][x];
-        }
-        CHOL_TS(7);
-        return;
-    }
-    // ---- workgroup 0: update A_kp,kp, eliminate [A_kp,kp | I], publish W_kp ----
-    CHOL_TS(0);
-    for (int e = tid; e < 64 * 64; e += 512) {
-        const int y = e & 63, x = e >> 6;
-        T[y][x] = (y <= x) ? A[(size_t)(ib + y) + (size_t)(ib + x) * lda] : 0.0;
-    }
-    __syncthreads();
-    CHOL_TS(1);
-    if (kp > 0) {
-        tile_update_lds(T, ib, ib, PTin, ldpt, true);
-        __syncthreads();
-    }
-    CHOL_TS(2);
-    // wave w owns rows 8w .. 8w+7; lane l owns columns 2l, 2l+1 of [A | I]
-    const int r0 = wid * 8;
-    const int c0 = lane * 2;
-    double a[8][2];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int row = r0 + i, col = c0 + q;
-            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
-        }
-    for (int b = 0; b < 8; ++b) {
-        const int sb = b & 1;
-        if (wid == b) {
-            // wave-local factorisation of rows 8b .. 8b+7
-            double invs[8];
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const int c = 8 * b + ci;
-                a[ci][0] = (c0 < c) ? 0.0 : a[ci][0];
-                a[ci][1] = (c0 + 1 < c) ? 0.0 : a[ci][1];
-                const double pv = readlane_d(a[ci][ci & 1], 4 * b + (ci >> 1));
-                const double inv = fast_rcp(pv);
-                invs[ci] = inv;
-                if (lane == 0) piv[c] = pv;
-#pragma unroll
-                for (int i = ci + 1; i < 8; ++i) {
-                    const double li = readlane_d(a[ci][i & 1], 4 * b + (i >> 1)) * inv;
-                    a[i][0] = __builtin_fma(-li, a[ci][0], a[i][0]);
-                    a[i][1] = __builtin_fma(-li, a[ci][1], a[i][1]);
-                }
-            }
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci)
-                *(double2 *)&rows[sb][ci][c0] = make_double2(a[ci][0], a[ci][1]);
-            if (lane < 8) {
-                double v = 0.0;
-#pragma unroll
-                for (int ci = 0; ci < 8; ++ci) v = (lane == ci) ? invs[ci] : v;
-                rinv[sb][lane] = v;
-            }
-        }
-        __syncthreads();
-        if (wid > b) {
-            // rank-8 update of my rows with the published pivot rows 8b .. 8b+7
-            double m[8][8];
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const double iv = rinv[sb][ci];
-#pragma unroll
-                for (int i = 0; i < 8; i += 2) {
-                    const double2 t2 = *(const double2 *)&rows[sb][ci][r0 + i];
-                    m[ci][i] = t2.x * iv;
-                    m[ci][i + 1] = t2.y * iv;
-                }
-            }
-#pragma unroll
-            for (int ci = 0; ci < 8; ++ci) {
-                const double2 rv = *(const double2 *)&rows[sb][ci][c0];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    a[i][0] = __builtin_fma(-m[ci][i], rv.x, a[i][0]);
-                    a[i][1] = __builtin_fma(-m[ci][i], rv.y, a[i][1]);
-                }
-            }
-        }
-        // the next block's publisher writes rows[sb ^ 1]; rows[sb] is rewritten two blocks
-        // later, after the barrier that follows every wave's reads of it
-    }
-    CHOL_TS(3);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const double pv = piv[r0 + i];
-        if (!(pv > 0.0) && err && lane == 0) atomicOr(err, 8u);
-        const double dinv = 1.0 / sqrt(pv);
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * dinv;
-    }
-    __syncthreads();
-    double *W = Wd + (size_t)kp * kNB * kNB;
-    for (int e = tid; e < 64 * 64; e += 512) {
-        const int y = e & 63, x = e >> 6;
-        W[(size_t)x * kNB + y] = T[y][x];  // W[y][x], column-major
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&flags[kp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    CHOL_TS(4);
-}
-
 // ---------------------------------------------------------------------------
-// Persistent dataflow Cholesky (the default): ONE launch factors the whole matrix.
+// Persistent dataflow Cholesky: ONE launch factors the whole matrix.
 //   workgroup 0 (the chain) owns the critical path: for k = 0 .. nblk-1 it eliminates the
 //     diagonal block D_k (held in LDS, all updates applied) -> W_k = U_kk^-T, publishes W_k,
 //     then takes the hand-off tiles A_{k,k+1}, A_{k+1,k+1} (updated by their owners through
@@ -1596,14 +1315,6 @@ static unsigned int flag_epoch(unsigned int *flags, size_t words, hipStream_t s,
     return ++e;
 }
 
-static int chol_mode() {
-    static int m = [] {
-        const char *e = getenv("BB_CHOL");
-        return (e && strcmp(e, "steps") == 0) ? 1 : 0;
-    }();
-    return m;
-}
-
 static int device_cus() {
     static int n = [] {
         int dev = 0, v = 0;
@@ -1617,85 +1328,17 @@ static int device_cus() {
 }
 
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *PT, double *Wd, unsigned int *flags, unsigned long long *trace) {
-    if (chol_mode() == 0) {
-        const int nblk = m_pad / kNB;
-        const int ncb = nblk + nrhs_blocks;
-        const size_t words = chol_flag_words(m_pad, nrhs_blocks);
-        const unsigned int ep = flag_epoch(flags, words, s, true);
-        CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb, ep};
-        const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
-        const int grid = std::min(device_cus(), 1 + ntiles);
-        k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
-        return;
-    }
+                 double *Wd, unsigned int *flags, unsigned long long *trace) {
     const int nblk = m_pad / kNB;
     const int ncb = nblk + nrhs_blocks;
-    const int ldpt = ncb * kNB;
-    double *pt[2] = {PT, PT + (size_t)kNB * ldpt};
-    (void)hipMemsetAsync(flags, 0, sizeof(unsigned int) * ((nblk + 3) & ~3), s);
-    for (int kp = 0; kp < nblk; ++kp) {
-        const int npanel = ncb - kp - 1;
-        const int a = nblk - kp - 1;
-        const int tiles = kp > 0 ? (a * (a + 1) / 2 + a * nrhs_blocks) : 0;
-        // tiles of rows > kp receive step kp-1's update; at kp = 0 there is none
-        const int ntrail = (kp > 0) ? tiles : 0;
-        const double *pin = pt[(kp + 1) & 1];  // PT of step kp - 1
-        k_chol_step<<<1 + npanel + ntrail, 512, 0, s>>>(A, lda, kp, nblk, ncb, pin, pt[kp & 1],
-                                                      ldpt, Wd, flags, err, trace);
-    }
+    const size_t words = chol_flag_words(m_pad, nrhs_blocks);
+    const unsigned int ep = flag_epoch(flags, words, s, true);
+    CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb, ep};
+    const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
+    const int grid = std::min(device_cus(), 1 + ntiles);
+    k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
 }
 
-
-// Backward solve step k: every workgroup forms w_k = U_kk^-1 y_k = W_k' y_k;
-// workgroup 0 stores it; workgroup i < k applies y_i -= U_ik w_k.
-__global__ __launch_bounds__(256) void k_bsolve_step(const double *A, int lda, int k,
-                                                     int m_pad, const double *__restrict__ Wd,
-                                                     double *Y, double *Wout, int nrhs) {
-    __shared__ double yv[2][64];
-    __shared__ double part[4][2][64];
-    __shared__ double wv[2][64];
-    const int tid = threadIdx.x, x = tid & 63, g = tid >> 6;  // g: 16-row slice
-    const int kb = k * kNB;
-    if (tid < 64 * nrhs) yv[tid >> 6][tid & 63] = Y[(size_t)(tid >> 6) * m_pad + kb + (tid & 63)];
-    __syncthreads();
-    const double *W = Wd + (size_t)k * kNB * kNB;
-    // w[x] = sum_r W[r][x] y[r]; W column-major: column x contiguous in r
-    for (int q = 0; q < nrhs; ++q) {
-        double acc = 0.0;
-        const double *col = W + (size_t)x * kNB + g * 16;
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr) acc += col[rr] * yv[q][g * 16 + rr];
-        part[g][q][x] = acc;
-    }
-    __syncthreads();
-    if (tid < 64 * nrhs) {
-        const int q = tid >> 6;
-        wv[q][x] = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
-    }
-    __syncthreads();
-    if (blockIdx.x == 0 && tid < 64 * nrhs)
-        Wout[(size_t)(tid >> 6) * m_pad + kb + x] = wv[tid >> 6][x];
-    if (k > 0) {
-        const int ib = blockIdx.x * kNB;
-        // y_i[r] -= sum_c U_ik[r][c] w[c]; thread (r = x, slice g over c)
-        for (int q = 0; q < nrhs; ++q) {
-            double acc = 0.0;
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc) {
-                const int c = g * 16 + cc;
-                acc += A[(size_t)(ib + x) + (size_t)(kb + c) * lda] * wv[q][c];
-            }
-            part[g][q][x] = acc;
-        }
-        __syncthreads();
-        if (tid < 64 * nrhs) {
-            const int q = tid >> 6;
-            const double acc = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
-            Y[(size_t)q * m_pad + ib + x] -= acc;
-        }
-    }
-}
 
 // Backward solve of kBsNB consecutive blocks per launch (kb, kb-1, .., kb-nb+1): every
 // workgroup redundantly runs the short chain w_k = W_k' (y_k - sum_{k' in (k, kb]} U_kk' w_k')
@@ -1846,18 +1489,12 @@ __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda
     flag_release(&fl[i], ep);
 }
 
-static bool bsolve_persistent() {
-    static const bool on = [] {
-        const char *e = getenv("BB_BSOLVE");
-        return !(e && std::strcmp(e, "multi") == 0);
-    }();
-    return on;
-}
-
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
                  double *Y, double *W, int nrhs, unsigned int *flags, uint32_t *err) {
     const int nblk = m_pad / kNB;
-    if (flags && err && bsolve_persistent() && nblk <= device_cus()) {
+    // one persistent launch (a workgroup per 64-row block, resident together) after the
+    // factorisation that filled `flags`; otherwise one launch per kBsNB blocks
+    if (flags && err && nblk <= device_cus()) {
         // the solve's flags have their own epoch sequence (one per solve)
         unsigned int *bf = flags + bsolve_flag_offset(m_pad, 1);
         const unsigned int ep = flag_epoch(bf, (size_t)nblk, s, true);

@@ -5,8 +5,7 @@
 // fp64 rounding of the scaled value, relative to the row's bound).  The exact integer Gram
 // C = Yh Yh' (|C| <= K 2^2b < M/2) is recovered from its residues modulo kOzMods pairwise
 // coprime moduli m_k <= 247:  C mod m_k = (Yh mod m_k)(Yh mod m_k)' mod m_k, each an int8
-// GEMM with exact int32 accumulation on v_mfma_i32_16x16x64_i8 (k_oz_gemm16; the
-// v_mfma_i32_32x32x32_i8 form k_oz_gemm is kept for A/B runs, BB_OZ_SHAPE=32).  Garner's mixed-radix
+// GEMM with exact int32 accumulation on v_mfma_i32_16x16x64_i8 (k_oz_gemm16u).  Garner's mixed-radix
 // reconstruction (balanced digits) gives C exactly as a 128-bit integer, which is rounded
 // once to fp64 and scaled back: G_ik = C_ik 2^(e_i + e_k).
 //

@@ -331,24 +331,16 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
 
 // ---------------------------------------------------------------------------
 // int8 GEMM per (modulus, lower tile, K split): C = R_I R_K' (exact int32), stored mod m.
-// (32x32x32 form; production runs k_oz_gemm16 below, which shares this staging protocol.)
-// 256 threads = 4 waves in 2x2, each wave 128x128 = 4x4 v_mfma_i32_32x32x32_i8 blocks (256
-// accumulator registers; one workgroup per CU).
-// Staging: a 4-stage LDS ring (32 KB per stage: A then B, 256 rows x 64 B each) filled by
-// global_load_lds_dwordx4 three chunks ahead; one wave-instruction moves 16 rows (1 KB,
-// lane-linear in LDS).  The 16-byte unit u of row r is stored at unit u ^ ((r >> 2) & 3)
-// (swizzle applied on the per-lane SOURCE address, undone on the fragment read) so that a
-// ds_read_b128 phase of 16 rows hits 16 distinct bank groups.  Per chunk: counted
-// s_waitcnt vmcnt (two stages stay in flight), raw s_barrier, issue chunk + 3, 16
-// ds_read_b128, 32 MFMAs.
-// Operand lane map: lane l holds row (l & 31), bytes 16 (l >> 5) .. +15 of the 32-byte K
-// step -- A and B use the same K map, so the product is the exact dot product.  C/D map:
-// col = l & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (l >> 5).
+// 256 threads = 4 waves; one workgroup per CU.  Staging: a 4-stage LDS ring (32 KB per
+// stage: A then B, 256 rows x 64 B each) filled by global_load_lds_dwordx4 three chunks
+// ahead; one wave-instruction moves one 1 KB block of 16 rows, lane-linearly (the residue
+// image is stored in that [16-row block][unit][row][16 B] order, so fragment reads need no
+// swizzle).  Per chunk: counted s_waitcnt vmcnt (two stages stay in flight), raw s_barrier,
+// MFMAs interleaved with the next chunk's fragment reads and the refill pieces.
 // XCD grouping: block b runs on XCD b % 8; all tiles of one (modulus, split) unit are given
 // to one XCD so that their shared row blocks stay in that XCD's L2.
 // ---------------------------------------------------------------------------
 constexpr int kOzStages = 4;
-constexpr int kOzStages16 = 4;  // k_oz_gemm16 (5 stages, the whole 160 KB LDS, measured no better)
 constexpr int kOzOpBytes = kOzT * kOzKC;          // 16 KB per operand per stage
 constexpr int kOzStageBytes = 2 * kOzOpBytes;     // 32 KB
 
@@ -357,158 +349,8 @@ __device__ __forceinline__ void oz_glds(const int8_t *src, int8_t *lds) {
                                      (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
 
-// byte offset of (row, 16-byte unit) in a residue tile image: [16-row block][unit][row][16 B]
-__device__ __forceinline__ int oz_swz(int row, int unit) {
-    return (row >> 4) * 1024 + unit * 256 + (row & 15) * 16;
-}
-
-// dbg (timing ablations for tools/bench_ozaki.py only; 0 in production): bit 0 skips the
-// in-loop LDS-DMA refills, bit 1 the fragment reads, bit 2 the waits and barrier.
-template <int dbg>
-__global__ __launch_bounds__(256, 1) void k_oz_gemm(const int8_t *__restrict__ R, int n_oz,
-                                                    int nkc, int nsplit, int8_t *__restrict__ P,
-                                                    OzConsts C) {
-    __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
-    const int nt = n_oz / kOzT;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-    const int u = xcd + 8 * (q / ntiles);
-    const int tile = q % ntiles;
-    const int mod = u % kOzMods;
-    const int split = u / kOzMods;
-    if (split >= nsplit) return;
-    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-    while (I * (I + 1) / 2 > tile) --I;
-    I = __builtin_amdgcn_readfirstlane(I);
-    const int K = tile - I * (I + 1) / 2;
-    const int per = (nkc + nsplit - 1) / nsplit;
-    const int c0 = split * per;
-    const int nch = max(0, min(nkc, c0 + per) - c0);
-    const size_t kstride = (size_t)n_oz * kOzKC;
-    // residue plane (mod, chunk) layout: [16-row block][unit 0..3][row in block][16 B]
-    // (k_oz_residues); a 256-row tile is 16 consecutive 1 KB blocks
-    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
-    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid >> 1, wc = wid & 1;
-
-    // this wave's 4 glds per operand: 16-row blocks 4 wid + i
-    // (one instruction copies the 1 KB block of 16 rows lane-linearly: the LDS image keeps
-    // the global [unit][row][16 B] order, whose 16-row runs make every ds_read_b128 lane
-    // group hit 16 distinct 16-byte bank slots without a swizzle)
-    const int voff = wid * 4096 + lane * 16;  // the only per-lane part of a piece's source
-    // glds number g (0..7) of a stage: operand g >> 2, wave-slice g & 3
-    auto glds_one = [&](int kc, int stage, int g) {
-        int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
-        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
-        oz_glds(src + voff, sb + (4 * wid + (g & 3)) * 1024);
-    };
-    auto issue = [&](int kc, int stage) {
-#pragma unroll
-        for (int g = 0; g < 8; ++g) glds_one(kc, stage, g);
-    };
-
-    v16i acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
-
-    auto frag_a = [&](int chunk, int ks, int i) {
-        const int8_t *A_ = smem + (chunk % kOzStages) * kOzStageBytes;
-        return *(const v4i *)&A_[oz_swz(wr * 128 + i * 32 + (lane & 31), ks * 2 + (lane >> 5))];
-    };
-    auto frag_b = [&](int chunk, int ks, int j) {
-        const int8_t *B_ = smem + (chunk % kOzStages) * kOzStageBytes + kOzOpBytes;
-        return *(const v4i *)&B_[oz_swz(wc * 128 + j * 32 + (lane & 31), ks * 2 + (lane >> 5))];
-    };
-    auto read_frags = [&](int chunk, v4i (&fa)[2][4], v4i (&fb)[2][4]) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                fa[ks][i] = frag_a(chunk, ks, i);
-                fb[ks][i] = frag_b(chunk, ks, i);
-            }
-    };
-    // One step: (my reads of chunk `it` are done) -> chunk it+1 landed for every wave and
-    // chunk it's stage free -> 8 groups of {4 MFMAs of chunk it from registers, 2 fragment
-    // reads of chunk it+1, 1 LDS-DMA load of chunk it+4 into the freed stage}, pinned by
-    // sched_barrier: one wave per SIMD issues in order, so a block of loads would idle the
-    // matrix pipe.  Past the end the refill re-loads the last chunk into the freed stage
-    // and the extra reads land in dead registers, keeping every step identical (two
-    // stages always in flight at the wait: vmcnt(16)).
-    auto step = [&](int it, v4i (&fa_c)[2][4], v4i (&fb_c)[2][4], v4i (&fa_n)[2][4],
-                    v4i (&fb_n)[2][4]) {
-        if (!(dbg & 4)) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        asm volatile("" ::: "memory");
-        const int kc_next = c0 + min(it + kOzStages, nch - 1);
-        const int st_next = (it + kOzStages) % kOzStages;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const int ks = g >> 2, i = g & 3;
-            acc[i][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][0],
-                                                              acc[i][0], 0, 0, 0);
-            if (!(dbg & 1)) glds_one(kc_next, st_next, g);
-            if (!(dbg & 2)) fa_n[ks][i] = frag_a(it + 1, ks, i);
-            acc[i][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][1],
-                                                              acc[i][1], 0, 0, 0);
-            if (!(dbg & 2)) fb_n[ks][i] = frag_b(it + 1, ks, i);
-            acc[i][2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][2],
-                                                              acc[i][2], 0, 0, 0);
-            acc[i][3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa_c[ks][i], fb_c[ks][3],
-                                                              acc[i][3], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-
-    v4i fa0[2][4], fb0[2][4], fa1[2][4], fb1[2][4];
-    if (nch > 0) {
-#pragma unroll
-        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
-        read_frags(0, fa0, fb0);
-    }
-    int it = 0;
-    for (; it + 1 < nch; it += 2) {
-        step(it, fa0, fb0, fa1, fb1);
-        step(it + 1, fa1, fb1, fa0, fb0);
-    }
-    if (it < nch) step(it, fa0, fb0, fa1, fb1);
-    // the refills issued past the end must land before the workgroup's LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
-    const int m = C.m[mod];
-    const double im = C.inv_m[mod];
-    const int hi = m / 2, lo = hi - m + 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int rowl = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                const int col = wc * 128 + j * 32 + (lane & 31);
-                const int cval = acc[i][j][r];
-                int rr = cval - (int)rint((double)cval * im) * m;
-                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
-                out[rowl * kOzT + col] = (int8_t)rr;
-            }
-}
-
 // ---------------------------------------------------------------------------
-// The same tile, staging and schedule on v_mfma_i32_16x16x64_i8: one K step is a whole
+// The tile on v_mfma_i32_16x16x64_i8: one K step is a whole
 // 64-byte chunk, and a 16-row operand fragment (lane l: row l & 15, unit l >> 4) is exactly
 // one 1 KB block of the residue image, read lane-linearly.  Per wave 8 x 8 accumulator
 // blocks of 16 x 16 (256 registers), 64 MFMAs of 16 cycles per chunk.  The MFMA is issued
@@ -522,9 +364,6 @@ __device__ __forceinline__ void oz_mfma16(v4i &acc, const v4i &a, const v4i &b) 
     asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-// NW = 4: waves in 2 x 2, each 128 x 128 (8 x 8 blocks, 256 accumulator registers, one wave
-// per SIMD).  NW = 8: waves in 2 x 4, each 128 x 64 (8 x 4 blocks, 128 registers), two waves
-// per SIMD, so that one wave's MFMAs run while the other issues its LDS-DMA pieces.
 // s_waitcnt vmcnt(N) (expcnt, lgkmcnt left open): every piece older than the newest N landed
 template <int N>
 __device__ __forceinline__ void oz_wait_vm() {
@@ -532,286 +371,6 @@ __device__ __forceinline__ void oz_wait_vm() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
     asm volatile("" ::: "memory");
-}
-
-// TM = 0: every lower tile; TM = 1: only the off-diagonal tiles (I > K), the diagonal ones
-// then run paired in k_oz_gemm16d.  P keeps one slot per lower tile, t = I (I+1)/2 + K.
-template <int dbg, int NW, int ST, int TM = 0>
-__global__ __launch_bounds__(NW * 64, 1) void k_oz_gemm16(const int8_t *__restrict__ R, int n_oz,
-                                                          int nkc, int nsplit,
-                                                          int8_t *__restrict__ P, OzConsts C) {
-    constexpr int WN = NW / 2;        // wave columns
-    constexpr int FJ = 16 / WN;       // 16 x 16 column blocks per wave: 8 (NW 4) or 4 (NW 8)
-    constexpr int PP = 32 / NW;       // LDS-DMA pieces per wave and stage (32 per stage)
-    constexpr int PH = PP / 2;        // pieces per operand
-    __shared__ __attribute__((aligned(1024))) int8_t smem[ST * kOzStageBytes];
-    const int nt = n_oz / kOzT;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int nenum = TM ? nt * (nt - 1) / 2 : ntiles;  // tiles this launch enumerates
-    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-    const int u = xcd + 8 * (q / nenum);
-    const int te = q % nenum;
-    const int mod = u % kOzMods;
-    const int split = u / kOzMods;
-    if (split >= nsplit) return;
-    // enumerated index -> (I, K): all lower tiles te = I (I+1)/2 + K, or the strictly
-    // lower ones te = I (I-1)/2 + K
-    const int sh = TM ? 1 : 0;
-    int I = (int)((sqrt(8.0 * te + 1.0) + (TM ? 1.0 : -1.0)) * 0.5);
-    while ((I + 1) * (I + 2 - 2 * sh) / 2 <= te) ++I;
-    while (I * (I + 1 - 2 * sh) / 2 > te) --I;
-    I = __builtin_amdgcn_readfirstlane(I);
-    const int K = te - I * (I + 1 - 2 * sh) / 2;
-    const int tile = I * (I + 1) / 2 + K;
-    const int per = (nkc + nsplit - 1) / nsplit;
-    const int c0 = split * per;
-    const int nch = max(0, min(nkc, c0 + per) - c0);
-    const size_t kstride = (size_t)n_oz * kOzKC;
-    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
-    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid / WN, wc = wid % WN;
-
-    // piece g of a stage: operand g / PH, 16-row block PH wid + g % PH (1 KB, lane-linear)
-    const int voff = wid * PH * 1024 + lane * 16;  // the only per-lane part of a source
-    auto glds_one = [&](int kc, int stage, int g) {
-        int8_t *sb = smem + stage * kOzStageBytes + (g / PH) * kOzOpBytes;
-        const int8_t *src = ((g / PH) ? baseB : baseA) + (size_t)kc * kstride + (g % PH) * 1024;
-        oz_glds(src + voff, sb + (PH * wid + (g % PH)) * 1024);
-    };
-    auto issue = [&](int kc, int stage) {
-#pragma unroll
-        for (int g = 0; g < PP; ++g) glds_one(kc, stage, g);
-    };
-
-    v4i acc[8][FJ];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
-
-    auto frag_a = [&](int chunk, int i) {
-        const int8_t *A_ = smem + (chunk % ST) * kOzStageBytes;
-        return *(const v4i *)&A_[(wr * 8 + i) * 1024 + lane * 16];
-    };
-    auto frag_b = [&](int chunk, int j) {
-        const int8_t *B_ = smem + (chunk % ST) * kOzStageBytes + kOzOpBytes;
-        return *(const v4i *)&B_[(wc * FJ + j) * 1024 + lane * 16];
-    };
-    auto read_frags = [&](int chunk, v4i (&fa)[8], v4i (&fb)[FJ]) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) fa[i] = frag_a(chunk, i);
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) fb[j] = frag_b(chunk, j);
-    };
-    // same protocol as k_oz_gemm: 8 groups of {FJ MFMAs, PP/8 LDS-DMA pieces, the next
-    // chunk's A fragment g and (spread evenly) B fragments}
-    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[FJ], v4i (&fa_n)[8], v4i (&fb_n)[FJ]) {
-        if (!(dbg & 4)) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            oz_wait_vm<PP * (ST - 2)>();
-            __builtin_amdgcn_s_barrier();
-        }
-        asm volatile("" ::: "memory");
-        const int kc_next = (dbg & 8) ? c0 : c0 + min(it + ST, nch - 1);
-        const int st_next = (it + ST) % ST;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
-            if (!(dbg & 1) && (PP == 8 || (g & 1))) glds_one(kc_next, st_next, PP == 8 ? g : g >> 1);
-            oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
-            if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
-            oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
-            if (!(dbg & 2) && (FJ == 8 || !(g & 1))) fb_n[g * FJ / 8] = frag_b(it + 1, g * FJ / 8);
-            oz_mfma16(acc[g][3], fb_c[3], fa_c[g]);
-#pragma unroll
-            for (int j = 4; j < FJ; ++j) oz_mfma16(acc[g][j], fb_c[j], fa_c[g]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-
-    v4i fa0[8], fb0[FJ], fa1[8], fb1[FJ];
-    if (nch > 0) {
-#pragma unroll
-        for (int st = 0; st < ST - 1; ++st) issue(c0 + min(st, nch - 1), st);
-        oz_wait_vm<PP * (ST - 2)>();
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        issue(c0 + min(ST - 1, nch - 1), ST - 1);
-        read_frags(0, fa0, fb0);
-    }
-    int it = 0;
-    for (; it + 1 < nch; it += 2) {
-        step(it, fa0, fb0, fa1, fb1);
-        step(it + 1, fa1, fb1, fa0, fb0);
-    }
-    if (it < nch) step(it, fa0, fb0, fa1, fb1);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
-    const int m = C.m[mod];
-    const double im = C.inv_m[mod];
-    const int hi = m / 2, lo = hi - m + 1;
-    // acc[i][j] = (B block j)(A block i)': lane l, reg r holds row (I side) i*16 + (l & 15),
-    // column (K side) j*16 + 4 (l >> 4) + r, so a lane's four registers are four consecutive
-    // bytes of the tile row: one dword store per block
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) {
-            const int rowl = wr * 128 + i * 16 + (lane & 15);
-            const int col = wc * FJ * 16 + j * 16 + 4 * (lane >> 4);
-            unsigned int wv = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int cval = acc[i][j][r];
-                int rr = cval - (int)rint((double)cval * im) * m;
-                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
-                wv |= ((unsigned int)rr & 0xffu) << (8 * r);
-            }
-            *(unsigned int *)(out + rowl * kOzT + col) = wv;
-        }
-}
-
-// ---------------------------------------------------------------------------
-// Register-staged variant of k_oz_gemm16 (BB_OZ_SHAPE=16r): each wave moves its 8 KB of a
-// chunk with 8 plain global_load_dwordx4 into a 2-deep register ring and 8 ds_write_b128
-// into a 2-stage LDS ring (64 KB), instead of 8 LDS-DMA pieces (whose issue cost beside
-// MFMAs is 60-185 cycles each, MI355X_MICROARCH.md).  Step it: MFMAs on chunk it (frags in
-// registers), fragment reads of chunk it+1 (LDS stage (it+1)%2), ds_write of chunk it+2
-// (ring slot it%2, loaded two steps ago) into stage it%2, then the loads of chunk it+4 into
-// the slot just written.  Piece g's write waits for its load with 15 loads still in flight
-// (the rest of chunk it+2, all of chunk it+3, pieces < g of chunk it+4).
-// ---------------------------------------------------------------------------
-template <int dbg>
-__global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict__ R, int n_oz,
-                                                       int nkc, int nsplit,
-                                                       int8_t *__restrict__ P, OzConsts C) {
-    __shared__ __attribute__((aligned(1024))) int8_t smem[2 * kOzStageBytes];
-    const int nt = n_oz / kOzT;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-    const int u = xcd + 8 * (q / ntiles);
-    const int tile = q % ntiles;
-    const int mod = u % kOzMods;
-    const int split = u / kOzMods;
-    if (split >= nsplit) return;
-    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-    while (I * (I + 1) / 2 > tile) --I;
-    I = __builtin_amdgcn_readfirstlane(I);
-    const int K = tile - I * (I + 1) / 2;
-    const int per = (nkc + nsplit - 1) / nsplit;
-    const int c0 = split * per;
-    const int nch = max(0, min(nkc, c0 + per) - c0);
-    const size_t kstride = (size_t)n_oz * kOzKC;
-    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I * kOzT * kOzKC;
-    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)K * kOzT * kOzKC;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wid >> 1, wc = wid & 1;
-    const int voff = wid * 4096 + lane * 16;
-
-    // piece g: operand g >> 2, 16-row block 4 wid + (g & 3); chunk index clamped to the split
-    auto gload = [&](int it, int g) -> v4i {
-        const int kc = c0 + min(it, nch - 1);
-        const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
-        return *(const v4i *)(src + voff);
-    };
-    auto lwrite = [&](int it, int g, v4i v) {
-        int8_t *dst = smem + (it & 1) * kOzStageBytes + (g >> 2) * kOzOpBytes + voff + (g & 3) * 1024;
-        *(v4i *)dst = v;
-    };
-
-    v4i acc[8][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
-
-    auto frag_a = [&](int chunk, int i) {
-        const int8_t *A_ = smem + (chunk & 1) * kOzStageBytes;
-        return *(const v4i *)&A_[(wr * 8 + i) * 1024 + lane * 16];
-    };
-    auto frag_b = [&](int chunk, int j) {
-        const int8_t *B_ = smem + (chunk & 1) * kOzStageBytes + kOzOpBytes;
-        return *(const v4i *)&B_[(wc * 8 + j) * 1024 + lane * 16];
-    };
-    v4i ring0[8], ring1[8];
-    auto step = [&](int it, v4i (&fa_c)[8], v4i (&fb_c)[8], v4i (&fa_n)[8], v4i (&fb_n)[8],
-                    v4i (&rg)[8]) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            oz_mfma16(acc[g][0], fb_c[0], fa_c[g]);
-            if (!(dbg & 1)) lwrite(it + 2, g, rg[g]);
-            oz_mfma16(acc[g][1], fb_c[1], fa_c[g]);
-            if (!(dbg & 2)) fa_n[g] = frag_a(it + 1, g);
-            oz_mfma16(acc[g][2], fb_c[2], fa_c[g]);
-            if (!(dbg & 1)) rg[g] = gload(it + 4, g);
-            oz_mfma16(acc[g][3], fb_c[3], fa_c[g]);
-            if (!(dbg & 2)) fb_n[g] = frag_b(it + 1, g);
-            oz_mfma16(acc[g][4], fb_c[4], fa_c[g]);
-            oz_mfma16(acc[g][5], fb_c[5], fa_c[g]);
-            oz_mfma16(acc[g][6], fb_c[6], fa_c[g]);
-            oz_mfma16(acc[g][7], fb_c[7], fa_c[g]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-
-    v4i fa0[8], fb0[8], fa1[8], fb1[8];
-    if (nch > 0) {
-        // chunks 0, 1 -> LDS stages 0, 1; chunks 2, 3 -> ring slots 0, 1
-#pragma unroll
-        for (int g = 0; g < 8; ++g) ring0[g] = gload(0, g);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) ring1[g] = gload(1, g);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) lwrite(0, g, ring0[g]);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) lwrite(1, g, ring1[g]);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) ring0[g] = gload(2, g);
-#pragma unroll
-        for (int g = 0; g < 8; ++g) ring1[g] = gload(3, g);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            fa0[i] = frag_a(0, i);
-            fb0[i] = frag_b(0, i);
-        }
-    }
-    int it = 0;
-    for (; it + 1 < nch; it += 2) {
-        step(it, fa0, fb0, fa1, fb1, ring0);
-        step(it + 1, fa1, fb1, fa0, fb0, ring1);
-    }
-    if (it < nch) step(it, fa0, fb0, fa1, fb1, ring0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
-    const int m = C.m[mod];
-    const double im = C.inv_m[mod];
-    const int hi = m / 2, lo = hi - m + 1;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int rowl = wr * 128 + i * 16 + (lane & 15);
-            const int col = wc * 128 + j * 16 + 4 * (lane >> 4);
-            unsigned int wv = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int cval = acc[i][j][r];
-                int rr = cval - (int)rint((double)cval * im) * m;
-                rr = rr > hi ? rr - m : (rr < lo ? rr + m : rr);
-                wv |= ((unsigned int)rr & 0xffu) << (8 * r);
-            }
-            *(unsigned int *)(out + rowl * kOzT + col) = wv;
-        }
 }
 
 // ---------------------------------------------------------------------------
@@ -824,7 +383,7 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16r(const int8_t *__restrict_
 // wid - 2 (72 MFMAs: D1 lower blocks in acc[i][j], i >= j; D2 strictly lower in acc[j][i];
 // D2's diagonal blocks in 8 VGPR accumulators).  Every wave reads the same 16 fragments of
 // its slot per chunk (blocks 8..15 as the A side, 0..7 as the K side).  The DMA ring and
-// the per-chunk protocol are k_oz_gemm16's.  The grid is tiles / 2 instead of tiles
+// the per-chunk protocol are oz_full_pass's.  The grid is tiles / 2 instead of tiles
 // workgroups for the diagonal band.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void oz_mfma16v(v4i &acc, const v4i &a, const v4i &b) {
@@ -951,8 +510,8 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
     }
 }
 
-// A full 256 x 256 off-diagonal tile on 4 waves (2 x 2, 128 x 128 each): k_oz_gemm16's
-// body with NW = 4, as a device pass for the unified launch below.
+// A full 256 x 256 off-diagonal tile on 4 waves (2 x 2, 128 x 128 each, 8 x 8 blocks of
+// 16 x 16 per wave, 256 AGPR accumulators), a device pass of the unified launch below.
 template <int dbg>
 __device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
                                              const int8_t *baseB, size_t kstride, int c0,
@@ -1098,110 +657,21 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
     }
 }
 
-template <int dbg>
-__global__ __launch_bounds__(256, 1) void k_oz_gemm16d(const int8_t *__restrict__ R, int n_oz,
-                                                       int nkc, int nsplit,
-                                                       int8_t *__restrict__ P, OzConsts C) {
-    __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
-    const int nt = n_oz / kOzT;
-    const int ntiles = nt * (nt + 1) / 2;
-    const int npair = (nt + 1) / 2;
-    const int b = blockIdx.x;
-    const int u = b / npair, pr = b % npair;
-    const int mod = u % kOzMods;
-    const int split = u / kOzMods;
-    if (split >= nsplit) return;
-    const int I1 = 2 * pr, I2 = min(2 * pr + 1, nt - 1);  // odd nt: the last tile twice
-    const int per = (nkc + nsplit - 1) / nsplit;
-    const int c0 = split * per;
-    const int nch = max(0, min(nkc, c0 + per) - c0);
-    const size_t kstride = (size_t)n_oz * kOzKC;
-    const int8_t *baseA = R + (size_t)mod * nkc * kstride + (size_t)I1 * kOzT * kOzKC;
-    const int8_t *baseB = R + (size_t)mod * nkc * kstride + (size_t)I2 * kOzT * kOzKC;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int slot = wid & 1;
-    const int Iw = slot ? I2 : I1;
-    const int tile = Iw * (Iw + 1) / 2 + Iw;
-    int8_t *out = P + (((size_t)split * kOzMods + mod) * ntiles + tile) * (size_t)(kOzT * kOzT);
-    if (wid < 2)
-        oz_diag_pass<dbg, false>(smem, baseA, baseB, kstride, c0, nch, wid, slot, out, C.m[mod],
-                                 C.inv_m[mod]);
-    else
-        oz_diag_pass<dbg, true>(smem, baseA, baseB, kstride, c0, nch, wid, slot, out, C.m[mod],
-                                C.inv_m[mod]);
-}
-
-static int oz_shape() {
-    static const int s = [] {
-        const char *e = getenv("BB_OZ_SHAPE");
-        if (e && std::strcmp(e, "16r") == 0) return 17;  // register-staged 16x16x64
-        return e ? atoi(e) : 16;
-    }();
-    return s;
-}
-
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
                     int dbg) {
     const int nt = n_oz / kOzT;
-    const int ntiles = nt * (nt + 1) / 2;
     const int nkc = p_pad / kOzKC;
-    // kOzMods * nsplit units, a multiple of 8 (kOzMods = 16): unit u -> XCD u % 8
-    const unsigned g = ntiles * kOzMods * nsplit;
     const OzConsts &C = oz_consts();
-    const int shape = oz_shape();
-    if (shape == 17) {
-        switch (dbg) {
-            case 1: k_oz_gemm16r<1><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 2: k_oz_gemm16r<2><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 3: k_oz_gemm16r<3><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            default: k_oz_gemm16r<0><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
-        }
-        return;
-    }
-    static const bool diag_pairs = [] {
-        const char *e = getenv("BB_OZ_DIAG");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    if (shape == 16 && diag_pairs) {
-        // off-diagonal tiles and diagonal pairs in one launch (k_oz_gemm16u)
-        const unsigned gu = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
-        switch (dbg) {
-            case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-            default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
-        }
-        return;
-    }
-    if (shape == 16 || shape == 8) {
-        const int nw = shape == 8 ? 8 : 4;
-#define BB_OZ16(D, W) k_oz_gemm16<D, W, kOzStages16><<<g, W * 64, 0, s>>>(R, n_oz, nkc, nsplit, P, C)
-#define BB_OZ(D)                                 \
-    case D:                                      \
-        if (nw == 8) BB_OZ16(D, 8);              \
-        else BB_OZ16(D, 4);                      \
-        break;
-        switch (dbg) {
-            BB_OZ(1) BB_OZ(2) BB_OZ(3) BB_OZ(4) BB_OZ(7) BB_OZ(8)
-            default:
-                if (nw == 8) BB_OZ16(0, 8);
-                else BB_OZ16(0, 4);
-        }
-#undef BB_OZ
-#undef BB_OZ16
-        return;
-    }
-    switch (dbg) {
-#define BB_OZ(D)                                                                  \
-    case D:                                                                       \
-        k_oz_gemm<D><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);                \
-        break;
-        BB_OZ(1) BB_OZ(2) BB_OZ(3) BB_OZ(4) BB_OZ(7)
-#undef BB_OZ
-        default:
-            k_oz_gemm<0><<<g, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
+    // per (modulus, split) unit -- kOzMods * nsplit units, a multiple of 8 (unit u -> XCD
+    // u % 8) -- the off-diagonal tiles and the diagonal pairs in one launch
+    const unsigned gu = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
+    switch (dbg) {  // dbg != 0: timing ablations of bb_bench_ozaki only (results meaningless)
+        case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
     }
 }
 

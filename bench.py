@@ -248,8 +248,8 @@ def main():
                     help="drive --gpus N devices from ONE process through an RCCL shard group "
                          "(ncclCommInitAll) -- the path the .C entry points use under R")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
-                    help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: env "
-                         "BB_GRAM_MODE, else the library default)")
+                    help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: the "
+                         "library default, Ozaki)")
     args = ap.parse_args()
     wn, wp, walpha, kind = WORKLOADS[args.workload]
     sparse, logit = kind == "sparse", kind == "logit"

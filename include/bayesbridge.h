@@ -199,7 +199,7 @@ typedef struct bb_config {
     uint64_t seed, stream;
     int device;
     int gram_mode;      /* Woodbury Gram: 0 fp64 MFMA, 1 Ozaki-II on int8 MFMA (fp64-accurate);
-                           default 1, or 0 when env BB_GRAM_MODE=fp64 */
+                           default 1 */
     int betaburn;       /* triangle method: rtnorm_gibbs passes per sweep - 1 */
 } bb_config;
 
