@@ -530,55 +530,87 @@ struct bb_engine {
 
 namespace {
 
-// Symmetric eigendecomposition G = V diag(ev) V' by cyclic Jacobi rotations (host, one-time
-// setup of the triangle method; O(p^3) per sweep of rotations, practical for p up to a few
-// hundred).  Column-major p x p; on return V's columns are eigenvectors.
-void jacobi_eigen(std::vector<double> A, int p, std::vector<double> &V, std::vector<double> &ev) {
+// Right singular vectors and singular values of X (n x p, column-major, n >= p) without
+// forming X'X, whose condition number is the square of X's: Householder QR X = Q R on the
+// host, then one-sided (Hestenes) Jacobi on the columns of R until every pair is orthogonal
+// to fp64 precision.  R V = U diag(d) gives X = (Q U) diag(d) V'.  O(n p^2 + sweeps p^3).
+void svd_right(const double *Xh, int n, int p, std::vector<double> &V, std::vector<double> &d) {
+    std::vector<double> A(Xh, Xh + (size_t)n * p);
+    auto col = [&](int j) { return &A[(size_t)j * n]; };
+    for (int k = 0; k < p && k < n; ++k) {
+        double *ak = col(k);
+        double nrm = 0.0;
+        for (int i = k; i < n; ++i) nrm += ak[i] * ak[i];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) continue;
+        const double alpha = ak[k] >= 0 ? -nrm : nrm;
+        ak[k] -= alpha;  // v = x - alpha e1 (stored in place)
+        double vv = 0.0;
+        for (int i = k; i < n; ++i) vv += ak[i] * ak[i];
+        for (int j = k + 1; j < p; ++j) {
+            double *aj = col(j);
+            double sdot = 0.0;
+            for (int i = k; i < n; ++i) sdot += ak[i] * aj[i];
+            const double f = 2.0 * sdot / vv;
+            for (int i = k; i < n; ++i) aj[i] -= f * ak[i];
+        }
+        ak[k] = alpha;
+        for (int i = k + 1; i < n; ++i) ak[i] = 0.0;
+    }
+    // W = R (p x p), V = I
+    std::vector<double> W((size_t)p * p, 0.0);
+    for (int j = 0; j < p; ++j)
+        for (int i = 0; i <= j && i < n; ++i) W[(size_t)j * p + i] = A[(size_t)j * n + i];
     V.assign((size_t)p * p, 0.0);
     for (int i = 0; i < p; ++i) V[(size_t)i * p + i] = 1.0;
-    auto at = [&](int i, int j) -> double & { return A[(size_t)j * p + i]; };
-    double fro = 0.0;
-    for (double x : A) fro += x * x;
-    for (int sweep = 0; sweep < 100; ++sweep) {
-        double off = 0.0;
-        for (int j = 0; j < p; ++j)
-            for (int i = 0; i < j; ++i) off += at(i, j) * at(i, j);
-        if (off <= 1e-32 * fro || off == 0.0) break;
-        for (int q = 1; q < p; ++q) {
-            for (int r = 0; r < q; ++r) {
-                const double arq = at(r, q);
-                if (arq == 0.0) continue;
-                const double theta = (at(q, q) - at(r, r)) / (2.0 * arq);
-                const double tt = (theta >= 0 ? 1.0 : -1.0) /
-                                  (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double cs = 1.0 / sqrt(tt * tt + 1.0), sn = tt * cs;
-                for (int k = 0; k < p; ++k) {  // columns r, q
-                    const double akr = at(k, r), akq = at(k, q);
-                    at(k, r) = cs * akr - sn * akq;
-                    at(k, q) = sn * akr + cs * akq;
-                }
-                for (int k = 0; k < p; ++k) {  // rows r, q
-                    const double ark = at(r, k), aqk = at(q, k);
-                    at(r, k) = cs * ark - sn * aqk;
-                    at(q, k) = sn * ark + cs * aqk;
-                }
+    std::vector<double> nrm2(p);
+    for (int sweep = 0; sweep < 80; ++sweep) {
+        long rotated = 0;
+        // squared column norms, refreshed every sweep and carried through each rotation
+        // (||w_i'||^2 = a - t c, ||w_j'||^2 = b + t c)
+        for (int j = 0; j < p; ++j) {
+            double s2 = 0.0;
+            for (int k = 0; k < p; ++k) s2 += W[(size_t)j * p + k] * W[(size_t)j * p + k];
+            nrm2[j] = s2;
+        }
+        for (int i = 0; i < p - 1; ++i) {
+            double *wi = &W[(size_t)i * p], *vi = &V[(size_t)i * p];
+            for (int j = i + 1; j < p; ++j) {
+                double *wj = &W[(size_t)j * p], *vj = &V[(size_t)j * p];
+                const double a = nrm2[i], b = nrm2[j];
+                double c = 0.0;
+                for (int k = 0; k < p; ++k) c += wi[k] * wj[k];
+                if (c == 0.0 || fabs(c) <= 1e-15 * sqrt(a * b)) continue;
+                ++rotated;
+                const double zeta = (b - a) / (2.0 * c);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double cs = 1.0 / sqrt(1.0 + t * t), sn = cs * t;
+                nrm2[i] = a - t * c;
+                nrm2[j] = b + t * c;
                 for (int k = 0; k < p; ++k) {
-                    double &vr = V[(size_t)r * p + k], &vq = V[(size_t)q * p + k];
-                    const double a0 = vr, b0 = vq;
-                    vr = cs * a0 - sn * b0;
-                    vq = sn * a0 + cs * b0;
+                    const double x = wi[k], y = wj[k];
+                    wi[k] = cs * x - sn * y;
+                    wj[k] = sn * x + cs * y;
+                    const double u = vi[k], w = vj[k];
+                    vi[k] = cs * u - sn * w;
+                    vj[k] = sn * u + cs * w;
                 }
             }
         }
+        if (rotated == 0) break;
     }
-    ev.resize(p);
-    for (int i = 0; i < p; ++i) ev[i] = at(i, i);
+    d.resize(p);
+    for (int j = 0; j < p; ++j) {
+        double s2 = 0.0;
+        for (int k = 0; k < p; ++k) s2 += W[(size_t)j * p + k] * W[(size_t)j * p + k];
+        d[j] = sqrt(s2);
+    }
 }
 
-// X = U diag(d) V' from G = X'X (BridgeRegression.cpp:47-57, svd 'S' for n > p): tV = V'
-// with singular values in decreasing order, each right singular vector signed so its
-// largest-magnitude entry is positive; a = d * U'y = V' X'y.
-void tri_setup(bb_engine *e) {
+// X = U diag(d) V' (BridgeRegression.cpp:47-57, svd 'S' for n > p): tV = V' with singular
+// values in decreasing order, each right singular vector signed so its largest-magnitude
+// entry is positive; a = d * U'y = V' X'y.
+void tri_setup(bb_engine *e, const double *Xh) {
     const int p = e->p, pp = e->p_pad;
     std::vector<double> Gp((size_t)pp * pp), c(pp);
     HIPCHECK(hipStreamSynchronize(e->stream));
@@ -590,11 +622,11 @@ void tri_setup(bb_engine *e) {
             const int r = i < j ? i : j, q = i < j ? j : i;
             G[(size_t)j * p + i] = Gp[(size_t)q * pp + r];
         }
-    std::vector<double> V, ev;
-    jacobi_eigen(G, p, V, ev);
+    std::vector<double> V, sv;
+    svd_right(Xh, e->n, p, V, sv);
     std::vector<int> ord(p);
     for (int i = 0; i < p; ++i) ord[i] = i;
-    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ev[x] > ev[y]; });
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return sv[x] > sv[y]; });
     e->h_tV.assign((size_t)p * p, 0.0);
     e->h_a.assign(p, 0.0);
     e->h_d.assign(p, 0.0);
@@ -613,7 +645,7 @@ void tri_setup(bb_engine *e) {
             a += x * c[j];
         }
         e->h_a[i] = a;
-        e->h_d[i] = sqrt(ev[ord[i]] > 0 ? ev[ord[i]] : 0.0);
+        e->h_d[i] = sv[ord[i]];
     }
     auto &o = e->owned;
     e->tVc = dalloc<double>((size_t)p * p, o);
@@ -789,7 +821,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->gdiag);
         }
     }
-    if (e->method == 4) tri_setup(e);
+    if (e->method == 4) tri_setup(e, Xh);
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -1538,7 +1570,7 @@ int bb_trunc_batch(int mode, int num, double *x, const double *p0, const double 
                 if (std::isnan(p0[i]) || std::isnan(p1[i]) || std::isnan(p2[i]) ||
                     std::isinf(p0[i]))
                     fprintf(stderr, "rtexpon_rate: caught non finite left value: %g; x[i] = %g.\n",
-                            p0[i], x[i]);
+                            p0[i], (double)NAN);  // printed before the draw overwrites it
         }
         rc = (f & (64u | 128u)) ? -2 : 0;
         if (rc) set_error("truncated draw: %s (flags %u)",

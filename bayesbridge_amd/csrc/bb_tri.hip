@@ -321,8 +321,9 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
                 shmin[i & 1][wv] = rmin;
             }
             // LDS-only barrier: __syncthreads() would also drain the row prefetch (vmcnt(0))
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            // LDS writes visible, then the barrier, in ONE asm statement with a memory
+            // clobber so no LDS access can be scheduled across the pair
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             double L = shmax[i & 1][0], R = shmin[i & 1][0];
 #pragma unroll
             for (int w = 1; w < kTriNT / 64; ++w) {
@@ -417,13 +418,12 @@ __global__ __launch_bounds__(256) void k_trunc_batch(int mode, int num, double *
             out = texpon(p0[i], p1[i], p2[i], e.r[0]);
             break;
         default: {  // rtexpon_rate(left, right, rate) (:805-830)
+            // the reference sets x = NaN and prints for a non-finite input, then the draw
+            // below overwrites it (no else): a non-finite right means left truncation only
             const double l = p0[i], rt = p1[i], rate = p2[i];
-            if (isnan(l) || isnan(rt) || isnan(rate) || isinf(l)) {
-                out = __builtin_nan("");
+            if (isnan(l) || isnan(rt) || isnan(rate) || isinf(l))
                 atomicOr(err, 256u);  // the host prints the reference's stderr line
-            } else {
-                out = texpon(l, isinf(rt) ? inf : rt, rate, e.r[0]);
-            }
+            out = texpon(l, isfinite(rt) ? rt : inf, rate, e.r[0]);
             break;
         }
     }

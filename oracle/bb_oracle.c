@@ -555,9 +555,10 @@ long bbo_trunc_batch(int mode, long num, double *x, const double *p0, const doub
         case 3: x[i] = bbo_texpon(p0[i], inf, p1[i], e[0]); break;
         case 4: x[i] = bbo_texpon(p0[i], p1[i], p2[i], e[0]); break;
         default: {
+            /* BridgeWrapper.cpp:816-828: the NaN set for a non-finite input is overwritten by
+             * the draw (no else); a non-finite right is left truncation only */
             const double l = p0[i], r = p1[i], rate = p2[i];
-            if (isnan(l) || isnan(r) || isnan(rate) || isinf(l)) x[i] = NAN;
-            else x[i] = bbo_texpon(l, isinf(r) ? inf : r, rate, e[0]);
+            x[i] = bbo_texpon(l, isfinite(r) ? r : inf, rate, e[0]);
         }
         }
         fails += f != 0;

@@ -1,8 +1,9 @@
 """GPU parity of the triangle-mixture sampler (bridge.reg.tri, .C("bridge_regression"))
 against the CPU oracle on the same Philox counters.
 
-The engine computes the design basis X = U diag(d) V' at setup (host Jacobi on the device
-Gram); the basis is checked on its own (orthonormal, reconstructs X'X, a = V'X'y) and then
+The engine computes the design basis X = U diag(d) V' at setup (host Householder QR of X,
+then one-sided Jacobi on R -- X'X is never formed, so the small singular values keep fp64
+accuracy relative to themselves up to cond(X)); the basis is checked on its own (orthonormal, reconstructs X'X, a = V'X'y) and then
 handed to the oracle, so the chain comparison covers everything downstream of it.
 Finding: free-running triangle chains are chaotic under fp64 roundoff.  A 3e-14 difference
 in the least-squares start grows about 3x per sweep (measured with tools/tri_diag.py:
@@ -51,17 +52,43 @@ def test_engine_basis_is_the_svd_of_x(gpu_lib, n, p):
     assert np.allclose(a, tV @ (X.T @ y), rtol=1e-10, atol=1e-10 * np.abs(a).max())
 
 
+def test_engine_basis_ill_conditioned(gpu_lib):
+    """Singular values spanning 7 decades (near-collinear columns): the engine's basis keeps
+    the smallest ones to ~1e-9 relative, where an eigendecomposition of X'X loses ~1e-3."""
+    rng = np.random.default_rng(8)
+    n, p = 200, 30
+    U, _ = np.linalg.qr(rng.standard_normal((n, p)))
+    W, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    s = np.logspace(0, -7, p)
+    X = np.asfortranarray(U @ np.diag(s) @ W.T)
+    y = rng.standard_normal(n)
+    _, (tV, a, d) = engine_basis(X, y)
+    assert np.max(np.abs(d - s) / s) < 1e-8
+    assert np.allclose(tV @ tV.T, np.eye(p), atol=1e-12)
+    # right singular vectors: |V' W| is a permutation-free identity (distinct values)
+    assert np.allclose(np.abs(tV @ W), np.eye(p), atol=1e-6)
+
+
 CASES = ["c1", "unknown_alpha", "betaburn", "known_tau_sig2", "ortho"]
+# larger p: all four waves of the 256-thread workgroup, strided ownership (e >= 1 for
+# p > 256), the cross-wave max/min exchange, p not a multiple of 64
+WIDE = [("c1", 700, 300), ("betaburn", 900, 517), ("ortho", 800, 600)]
 
 
-@pytest.mark.parametrize("case", CASES)
-def test_tri_sweeps_teacher_forced(gpu_lib, case):
-    n, p = (100, 20) if case != "betaburn" else (80, 33)
+@pytest.mark.parametrize("case,n,p", [(c, None, None) for c in CASES] + WIDE)
+def test_tri_sweeps_teacher_forced(gpu_lib, case, n, p):
+    if n is None:
+        n, p = (100, 20) if case != "betaburn" else (80, 33)
     X, y, _ = synthetic_problem(n, p, seed=5)
     alpha = 0.0 if case == "unknown_alpha" else 0.5
     betaburn = 2 if case == "betaburn" else 0
     tk = dict(true_sig2=1.5, true_tau=0.8) if case == "known_tau_sig2" else {}
-    seed, M = 777, 40
+    seed, M = 777, (40 if p < 100 else 12)
+    # one sweep is a chain of p sequential truncated-normal draws, each conditioned on the
+    # ones before: ulp-level differences (libm vs ocml, the partial-sum order of the
+    # conditional means) grow along it, measured ~5e-9 relative at p = 300 with identical
+    # mixture shapes (no decision flip); 1e-10 holds for p <= 33
+    tol = 1e-10 if p < 100 else 1e-8
     ortho = case == "ortho"
     e, basis = engine_basis(X, y, seed=seed, stream=0, true_alpha=alpha, betaburn=betaburn,
                             trace_capacity=1, ortho=ortho, **tk)
@@ -76,9 +103,9 @@ def test_tri_sweeps_teacher_forced(gpu_lib, case):
         g, gt = e.trace(0, 1), e.tri_trace(0, 1)
         assert np.array_equal(gt["shape"][:, 0], o["shape"][i]), i
         err = rel_l2(g["beta"][:, 0], o["beta"][i])
-        assert err < 1e-10, (i, err)
-        assert rel_l2(gt["u"][:, 0], o["u"][i]) < 1e-10, i
-        assert rel_l2(g["lambda"][:, 0], o["w"][i]) < 1e-10, i
+        assert err < tol, (i, err)
+        assert rel_l2(gt["u"][:, 0], o["u"][i]) < tol, i
+        assert rel_l2(g["lambda"][:, 0], o["w"][i]) < tol, i
         for k in ("tau", "sig2", "alpha"):
             assert rel(g[k][0], o[k][i]) < 1e-10, (i, k)
     assert e.error_flags() == 0

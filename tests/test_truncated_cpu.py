@@ -46,9 +46,15 @@ def test_special_values():
     x = oracle.trunc_batch("rtnorm", [np.array([np.nan, 0.0]), np.array([1.0, 1.0]),
                                       np.array([0.0, np.nan]), np.ones(2)], seed=4)
     assert np.all(np.isnan(x))
-    x = oracle.trunc_batch("rtexpon_rate", [np.array([-np.inf, 0.0, 0.0]),
-                                            np.array([1.0, np.inf, 2.0]), np.ones(3)], seed=4)
-    assert np.isnan(x[0]) and x[1] >= 0 and 0 <= x[2] <= 2
+    # rtexpon_rate (BridgeWrapper.cpp:816-828): the NaN the reference assigns for a
+    # non-finite input is overwritten by the draw that follows (no else), and a non-finite
+    # right bound means left truncation only -- reproduced, not replaced by NaN
+    x = oracle.trunc_batch("rtexpon_rate", [np.array([-np.inf, 0.0, 0.0, 1.0, np.nan, np.inf]),
+                                            np.array([1.0, np.inf, 2.0, np.nan, 2.0, np.inf]),
+                                            np.ones(6)], seed=4)
+    assert x[0] == -np.inf and x[1] >= 0 and 0 <= x[2] <= 2
+    assert x[3] >= 1.0 and np.isfinite(x[3])  # right = NaN: left-truncated draw
+    assert np.isnan(x[4]) and x[5] == np.inf
 
 
 def test_mytest_flags_r_special_values():

@@ -19,8 +19,11 @@ CASES = {
                np.inf, 2.0), rng.normal(0, 2, M), rng.uniform(0.1, 2, M)],
     "rtexpon_rate_left": [rng.normal(0, 3, M), rng.uniform(0.1, 5, M)],
     "rtexpon_rate_both": [np.zeros(M), rng.uniform(0.01, 4, M), rng.uniform(0.1, 5, M)],
-    "rtexpon_rate": [np.where(rng.random(M) < 0.05, np.nan, 1.0),
-                     np.where(rng.random(M) < 0.5, np.inf, 3.0), rng.uniform(0.1, 5, M)],
+    "rtexpon_rate": [np.where(rng.random(M) < 0.05, np.nan,
+                              np.where(rng.random(M) < 0.05, np.inf, 1.0)),
+                     np.where(rng.random(M) < 0.5, np.inf,
+                              np.where(rng.random(M) < 0.05, np.nan, 3.0)),
+                     rng.uniform(0.1, 5, M)],
 }
 CASES["rtnorm_both"][1] = np.maximum(CASES["rtnorm_both"][1], -0.5)
 
@@ -31,7 +34,9 @@ def test_trunc_batch_matches_oracle(gpu_lib, name):
     g = bb.trunc_batch(name, params, seed=123, stream=4)
     o = oracle.trunc_batch(name, params, seed=123, stream=4)
     assert np.array_equal(np.isnan(g), np.isnan(o))
-    ok = ~np.isnan(o)
+    assert np.array_equal(np.isinf(g), np.isinf(o)) and np.array_equal(g[np.isinf(o)],
+                                                                        o[np.isinf(o)])
+    ok = np.isfinite(o)
     assert np.allclose(g[ok], o[ok], rtol=1e-12, atol=1e-300)
 
 
