@@ -515,3 +515,82 @@ def test_bridge_em_batch_matches_oracle(gpu_lib, n, p):
         assert np.max(np.abs(beta[r] - o)) <= 1e-9 * scale, ratio
     tr = bb.trace_beta(y, X, ratio_grid=grid)
     assert np.array_equal(tr["beta"], beta)
+
+
+# ---------------------------------------------------------------------------------------
+# The Ozaki-II Gram on the prior variances the chain actually produces, and a long
+# free-running p > n chain against an independent oracle chain (statistical parity).
+# ---------------------------------------------------------------------------------------
+def _gram_errors(bb, Y, w, rows):
+    """Max error of the Ozaki and fp64 Grams over the rows x rows block against an 80-bit
+    reference, relative to (|Y| w |Y|')_ik."""
+    Cz = bb.gram(Y, w, mode=bb.GRAM_OZAKI)[np.ix_(rows, rows)]
+    C6 = bb.gram(Y, w)[np.ix_(rows, rows)]
+    Yl = Y[rows].astype(np.longdouble)
+    ref = (Yl * w.astype(np.longdouble)) @ Yl.T
+    scale = (np.abs(Y[rows]) * w) @ np.abs(Y[rows]).T
+    return (float(np.max(np.abs(Cz - ref) / scale)), float(np.max(np.abs(C6 - ref) / scale)))
+
+
+def test_gram_ozaki_on_c3_chain_prior_variances(gpu_lib):
+    """D = tau^2 / lambda after 120 sweeps of the C3 bench chain (beta_j ~ 0 for most j, so
+    lambda comes from the h = 0 stable law and D spans many decades): the Ozaki Gram keeps
+    the 2e-15 / 4x-fp64 bounds of test_gram_ozaki_fp64_accuracy on that D."""
+    import bench
+    bb = gpu_lib
+    n, p = 2000, 50000
+    X = bench.make_columns(n, 0, p)
+    y, _ = bench.make_problem_y(n, p)
+    e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, gram_mode=bb.GRAM_OZAKI), X, y)
+    e.init_state()
+    e.run(1, 120)
+    s = e.state()
+    e.close()
+    D = s["tau"] ** 2 / s["lambda"]
+    span = np.log10(D.max() / D.min())
+    assert span > 10, span
+    rows = np.sort(np.random.default_rng(4).choice(n, 48, replace=False))
+    e_oz, e_64 = _gram_errors(bb, np.asfortranarray(X), D, rows)
+    assert e_oz < 2e-15, (e_oz, e_64, span)
+    assert e_oz < 4 * max(e_64, 1e-16), (e_oz, e_64)
+
+
+def test_gram_ozaki_thirty_decades(gpu_lib):
+    bb = gpu_lib
+    rng = np.random.default_rng(30)
+    Y = rng.standard_normal((300, 3000))
+    w = 10.0 ** rng.uniform(-25, 5, 3000)
+    e_oz, e_64 = _gram_errors(bb, Y, w, np.arange(300))
+    assert e_oz < 2e-15, (e_oz, e_64)
+    assert e_oz < 4 * max(e_64, 1e-16), (e_oz, e_64)
+
+
+def test_long_free_running_wide_chain_statistics(gpu_lib):
+    """A free-running p > n chain (60 x 250, 5000 samples) decouples from any same-seed
+    oracle chain within ~100 sweeps, so its parity is statistical: posterior
+    means and sds against an independent long oracle chain (another key), within
+    Monte-Carlo error from coda-style effective sample sizes."""
+    from bayesbridge_amd.diagnostics import effective_size
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(60, 250, seed=11)
+    M, B = 5000, 500
+    # sig2 known: with p > n and the Jeffreys sig2 prior the posterior has a degenerate mode
+    # at sig2 -> 0 (an exact fit); the oracle chain itself falls into it near sweep 1860
+    # (sig2 ~ 5e-15, I + X D X'/sig2 numerically singular)
+    bb.set_seed(SEED + 40)
+    g = bb.bridge_reg_stb(y, X, nsamp=M, burn=B, sig2_true=1.0)["beta"]
+    o = gibbs.bridge_regression_stable(y, X, M, burn=B, seed=SEED + 41, stream=0,
+                                       method="woodbury", true_sig2=1.0)["beta"].T
+    for tr in (g, o):
+        assert np.all(np.isfinite(tr))
+    mg, mo = g.mean(axis=0), o.mean(axis=0)
+    sg, so = g.std(axis=0), o.std(axis=0)
+    eg = np.maximum(effective_size(g), 20.0)
+    eo = np.maximum(effective_size(o), 20.0)
+    z = (mg - mo) / np.sqrt(sg ** 2 / eg + so ** 2 / eo)
+    assert np.max(np.abs(z)) < 5.0, float(np.max(np.abs(z)))
+    assert 0.3 < np.sqrt(np.mean(z ** 2)) < 1.6, float(np.sqrt(np.mean(z ** 2)))
+    # posterior sds of the larger half agree to 30 % (two oracle chains with different keys:
+    # max deviation 18 %, max |z| 3.7, rms z 1.16)
+    big = sg > np.median(sg)
+    assert np.max(np.abs(sg[big] / so[big] - 1)) < 0.3
