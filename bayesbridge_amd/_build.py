@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SO_PATH = os.path.join(HERE, "BayesBridge.so")
 SOURCES = ["bb_kernels.hip", "bb_ozaki.hip", "bb_tri.hip", "bb_sparse.hip", "bb_logit.hip",
-           "bb_engine.cpp"]
+           "bb_small.hip", "bb_engine.cpp"]
 HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h", "bb_sparse.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 

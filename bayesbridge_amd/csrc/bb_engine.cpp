@@ -264,6 +264,7 @@ struct bb_engine {
     int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture, 5 sparse woodbury,
                      // 6 logistic (Polya-Gamma)
     int group = 1;
+    bool fused = false;  // small p: whole sweeps in one launch (bb_small.hip)
     SparseDesign spd;  // method 5: CSC/CSR design and the Gram pair list
     Hyper hy{};
     hipStream_t stream = nullptr;
@@ -510,6 +511,26 @@ struct bb_engine {
 
     size_t red1_count() const { return (size_t)nbS + n_pad; }
     size_t red2_count() const { return tri_count(n_pad) + n_pad; }
+
+    // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
+    void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
+        if (fused) {
+            if (timing) {
+                sweep_marks.emplace_back();
+                mark(PH_BETA);
+            }
+            launch_small_chain(stream, X, n_pad, n, p, y, G, p_pad, cvec, gdiag, method == 3,
+                               beta, lam, sc, hy, cfg.seed, cfg.stream, t0, count, first_slot,
+                               slot_step, cap, tr_beta, tr_lam, tr_sig2, tr_tau, tr_alpha, err);
+            if (timing) mark(PH_END);
+            xbeta();  // keeps the X beta partials current for anything run after
+            return;
+        }
+        for (int k = 0; k < count; ++k) {
+            const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
+            sweep(t0 + (uint64_t)k, slot, mcmc_phase);
+        }
+    }
 
     void sweep(uint64_t t, int slot, int mcmc_phase) {
         phase_a(t);
@@ -822,6 +843,9 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         }
     }
     if (e->method == 4) tri_setup(e, Xh);
+    // small p, one device, alpha known: whole sweeps in one single-workgroup launch
+    e->fused = (e->method == 1 || e->method == 3) && c.p <= kSmallChainMaxP && c.world == 1 &&
+               e->hy.know_alpha && e->cvec && e->gdiag && (e->method == 3 || e->G);
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -886,6 +910,11 @@ void engine_init_state(bb_engine *e) {
         e->pre_and_scalars(0, 0, 1);  // :262
     }
     HIPCHECK(hipStreamSynchronize(e->stream));
+}
+
+// one contiguous run of trace-ring doubles to the host (one copy, not one per sample)
+void ring_copy(double *dst, const double *src, size_t count) {
+    HIPCHECK(hipMemcpy(dst, src, count * sizeof(double), hipMemcpyDeviceToHost));
 }
 
 }  // namespace
@@ -1043,10 +1072,7 @@ int bb_engine_run(bb_engine *e, uint64_t t0, int count, int first_slot, int slot
                   int mcmc_phase) {
     try {
         HIPCHECK(hipSetDevice(e->cfg.device));
-        for (int k = 0; k < count; ++k) {
-            const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
-            e->sweep(t0 + (uint64_t)k, slot, mcmc_phase);
-        }
+        e->run(t0, count, first_slot, slot_step, mcmc_phase);
         HIPCHECK(hipGetLastError());
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -1069,22 +1095,17 @@ int bb_engine_get_trace(bb_engine *e, int slot0, int count, double *beta, double
                         double *sig2, double *tau, double *alpha) {
     try {
         HIPCHECK(hipStreamSynchronize(e->stream));
-        for (int k = 0; k < count; ++k) {
+        const size_t pl = (size_t)e->p_loc;
+        // slots [slot0, slot0 + count) of the ring: at most two contiguous runs per trace
+        for (int k = 0; k < count;) {
             const int s = (slot0 + k) % e->cap;
-            const size_t pl = (size_t)e->p_loc;
-            if (beta)
-                HIPCHECK(hipMemcpy(beta + k * pl, e->tr_beta + s * pl, pl * sizeof(double),
-                                   hipMemcpyDeviceToHost));
-            if (lambda)
-                HIPCHECK(hipMemcpy(lambda + k * pl, e->tr_lam + s * pl, pl * sizeof(double),
-                                   hipMemcpyDeviceToHost));
-            if (sig2)
-                HIPCHECK(hipMemcpy(sig2 + k, e->tr_sig2 + s, sizeof(double), hipMemcpyDeviceToHost));
-            if (tau)
-                HIPCHECK(hipMemcpy(tau + k, e->tr_tau + s, sizeof(double), hipMemcpyDeviceToHost));
-            if (alpha)
-                HIPCHECK(
-                    hipMemcpy(alpha + k, e->tr_alpha + s, sizeof(double), hipMemcpyDeviceToHost));
+            const int run = std::min(count - k, e->cap - s);
+            if (beta) ring_copy(beta + k * pl, e->tr_beta + s * pl, run * pl);
+            if (lambda) ring_copy(lambda + k * pl, e->tr_lam + s * pl, run * pl);
+            if (sig2) ring_copy(sig2 + k, e->tr_sig2 + s, run);
+            if (tau) ring_copy(tau + k, e->tr_tau + s, run);
+            if (alpha) ring_copy(alpha + k, e->tr_alpha + s, run);
+            k += run;
         }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -1155,14 +1176,12 @@ int bb_engine_get_tri_trace(bb_engine *e, int slot0, int count, double *u, doubl
         if (e->method != 4) throw HipError("not a triangle-method engine");
         HIPCHECK(hipStreamSynchronize(e->stream));
         const size_t pl = (size_t)e->p_loc;
-        for (int k = 0; k < count; ++k) {
+        for (int k = 0; k < count;) {
             const int s = (slot0 + k) % e->cap;
-            if (u)
-                HIPCHECK(hipMemcpy(u + k * pl, e->tr_u + s * pl, pl * sizeof(double),
-                                   hipMemcpyDeviceToHost));
-            if (shape)
-                HIPCHECK(hipMemcpy(shape + k * pl, e->tr_shape + s * pl, pl * sizeof(double),
-                                   hipMemcpyDeviceToHost));
+            const int run = std::min(count - k, e->cap - s);
+            if (u) ring_copy(u + k * pl, e->tr_u + s * pl, run * pl);
+            if (shape) ring_copy(shape + k * pl, e->tr_shape + s * pl, run * pl);
+            k += run;
         }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());

@@ -182,6 +182,18 @@ void launch_pg(hipStream_t s, const double *psi, int n, int n_pad, uint64_t k0, 
                uint64_t t, double *omega, uint32_t *err);
 void launch_kappa(hipStream_t s, const double *y, int n, int n_pad, double *kappa);
 
+// Small-p fused chain (bb_small.hip): `count` whole sweeps (tau, sig2, lambda, beta by the
+// p x p Cholesky draw, or the orthogonal-design draw) in ONE single-workgroup launch, for
+// p <= kSmallChainMaxP and alpha known.  Sweep k uses counter t0 + k and trace slot
+// (first_slot + k slot_step) % cap (first_slot < 0: none).
+constexpr int kSmallChainMaxP = 16;
+void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
+                        const double *G, int ldg, const double *cvec, const double *gdiag,
+                        int ortho, double *beta, double *lam, DevScalars *sc, Hyper hy,
+                        uint64_t k0, uint64_t k1, uint64_t t0, int count, int first_slot,
+                        int slot_step, int cap, double *tr_beta, double *tr_lam, double *tr_sig2,
+                        double *tr_tau, double *tr_alpha, uint32_t *err);
+
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
                            double *sig2_tr, double *alpha_tr);

@@ -86,6 +86,15 @@ __device__ __forceinline__ double normal_at(Key key, uint64_t t, unsigned kind, 
     return bm_normal(u.r[0], u.r[1]);
 }
 
+// Attempt caps of the rejection loops (a debug build lowers them so that a bad input ends
+// in an error flag within microseconds instead of seconds)
+#ifndef BB_MAX_GAMMA_ATTEMPTS
+#define BB_MAX_GAMMA_ATTEMPTS (1ull << 24)
+#endif
+#ifndef BB_MAX_STABLE_ROUNDS
+#define BB_MAX_STABLE_ROUNDS (1 << 22)
+#endif
+
 // Ga(shape, rate 1): Marsaglia & Tsang (2000), one Philox block per attempt,
 // boost u^(1/a) for shape < 1.  Stream (t, kind, j=0, attempt, 0).
 __device__ inline double gamma1(double shape, Key key, uint64_t t, unsigned kind,
@@ -98,7 +107,7 @@ __device__ inline double gamma1(double shape, Key key, uint64_t t, unsigned kind
     }
     double d = a - 1.0 / 3.0;
     double cc = 1.0 / sqrt(9.0 * d);
-    for (uint64_t k = 0; k < (1ull << 24); ++k) {
+    for (uint64_t k = 0; k < BB_MAX_GAMMA_ATTEMPTS; ++k) {
         U4 u = uniforms(key, t, kind, 0, k, 0);
         double x = bm_normal(u.r[0], u.r[1]);
         double v = 1.0 + cc * x;
@@ -298,7 +307,7 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
         s = stable_params(h, alpha, V0);
     }
     uint64_t o = 0, ib = 0;
-    for (int iter = 0; iter < (1 << 22); ++iter) {
+    for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
         bool acc = false;
         double U = 0.0, z = 0.0, Z = 0.0;
         if (!done) acc = stable_inner<NI>(s, key, t, j, o, ib + (uint64_t)g, U, z, Z);
@@ -319,6 +328,76 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
                     ++o;
                     ib = 0;
                 }
+            }
+        }
+        if (__all(done)) break;
+    }
+    if (!done) {
+        atomicOr(err, 2u);
+        result = __builtin_nan("");
+    }
+    return result;
+}
+
+// Latency-oriented variant for chains with few coefficients (bb_small.hip): the L lanes of a
+// group are O = L / I segments of I lanes, and segment k evaluates I inner attempts of outer
+// attempt o0 + k and then that attempt's outer test, so one round covers O outer attempts.
+// Scanning the segments in counter order, the first one that either accepted no inner
+// attempt (continue its inner loop next round) or passed its outer test (done) decides;
+// outer attempts before it were rejected exactly as the sequential loop rejects them, so the
+// draw is the same as stable_group_draw's.  About 1 in 8 draws needs a second round at
+// I = 8, O = 4 (inner acceptance ~0.3, outer ~0.7 at alpha = 0.25).
+template <int L, int I>
+__device__ inline double stable_spec_draw(bool active, double h, double alpha, double V0, Key key,
+                                          uint64_t t, uint64_t j, uint32_t *err) {
+    static_assert(L <= 64 && (L & (L - 1)) == 0 && L % I == 0 && I < 64, "group shape");
+    constexpr int O = L / I;
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (L - 1), gbase = lane & ~(L - 1);
+    const int seg = g / I, ii = g % I;
+    const uint64_t imask = (1ull << I) - 1ull;
+    if (active && alpha == 1.) active = false;  // retstable.cpp:104-110
+    double result = V0;
+    bool done = !active;
+    StableParams s;
+    if (active) {
+        if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) atomicOr(err, 4u);  // :112-115
+        s = stable_params(h, alpha, V0);
+    }
+    uint64_t o0 = 0, ib = 0;  // window's first outer attempt, its next inner attempt
+    for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
+        const uint64_t o = o0 + (uint64_t)seg;
+        double U = 0.0, z = 0.0, Z = 0.0;
+        bool acc = false;
+        if (!done)
+            acc = stable_inner<false>(s, key, t, j, o, (seg == 0 ? ib : 0) + (uint64_t)ii, U, z, Z);
+        const uint64_t sb = ((__ballot(acc) >> gbase) >> (seg * I)) & imask;
+        const int src = gbase + seg * I + (sb ? (__ffsll((unsigned long long)sb) - 1) : 0);
+        const double Uw = __shfl(U, src, 64), zw = __shfl(z, src, 64), Zw = __shfl(Z, src, 64);
+        double X = 0.0;
+        bool oacc = false;
+        if (!done && sb) oacc = stable_outer<false>(s, key, t, j, o, Uw, zw, Zw, X);
+        const uint64_t hb = __ballot(ii == 0 && sb != 0) >> gbase;
+        const uint64_t ab = __ballot(ii == 0 && oacc) >> gbase;
+        unsigned H = 0, A = 0;
+#pragma unroll
+        for (int k = 0; k < O; ++k) {
+            H |= (unsigned)((hb >> (k * I)) & 1ull) << k;
+            A |= (unsigned)((ab >> (k * I)) & 1ull) << k;
+        }
+        const unsigned stop = (~H & ((1u << O) - 1u)) | A;
+        const int k = stop ? (__ffs(stop) - 1) : O;
+        const double Xk = __shfl(X, gbase + (k < O ? k : 0) * I, 64);
+        if (!done) {
+            if (k == O) {  // all O outer attempts rejected
+                o0 += O;
+                ib = 0;
+            } else if ((A >> k) & 1u) {
+                result = stable_finish(s, Xk);
+                done = true;
+            } else {  // outer attempt o0 + k needs more inner attempts
+                ib = (k == 0) ? ib + I : (uint64_t)I;
+                o0 += (uint64_t)k;
             }
         }
         if (__all(done)) break;

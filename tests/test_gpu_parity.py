@@ -185,10 +185,15 @@ def compare_chain(g, o, tol_mean=1e-8, tol_elem=1e-6):
     dict(tau_true=0.8),
     dict(alpha=0.3, nu_shape=0.5, nu_rate=0.5),
 ])
-def test_chain_small_p_matches_oracle(gpu_lib, kw):
-    """C1 (n=100, p=20): reference-literal p x p Cholesky path, full chain."""
+@pytest.mark.parametrize("n,p", [(100, 20), (120, 40), (50, 6), (200, 16), (100, 13),
+                                 (3000, 8)])
+def test_chain_small_p_matches_oracle(gpu_lib, kw, n, p):
+    """C1 (n=100, p=20): reference-literal p x p Cholesky draw, full chain -- through the
+    general path (p = 20, 40) and the fused single-launch kernel (p <= 16, bb_small.hip: 64
+    lanes per lambda draw and an 8 x 8 padded system at p = 6, 8; 32 lanes and 16 x 16 at
+    p = 13, 16; X from HBM instead of LDS at n = 3000)."""
     bb = gpu_lib
-    X, y, _ = synthetic_problem(100, 20)
+    X, y, _ = synthetic_problem(n, p)
     bb.set_seed(SEED)
     g = bb.bridge_reg_stb(y, X, nsamp=300, burn=100, **kw)
     o = gibbs.bridge_regression_stable(
