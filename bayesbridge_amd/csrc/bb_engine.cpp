@@ -276,6 +276,7 @@ struct bb_engine {
     uint32_t *err = nullptr;
     double *xb_part = nullptr, *red1 = nullptr;
     int nparts = 0, nbS = 0;
+    bool xb_stale = false;  // a fused run left the X beta partials behind beta
     // woodbury
     double *slabs = nullptr, *xu_part = nullptr, *red2 = nullptr, *M = nullptr, *w = nullptr,
            *Wd = nullptr;
@@ -357,6 +358,7 @@ struct bb_engine {
 
     // X beta of the current beta into the partials k_pre sums next
     void xbeta() {
+        xb_stale = false;
         if (method == 5) {
             launch_sp_rows(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, beta, nullptr,
                            xb_part, nullptr);
@@ -368,6 +370,7 @@ struct bb_engine {
     }
 
     void pre_and_scalars(uint64_t t, int slot, int tau_only) {
+        if (xb_stale) xbeta();
         launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
         allreduce(red1, (size_t)nbS + n_pad);
         launch_scalars(stream, red1, nbS, y, n, p, sc, hy, cfg.seed, cfg.stream, t,
@@ -383,6 +386,7 @@ struct bb_engine {
         (void)t;
         if (timing) sweep_marks.emplace_back();
         mark(PH_PRE);
+        if (xb_stale) xbeta();
         launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
     }
 
@@ -519,11 +523,18 @@ struct bb_engine {
                 sweep_marks.emplace_back();
                 mark(PH_BETA);
             }
-            launch_small_chain(stream, X, n_pad, n, p, y, G, p_pad, cvec, gdiag, method == 3,
-                               beta, lam, sc, hy, cfg.seed, cfg.stream, t0, count, first_slot,
-                               slot_step, cap, tr_beta, tr_lam, tr_sig2, tr_tau, tr_alpha, err);
+            if (method == 4)
+                launch_tri_chain(stream, X, n_pad, n, p, y, tVc, tVr, tri_a, tri_d, beta, u, lam,
+                                 D, sc, hy, cfg.betaburn, cfg.seed, cfg.stream, t0, count,
+                                 first_slot, slot_step, cap, tr_beta, tr_u, tr_lam, tr_shape,
+                                 tr_sig2, tr_tau, tr_alpha, err);
+            else
+                launch_small_chain(stream, X, n_pad, n, p, y, G, p_pad, cvec, gdiag, method == 3,
+                                   beta, lam, sc, hy, cfg.seed, cfg.stream, t0, count,
+                                   first_slot, slot_step, cap, tr_beta, tr_lam, tr_sig2, tr_tau,
+                                   tr_alpha, err);
             if (timing) mark(PH_END);
-            xbeta();  // keeps the X beta partials current for anything run after
+            xb_stale = true;  // X beta partials refreshed only if a general sweep needs them
             return;
         }
         for (int k = 0; k < count; ++k) {
@@ -846,6 +857,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     // small p, one device, alpha known: whole sweeps in one single-workgroup launch
     e->fused = (e->method == 1 || e->method == 3) && c.p <= kSmallChainMaxP && c.world == 1 &&
                e->hy.know_alpha && e->cvec && e->gdiag && (e->method == 3 || e->G);
+    if (e->method == 4)  // bb_tri.hip k_tri_chain: non-orthogonal design only
+        e->fused = !c.ortho && c.p <= kTriChainMaxP && c.world == 1 && e->hy.know_alpha;
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -2380,6 +2393,7 @@ struct Chain {
         for (auto *e : eng) bb_engine_destroy(e);
     }
     int init() { return grp ? bb_group_init_state(grp) : bb_engine_init_state(eng[0]); }
+    bool fused() const { return !grp && eng.size() == 1 && eng[0]->fused; }
     int run(uint64_t t0, int count, int slot, int step, int mcmc) {
         return grp ? bb_group_run(grp, t0, count, slot, step, mcmc)
                    : bb_engine_run(eng[0], t0, count, slot, step, mcmc);
@@ -2479,7 +2493,10 @@ enum Outcome { OUT_OK = 0, OUT_ERROR = 1, OUT_INTERRUPTED = 2 };
 Outcome drive_chain(Chain &ch, int nburn, uint64_t t_base, int m, int b, double *betap,
                     double *lambdap, double *sig2p, double *taup, double *alphap,
                     double *runtime, double *up = nullptr, double *shapep = nullptr) {
-    constexpr int kBlock = 10;  // BridgeWrapper.cpp:273-275, 295-297: every 10 sweeps
+    // BridgeWrapper.cpp:273-275, 295-297 poll every 10 sweeps.  A fused engine runs a
+    // whole block in one launch at ~15-30 us per sweep, so it polls every 50 (< 2 ms) and
+    // pays the launch and LDS-staging prologue once per 50 sweeps instead of per 10.
+    const int kBlock = ch.fused() ? 50 : 10;
     *runtime = 0.0;
     if (ch.init() != 0) return OUT_ERROR;
     bool interrupted = false;

@@ -194,6 +194,19 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
                         int slot_step, int cap, double *tr_beta, double *tr_lam, double *tr_sig2,
                         double *tr_tau, double *tr_alpha, uint32_t *err);
 
+// Whole triangle-mixture sweeps (non-orthogonal design, alpha known, p <= kTriChainMaxP) in
+// one single-workgroup launch (bb_tri.hip k_tri_chain): S_alpha / rss, tau and sig2, then
+// omega, u and the rtnorm_gibbs passes of launch_tri_update in one wave, `count` sweeps from
+// t0 with the trace-slot convention of launch_small_chain.
+constexpr int kTriChainMaxP = 32;
+void launch_tri_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
+                      const double *tVc, const double *tVr, const double *a, const double *d,
+                      double *beta, double *u, double *omega, double *shape, DevScalars *sc,
+                      Hyper hy, int betaburn, uint64_t k0, uint64_t k1, uint64_t t0, int count,
+                      int first_slot, int slot_step, int cap, double *tr_beta, double *tr_u,
+                      double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,
+                      double *tr_alpha, uint32_t *err);
+
 // Copy the scalars into trace slots (known parameters / alpha when known).
 void launch_record_scalars(hipStream_t s, const DevScalars *sc, double *tau_tr,
                            double *sig2_tr, double *alpha_tr);

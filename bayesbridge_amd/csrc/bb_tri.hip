@@ -39,6 +39,13 @@ struct Pre {
     double r0, r1, x0;
 };
 
+__device__ __forceinline__ double readlane_dd(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ __forceinline__ void attempt(Key key, uint64_t t, uint64_t i, uint64_t it, long k,
                                         const Pre &pre, double &r0, double &r1, double &x0,
                                         bool need_x) {
@@ -56,13 +63,15 @@ __device__ __forceinline__ void attempt(Key key, uint64_t t, uint64_t i, uint64_
 
 // Force-inlined: the compiler outlined tnorm, and an out-of-line call inside the
 // coordinate loop costs its prologue's s_waitcnt vmcnt(0), which drains the row prefetch
-// on every coordinate.
-__device__ __forceinline__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i, uint64_t it,
-                         const Pre &pre, uint32_t *err) {
+// on every coordinate.  k0 > 0 resumes the rejection loop at attempt k0 (k_tri_chain's
+// fall-through after its parallel attempts; `pre` is then unused).
+__device__ __forceinline__ double tn_pos(double a, double b, Key key, uint64_t t, uint64_t i,
+                                         uint64_t it, const Pre &pre, uint32_t *err,
+                                         long k0 = 0) {
     const double sq = sqrt(a * a + 4.0);
     const double as = 0.5 * (a + sq);
     const double thr = a + 2.0 / (a + sq) * exp(0.5 + 0.25 * (a * a - a * sq));
-    for (long k = 0; k < kTnMaxAttempts; ++k) {
+    for (long k = k0; k < kTnMaxAttempts; ++k) {
         double r0, r1, x0;
         attempt(key, t, i, it, k, pre, r0, r1, x0, false);
         if (b <= thr) {
@@ -78,8 +87,9 @@ __device__ __forceinline__ double tn_pos(double a, double b, Key key, uint64_t t
     return a;
 }
 
-__device__ __forceinline__ double tnorm(double lo, double hi, double mu, double sd, Key key, uint64_t t,
-                        uint64_t i, uint64_t it, const Pre &pre, uint32_t *err) {
+__device__ __forceinline__ double tnorm(double lo, double hi, double mu, double sd, Key key,
+                                        uint64_t t, uint64_t i, uint64_t it, const Pre &pre,
+                                        uint32_t *err, long k0 = 0) {
     const double a = (lo - mu) / sd, b = (hi - mu) / sd;
     if (!(a < b)) {
         atomicOr(err, 128u);
@@ -87,7 +97,7 @@ __device__ __forceinline__ double tnorm(double lo, double hi, double mu, double 
     }
     if (a <= 0.0 && b >= 0.0) {
         const bool wide = (b - a) >= 2.5066282746310002;  // sqrt(2 pi)
-        for (long k = 0; k < kTnMaxAttempts; ++k) {
+        for (long k = k0; k < kTnMaxAttempts; ++k) {
             double r0, r1, x0;
             attempt(key, t, i, it, k, pre, r0, r1, x0, wide);
             if (wide) {
@@ -100,8 +110,54 @@ __device__ __forceinline__ double tnorm(double lo, double hi, double mu, double 
         atomicOr(err, 64u);
         return lo;
     }
-    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, pre, err);
-    return mu - sd * tn_pos(-b, -a, key, t, i, it, pre, err);
+    if (a > 0.0) return mu + sd * tn_pos(a, b, key, t, i, it, pre, err, k0);
+    return mu - sd * tn_pos(-b, -a, key, t, i, it, pre, err, k0);
+}
+
+// The same draw with attempts 0 .. K-1 evaluated in parallel, attempt k in lane k from its
+// precomputed (r0, r1, x0): the lowest accepted attempt is the sequential loop's answer;
+// if none of the K is accepted the loop resumes at attempt K.  lo, hi, mu, sd uniform; every
+// lane of the wave calls this.
+template <int K>
+__device__ __forceinline__ double tnorm_par(double lo, double hi, double mu, double sd,
+                                            double r0, double r1, double x0, Key key,
+                                            uint64_t t, uint64_t i, uint64_t it, uint32_t *err) {
+    const int lane = threadIdx.x & 63;
+    const double a = (lo - mu) / sd, b = (hi - mu) / sd;
+    if (!(a < b)) {
+        atomicOr(err, 128u);
+        return lo;
+    }
+    bool acc = false;
+    double val = 0.0;
+    if (a <= 0.0 && b >= 0.0) {
+        if ((b - a) >= 2.5066282746310002) {  // sqrt(2 pi)
+            acc = x0 >= a && x0 <= b;
+            val = mu + sd * x0;
+        } else {
+            const double x = a + (b - a) * r0;
+            acc = r1 <= exp(-0.5 * x * x);
+            val = mu + sd * x;
+        }
+    } else {
+        const double pa = a > 0.0 ? a : -b, pb = a > 0.0 ? b : -a;  // tn_pos's (a, b)
+        const double sq = sqrt(pa * pa + 4.0);
+        const double as = 0.5 * (pa + sq);
+        const double thr = pa + 2.0 / (pa + sq) * exp(0.5 + 0.25 * (pa * pa - pa * sq));
+        double x;
+        if (pb <= thr) {
+            x = pa + (pb - pa) * r0;
+            acc = r1 <= exp(0.5 * (pa * pa - x * x));
+        } else {
+            x = pa - log(r0) / as;
+            const double e = x - as;
+            acc = x <= pb && r1 <= exp(-0.5 * e * e);
+        }
+        val = a > 0.0 ? mu + sd * x : mu - sd * x;
+    }
+    const uint64_t m = __ballot(acc && lane < K);
+    if (m) return readlane_dd(val, __ffsll((unsigned long long)m) - 1);
+    return tnorm(lo, hi, mu, sd, key, t, i, it, Pre{0.0, 0.0, 0.0}, err, K);
 }
 
 // Row-of-16 max / min through DPP (quad xor 1, quad xor 2, half-row mirror, row mirror):
@@ -365,6 +421,253 @@ __global__ __launch_bounds__(kTriNT) void k_tri_update(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Whole sweeps for small p (the reference's published designs, p = 10, 13): the general
+// path's four launches per sweep (S_alpha / X beta partials, tau and sig2, k_tri_update,
+// X beta) cost more than the arithmetic.  k_tri_chain keeps the chain in LDS and runs
+// `count` sweeps per launch: all 512 threads for S_alpha / rss, two lanes for tau and sig2,
+// then wave 0 alone (lane j = coefficient j) for omega, u and the coordinate passes, whose
+// bound reductions are DPP + readlane inside the wave (no barrier per coordinate) and whose
+// truncated-normal draws test kTcK attempts at once (tnorm_par).  While wave 0 runs the
+// serial part, waves 1..7 draw every counter-only variate of the NEXT sweep into the other
+// half of a double buffer: the tau / sig2 gamma variates, the omega / u uniforms and
+// attempts 0..kTcK-1 of each coordinate's first-pass truncated normal.  The arithmetic is
+// k_tri_update's, expression for expression.
+// ---------------------------------------------------------------------------
+constexpr int kTcNT = 512;
+constexpr int kTcK = 16;                // parallel truncated-normal attempts
+constexpr size_t kTcXLds = 96 * 1024;  // X staged in LDS up to this size
+constexpr int kTcP = kTriChainMaxP;
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+struct TcVariates {  // counter-only variates of one sweep
+    double gt, gs;                 // Ga(tau shape, 1), Ga(sig2 shape, 1)
+    double om[kTcP][3], uu[kTcP];  // omega: r0 and the Ga(1, 1) / Ga(2, 1) variates; u
+    double r[kTcP][kTcK][2];       // attempt k of coordinate i (pass 0): r0, r1
+    double x[kTcP][kTcK];          //   and its Box-Muller normal
+};
+
+// Item e of sweep tt's variates (e < 2 + p (1 + kTcK)).
+__device__ __forceinline__ void tc_variate(TcVariates &v, int e, int p, double tau_shape,
+                                           double sig2_shape, const Hyper &hy, Key key,
+                                           uint64_t tt, uint32_t *err) {
+    if (e == 0) {
+        if (!hy.know_tau) v.gt = gamma1(tau_shape, key, tt, KIND_TAU, err);
+    } else if (e == 1) {
+        if (!hy.know_sig2) v.gs = gamma1(sig2_shape, key, tt, KIND_SIG2, err);
+    } else if (e < 2 + p) {
+        const int j = e - 2;
+        const U4 r = uniforms(key, tt, KIND_TRI_OMEGA, (uint64_t)j, 0, 0);
+        v.om[j][0] = r.r[0];
+        v.om[j][1] = -log(r.r[1]);                // Ga(1, 1)
+        v.om[j][2] = -log(r.r[1]) - log(r.r[2]);  // Ga(2, 1)
+        v.uu[j] = uniforms(key, tt, KIND_TRI_U, (uint64_t)j, 0, 0).r[0];
+    } else {
+        const int q = e - 2 - p, i = q / kTcK, k = q % kTcK;
+        const U4 r = uniforms(key, tt, KIND_TRI_Z, (uint64_t)i, 0, (uint64_t)k);
+        v.r[i][k][0] = r.r[0];
+        v.r[i][k][1] = r.r[1];
+        v.x[i][k] = bm_normal(r.r[0], r.r[1]);
+    }
+}
+
+__global__ __launch_bounds__(kTcNT) void k_tri_chain(
+    const double *__restrict__ X, int ldx, int n, int p, const double *__restrict__ y,
+    const double *__restrict__ tVc, const double *__restrict__ tVr,
+    const double *__restrict__ av, const double *__restrict__ dv, int x_lds, double *beta,
+    double *u, double *omega, double *shape, DevScalars *sc, Hyper hy, int betaburn, Key key,
+    uint64_t t0, int count, int first_slot, int slot_step, int cap, double *tr_beta,
+    double *tr_u, double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,
+    double *tr_alpha, uint32_t *err) {
+    extern __shared__ double sX[];
+    __shared__ double sTc[kTcP * kTcP], sTr[kTcP * kTcP];
+    __shared__ double sb[kTcP];
+    __shared__ TcVariates vb[2];
+    __shared__ double red[2][kTcNT / 64];
+    __shared__ double s_tau, s_sig2;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int e = tid; e < p * p; e += kTcNT) {
+        sTc[e] = tVc[e];
+        sTr[e] = tVr[e];
+    }
+    if (x_lds)
+        for (int e = tid; e < n * p; e += kTcNT) sX[e] = X[(size_t)(e % n) + (size_t)(e / n) * ldx];
+    const double *Xs = x_lds ? sX : X;
+    const int lds_x = x_lds ? n : ldx;
+    const bool act = wid == 0 && lane < p;  // wave 0, lane j = coefficient / coordinate j
+    double uj = 0.0, om = 0.0, sh = 0.0, aj_c = 0.0, dj_c = 0.0;
+    if (tid < p) {
+        sb[tid] = beta[tid];
+        uj = u[tid];
+        aj_c = av[tid];
+        dj_c = dv[tid];
+    }
+    if (tid == 0) {
+        s_tau = sc->tau;
+        s_sig2 = sc->sig2;
+    }
+    const double alpha = sc->alpha;
+    const double tau_shape = hy.nu_shape + ((double)p) / alpha;
+    const double sig2_shape = hy.sig2_shape + 0.5 * (double)n;
+    const int nvar = 2 + p * (1 + kTcK);
+    for (int e = tid; e < nvar; e += kTcNT)  // sweep 0's variates
+        tc_variate(vb[0], e, p, tau_shape, sig2_shape, hy, key, t0, err);
+    __syncthreads();
+    for (int k = 0; k < count; ++k) {
+        TcVariates &v = vb[k & 1];
+        const uint64_t t = t0 + (uint64_t)k;
+        const int slot = first_slot < 0 ? -1 : (first_slot + k * slot_step) % cap;
+        // ---- S_alpha = sum |beta_j|^alpha and rss = |y - X beta|^2 ----
+        double sa = 0.0, rs = 0.0;
+        if (tid < p) sa = exp(alpha * log(fabs(sb[tid])));
+        for (int i = tid; i < n; i += kTcNT) {
+            double xb = 0.0;
+            for (int j = 0; j < p; ++j) xb += Xs[(size_t)i + (size_t)j * lds_x] * sb[j];
+            const double r = y[i] - xb;
+            rs += r * r;
+        }
+        sa = wave_sum64(sa);
+        rs = wave_sum64(rs);
+        if (lane == 0) {
+            red[0][wid] = sa;
+            red[1][wid] = rs;
+        }
+        __syncthreads();
+        // tau | beta (wave 0) and sig2 | beta (wave 1), as k_scalars
+        if (tid == 0 || tid == 64) {
+            double S = red[tid == 0 ? 0 : 1][0];
+#pragma unroll
+            for (int w = 1; w < kTcNT / 64; ++w) S += red[tid == 0 ? 0 : 1][w];
+            if (tid == 0) {
+                if (!hy.know_tau) s_tau = exp(-1.0 * log(v.gt / (hy.nu_rate + S)) / alpha);
+                if (slot >= 0) {
+                    tr_tau[slot] = s_tau;
+                    tr_alpha[slot] = alpha;
+                }
+            } else {
+                if (!hy.know_sig2) s_sig2 = (hy.sig2_scale + 0.5 * S) / v.gs;
+                if (slot >= 0) tr_sig2[slot] = s_sig2;
+            }
+        }
+        __syncthreads();
+        if (wid > 0) {
+            // the next sweep's variates, off wave 0's serial chain
+            if (k + 1 < count)
+                for (int e = tid - 64; e < nvar; e += kTcNT - 64)
+                    tc_variate(vb[(k + 1) & 1], e, p, tau_shape, sig2_shape, hy, key, t + 1, err);
+        } else {
+            const double tau = s_tau, sig2 = s_sig2, sig = sqrt(sig2);
+            double bj = 0.0;
+            if (act) {
+                // sample_omega, sample_u, the bound of sample_beta (BridgeRegression.cpp:97-146,
+                // :410-412)
+                const double betaj = sb[lane];
+                const double aj = exp(alpha * log(fabs(betaj) / ((1.0 - uj) * tau)));
+                const double prob = alpha / (1.0 + alpha * aj);
+                double w;
+                if (v.om[lane][0] > prob) {
+                    sh = 1.0;
+                    w = v.om[lane][1];
+                } else {
+                    sh = 2.0;
+                    w = v.om[lane][2];
+                }
+                om = w + aj;
+                const double right = 1.0 - fabs(betaj) / tau * exp(-1.0 * log(om) / alpha);
+                uj = right * v.uu[lane];
+                bj = (1.0 - uj) * exp(log(om) / alpha) * tau;
+                if (slot >= 0) {
+                    tr_omega[(size_t)slot * p + lane] = om;
+                    tr_shape[(size_t)slot * p + lane] = sh;
+                    tr_u[(size_t)slot * p + lane] = uj;
+                }
+            }
+            // conditional mean a_i / d_i^2 and sd sigma / d_i of coordinate i (lane i)
+            const bool ok = dj_c > 1e-16;
+            const double ci = ok ? aj_c / (dj_c * dj_c) : 0.0;
+            const double si = ok ? sig / dj_c : -1.0;
+            double zr = 0.0;
+            for (int it = 0; it <= betaburn; ++it) {
+                Pre pr{0.0, 0.0, 0.0};  // attempt 0 of coordinate `lane` (passes >= 1)
+                if (it > 0 && act) {
+                    const U4 q = uniforms(key, t, KIND_TRI_Z, (uint64_t)lane, (uint64_t)it, 0);
+                    pr = Pre{q.r[0], q.r[1], bm_normal(q.r[0], q.r[1])};
+                }
+                // z = tV beta (:246), then beta_cur = tV' z, in k_tri_update's order
+                zr = 0.0;
+                if (act)
+                    for (int j = 0; j < p; ++j) zr += sTc[lane + j * p] * sb[j];
+                double bc = 0.0;
+                for (int kk = 0; kk < p; ++kk) {
+                    const double zk = readlane_d(zr, kk);
+                    if (act) bc += sTr[kk * p + lane] * zk;
+                }
+                for (int i = 0; i < p; ++i) {  // :250-283
+                    const double vi = act ? sTr[i * p + lane] : 0.0;
+                    const double zi = readlane_d(zr, i);
+                    double lmax = -1.0 * 1.7976931348623157e308, rmin = 1.7976931348623157e308;
+                    if (act) {
+                        const double rji = bc - vi * zi;
+                        const double dif = bj - rji, sum = bj + rji;
+                        const double left = (vi > 0 ? -sum : -dif) / fabs(vi);
+                        const double right = (vi > 0 ? dif : sum) / fabs(vi);
+                        lmax = lmax > left ? lmax : left;
+                        rmin = rmin < right ? rmin : right;
+                    }
+                    const double L = rows_max(row16_max(lmax));
+                    const double R = rows_min(row16_min(rmin));
+                    const double sdi = readlane_d(si, i);
+                    double zn;
+                    if (it == 0) {
+                        const int ka = lane < kTcK ? lane : 0;
+                        if (sdi > 0.0)
+                            zn = tnorm_par<kTcK>(L, R, readlane_d(ci, i), sdi, v.r[i][ka][0],
+                                                 v.r[i][ka][1], v.x[i][ka], key, t, (uint64_t)i,
+                                                 0, err);
+                        else
+                            zn = L + (R - L) * v.r[i][0][0];
+                    } else {
+                        const Pre pi{readlane_d(pr.r0, i), readlane_d(pr.r1, i),
+                                     readlane_d(pr.x0, i)};
+                        if (sdi > 0.0)
+                            zn = tnorm(L, R, readlane_d(ci, i), sdi, key, t, (uint64_t)i,
+                                       (uint64_t)it, pi, err);
+                        else
+                            zn = L + (R - L) * pi.r0;
+                    }
+                    bc += vi * (zn - zi);
+                    if (lane == i) zr = zn;
+                }
+                // beta = tV' z (:285)
+                double bn = 0.0;
+                for (int kk = 0; kk < p; ++kk) {
+                    const double zk = readlane_d(zr, kk);
+                    if (act) bn += sTr[kk * p + lane] * zk;
+                }
+                if (act) sb[lane] = bn;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // sb read by other lanes next
+            }
+            if (act && slot >= 0) tr_beta[(size_t)slot * p + lane] = sb[lane];
+        }
+        __syncthreads();
+    }
+    if (act) {
+        beta[lane] = sb[lane];
+        u[lane] = uj;
+        omega[lane] = om;
+        shape[lane] = sh;
+    }
+    if (tid == 0) {
+        sc->tau = s_tau;
+        sc->sig2 = s_sig2;
+    }
+}
+
 // Truncated normal / exponential batches behind the .C utilities rtnorm_left, rtnorm_both,
 // rtnorm, rtexpon_rate_left, rtexpon_rate_both, rtexpon_rate (BridgeWrapper.cpp:762-935):
 // one lane per draw; draw i uses counters (0, 10 << 56 | i, 0, k) for truncated-normal
@@ -507,6 +810,28 @@ void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, do
     hipLaunchKernelGGL(k_tri_update, dim3(1), dim3(kTriNT), 0, s, beta, u, omega, shape, p, tVc,
                        tVr, a, d, Gf, c, ortho, sc, betaburn, Key{k0, k1}, t, tr_beta, tr_u,
                        tr_omega, tr_shape, err);
+}
+
+void launch_tri_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
+                      const double *tVc, const double *tVr, const double *a, const double *d,
+                      double *beta, double *u, double *omega, double *shape, DevScalars *sc,
+                      Hyper hy, int betaburn, uint64_t k0, uint64_t k1, uint64_t t0, int count,
+                      int first_slot, int slot_step, int cap, double *tr_beta, double *tr_u,
+                      double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,
+                      double *tr_alpha, uint32_t *err) {
+    if (count <= 0 || p < 1 || p > kTriChainMaxP) return;  // the engine checks p at setup
+    const size_t xbytes = (size_t)n * p * sizeof(double);
+    const int x_lds = xbytes <= kTcXLds;
+    static bool attr = false;  // one-time opt-in above the 64 KB default
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)k_tri_chain,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcXLds);
+        attr = true;
+    }
+    k_tri_chain<<<1, kTcNT, x_lds ? xbytes : 0, s>>>(
+        X, ldx, n, p, y, tVc, tVr, a, d, x_lds, beta, u, omega, shape, sc, hy, betaburn,
+        Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta, tr_u, tr_omega, tr_shape,
+        tr_sig2, tr_tau, tr_alpha, err);
 }
 
 }  // namespace bb

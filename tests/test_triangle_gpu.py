@@ -69,16 +69,23 @@ def test_engine_basis_ill_conditioned(gpu_lib):
     assert np.allclose(np.abs(tV @ W), np.eye(p), atol=1e-6)
 
 
-CASES = ["c1", "unknown_alpha", "betaburn", "known_tau_sig2", "ortho"]
+# (n, p, betaburn).  Non-orthogonal designs with alpha known and p <= 32 run the fused
+# single-launch chain (bb_tri.hip k_tri_chain); "betaburn" (p = 33), "unknown_alpha" and
+# "ortho" the general per-sweep path.  "x_in_hbm": n p 8 bytes above the fused kernel's LDS
+# staging limit, so X is read from HBM.
+SHAPES = {"c1": (100, 20, 0), "unknown_alpha": (100, 20, 0), "betaburn": (80, 33, 2),
+          "betaburn_fused": (80, 24, 2), "x_in_hbm": (400, 32, 0),
+          "known_tau_sig2": (100, 20, 0), "ortho": (100, 20, 0)}
+CASES = list(SHAPES)
 
 
 @pytest.mark.parametrize("case,n,p", [(c, None, None) for c in CASES] + [("ortho", 800, 600)])
 def test_tri_sweeps_teacher_forced(gpu_lib, case, n, p):
+    betaburn = SHAPES[case][2]
     if n is None:
-        n, p = (100, 20) if case != "betaburn" else (80, 33)
+        n, p = SHAPES[case][:2]
     X, y, _ = synthetic_problem(n, p, seed=5)
     alpha = 0.0 if case == "unknown_alpha" else 0.5
-    betaburn = 2 if case == "betaburn" else 0
     tk = dict(true_sig2=1.5, true_tau=0.8) if case == "known_tau_sig2" else {}
     seed, M = 777, (40 if p < 100 else 12)
     tol = 1e-10
@@ -148,12 +155,11 @@ def test_tri_wide_p_sweep(gpu_lib, n, p, betaburn):
 
 @pytest.mark.parametrize("case", CASES)
 def test_tri_chain_matches_oracle(gpu_lib, case):
-    n, p = (100, 20) if case != "betaburn" else (80, 33)
+    n, p, betaburn = SHAPES[case]
     X, y, _ = synthetic_problem(n, p, seed=5)
     kw = dict(alpha=0.5, nu_shape=2.0, nu_rate=2.0)
     if case == "unknown_alpha":
         kw["alpha"] = 0.0
-    betaburn = 2 if case == "betaburn" else 0
     tk = dict(true_sig2=1.5, true_tau=0.8) if case == "known_tau_sig2" else {}
     _, basis = engine_basis(X, y)
     bb.set_seed(4321)

@@ -88,9 +88,13 @@ def main():
     nsamp = int(os.environ.get("NSAMP", "100000"))
     burn = int(os.environ.get("BURN", "10000"))
     bb.set_verbose(0)
+    only_d = os.environ.get("DESIGNS", "DB,DBI,BH,BHI").split(",")
+    only_m = os.environ.get("METHODS", "stable,tri,stable_orth").split(",")
     recs = []
     for name, (X, y) in designs().items():
-        for method in ("stable", "tri", "stable_orth"):
+        if name not in only_d:
+            continue
+        for method in only_m:
             Xm = orth(X) if method == "stable_orth" else X
             recs.append(run(name, Xm, y, method, nsamp, burn))
             print(json.dumps(recs[-1]), file=sys.stderr, flush=True)
