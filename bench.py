@@ -176,10 +176,23 @@ def cpu_baseline_sparse(n, p, alpha, sweeps, log_every=True):
     return float(np.median(times)), threads
 
 
-def cpu_baseline(n, p, alpha, sweeps, log_every=True):
-    """Oracle Woodbury sweeps on the host: the CPU restatement of the reference sweep,
-    algorithm-matched to the GPU path (reference-literal p x p Cholesky at p=50000 needs a
-    20 GB Gram and ~4e13 flop per sweep)."""
+def blas_threads(threads):
+    """Context limiting the BLAS pools to `threads` (None: leave them as they are)."""
+    import contextlib
+
+    if threads is None:
+        return contextlib.nullcontext()
+    from threadpoolctl import threadpool_limits
+    return threadpool_limits(limits=threads)
+
+
+def cpu_baseline(n, p, alpha, sweeps, log_every=True, threads=None, literal=False):
+    """Oracle sweeps on the host: the CPU restatement of the reference sweep.  Default: the
+    Woodbury draw, algorithm-matched to the GPU path (reference-literal p x p Cholesky at
+    p=50000 needs a 20 GB Gram and ~4e13 flop per sweep).  literal=True: the reference's own
+    p x p path (BridgeRegression.cpp:24-25 X'X and X'y once, then per sweep
+    :552-575 dpotrf of X'X + diag(lambda sig2 / tau^2) and three triangular solves).
+    threads: BLAS threads (None = the environment's).  Returns (median s per sweep, threads)."""
     import oracle
     from oracle import gibbs
 
@@ -187,24 +200,31 @@ def cpu_baseline(n, p, alpha, sweeps, log_every=True):
     y, _ = make_problem_y(n, p)
     beta = np.zeros(p)
     tau, sig2 = 1.0, 1.0
-    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
     times = []
-    for t in range(1, sweeps + 1):
-        t0 = time.perf_counter()
-        tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, 2.0, 2.0, 1, 0, t)
-        r = y - X @ beta
-        sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, 1, 0, t)
-        lam = oracle.sample_lambda(beta, alpha, tau, 1, 0, t)
-        z = oracle.normals(p, 1, 0, t, oracle.KIND_BETA_Z)
-        d = oracle.normals(n, 1, 0, t, oracle.KIND_DELTA)
-        beta = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
-        times.append(time.perf_counter() - t0)
-        if log_every:
-            log(f"[cpu_baseline] sweep {t}: {times[-1]:.3f} s")
-    del hyper
+    with blas_threads(threads):
+        if literal:
+            G, c = X.T @ X, X.T @ y
+        for t in range(1, sweeps + 1):
+            t0 = time.perf_counter()
+            tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, 2.0, 2.0, 1, 0,
+                                      t)
+            r = y - X @ beta
+            sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, 1, 0, t)
+            lam = oracle.sample_lambda(beta, alpha, tau, 1, 0, t)
+            z = oracle.normals(p, 1, 0, t, oracle.KIND_BETA_Z)
+            if literal:
+                beta = gibbs.beta_step_chol(G, c, lam, sig2, tau, z)
+            else:
+                d = oracle.normals(n, 1, 0, t, oracle.KIND_DELTA)
+                beta = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
+            times.append(time.perf_counter() - t0)
+            if log_every:
+                log(f"[cpu_baseline] {'literal' if literal else 'woodbury'} "
+                    f"threads={threads or 'env'} sweep {t}: {times[-1]:.3f} s")
     # first sweep starts from beta = 0 (all lambda draws at h = 0); report the median
     per = float(np.median(times))
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return per, threads
 
 
@@ -442,6 +462,25 @@ def main():
                          f"{threads} threads, + C tilted-stable sampler) at n={n}, p={p}; "
                          f"median sweep {per_sweep:.3f} s"}
 
+    # C2: the CPU baseline at 1 core and all cores, for the Woodbury port and
+    # for the reference-literal p x p path (dpotrf at p = 5000)
+    cpu_more = None
+    if (cpu is not None and args.workload == "c2" and p <= 8000):
+        cpu_more = []
+        for lit in (False, True):
+            for th in (1, None):
+                if not lit and th is None:
+                    per_sweep, threads = 1.0 / cpu["value"], cpu["cores"]
+                else:
+                    per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps, threads=th,
+                                                      literal=lit)
+                cpu_more.append({
+                    "value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads,
+                    "kind": "port",
+                    "path": ("reference-literal p x p Cholesky (dpotrf p=%d)" % p if lit
+                             else "Woodbury (algorithm-matched to the GPU)"),
+                    "sample": f"{cpu_sweeps} sweeps, median {per_sweep:.3f} s"})
+
     if rank == 0:
         wl = {"c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
               "c4": "C4 logistic bridge (Polya-Gamma)",
@@ -493,6 +532,8 @@ def main():
             "cpu_baseline": cpu,
             "setup_s": setup_s,
         }
+        if cpu_more:
+            rec["cpu_baselines"] = cpu_more
         print(json.dumps(rec), flush=True)
     eng.close()
     if dist:
