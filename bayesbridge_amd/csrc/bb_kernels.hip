@@ -925,12 +925,14 @@ __device__ __forceinline__ void tile_store(const double (*L)[65], double *A, int
 
 // C[y][x] = sum_s P[s][y] Q[s][x] over 64 s (P'Q), 8 waves x 2 blocks of 16x16 (fp64 MFMA);
 // the lane's results are acc[h][r] at y = by*16 + (lane>>4) + 4r, x = bx*16 + (lane&15).
+// ACC: add to acc instead of overwriting it.
+template <bool ACC = false>
 __device__ __forceinline__ void mm_tn(const double (*P)[65], const double (*Q)[65], v4d acc[2]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
-        acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+        if (!ACC) acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
         for (int kk = 0; kk < 16; ++kk) {
             const int sr = kk * 4 + (lane >> 4);
@@ -1074,6 +1076,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     __shared__ __attribute__((aligned(16))) double Lb[3][64][65];
     __shared__ double piv[64];
     __shared__ int cnt;
+    __shared__ int pre_ready;  // owner: the next update's panels are published
     double(*T)[65] = Lb[0];
     double(*S)[65] = Lb[1];
     double(*Q)[65] = Lb[2];
@@ -1225,20 +1228,64 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     } while (0)
         tile_load(T, A, lda, i, j, diag);
         __syncthreads();
+        // An owner that lags the chain finds the next panels already published: their loads
+        // (into registers) are issued before this update's MFMAs and land in S / Q after
+        // them, so a lagging owner's update costs max(load, MFMA) instead of their sum
+        // (at m = 5120 the owners, not the chain, set the pace through the middle third).
+        // The updates sum in the MFMA accumulators, T -= sum once at the end: no LDS
+        // read-modify-write of T and one barrier fewer per update.
+        bool have = false;  // S (and Q) already hold panel k
+        acc[0] = acc[1] = (v4d){0.0, 0.0, 0.0, 0.0};
         for (int k = 0; k < nupd; ++k) {
             if (k == nupd - 1) OWN_TS(0);
-            flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], F.ep, err);
-            if (k == nupd - 1) OWN_TS(1);
-            tile_load(S, A, lda, k, i, false);
-            if (!diag) tile_load(Q, A, lda, k, j, false);
+            if (!have) {
+                flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], F.ep,
+                              err);
+                if (k == nupd - 1) OWN_TS(1);
+                tile_load(S, A, lda, k, i, false);
+                if (!diag) tile_load(Q, A, lda, k, j, false);
+            }
+            if (tid == 0) {
+                bool rdy = k + 1 < nupd;
+                if (rdy)
+                    rdy = __hip_atomic_load(&F.P[(k + 1) * F.ncb + i], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) == F.ep &&
+                          (diag || __hip_atomic_load(&F.P[(k + 1) * F.ncb + j], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) == F.ep);
+                pre_ready = rdy;
+            }
             __syncthreads();
+            const bool pre = pre_ready;
             if (k == nupd - 1) OWN_TS(2);
-            mm_tn(S, diag ? S : Q, acc);
+            double vs[8], vq[8];
+            if (pre) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                    vs[q] = ld_sc1(&A[(size_t)((k + 1) * kNB + y) + (size_t)(i * kNB + x) * lda]);
+                    vq[q] = diag ? 0.0
+                                 : ld_sc1(&A[(size_t)((k + 1) * kNB + y) +
+                                             (size_t)(j * kNB + x) * lda]);
+                }
+            }
+            mm_tn<true>(S, diag ? S : Q, acc);
+            __syncthreads();  // every wave has read S and Q
+            if (pre) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                    S[y][x] = vs[q];
+                    if (!diag) Q[y][x] = vq[q];
+                }
+            }
+            have = pre;
+            if (k == nupd - 1) OWN_TS(3);
+        }
+        if (nupd > 0) {
             MM_FOR(h, r, y, x) {
                 if (!diag || y <= x) T[y][x] -= acc[h][r];
             }
             __syncthreads();
-            if (k == nupd - 1) OWN_TS(3);
         }
         if (handoff) {
             tile_store(T, A, lda, i, j);
