@@ -186,7 +186,7 @@ void launch_kappa(hipStream_t s, const double *y, int n, int n_pad, double *kapp
 // p x p Cholesky draw, or the orthogonal-design draw) in ONE single-workgroup launch, for
 // p <= kSmallChainMaxP and alpha known.  Sweep k uses counter t0 + k and trace slot
 // (first_slot + k slot_step) % cap (first_slot < 0: none).
-constexpr int kSmallChainMaxP = 16;
+constexpr int kSmallChainMaxP = 32;
 void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
                         const double *G, int ldg, const double *cvec, const double *gdiag,
                         int ortho, double *beta, double *lam, DevScalars *sc, Hyper hy,

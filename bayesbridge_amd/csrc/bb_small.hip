@@ -22,8 +22,7 @@ namespace bb {
 namespace {
 
 constexpr int kSmallMaxP = kSmallChainMaxP;
-constexpr int kSmallNT = 512;
-constexpr size_t kSmallXLds = 128 * 1024;
+constexpr size_t kSmallXLds = 112 * 1024;
 constexpr int kSmallPre = 32;  // sweeps of counter-only variates drawn ahead  // X staged in LDS up to this size
 
 __device__ __forceinline__ double wave_sum_all(double v) {
@@ -69,10 +68,10 @@ void small_phase_ticks(unsigned long long out[4]) {
 #endif
 
 // L lanes per coefficient in the lambda draw (stable_spec_draw<L, I>), the p x p system
-// padded to PP (8 or 16: the unrolled register factorisation spills beyond 16); dynamic LDS holds
+// dynamic LDS holds
 // X (n x p, column-major) when it fits, else X is read from HBM each sweep.
-template <int L, int I, int PP>
-__global__ __launch_bounds__(kSmallNT) void k_small_chain(
+template <int NT, int L, int I>
+__global__ __launch_bounds__(NT) void k_small_chain(
     const double *__restrict__ X, int ldx, int n, int p, const double *__restrict__ y,
     const double *__restrict__ G, int ldg, const double *__restrict__ cvec,
     const double *__restrict__ gdiag, int ortho, int x_lds, double *beta, double *lam,
@@ -87,16 +86,16 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
     // sweeps: their shapes are constant along the chain (alpha known), so they depend on
     // their counters alone and come off the serial chain
     __shared__ double s_gt[kSmallPre], s_gs[kSmallPre], s_z[kSmallPre][kSmallMaxP];
-    __shared__ double red[2][kSmallNT / 64];
+    __shared__ double red[2][NT / 64];
     __shared__ double s_tau, s_sig2;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (int e = tid; e < p * p; e += kSmallNT) {
+    for (int e = tid; e < p * p; e += NT) {
         const int r = e % p, c = e / p;
         const int lo = r < c ? r : c, hi = r < c ? c : r;  // G holds its upper triangle
         sG[r][c] = ortho ? 0.0 : G[(size_t)lo + (size_t)hi * ldg];
     }
     if (x_lds)
-        for (int e = tid; e < n * p; e += kSmallNT) sX[e] = X[(size_t)(e % n) + (size_t)(e / n) * ldx];
+        for (int e = tid; e < n * p; e += NT) sX[e] = X[(size_t)(e % n) + (size_t)(e / n) * ldx];
     const double *Xs = x_lds ? sX : X;
     const int lds_x = x_lds ? n : ldx;
     if (tid < p) {
@@ -115,6 +114,20 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
     __syncthreads();
     const double tau_shape = hy.nu_shape + ((double)p) / alpha;
     const double sig2_shape = hy.sig2_shape + 0.5 * (double)n;
+    // upper-triangle entries owned by this thread: e = tid and tid + NT, e = j (j + 1) / 2 + i
+    bool own[2];
+    int oi[2], oj[2];
+    double av[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int e = tid + h * NT;
+        own[h] = !ortho && e < p * (p + 1) / 2;
+        int j = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+        while ((j + 1) * (j + 2) / 2 <= e) ++j;
+        while (j * (j + 1) / 2 > e) --j;
+        oj[h] = j;
+        oi[h] = e - j * (j + 1) / 2;
+    }
     for (int k = 0; k < count; ++k) {
         if (k % kSmallPre == 0) {
             // wave 0: tau's gamma variates, wave 1: sig2's, waves 2..: the normals
@@ -123,7 +136,7 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
                 s_gt[lane] = gamma1(tau_shape, key, t0 + (uint64_t)(k + lane), KIND_TAU, err);
             else if (wid == 1 && lane < nb && !hy.know_sig2)
                 s_gs[lane] = gamma1(sig2_shape, key, t0 + (uint64_t)(k + lane), KIND_SIG2, err);
-            for (int e = tid - 128; e >= 0 && e < nb * p; e += kSmallNT - 128) {
+            for (int e = tid - 128; e >= 0 && e < nb * p; e += NT - 128) {
                 const int kk = e / p, j = e % p;
                 s_z[kk][j] = normal_at(key, t0 + (uint64_t)(k + kk), KIND_BETA_Z, (uint64_t)j);
             }
@@ -136,7 +149,7 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
         // ---- S_alpha = sum |beta_j|^alpha and rss = |y - X beta|^2 ----
         double sa = 0.0, rs = 0.0;
         if (tid < p) sa = exp(alpha * log(fabs(sb[tid])));
-        for (int i = tid; i < n; i += kSmallNT) {
+        for (int i = tid; i < n; i += NT) {
             double xb = 0.0;
             for (int j = 0; j < p; ++j) xb += Xs[(size_t)i + (size_t)j * lds_x] * sb[j];
             const double r = y[i] - xb;
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
         if (tid == 0 || tid == 64) {
             double S = red[tid == 0 ? 0 : 1][0];
 #pragma unroll
-            for (int w = 1; w < kSmallNT / 64; ++w) S += red[tid == 0 ? 0 : 1][w];
+            for (int w = 1; w < NT / 64; ++w) S += red[tid == 0 ? 0 : 1][w];
             if (tid == 0) {
                 if (!hy.know_tau) {
                     const double nu = s_gt[kp] / (hy.nu_rate + S);
@@ -174,7 +187,7 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
         SMALL_PHASE(2);
         const double tau = s_tau, sig2 = s_sig2;
         // ---- lambda_j = 2 retstable(beta_j^2 / tau^2, alpha / 2, 1) ----
-        for (int jb = 0; jb < p; jb += kSmallNT / L) {
+        for (int jb = 0; jb < p; jb += NT / L) {
             const int j = jb + tid / L;
             const bool act = j < p;
             const double b = act ? sb[j] : 0.0;
@@ -195,58 +208,66 @@ __global__ __launch_bounds__(kSmallNT) void k_small_chain(
                 const double m = sc_[tid] / uu;
                 sb[tid] = m + sd * s_z[kp][tid];
             }
-        } else if (wid == 0) {
-            // A = G + diag(lambda sig2 / tau^2) in registers, lane j holding column j, padded
-            // to PP with an identity block (whose rows and columns stay exact zeros/ones, so
-            // the real entries see the same operations), factored right-looking as A = U'U;
-            // row k of U goes to LDS and is read back as a broadcast (readlane broadcasts of
-            // every U(k, i) made the compiler hoist ~PP^2/2 scalar values and spill)
-            double a[PP];
-            const double dl = lane < p ? sl[lane] * sig2 / (tau * tau) : 0.0;
+        } else {
+            // A = G + diag(lambda sig2 / tau^2), factored right-looking as A = U'U with one
+            // thread per upper-triangle entry (i, j) (two for the last 16 at p = 32): per
+            // pivot k the owner of (k, k) takes the square root, the owners of row k divide
+            // (row k of U goes to LDS), every trailing owner subtracts U(k, i) U(k, j) -- the
+            // reference's operations entry by entry (BridgeRegression.cpp:560), two barriers
+            // per pivot and no register arrays
+            const double dl = tau * tau;
 #pragma unroll
-            for (int i = 0; i < PP; ++i)
-                a[i] = (i < p && lane < p) ? sG[i][lane] + (i == lane ? dl : 0.0)
-                                           : (i == lane ? 1.0 : 0.0);
-#pragma unroll
-            for (int kk = 0; kk < PP; ++kk) {
-                const double piv = readlane_f64(a[kk], kk);
-                if (!(piv > 0.0) && lane == 0) atomicOr(err, 8u);
-                const double d = sqrt(piv);
-                a[kk] = lane > kk ? a[kk] / d : (lane == kk ? d : a[kk]);
-                if (lane < PP) sU[kk][lane] = a[kk];
-                wave_lds_sync();
-#pragma unroll
-                for (int i = kk + 1; i < PP; ++i) {
-                    const double uki = sU[kk][i];
-                    if (lane >= i) a[i] -= uki * a[kk];
+            for (int h = 0; h < 2; ++h)
+                if (own[h]) {
+                    const int i = oi[h], j = oj[h];
+                    av[h] = sG[i][j] + (i == j ? sl[i] * sig2 / dl : 0.0);
                 }
-            }
-            // m: U'v = c (forward), U m = v (backward); x: U x = z; lane j holds entry j
-            double w = lane < p ? sc_[lane] : 0.0;
-            double z = lane < p ? s_z[kp][lane] : 0.0;
+            for (int kk = 0; kk < p; ++kk) {
 #pragma unroll
-            for (int kk = 0; kk < PP; ++kk) {
-                const double vk = readlane_f64(w, kk) / readlane_f64(a[kk], kk);
-                if (lane > kk) w -= a[kk] * vk;
-                if (lane == kk) w = vk;
-            }
-            wave_lds_sync();
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] == kk && oj[h] == kk) {
+                        if (!(av[h] > 0.0)) atomicOr(err, 8u);
+                        av[h] = sqrt(av[h]);
+                        sU[kk][kk] = av[h];
+                    }
+                __syncthreads();
+                const double d = sU[kk][kk];
 #pragma unroll
-            for (int kk = PP - 1; kk >= 0; --kk) {
-                const double ukk = sU[kk][kk];
-                const double mk = readlane_f64(w, kk) / ukk;
-                const double xk = readlane_f64(z, kk) / ukk;
-                if (lane < kk) {
-                    const double ulk = sU[lane][kk];
-                    w -= ulk * mk;
-                    z -= ulk * xk;
-                }
-                if (lane == kk) {
-                    w = mk;
-                    z = xk;
-                }
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] == kk && oj[h] > kk) {
+                        av[h] = av[h] / d;
+                        sU[kk][oj[h]] = av[h];
+                    }
+                __syncthreads();
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] > kk) av[h] -= sU[kk][oi[h]] * sU[kk][oj[h]];
             }
-            if (lane < p) sb[lane] = w + sqrt(sig2) * z;
+            if (wid == 0) {
+                // m: U'v = c (forward), U m = v (backward); x: U x = z; lane j holds entry j
+                double w = lane < p ? sc_[lane] : 0.0;
+                double z = lane < p ? s_z[kp][lane] : 0.0;
+                for (int kk = 0; kk < p; ++kk) {
+                    const double vk = readlane_f64(w, kk) / sU[kk][kk];
+                    if (lane > kk && lane < p) w -= sU[kk][lane] * vk;
+                    if (lane == kk) w = vk;
+                }
+                for (int kk = p - 1; kk >= 0; --kk) {
+                    const double ukk = sU[kk][kk];
+                    const double mk = readlane_f64(w, kk) / ukk;
+                    const double xk = readlane_f64(z, kk) / ukk;
+                    if (lane < kk) {
+                        const double ulk = sU[lane][kk];
+                        w -= ulk * mk;
+                        z -= ulk * xk;
+                    }
+                    if (lane == kk) {
+                        w = mk;
+                        z = xk;
+                    }
+                }
+                if (lane < p) sb[lane] = w + sqrt(sig2) * z;
+            }
         }
         __syncthreads();
         SMALL_PHASE(4);
@@ -272,21 +293,22 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
     const size_t xbytes = (size_t)n * p * sizeof(double);
     const int x_lds = xbytes <= kSmallXLds;
     const size_t shm = x_lds ? xbytes : 0;
-    auto go = [&](auto kern) {
+    auto go = [&](auto kern, int nt) {
         static bool attr = false;  // one-time opt-in above the 64 KB default
         if (!attr) {
             (void)hipFuncSetAttribute((const void *)kern,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kSmallXLds);
             attr = true;
         }
-        kern<<<1, kSmallNT, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, x_lds, beta,
-                                      lam, sc, hy, Key{k0, k1}, t0, count, first_slot, slot_step,
-                                      cap, tr_beta, tr_lam, tr_sig2, tr_tau, tr_alpha, err);
+        kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, x_lds, beta, lam, sc,
+                                hy, Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta,
+                                tr_lam, tr_sig2, tr_tau, tr_alpha, err);
     };
-    // lanes per coefficient: as many as kSmallNT allows for p coefficients at once
-    static_assert(kSmallMaxP == 16, "instances below cover p <= 16");
-    if (p <= 8) go(k_small_chain<64, 16, 8>);
-    else go(k_small_chain<32, 8, 16>);
+    // lanes per coefficient: as many as the workgroup allows for p coefficients at once
+    static_assert(kSmallMaxP == 32, "instances below cover p <= 32");
+    if (p <= 8) go(k_small_chain<512, 64, 16>, 512);
+    else if (p <= 16) go(k_small_chain<512, 32, 8>, 512);
+    else go(k_small_chain<512, 16, 8>, 512);
 }
 
 }  // namespace bb

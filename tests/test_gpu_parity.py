@@ -186,12 +186,12 @@ def compare_chain(g, o, tol_mean=1e-8, tol_elem=1e-6):
     dict(alpha=0.3, nu_shape=0.5, nu_rate=0.5),
 ])
 @pytest.mark.parametrize("n,p", [(100, 20), (120, 40), (50, 6), (200, 16), (100, 13),
-                                 (3000, 8)])
+                                 (3000, 8), (150, 32), (90, 17)])
 def test_chain_small_p_matches_oracle(gpu_lib, kw, n, p):
     """C1 (n=100, p=20): reference-literal p x p Cholesky draw, full chain -- through the
-    general path (p = 20, 40) and the fused single-launch kernel (p <= 16, bb_small.hip: 64
-    lanes per lambda draw and an 8 x 8 padded system at p = 6, 8; 32 lanes and 16 x 16 at
-    p = 13, 16; X from HBM instead of LDS at n = 3000)."""
+    fused single-launch kernel (p <= 32, bb_small.hip: 64 lanes per lambda draw at p = 6, 8;
+    32 at p = 13, 16; 16 at p = 17, 20, 32, where 16 threads own two Cholesky entries; X from
+    HBM instead of LDS at n = 3000) and the general path (p = 40)."""
     bb = gpu_lib
     X, y, _ = synthetic_problem(n, p)
     bb.set_seed(SEED)

@@ -37,7 +37,7 @@ T *up(const std::vector<T> &h) {
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 442, p = argc > 2 ? atoi(argv[2]) : 10;
     const int ortho = argc > 3 ? atoi(argv[3]) : 0, count = argc > 4 ? atoi(argv[4]) : 2000;
-    if (p > bb::kSmallChainMaxP) return 2;
+    if (p > bb::kSmallChainMaxP) return 2;  // the fused kernel's range
     std::mt19937_64 g(5);
     std::normal_distribution<double> N;
     std::vector<double> X((size_t)n * p), y(n), G((size_t)p * p), c(p), gd(p), b(p);
