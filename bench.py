@@ -74,6 +74,7 @@ SPARSE_DENSITY = 0.01  # C5: each X_ij non-zero independently with this probabil
 
 WORKLOADS = {
     # name: (n, p, alpha, kind)
+    "c1": (100, 20, 0.5, "small"),
     "c2": (1000, 5000, 0.5, "dense"),
     "c3": (2000, 50000, 0.5, "dense"),
     "c4": (10000, 1000, 0.5, "logit"),
@@ -279,6 +280,8 @@ def main():
     cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
         (2 if sparse else 20 if logit else 5)
 
+    if kind == "small":
+        return small_chain(args, n, p, alpha)
     if args.single_process:
         return single_process(args, n, p, alpha, kind)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -482,7 +485,7 @@ def main():
                     "sample": f"{cpu_sweeps} sweeps, median {per_sweep:.3f} s"})
 
     if rank == 0:
-        wl = {"c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
+        wl = {"c1": "C1 Gaussian bridge", "c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
               "c4": "C4 logistic bridge (Polya-Gamma)",
               "c5": f"C5 sparse CSC Gaussian bridge (density {SPARSE_DENSITY})"}[args.workload]
         config = {"workload": f"{wl} n={n} p={p} alpha={alpha}",
@@ -538,6 +541,62 @@ def main():
     eng.close()
     if dist:
         dist.destroy_process_group()
+
+
+def small_chain(args, n, p, alpha):
+    """C1 (BASELINE configs[0], p <= n): the reference-literal p x p path, run as the .C
+    driver runs it -- one bridge_reg_stable call, W burn-in and K recorded sweeps; with p <= 32
+    every block of sweeps is one single-workgroup launch.  `value` is K / the
+    call's post-burn runtime.  The CPU baseline is the oracle's reference-literal chain
+    (gibbs.bridge_regression_stable, method "chol": numpy/LAPACK p x p Cholesky + the C
+    samplers, one BLAS thread) over a bounded number of sweeps."""
+    import torch  # noqa: F401  (device init on the same footing as the other workloads)
+
+    import bayesbridge_amd as bb
+
+    X = make_columns(n, 0, p)
+    y, _ = make_problem_y(n, p)
+    bb.set_verbose(0)
+    bb.set_seed(0xB4E5B41D6E)
+    t_setup0 = time.perf_counter()
+    out = bb.bridge_reg_stb(y, X, nsamp=args.steps, burn=args.warmup, alpha=alpha)
+    wall = time.perf_counter() - t_setup0
+    runtime = float(out["runtime"])
+    value = args.steps / runtime
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import gibbs
+
+        ns = args.cpu_sweeps if args.cpu_sweeps is not None else 2000
+        with blas_threads(1):
+            t0 = time.perf_counter()
+            gibbs.bridge_regression_stable(y, X, ns, burn=0, alpha=alpha, seed=1, stream=0,
+                                           method="chol")
+            per = (time.perf_counter() - t0) / ns
+        cpu = {"value": 1.0 / per, "unit": "sweeps/s", "cores": 1, "kind": "port",
+               "sample": f"{ns} sweeps of the oracle's reference-literal chain (numpy/LAPACK "
+                         f"p x p Cholesky + C samplers, 1 thread) at n={n}, p={p}"}
+    # the p x p path's algorithmic flops per sweep (SURVEY.md 8(d), path p <= n):
+    # p^3/3 + 3 p^2 + 2 n p; the fused chain is latency-bound, far from any roofline
+    flops = p ** 3 / 3.0 + 3.0 * p * p + 2.0 * n * p
+    achieved = flops * value / 1e12
+    rec = {
+        "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
+        "value": value, "unit": "sweeps/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * runtime / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md 8(d) design, seed 20240501)",
+        "config": {"workload": f"C1 Gaussian bridge n={n} p={p} alpha={alpha}", "n": n, "p": p,
+                   "alpha": alpha, "beta_step": "p x p Cholesky (reference-literal)",
+                   "parallelism": "replicas only (p <= n)",
+                   "kernel": "k_small_chain (whole sweeps in one workgroup)"},
+        "roofline": {"bound": "mfma", "kernel": "k_small_chain", "achieved": achieved,
+                     "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "note": "latency-bound: one workgroup, a chain of dependent draws"},
+        "cpu_baseline": cpu, "call_wall_s": wall,
+    }
+    print(json.dumps(rec), flush=True)
 
 
 def single_process(args, n, p, alpha, kind):
