@@ -1055,17 +1055,19 @@ __device__ __forceinline__ void tile_store(const double (*L)[65], double *A, int
 template <bool ACC = false>
 __device__ __forceinline__ void mm_tn(const double (*P)[65], const double (*Q)[65], v4d acc[2]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
-        if (!ACC) acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
+    const int b0 = wid * 2, b1 = wid * 2 + 1;
+    const int bx0 = b0 >> 2, by0 = b0 & 3, bx1 = b1 >> 2, by1 = b1 & 3;
+    if (!ACC) acc[0] = acc[1] = (v4d){0.0, 0.0, 0.0, 0.0};
+    // the two blocks' accumulation chains interleaved: consecutive MFMAs are independent
 #pragma unroll 4
-        for (int kk = 0; kk < 16; ++kk) {
-            const int sr = kk * 4 + (lane >> 4);
-            acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(P[sr][by * 16 + (lane & 15)],
-                                                         Q[sr][bx * 16 + (lane & 15)], acc[h],
-                                                         0, 0, 0);
-        }
+    for (int kk = 0; kk < 16; ++kk) {
+        const int sr = kk * 4 + (lane >> 4);
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(P[sr][by0 * 16 + (lane & 15)],
+                                                     Q[sr][bx0 * 16 + (lane & 15)], acc[0], 0, 0,
+                                                     0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(P[sr][by1 * 16 + (lane & 15)],
+                                                     Q[sr][bx1 * 16 + (lane & 15)], acc[1], 0, 0,
+                                                     0);
     }
 }
 

@@ -49,27 +49,31 @@ def test_trace_ring_triangle(gpu_lib):
     _same(full, ring, ("beta", "u", "w", "shape", "sig2", "tau"))
 
 
-def test_interrupt_returns_partial_traces_and_rerun_is_clean(gpu_lib):
-    """An interrupt at the 4th poll (burn-in is 2 blocks of 10 sweeps, so it lands after
-    20 MCMC sweeps) stops the chain, returns the samples drawn so far -- identical to the
-    same samples of an uninterrupted run -- and leaves the library ready for the next call."""
+@pytest.mark.parametrize("p,block", [(40, 10), (20, 50)])
+def test_interrupt_returns_partial_traces_and_rerun_is_clean(gpu_lib, p, block):
+    """An interrupt at the 4th poll (burn-in is 2 blocks, so it lands after 2 blocks of MCMC
+    sweeps) stops the chain, returns the samples drawn so far -- identical to the same
+    samples of an uninterrupted run -- and leaves the library ready for the next call.
+    Blocks are 10 sweeps on the general path (p = 40) and 50 on the fused single-launch
+    path (p = 20)."""
     bb = gpu_lib
-    X, y, _ = synthetic_problem(100, 20, seed=5)
+    X, y, _ = synthetic_problem(100, p, seed=5)
+    burn, nsamp = 2 * block - 1, 6 * block
     bb.set_seed(SEED + 2)
-    full = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    full = bb.bridge_reg_stb(y, X, nsamp=nsamp, burn=burn)
     bb.set_seed(SEED + 2)
     bb.debug_interrupt_after(3)
-    part = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    part = bb.bridge_reg_stb(y, X, nsamp=nsamp, burn=burn)
     info = bb.last_call_info()
     assert info["interrupted"]
-    done = 21  # sample 0 (after burn-in) + two blocks of 10 MCMC sweeps
+    done = 1 + 2 * block  # sample 0 (after burn-in) + two blocks of MCMC sweeps
     for k in ("beta", "lambda"):
         assert np.array_equal(part[k][:done], full[k][:done]), k
         assert not part[k][done:].any(), k
     for k in ("sig2", "tau"):
         assert np.array_equal(part[k][:done], full[k][:done]), k
     bb.set_seed(SEED + 2)
-    again = bb.bridge_reg_stb(y, X, nsamp=200, burn=19)
+    again = bb.bridge_reg_stb(y, X, nsamp=nsamp, burn=burn)
     assert not bb.last_call_info()["interrupted"]
     _same(full, again)
 
