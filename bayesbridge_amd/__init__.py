@@ -647,7 +647,7 @@ def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=F
     if X.ndim == 1:
         X = X[:, None]
     P = X.shape[1]
-    if 1 <= P <= 64 and not use_cg:
+    if 1 <= P <= 128 and not use_cg:
         # the whole grid in one device launch (a workgroup per ratio)
         beta, _ = bridge_em_batch(y, X, ratio_grid, alpha=alpha,
                                   lambda_max=ratio_grid / tol, tol=tol, max_iter=max_iter)
@@ -660,7 +660,7 @@ def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=F
 
 
 def bridge_em_batch(y, X, ratios, alpha=0.5, lambda_max=None, tol=1e-9, max_iter=30):
-    """bridge.EM (direct solves) for every ratio in one device launch, p <= 64.
+    """bridge.EM (direct solves) for every ratio in one device launch, p <= 128.
     Returns (beta (len(ratios) x P), solves (len(ratios)))."""
     L = library()
     _require_gpu()

@@ -2150,7 +2150,7 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
     return ret;
 }
 
-// Batched EM over `count` ratios (trace.beta) for p <= 64, direct solves: X'X and X'y
+// Batched EM over `count` ratios (trace.beta) for p <= 128, direct solves: X'X and X'y
 // once, then one launch in which a workgroup per ratio runs the whole EM (k_em_batch).
 // beta: count x p (row r = ratio r); solves: count (as bb_bridge_em returns, -1 on a
 // non positive-definite system).  Returns 0, or -1 with bb_last_error().
@@ -2160,7 +2160,7 @@ int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double
     std::vector<void *> owned;
     int rc = 0;
     try {
-        if (p < 1 || p > 64) throw HipError("bb_bridge_em_batch: needs 1 <= p <= 64");
+        if (p < 1 || p > 128) throw HipError("bb_bridge_em_batch: needs 1 <= p <= 128");
         if (count < 1) throw HipError("bb_bridge_em_batch: empty ratio grid");
         HIPCHECK(hipSetDevice(g_device));
         const int n_pad = round_up(n, kGramTile), p_pad = round_up(p, 256);

@@ -94,7 +94,7 @@ void launch_em_form(hipStream_t s, const double *G, int ldg, const double *dlam,
 // Conjugate gradients on that system from x (in/out); work: 3 n doubles; *out_it = iterations.
 void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *b, double *x,
                   double tol, int max_it, double *work, int *out_it);
-// Batched bridge EM (direct solves) for p <= 64: one 64-lane workgroup per ratio, the EM
+// Batched bridge EM (direct solves) for p <= 128: one workgroup per ratio (a thread per row), the EM
 // loop entirely on the device.  beta_out: count x p; solves_out: count (-1: not PD).
 void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, int p,
                      const double *ratios, const double *lambda_max, int count, double alpha,

@@ -793,14 +793,14 @@ void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *
     k_em_cg<<<1, kEmCgThreads, 0, s>>>(A, lda, n, b, x, tol, max_it, work, out_it);
 }
 
-// Batched bridge EM over a ratio grid (trace.beta, Code/R/bridge-trace.R): one 64-lane
-// workgroup per ratio runs the whole EM of BR::EM (BridgeRegression.cpp:600-708, direct
-// solves) for p <= 64 with the system in LDS -- lane i owns row i; right-looking Cholesky,
-// forward and backward substitution; dropped coordinates are identity rows with a zero
-// right-hand side, as in k_em_form.  No host round trip per iteration.
-constexpr int kEmBatchMaxP = 64;
-
-__device__ bool em_lds_solve(double (*A)[kEmBatchMaxP + 1], double *y, int p) {
+// Batched bridge EM over a ratio grid (trace.beta, Code/R/bridge-trace.R): one workgroup
+// per ratio runs the whole EM of BR::EM (BridgeRegression.cpp:600-708, direct solves) with
+// the system in LDS -- thread i owns row i (MAXP = 64: one wave for p <= 64; MAXP = 128: two
+// waves and a 129 KB system for p <= 128); right-looking Cholesky, forward and backward
+// substitution; dropped coordinates are identity rows with a zero right-hand side, as in
+// k_em_form.  No host round trip per iteration.
+template <int MAXP>
+__device__ bool em_lds_solve(double (*A)[MAXP + 1], double *y, int p) {
     const int lane = threadIdx.x;
     bool ok = true;
     for (int k = 0; k < p; ++k) {
@@ -835,15 +835,18 @@ __device__ bool em_lds_solve(double (*A)[kEmBatchMaxP + 1], double *y, int p) {
     return ok;
 }
 
-__global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const double *bvec,
-                                                 int p, const double *ratios,
-                                                 const double *lambda_max, double alpha,
-                                                 double tol, int max_iter, double *beta_out,
-                                                 int *solves_out) {
-    __shared__ double A[kEmBatchMaxP][kEmBatchMaxP + 1];
-    __shared__ double x[kEmBatchMaxP], old[kEmBatchMaxP], lam[kEmBatchMaxP];
-    __shared__ int mask[kEmBatchMaxP];
-    __shared__ double red[64];
+template <int MAXP>
+__global__ __launch_bounds__(MAXP) void k_em_batch(const double *G, int ldg, const double *bvec,
+                                                   int p, const double *ratios,
+                                                   const double *lambda_max, double alpha,
+                                                   double tol, int max_iter, double *beta_out,
+                                                   int *solves_out) {
+    constexpr int NW = MAXP / 64;
+    __shared__ double A[MAXP][MAXP + 1];
+    __shared__ double x[MAXP], old[MAXP], lam[MAXP];
+    __shared__ int mask[MAXP];
+    __shared__ double red[MAXP];
+    __shared__ int wcount[NW];
     const int lane = threadIdx.x, r = blockIdx.x;
     const double tau = ratios[r], sig = 1.0, lmax = lambda_max[r];
     const double c1 = alpha * exp((2 - alpha) * (log(tau) - log(sig)));
@@ -869,7 +872,7 @@ __global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const
         __syncthreads();
     };
     form(false);
-    if (!em_lds_solve(A, x, p)) {
+    if (!em_lds_solve<MAXP>(A, x, p)) {
         if (lane < p) out[lane] = 0.0;
         if (lane == 0) solves_out[r] = -1;
         return;
@@ -890,8 +893,12 @@ __global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const
                 mask[lane] = 0;
             }
         }
+        const int wc = __popcll(__ballot(keep));
+        if ((lane & 63) == 0) wcount[lane >> 6] = wc;
         __syncthreads();
-        const int num = __popcll(__ballot(keep));
+        int num = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) num += wcount[w];
         if (num == 0) {
             if (lane < p) out[lane] = 0.0;
             if (lane == 0) solves_out[r] = it;
@@ -899,7 +906,7 @@ __global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const
         }
         pa = num;
         form(true);
-        if (!em_lds_solve(A, x, p)) {
+        if (!em_lds_solve<MAXP>(A, x, p)) {
             if (lane < p) out[lane] = 0.0;
             if (lane == 0) solves_out[r] = -1;
             return;
@@ -922,8 +929,12 @@ __global__ __launch_bounds__(64) void k_em_batch(const double *G, int ldg, const
 void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, int p,
                      const double *ratios, const double *lambda_max, int count, double alpha,
                      double tol, int max_iter, double *beta_out, int *solves_out) {
-    k_em_batch<<<count, 64, 0, s>>>(G, ldg, b, p, ratios, lambda_max, alpha, tol, max_iter,
-                                    beta_out, solves_out);
+    if (p <= 64)
+        k_em_batch<64><<<count, 64, 0, s>>>(G, ldg, b, p, ratios, lambda_max, alpha, tol,
+                                            max_iter, beta_out, solves_out);
+    else
+        k_em_batch<128><<<count, 128, 0, s>>>(G, ldg, b, p, ratios, lambda_max, alpha, tol,
+                                              max_iter, beta_out, solves_out);
 }
 
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
@@ -979,6 +990,7 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 // ---------------------------------------------------------------------------
 struct CholFlags {
     unsigned int *W, *P, *R;
+    unsigned int *H;  // H[i]: tile (i, i+2) updated through step i-1 and stored (i >= 1)
     int ncb;
     unsigned int ep;  // this factorisation's epoch
 };
@@ -1120,9 +1132,22 @@ __device__ __forceinline__ void elim_produce(double (&a)[8][2], double (*ROWS)[1
     }
 }
 
+// The chain's next hand-off tiles (k, k+1) -> S and (k+1, k+1) -> Q, fetched by waves 0..3
+// once their pivot groups are done (they are idle for the rest of the elimination): each
+// polls the two flags and has its sc1 loads in flight before the post-elimination barrier,
+// so the tiles land in LDS without a separate acquire + load phase.
+struct HandoffPrefetch {
+    const unsigned int *f1, *f2;  // nullptr: no prefetch (last step)
+    unsigned int ep;
+    const double *t1, *t2;        // tile origins in the column-major matrix
+    int lda;
+    double (*S)[65], (*Q)[65];
+};
+
 __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[128], double *piv,
                                                int *cnt, uint32_t *err,
-                                               unsigned long long *gts = nullptr) {
+                                               unsigned long long *gts = nullptr,
+                                               const HandoffPrefetch *pf = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int r0 = wid * 8, c0 = lane * 2;
     double(*MUL)[64] = (double(*)[64]) & T[0][0];
@@ -1178,7 +1203,28 @@ __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[1
     }
     __builtin_amdgcn_s_setprio(0);
     if (gts && lane == 0) gts[8 + wid] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();  // every wave is done with MUL (= T)
+    const bool fetch = pf && pf->f1 && wid < 4;
+    double h1[16], h2[16];
+    if (fetch) {
+        for (unsigned spins = 0;;) {
+            const unsigned int v1 = __hip_atomic_load(pf->f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned int v2 = __hip_atomic_load(pf->f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane((int)(v1 == pf->ep && v2 == pf->ep))) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 25)) {
+                if (lane == 0) atomicOr(err, 16u);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int e = tid + q * 256, y = e & 63, x = e >> 6;
+            h1[q] = ld_sc1(&pf->t1[(size_t)y + (size_t)x * pf->lda]);
+            h2[q] = ld_sc1(&pf->t2[(size_t)y + (size_t)x * pf->lda]);
+        }
+    }
+    __syncthreads();  // every wave is done with MUL (= T) and ROWS (= S, Q)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const double pv = piv[r0 + i];
@@ -1190,6 +1236,14 @@ __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[1
 #pragma unroll
         for (int q = 0; q < 2; ++q)
             if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * r;
+    }
+    if (fetch) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int e = tid + q * 256, y = e & 63, x = e >> 6;
+            pf->S[y][x] = h1[q];
+            pf->Q[y][x] = h2[q];
+        }
     }
     __syncthreads();
 }
@@ -1225,7 +1279,16 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     } while (0)
         for (int k = 0; k < nblk; ++k) {
             CHAIN_TS(0);
-            diag_eliminate(T, ROWS, piv, &cnt, err, trace ? trace + k * 32 + 16 : nullptr);
+            // hand-off tiles (k, k+1) -> S, (k+1, k+1) -> Q (updated by their owners through
+            // step k-1) are fetched during the elimination by the waves done pivoting
+            HandoffPrefetch pf{nullptr, nullptr, F.ep, nullptr, nullptr, lda, S, Q};
+            if (k + 1 < nblk) {
+                pf.f1 = &F.R[2 * k + 1];
+                pf.f2 = &F.R[2 * (k + 1)];
+                pf.t1 = A + (size_t)k * kNB + (size_t)(k + 1) * kNB * lda;
+                pf.t2 = A + (size_t)(k + 1) * kNB + (size_t)(k + 1) * kNB * lda;
+            }
+            diag_eliminate(T, ROWS, piv, &cnt, err, trace ? trace + k * 32 + 16 : nullptr, &pf);
             CHAIN_TS(1);
             double *W = Wd + (size_t)k * kNB * kNB;
             for (int e = tid; e < 64 * 64; e += 512) {  // stores drain behind the next work
@@ -1234,42 +1297,44 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             }
             CHAIN_TS(2);
             if (k + 1 < nblk) {
-                // hand-off tiles, updated by their owners through step k-1
-                flag_acquire2(&F.R[2 * k + 1], &F.R[2 * (k + 1)], F.ep, err);
                 CHAIN_TS(3);
-                {
-                    // all 16 loads of the two tiles in flight before the first LDS write
-                    double vs[8], vq[8];
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        const int e = tid + q * 512, y = e & 63, x = e >> 6;
-                        vs[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda]);
-                        vq[q] = ld_sc1(
-                            &A[(size_t)((k + 1) * kNB + y) + (size_t)((k + 1) * kNB + x) * lda]);
-                    }
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        const int e = tid + q * 512, y = e & 63, x = e >> 6;
-                        S[y][x] = vs[q];
-                        Q[y][x] = vq[q];
-                    }
-                }
-                __syncthreads();
                 CHAIN_TS(4);
                 // U_{k,k+1}[r][x] = sum_{s <= r} W[r][s] S[s][x]  (W = T lower triangular):
                 // block row by needs K steps 0 .. 4 by + 3 only; wave w takes column block
-                // w >> 1 and the row-block pair {0, 3} or {1, 2} (20 MFMAs per wave)
+                // w >> 1 and the row-block pair {0, 3} or {1, 2} (20 MFMAs per wave), the
+                // two blocks' chains interleaved and the longer one split even / odd
                 const int ubx = wid >> 1;
+                {
+                    auto wop = [&](int by, int kk) {
+                        return T[by * 16 + (lane & 15)][kk * 4 + (lane >> 4)];
+                    };
+                    auto sop = [&](int kk) { return S[kk * 4 + (lane >> 4)][ubx * 16 + (lane & 15)]; };
+                    v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = a0, b0 = a0, b1 = a0;
+                    if (!(wid & 1)) {  // by = 0 (4 steps) and by = 3 (16 steps)
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int by = (wid & 1) ? (h ? 2 : 1) : (h ? 3 : 0);
-                    acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
-                    for (int kk = 0; kk < 4 * (by + 1); ++kk) {
-                        const int sr = kk * 4 + (lane >> 4);
-                        acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                            T[by * 16 + (lane & 15)][sr], S[sr][ubx * 16 + (lane & 15)], acc[h],
-                            0, 0, 0);
+                        for (int kk = 0; kk < 16; kk += 2) {
+                            const double s0 = sop(kk), s1 = sop(kk + 1);
+                            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk), s0, b0, 0, 0, 0);
+                            if (kk < 4)
+                                a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk), s0, a0, 0, 0, 0);
+                            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk + 1), s1, b1, 0, 0, 0);
+                            if (kk < 4)
+                                a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk + 1), s1, a1, 0, 0, 0);
+                        }
+                    } else {  // by = 1 (8 steps) and by = 2 (12 steps)
+#pragma unroll
+                        for (int kk = 0; kk < 12; kk += 2) {
+                            const double s0 = sop(kk), s1 = sop(kk + 1);
+                            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk), s0, b0, 0, 0, 0);
+                            if (kk < 8)
+                                a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk), s0, a0, 0, 0, 0);
+                            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk + 1), s1, b1, 0, 0, 0);
+                            if (kk < 8)
+                                a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk + 1), s1, a1, 0, 0, 0);
+                        }
                     }
+                    acc[0] = a0 + a1;
+                    acc[1] = b0 + b1;
                 }
                 __syncthreads();  // all reads of S (and of W in T) done
 #pragma unroll
@@ -1278,37 +1343,54 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int y = by * 16 + (lane >> 4) + 4 * r, x = ubx * 16 + (lane & 15);
-                        const double v = acc[h][r];
-                        S[y][x] = v;  // U_{k,k+1}
-                        st_sc1(&A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda], v);
+                        S[y][x] = acc[h][r];  // U_{k,k+1}
                     }
                 }
                 __syncthreads();
+                tile_store(S, A, lda, k, k + 1);  // coalesced; drains behind D_{k+1}
                 CHAIN_TS(5);
                 // D_{k+1} = A_{k+1,k+1} - U' U on the 10 upper 16x16 blocks (waves 0, 1 take
-                // two); the strictly lower blocks of T are zeroed
+                // two, all chains interleaved and split even / odd); the strictly lower
+                // blocks of T are zeroed
                 {
-                    const int nb = wid < 2 ? 2 : 1;
-                    for (int h = 0; h < nb; ++h) {
-                        const int blk = h ? 8 + wid : wid;
-                        // upper blocks in order (0,0) (0,1) (1,1) (0,2) (1,2) (2,2) (0,3) ...
-                        const int bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
-                        const int by = blk - bx * (bx + 1) / 2;
-                        v4d d = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-                        for (int kk = 0; kk < 16; ++kk) {
-                            const int sr = kk * 4 + (lane >> 4);
-                            d = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                                S[sr][by * 16 + (lane & 15)], S[sr][bx * 16 + (lane & 15)], d, 0,
-                                0, 0);
+                    // upper blocks in order (0,0) (0,1) (1,1) (0,2) (1,2) (2,2) (0,3) ...
+                    auto bxy = [](int blk, int &by, int &bx) {
+                        bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
+                        by = blk - bx * (bx + 1) / 2;
+                    };
+                    int by0, bx0, by1, bx1;
+                    bxy(wid, by0, bx0);
+                    bxy(8 + (wid & 1), by1, bx1);
+                    auto sop = [&](int kk, int b) {
+                        return S[kk * 4 + (lane >> 4)][b * 16 + (lane & 15)];
+                    };
+                    v4d d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, e0 = d0, e1 = d0;
+                    if (wid < 2) {
+#pragma unroll
+                        for (int kk = 0; kk < 16; kk += 2) {
+                            d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk, by0), sop(kk, bx0), d0, 0, 0, 0);
+                            e0 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk, by1), sop(kk, bx1), e0, 0, 0, 0);
+                            d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk + 1, by0), sop(kk + 1, bx0), d1, 0, 0, 0);
+                            e1 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk + 1, by1), sop(kk + 1, bx1), e1, 0, 0, 0);
                         }
+                    } else {
+#pragma unroll
+                        for (int kk = 0; kk < 16; kk += 2) {
+                            d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk, by0), sop(kk, bx0), d0, 0, 0, 0);
+                            d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(sop(kk + 1, by0), sop(kk + 1, bx0), d1, 0, 0, 0);
+                        }
+                    }
+                    const v4d dd = d0 + d1, ee = e0 + e1;
+                    auto put = [&](int by, int bx, const v4d &d) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int y = by * 16 + (lane >> 4) + 4 * r, x = bx * 16 + (lane & 15);
                             T[y][x] = (y <= x) ? Q[y][x] - d[r] : 0.0;
                             if (by != bx) T[x][y] = 0.0;  // the mirrored lower block
                         }
-                    }
+                    };
+                    put(by0, bx0, dd);
+                    if (wid < 2) put(by1, bx1, ee);
                 }
                 CHAIN_TS(6);
                 // publish W_k and U_{k,k+1} together (their sc1 stores have drained meanwhile)
@@ -1342,7 +1424,13 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         if (i == 0 && j == 0) continue;  // the chain starts from A_00 itself
         const bool diag = (j == i);
         const bool handoff = diag || (j == i + 1 && j < nblk);
+        // (i, i+2): only updated and stored; the owner of (i+1, i+2) forms U_{i,i+2} itself
+        // (one flag hop less on the path that feeds the chain).  (0, 2) is read raw.
+        const bool hstore = (j == i + 2 && j < nblk);
+        if (hstore && i == 0) continue;
+        const bool merge = (j == i + 1 && j < nblk && i >= 1);
         const int nupd = diag ? i - 1 : i;  // (i,i): updates 0..i-2, the chain applies i-1
+        const int nstd = merge ? nupd - 1 : nupd;  // merge: the last update is formed below
         // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1)
         constexpr int kt = 6;
         unsigned long long *otr = nullptr;
@@ -1364,7 +1452,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         // read-modify-write of T and one barrier fewer per update.
         bool have = false;  // S (and Q) already hold panel k
         acc[0] = acc[1] = (v4d){0.0, 0.0, 0.0, 0.0};
-        for (int k = 0; k < nupd; ++k) {
+        for (int k = 0; k < nstd; ++k) {
             if (k == nupd - 1) OWN_TS(0);
             if (!have) {
                 flag_acquire2(&F.P[k * F.ncb + i], diag ? nullptr : &F.P[k * F.ncb + j], F.ep,
@@ -1374,7 +1462,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 if (!diag) tile_load(Q, A, lda, k, j, false);
             }
             if (tid == 0) {
-                bool rdy = k + 1 < nupd;
+                bool rdy = k + 1 < nstd;
                 if (rdy)
                     rdy = __hip_atomic_load(&F.P[(k + 1) * F.ncb + i], __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT) == F.ep &&
@@ -1409,11 +1497,75 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             have = pre;
             if (k == nupd - 1) OWN_TS(3);
         }
+        if (merge) {
+            // last update k = i-1 of the hand-off tile (i, i+1): U_{k,i+1} = W_k A_{k,i+1}
+            // (A_{k,i+1} stored by its owner through step k-1, raw for k = 0) is formed and
+            // published here, then A_{i,i+1} -= U_{k,i}' U_{k,i+1}
+            const int k = i - 1;
+            OWN_TS(0);
+            flag_acquire2(&F.W[k], k >= 1 ? &F.H[k] : nullptr, F.ep, err);
+            OWN_TS(1);
+            const double *Wk = Wd + (size_t)k * kNB * kNB;
+            double vw[8], va[8], vu[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                vw[q] = ld_sc1(&Wk[(size_t)x * kNB + y]);
+                va[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(j * kNB + x) * lda]);
+                vu[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(i * kNB + x) * lda]);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                Q[y][x] = vw[q];  // Q[r][s] = W_k[r][s]
+                S[y][x] = va[q];
+            }
+            __syncthreads();
+            v4d u2[2];
+            {
+                const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
+                    v4d c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
+                    // W_k lower triangular: block row by needs K steps 0 .. 4 by + 3
+                    for (int kk = 0; kk < 4 * (by + 1); kk += 2) {
+                        const int s0 = kk * 4 + (lane >> 4), s1 = s0 + 4;
+                        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            Q[by * 16 + (lane & 15)][s0], S[s0][bx * 16 + (lane & 15)], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                            Q[by * 16 + (lane & 15)][s1], S[s1][bx * 16 + (lane & 15)], c1, 0, 0, 0);
+                    }
+                    u2[h] = c0 + c1;
+                }
+            }
+            OWN_TS(2);
+            __syncthreads();  // every wave has read W_k and A_{k,i+1}
+            MM_FOR(h, r, y, x) { Q[y][x] = u2[h][r]; }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                S[y][x] = vu[q];
+            }
+            __syncthreads();
+            // U_{k,i+1} published first (coalesced write-through stores from LDS): the
+            // diagonal hand-off (i+1, i+1) needs it for its last update
+            tile_store(Q, A, lda, k, j);
+            flag_release(&F.P[k * F.ncb + j], F.ep);
+            mm_tn<true>(S, Q, acc);
+            OWN_TS(3);
+        }
         if (nupd > 0) {
             MM_FOR(h, r, y, x) {
                 if (!diag || y <= x) T[y][x] -= acc[h][r];
             }
             __syncthreads();
+        }
+        if (hstore) {
+            tile_store(T, A, lda, i, j);
+            flag_release(&F.H[i], F.ep);
+            OWN_TS(4);
+            continue;
         }
         if (handoff) {
             tile_store(T, A, lda, i, j);
@@ -1456,9 +1608,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             }
         }
         OWN_TS(6);
-        MM_FOR(h, r, y, x) {
-            st_sc1(&A[(size_t)(i * kNB + y) + (size_t)(j * kNB + x) * lda], acc[h][r]);
-        }
+        __syncthreads();  // every wave has read T
+        MM_FOR(h, r, y, x) { T[y][x] = acc[h][r]; }
+        __syncthreads();
+        tile_store(T, A, lda, i, j);  // coalesced write-through stores
         flag_release(&F.P[i * F.ncb + j], F.ep);
         OWN_TS(7);
 #undef OWN_TS
@@ -1471,8 +1624,9 @@ static size_t bsolve_flag_offset(int m_pad, int nrhs_blocks) {
     return nblk + nblk * ncb + 2 * nblk + 4;
 }
 
+// [... | backward-solve: nblk | H: nblk]
 size_t chol_flag_words(int m_pad, int nrhs_blocks) {
-    return bsolve_flag_offset(m_pad, nrhs_blocks) + (size_t)m_pad / kNB;
+    return bsolve_flag_offset(m_pad, nrhs_blocks) + 2 * ((size_t)m_pad / kNB);
 }
 
 // Host-side epoch per flag buffer: advance = true starts a new use (zeroing `words` flags
@@ -1508,7 +1662,8 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
     const int ncb = nblk + nrhs_blocks;
     const size_t words = chol_flag_words(m_pad, nrhs_blocks);
     const unsigned int ep = flag_epoch(flags, words, s, true);
-    CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb, ncb, ep};
+    CholFlags F{flags, flags + nblk, flags + nblk + (size_t)nblk * ncb,
+                flags + bsolve_flag_offset(m_pad, nrhs_blocks) + nblk, ncb, ep};
     const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
     const int grid = std::min(device_cus(), 1 + ntiles);
     k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);

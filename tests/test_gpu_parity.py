@@ -501,9 +501,9 @@ def test_bridge_em_all_dropped_and_trace(gpu_lib):
     assert np.all(np.diff(l1) >= -1e-9 * l1.max())
 
 
-@pytest.mark.parametrize("n,p", [(442, 10), (300, 64)])
+@pytest.mark.parametrize("n,p", [(442, 10), (300, 64), (506, 103), (400, 128)])
 def test_bridge_em_batch_matches_oracle(gpu_lib, n, p):
-    """trace.beta's grid in one launch (a workgroup per ratio, p <= 64) against the EM
+    """trace.beta's grid in one launch (a workgroup per ratio, p <= 128) against the EM
     oracle ratio by ratio: same active sets and solve counts, estimates to 1e-9."""
     from oracle import em
     bb = gpu_lib

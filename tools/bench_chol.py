@@ -34,9 +34,8 @@ for m in (512, 1024, 2048, 4096):
         acq = ts[kt, 3].astype(np.int64)         # chain acquired step kt's hand-off
         rel = lambda v: (v - w_pub) * 0.01
         print(f"owner hops feeding step {kt} (us after the chain released W_{kt-1}):")
-        print("  hop A (tile (kt-1,kt+1)): last update acquired %.2f, U phase: wait W %.2f -> "
-              "acquired %.2f -> MFMA done %.2f -> released %.2f" %
-              (rel(o[1]), rel(o[4]), rel(o[5]), rel(o[6]), rel(o[7])))
-        print("  hop B (tile (kt,kt+1)): waits last update %.2f -> acquired %.2f -> loaded %.2f "
-              "-> updated %.2f -> handed off %.2f;  chain acquired %.2f" %
+        print("  tile (kt-1,kt+1) [updated, stored]: last update acquired %.2f -> stored %.2f" %
+              (rel(o[1]), rel(o[4])))
+        print("  tile (kt,kt+1) [hand-off; last update from the chain's panels]: waits %.2f -> "
+              "acquired %.2f -> loaded %.2f -> updated %.2f -> handed off %.2f;  chain acquired %.2f" %
               (rel(o[8]), rel(o[9]), rel(o[10]), rel(o[11]), rel(o[12]), rel(acq)))
