@@ -797,7 +797,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     const bool small = c.p <= c.n && c.world == 1 && e->method != 5 && e->method != 6;
     // the Cholesky scratch covers the n x n (Woodbury) and any p x p (chol, LS start) system
     const int m_sys = (e->woodbury() && !small) ? n_pad : (n_pad > p_pad ? n_pad : p_pad);
-    e->Wd = dalloc<double>((size_t)kNB * m_sys, o);
+    e->Wd = dalloc<double>(chol_wd_words(m_sys), o);
     e->flags = dalloc<unsigned int>(chol_flag_words(m_sys, 1), o);
     if (e->method == 6) {
         // logistic: X' resident (p_pad x n_pad), K-split slabs of X'Omega X, c = X'kappa
@@ -1727,7 +1727,7 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
         for (int r = 0; r < m_pad; ++r) h[(size_t)r + (size_t)m_pad * m_pad] = 1.0;
         double *src = dalloc<double>(h.size(), owned), *dA = dalloc<double>(h.size(), owned);
         HIPCHECK(hipMemcpy(src, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
+        double *Wd = dalloc<double>(chol_wd_words(m_pad), owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
@@ -1986,7 +1986,7 @@ int bb_chol_solve(double *x, const double *Ah, const double *bh, int m, int nrhs
         for (int q = 0; q < nrhs; ++q)
             for (int r = 0; r < m; ++r) h[(size_t)r + (size_t)(m_pad + q) * m_pad] = bh[r + (size_t)q * m];
         HIPCHECK(hipMemcpy(dA, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        double *Wd = dalloc<double>((size_t)kNB * m_pad, owned);
+        double *Wd = dalloc<double>(chol_wd_words(m_pad), owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(m_pad, 1), owned);
         double *W = dalloc<double>((size_t)m_pad * nrhs, owned);
         uint32_t *de = dalloc<uint32_t>(1, owned);
@@ -2051,7 +2051,7 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
         double *bvec = dalloc<double>(p_pad, owned);
         launch_coldot(0, dX, n_pad, n_pad, dy, p, bvec);
         double *A = dalloc<double>((size_t)p_pad * (p_pad + kNB), owned);
-        double *Wd = dalloc<double>((size_t)kNB * p_pad, owned);
+        double *Wd = dalloc<double>(chol_wd_words(p_pad), owned);
         unsigned int *fl = dalloc<unsigned int>(chol_flag_words(p_pad, 1), owned);
         double *W = dalloc<double>(p_pad, owned);
         double *dlam = dalloc<double>(p_pad, owned);

@@ -110,6 +110,8 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 // flags tagged with a per-buffer epoch; zeroed only when first seen).  trace: optional
 // timestamps (bb_bench_chol).
 size_t chol_flag_words(int m_pad, int nrhs_blocks);
+// doubles of the Wd buffer chol_factor needs (W_k blocks + scratch tiles)
+size_t chol_wd_words(int m_pad);
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *Wd, unsigned int *flags, unsigned long long *trace = nullptr);
 

@@ -1410,6 +1410,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         return;
     }
     // ------------------------------ tile owners ------------------------------
+    double *Hs = Wd + (size_t)nblk * kNB * kNB;  // scratch tiles behind the W_k blocks
     const int nowner = gridDim.x - 1;
     int n = blockIdx.x - 1;
     int ti = 0, tj = 0, base = 0;  // tile (ti, tj) = the n-th tile in row-major order
@@ -1426,11 +1427,18 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         const bool handoff = diag || (j == i + 1 && j < nblk);
         // (i, i+2): only updated and stored; the owner of (i+1, i+2) forms U_{i,i+2} itself
         // (one flag hop less on the path that feeds the chain).  (0, 2) is read raw.
+        // (i, i+2): updated through step i-1 and stored into the scratch tile Hs[i] (raw for
+        // i = 0) for the owners of (i+1, i+2) and (i+2, i+2), which form U_{i,i+2} from it;
+        // the published U_{i,i+2} must not alias it (those two read it at different times)
         const bool hstore = (j == i + 2 && j < nblk);
-        if (hstore && i == 0) continue;
+        // (i, i+1), i >= 1, and (i, i), i >= 2: the last owner update k (k = i-1 resp. i-2)
+        // needs U_{k,j} with j = k+2, which the owner forms itself from W_k and the stored
+        // tile (k, k+2): the hand-offs are one flag hop behind W_k
         const bool merge = (j == i + 1 && j < nblk && i >= 1);
+        const bool dmerge = diag && i >= 2;
         const int nupd = diag ? i - 1 : i;  // (i,i): updates 0..i-2, the chain applies i-1
-        const int nstd = merge ? nupd - 1 : nupd;  // merge: the last update is formed below
+        const int nstd = (merge || dmerge) ? nupd - 1 : nupd;
+        bool pub = false;  // merge: U_{k,j} (in Q) is published with the hand-off
         // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1)
         constexpr int kt = 6;
         unsigned long long *otr = nullptr;
@@ -1497,13 +1505,12 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             have = pre;
             if (k == nupd - 1) OWN_TS(3);
         }
-        if (merge) {
-            // last update k = i-1 of the hand-off tile (i, i+1): U_{k,i+1} = W_k A_{k,i+1}
-            // (A_{k,i+1} stored by its owner through step k-1, raw for k = 0) is formed and
-            // published here, then A_{i,i+1} -= U_{k,i}' U_{k,i+1}
-            const int k = i - 1;
+        if (merge || dmerge) {
+            // U_{k,j} = W_k A_{k,j} (A_{k,j} stored by its owner through step k-1, raw for
+            // k = 0); merge: A_{i,i+1} -= U_{k,i}' U_{k,j}, dmerge: A_{i,i} -= U_{k,i}' U_{k,i}
+            const int k = merge ? i - 1 : i - 2;
             OWN_TS(0);
-            flag_acquire2(&F.W[k], k >= 1 ? &F.H[k] : nullptr, F.ep, err);
+            flag_acquire2(&F.W[k], &F.H[k], F.ep, err);
             OWN_TS(1);
             const double *Wk = Wd + (size_t)k * kNB * kNB;
             double vw[8], va[8], vu[8];
@@ -1511,8 +1518,8 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             for (int q = 0; q < 8; ++q) {
                 const int e = tid + q * 512, y = e & 63, x = e >> 6;
                 vw[q] = ld_sc1(&Wk[(size_t)x * kNB + y]);
-                va[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(j * kNB + x) * lda]);
-                vu[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(i * kNB + x) * lda]);
+                va[q] = ld_sc1(&Hs[(size_t)k * kNB * kNB + (size_t)y + (size_t)x * kNB]);
+                vu[q] = merge ? ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(i * kNB + x) * lda]) : 0.0;
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -1540,20 +1547,23 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 }
             }
             OWN_TS(2);
-            __syncthreads();  // every wave has read W_k and A_{k,i+1}
+            __syncthreads();  // every wave has read W_k and A_{k,j}
             MM_FOR(h, r, y, x) { Q[y][x] = u2[h][r]; }
+            if (merge) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int e = tid + q * 512, y = e & 63, x = e >> 6;
-                S[y][x] = vu[q];
+                for (int q = 0; q < 8; ++q) {
+                    const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                    S[y][x] = vu[q];
+                }
             }
             __syncthreads();
-            // U_{k,i+1} published first (coalesced write-through stores from LDS): the
-            // diagonal hand-off (i+1, i+1) needs it for its last update
-            tile_store(Q, A, lda, k, j);
-            flag_release(&F.P[k * F.ncb + j], F.ep);
-            mm_tn<true>(S, Q, acc);
+            if (merge) mm_tn<true>(S, Q, acc);
+            else mm_tn<true>(Q, Q, acc);
             OWN_TS(3);
+            if (merge) {
+                tile_store(Q, A, lda, k, j);  // U_{k,j}, released with the hand-off below
+                pub = true;
+            }
         }
         if (nupd > 0) {
             MM_FOR(h, r, y, x) {
@@ -1562,14 +1572,22 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             __syncthreads();
         }
         if (hstore) {
-            tile_store(T, A, lda, i, j);
+            tile_store(T, Hs + (size_t)i * kNB * kNB, kNB, 0, 0);
             flag_release(&F.H[i], F.ep);
             OWN_TS(4);
             continue;
         }
         if (handoff) {
             tile_store(T, A, lda, i, j);
-            flag_release(&F.R[2 * i + (diag ? 0 : 1)], F.ep);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_store(&F.R[2 * i + (diag ? 0 : 1)], F.ep, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (pub)
+                    __hip_atomic_store(&F.P[(i - 1) * F.ncb + j], F.ep, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
             OWN_TS(4);
             continue;
         }
@@ -1623,6 +1641,9 @@ static size_t bsolve_flag_offset(int m_pad, int nrhs_blocks) {
     const size_t nblk = (size_t)m_pad / kNB, ncb = nblk + nrhs_blocks;
     return nblk + nblk * ncb + 2 * nblk + 4;
 }
+
+// Wd: the nblk blocks W_k followed by nblk scratch tiles (chol_factor's Hs)
+size_t chol_wd_words(int m_pad) { return 2 * (size_t)kNB * m_pad; }
 
 // [... | backward-solve: nblk | H: nblk]
 size_t chol_flag_words(int m_pad, int nrhs_blocks) {
