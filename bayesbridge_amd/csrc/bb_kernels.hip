@@ -1083,6 +1083,51 @@ __device__ __forceinline__ void mm_tn(const double (*P)[65], const double (*Q)[6
     }
 }
 
+// C = Wl * B for a lower-triangular 64 x 64 Wl (K steps 0 .. 4 by + 3 of block row by):
+// wave w takes column block w >> 1 and the block-row pair {0, 3} (w even) or {1, 2} (w odd),
+// 20 MFMAs per wave with compile-time trip counts; the two chains interleaved and the longer
+// one split even / odd.  lo = block row 0 / 1, hi = block row 3 / 2.  wl_put stores them.
+__device__ __forceinline__ void wl_times(const double (*Wl)[65], const double (*B)[65], v4d &lo,
+                                         v4d &hi) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ubx = wid >> 1;
+    auto wop = [&](int by, int kk) { return Wl[by * 16 + (lane & 15)][kk * 4 + (lane >> 4)]; };
+    auto bop = [&](int kk) { return B[kk * 4 + (lane >> 4)][ubx * 16 + (lane & 15)]; };
+    v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = a0, b0 = a0, b1 = a0;
+    if (!(wid & 1)) {  // by = 0 (4 steps) and by = 3 (16 steps)
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 2) {
+            const double s0 = bop(kk), s1 = bop(kk + 1);
+            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk), s0, b0, 0, 0, 0);
+            if (kk < 4) a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk), s0, a0, 0, 0, 0);
+            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk + 1), s1, b1, 0, 0, 0);
+            if (kk < 4) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk + 1), s1, a1, 0, 0, 0);
+        }
+    } else {  // by = 1 (8 steps) and by = 2 (12 steps)
+#pragma unroll
+        for (int kk = 0; kk < 12; kk += 2) {
+            const double s0 = bop(kk), s1 = bop(kk + 1);
+            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk), s0, b0, 0, 0, 0);
+            if (kk < 8) a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk), s0, a0, 0, 0, 0);
+            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk + 1), s1, b1, 0, 0, 0);
+            if (kk < 8) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk + 1), s1, a1, 0, 0, 0);
+        }
+    }
+    lo = a0 + a1;
+    hi = b0 + b1;
+}
+
+__device__ __forceinline__ void wl_put(double (*L)[65], const v4d &lo, const v4d &hi) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, ubx = wid >> 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int by = (wid & 1) ? (h ? 2 : 1) : (h ? 3 : 0);
+        const v4d &v = h ? hi : lo;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            L[by * 16 + (lane >> 4) + 4 * r][ubx * 16 + (lane & 15)] = v[r];
+    }
+}
+
 #define MM_FOR(h, r, y, x)                                                                  \
     for (int h = 0; h < 2; ++h)                                                             \
         for (int r = 0; r < 4; ++r)                                                         \
@@ -1303,49 +1348,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 // block row by needs K steps 0 .. 4 by + 3 only; wave w takes column block
                 // w >> 1 and the row-block pair {0, 3} or {1, 2} (20 MFMAs per wave), the
                 // two blocks' chains interleaved and the longer one split even / odd
-                const int ubx = wid >> 1;
-                {
-                    auto wop = [&](int by, int kk) {
-                        return T[by * 16 + (lane & 15)][kk * 4 + (lane >> 4)];
-                    };
-                    auto sop = [&](int kk) { return S[kk * 4 + (lane >> 4)][ubx * 16 + (lane & 15)]; };
-                    v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = a0, b0 = a0, b1 = a0;
-                    if (!(wid & 1)) {  // by = 0 (4 steps) and by = 3 (16 steps)
-#pragma unroll
-                        for (int kk = 0; kk < 16; kk += 2) {
-                            const double s0 = sop(kk), s1 = sop(kk + 1);
-                            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk), s0, b0, 0, 0, 0);
-                            if (kk < 4)
-                                a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk), s0, a0, 0, 0, 0);
-                            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(3, kk + 1), s1, b1, 0, 0, 0);
-                            if (kk < 4)
-                                a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(0, kk + 1), s1, a1, 0, 0, 0);
-                        }
-                    } else {  // by = 1 (8 steps) and by = 2 (12 steps)
-#pragma unroll
-                        for (int kk = 0; kk < 12; kk += 2) {
-                            const double s0 = sop(kk), s1 = sop(kk + 1);
-                            b0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk), s0, b0, 0, 0, 0);
-                            if (kk < 8)
-                                a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk), s0, a0, 0, 0, 0);
-                            b1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(2, kk + 1), s1, b1, 0, 0, 0);
-                            if (kk < 8)
-                                a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(wop(1, kk + 1), s1, a1, 0, 0, 0);
-                        }
-                    }
-                    acc[0] = a0 + a1;
-                    acc[1] = b0 + b1;
-                }
+                // U_{k,k+1} = W_k A_{k,k+1}  (W = T lower triangular)
+                wl_times(T, S, acc[0], acc[1]);
                 __syncthreads();  // all reads of S (and of W in T) done
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int by = (wid & 1) ? (h ? 2 : 1) : (h ? 3 : 0);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int y = by * 16 + (lane >> 4) + 4 * r, x = ubx * 16 + (lane & 15);
-                        S[y][x] = acc[h][r];  // U_{k,k+1}
-                    }
-                }
+                wl_put(S, acc[0], acc[1]);  // U_{k,k+1}
                 __syncthreads();
                 tile_store(S, A, lda, k, k + 1);  // coalesced; drains behind D_{k+1}
                 CHAIN_TS(5);
@@ -1529,26 +1535,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             }
             __syncthreads();
             v4d u2[2];
-            {
-                const int lane = tid & 63, wid = tid >> 6;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
-                    v4d c0 = {0.0, 0.0, 0.0, 0.0}, c1 = c0;
-                    // W_k lower triangular: block row by needs K steps 0 .. 4 by + 3
-                    for (int kk = 0; kk < 4 * (by + 1); kk += 2) {
-                        const int s0 = kk * 4 + (lane >> 4), s1 = s0 + 4;
-                        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                            Q[by * 16 + (lane & 15)][s0], S[s0][bx * 16 + (lane & 15)], c0, 0, 0, 0);
-                        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                            Q[by * 16 + (lane & 15)][s1], S[s1][bx * 16 + (lane & 15)], c1, 0, 0, 0);
-                    }
-                    u2[h] = c0 + c1;
-                }
-            }
+            wl_times(Q, S, u2[0], u2[1]);  // U_{k,j} = W_k A_{k,j}
             OWN_TS(2);
             __syncthreads();  // every wave has read W_k and A_{k,j}
-            MM_FOR(h, r, y, x) { Q[y][x] = u2[h][r]; }
+            wl_put(Q, u2[0], u2[1]);
             if (merge) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -1610,24 +1600,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             }
         }
         __syncthreads();
-        {
-            const int lane = tid & 63, wid = tid >> 6;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int blk = wid * 2 + h, bx = blk >> 2, by = blk & 3;
-                acc[h] = (v4d){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-                for (int kk = 0; kk < 16; ++kk) {
-                    const int sr = kk * 4 + (lane >> 4);
-                    acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(
-                        Q[by * 16 + (lane & 15)][sr], T[sr][bx * 16 + (lane & 15)], acc[h], 0,
-                        0, 0);
-                }
-            }
-        }
+        wl_times(Q, T, acc[0], acc[1]);  // U_ij = W_i A_ij
         OWN_TS(6);
         __syncthreads();  // every wave has read T
-        MM_FOR(h, r, y, x) { T[y][x] = acc[h][r]; }
+        wl_put(T, acc[0], acc[1]);
         __syncthreads();
         tile_store(T, A, lda, i, j);  // coalesced write-through stores
         flag_release(&F.P[i * F.ncb + j], F.ep);
