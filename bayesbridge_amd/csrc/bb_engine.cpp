@@ -434,10 +434,24 @@ struct bb_engine {
             mark(PH_PG);
             // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums)
             launch_pg(stream, red1 + nbS, n, n_pad, cfg.seed, cfg.stream, t, omega, err);
-            mark(PH_GRAM);
-            launch_gram(stream, Xt, p_pad, omega, p_pad, n_pad, S, slabs, p_pad, slab_stride);
-            mark(PH_REDUCE);
-            launch_slab_sum(stream, slabs, S, slab_stride, p_pad, nullptr, 0, Gw, 0);
+            if (cfg.gram_mode == 1) {
+                // X'Omega X = Y Y', Y = X' diag(sqrt(omega)): the Ozaki-II Gram of the
+                // resident transpose (rows = coefficients, K = observations)
+                mark(PH_OZPREP);
+                launch_oz_scale(stream, omega, n_pad, oz_xmax, n_oz, oz_b, oz_rowbits, oz_rscale,
+                                oz_escale);
+                launch_oz_residues(stream, Xt, p_pad, p_pad, n_oz, n_pad, omega, oz_rscale, oz_R,
+                                   nullptr, nullptr);
+                mark(PH_GRAM);
+                launch_oz_gemm(stream, oz_R, n_oz, n_pad, oz_S, oz_P);
+                mark(PH_REDUCE);
+                launch_oz_crt(stream, oz_P, oz_S, n_oz, p_pad, oz_escale, nullptr, 0, Gw);
+            } else {
+                mark(PH_GRAM);
+                launch_gram(stream, Xt, p_pad, omega, p_pad, n_pad, S, slabs, p_pad, slab_stride);
+                mark(PH_REDUCE);
+                launch_slab_sum(stream, slabs, S, slab_stride, p_pad, nullptr, 0, Gw, 0);
+            }
         } else if (method == 4) {
             // BridgeWrapper.cpp:166-168: omega, u, then the rtnorm_gibbs beta passes
             mark(PH_BETA);
@@ -484,7 +498,7 @@ struct bb_engine {
             // logistic: A = X'Omega X + diag(lambda / tau^2) (sig2 = 1), c = X'kappa
             mark(PH_FORM);
             launch_form_a(stream, method == 6 ? Gw : G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad,
-                          p_pad);
+                          p_pad, method == 6 && cfg.gram_mode == 1);
             mark(PH_CHOL);
             chol_factor(stream, A, p_pad, p_pad, 1, err, Wd, flags);
             mark(PH_SOLVE);
@@ -803,10 +817,25 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         // logistic: X' resident (p_pad x n_pad), K-split slabs of X'Omega X, c = X'kappa
         e->Xt = dalloc<double>((size_t)p_pad * n_pad, o);
         launch_transpose(e->stream, e->X, n_pad, n_pad, p_pad, e->Xt, p_pad);
-        e->S = gram_splits_for(p_pad, n_pad);
-        e->slab_stride = (size_t)p_pad * p_pad;
-        e->slabs = dalloc<double>(e->slab_stride * e->S, o);
-        e->Gw = dalloc<double>((size_t)p_pad * p_pad + p_pad, o);
+        if (c.gram_mode == 1) {
+            // Ozaki-II X'Omega X (packed upper triangle into Gw): rows = p_pad, K = n_pad
+            e->n_oz = oz_rows(p_pad);
+            const int nkc = n_pad / kOzKC;
+            e->oz_b = oz_bits_for(n_pad);
+            e->oz_S = oz_splits_for(e->n_oz, nkc);
+            e->oz_xmax = dalloc<double>((size_t)nkc * e->n_oz, o);
+            e->oz_rowbits = dalloc<unsigned long long>(e->n_oz, o);
+            e->oz_rscale = dalloc<double>(e->n_oz, o);
+            e->oz_escale = dalloc<int>(e->n_oz, o);
+            e->oz_R = dalloc<int8_t>(oz_residue_bytes(e->n_oz, n_pad), o);
+            e->oz_P = dalloc<int8_t>(oz_partial_bytes(e->n_oz, e->oz_S), o);
+            launch_oz_xmax(e->stream, e->Xt, p_pad, p_pad, e->n_oz, n_pad, e->oz_xmax);
+        } else {
+            e->S = gram_splits_for(p_pad, n_pad);
+            e->slab_stride = (size_t)p_pad * p_pad;
+            e->slabs = dalloc<double>(e->slab_stride * e->S, o);
+        }
+        e->Gw = dalloc<double>(std::max((size_t)p_pad * p_pad, tri_count(p_pad)) + p_pad, o);
         e->omega = dalloc<double>(n_pad, o);
         e->kappa = dalloc<double>(n_pad, o);
         launch_kappa(e->stream, e->y, c.n, n_pad, e->kappa);

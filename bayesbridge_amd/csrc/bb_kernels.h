@@ -99,9 +99,10 @@ void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *
 void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, int p,
                      const double *ratios, const double *lambda_max, int count, double alpha,
                      double tol, int max_iter, double *beta_out, int *solves_out);
+// packed != 0: G is the packed upper triangle (tri_index, as k_oz_crt writes it)
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
-                   int rhs_col);
+                   int rhs_col, int packed = 0);
 
 // In-place upper Cholesky A = U'U of the leading m_pad x m_pad block with the
 // forward solve U'^-1 folded into the nrhs_blocks column blocks that follow (one persistent

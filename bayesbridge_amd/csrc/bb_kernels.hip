@@ -655,7 +655,8 @@ void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const do
 
 __global__ __launch_bounds__(256) void k_form_a(const double *G, int ldg, const double *lam,
                                                 const DevScalars *sc, const double *cvec, int p,
-                                                int p_pad, double *A, int lda, int rhs_col) {
+                                                int p_pad, double *A, int lda, int rhs_col,
+                                                int packed) {
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t tot = (size_t)p_pad * (p_pad + kNB);
     if (idx >= tot) return;
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(256) void k_form_a(const double *G, int ldg, const 
     double *dst = A + (size_t)r + (size_t)c * lda;
     if (c < p_pad) {
         if (r <= c) {
-            double v = G[(size_t)r + (size_t)c * ldg];
+            double v = G[packed ? tri_index(r, c) : (size_t)r + (size_t)c * ldg];
             if (r == c) {
                 if (r < p) {
                     if (lam) {
@@ -939,10 +940,10 @@ void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, i
 
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
-                   int rhs_col) {
+                   int rhs_col, int packed) {
     const size_t tot = (size_t)p_pad * (p_pad + kNB);
     k_form_a<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(G, ldg, lam, sc, c, p, p_pad, A, lda,
-                                                           rhs_col);
+                                                           rhs_col, packed);
 }
 
 // ---------------------------------------------------------------------------

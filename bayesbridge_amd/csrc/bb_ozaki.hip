@@ -117,9 +117,11 @@ int oz_splits_for(int n_oz, int nkc) {
     const int tiles = nt * (nt + 1) / 2;
     // grid = tiles x kOzMods x S workgroups, one per CU at a time: pick the S (power of two,
     // >= 16 chunks per split) with the best last-round fill over 256 CUs
+    // (at most 4: the CRT is specialised for 1, 2 and 4 splits, and every split adds a
+    // partial plane per modulus that it must read)
     int best = 1;
     double best_eff = 0.0;
-    for (int S = 1; S <= 64; S *= 2) {
+    for (int S = 1; S <= 4; S *= 2) {
         if (S > 1 && nkc / S < 16) break;
         const double wg = (double)tiles * kOzMods * S;
         const double rounds = std::ceil(wg / 256.0);

@@ -416,6 +416,15 @@ def main():
         kernel_ops = kernel_bytes
         alg_bytes = kernel_bytes
         traffic = pmc_traffic(n, p, world, kfull)
+    elif logit and gram_mode == bb.GRAM_OZAKI:
+        # Dominant kernel = the per-sweep X'Omega X as the Ozaki-II int8 Gram of X' diag(omega)
+        # (rows = coefficients, K = observations): kOzMods x p(p+1) n int8 ops per launch
+        kernel_ops = 16.0 * p * (p + 1) * n
+        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+        peak, unit, kname, bound = (INT8_MFMA_PEAK_TOPS, "TOP/s",
+                                    "k_oz_gemm16u X'Omega X (v_mfma_i32_16x16x64_i8)", "mfma")
+        alg_bytes = 16.0 * n * p
+        traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u")
     elif logit:
         # Dominant kernel = the per-sweep X'Omega X (fp64 MFMA k_gram over K = n rows):
         # n p (p + 1) algorithmic flops per launch (path p <= n, C4)
@@ -444,8 +453,10 @@ def main():
         traffic = pmc_traffic(n, p, world, "bb::k_gram")
     gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
     # the dense Gram's fp64-equivalent rate (meaningless for the sparse design)
+    if logit:
+        gram_flops = float(n) * p * (p + 1)
     fp64_equiv = (gram_flops / (gram_total_ms * 1e-3) / 1e12
-                  if gram_total_ms > 0 and kind == "dense" else None)
+                  if gram_total_ms > 0 and kind in ("dense", "logit") else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sweeps > 0:
@@ -500,7 +511,8 @@ def main():
             config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
                           nnz_local=si["nnz"], pairs_local=si["pairs"], max_row_nnz=si["max_row"])
         elif logit:
-            config["gram"] = "X'Omega X fp64 mfma"
+            config["gram"] = ("X'Omega X ozaki-II int8 (fp64-accurate)"
+                              if gram_mode == bb.GRAM_OZAKI else "X'Omega X fp64 mfma")
         else:
             config["gram"] = ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
                               else "fp64 mfma")

@@ -44,8 +44,11 @@ def test_pg_batch_matches_oracle(gpu_lib):
 
 
 @pytest.mark.parametrize("n,p,kw", [(500, 40, {}), (1500, 300, dict(alpha=0.3)),
-                                    (300, 25, dict(true_tau=0.7))])
+                                    (300, 25, dict(true_tau=0.7)),
+                                    (1500, 300, dict(gram_mode=0))])
 def test_logit_teacher_forced(gpu_lib, n, p, kw):
+    """25 teacher-forced sweeps; X'Omega X on the Ozaki-II int8 Gram (the default) and on the
+    fp64 MFMA Gram (gram_mode=0)."""
     bb = gpu_lib
     X, y, _ = logit_problem(n, p, n + p)
     alpha = kw.get("alpha", 0.5)
@@ -54,8 +57,10 @@ def test_logit_teacher_forced(gpu_lib, n, p, kw):
     o = gibbs.bridge_regression_logit(y, X, 25, burn=0, alpha=alpha, true_tau=true_tau,
                                       seed=seed, stream=stream, record_state=True)
     e = bb.Engine(bb.EngineConfig(n=n, p=p, method=6, seed=seed, stream=stream,
-                                  true_alpha=alpha, true_tau=true_tau), X, y)
+                                  true_alpha=alpha, true_tau=true_tau,
+                                  gram_mode=kw.get("gram_mode")), X, y)
     assert e.method() == 6
+    assert e.gram_mode() == kw.get("gram_mode", bb.GRAM_OZAKI)
     e.init_state()
     st = o["states"]
     for k in range(1, len(st)):
