@@ -25,8 +25,9 @@ for m in (512, 1024, 2048, 4096):
         g = ts[:, 16:].astype(np.int64)
         print("elimination groups (us): start offset / length per producer wave, step 5")
         k = 5
+        ngr = sum(1 for w in range(8) if g[k, w] > 0 and g[k, 8 + w] >= g[k, w])
         print("  " + "  ".join(f"{(g[k, w] - g[k, 0]) * 0.01:5.2f}/{(g[k, 8 + w] - g[k, w]) * 0.01:4.2f}"
-                               for w in range(8)) +
+                               for w in range(ngr)) +
               f"   (elim start -> group 0: {(g[k, 0] - ts[k, 0].astype(np.int64)) * 0.01:.2f})")
         o = ts[-1].astype(np.int64)
         kt = 6

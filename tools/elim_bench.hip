@@ -435,6 +435,114 @@ __device__ void elim_v6(double (*T)[65], double (*ROWS)[128], double *RINV, doub
     __syncthreads();
 }
 
+// ---------------- V7: V6 with a fraction-free in-wave chain ----------------
+// The block is equilibrated by exact powers of two (diagonal in [1, 4)).  Inside the
+// producing wave the remaining rows are updated as a_i <- (p a_i - m a_k) 2^-E(p_prev)
+// (Bareiss with the previous pivot's binary exponent as the divisor): the chain per pivot is
+// readlane -> one product -> one fma, and 1/p (for the published normalised row) is off it.
+// Every row of the group carries a common scale s (a_i = s * standard value), tracked off
+// the chain; published: ROWS = a_k / p (scale-free), MUL = a_k / s, piv = p / s.
+__device__ __forceinline__ double ldexp_d(double x, int e) { return __builtin_amdgcn_ldexp(x, e); }
+__device__ __forceinline__ int fexp_d(double x) { return __builtin_amdgcn_frexp_exp(x); }
+
+template <int W>
+__device__ __forceinline__ void produce_v7(double (&a)[8][2], double (*ROWS)[128], double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+    int ep = 0;        // binary exponent of the previous pivot (the exact divisor)
+    double s = 1.0;    // common scale of rows ci.. of this group
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double ak0 = ldexp_d(a[ci][0], -ep), ak1 = ldexp_d(a[ci][1], -ep);
+        const double pr = ldexp_d(pv, -ep);
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(pr, a[i][0], -(m * ak0));
+            a[i][1] = __builtin_fma(pr, a[i][1], -(m * ak1));
+        }
+        // off the chain
+        const double inv = fast_rcp(pv), invs = fast_rcp(s);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+        if (W < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(rs0, rs1);
+            if (lane < 32)
+                *(double2 *)&ROWS[64 + (c >> 1)][(c & 1) * 64 + c0] =
+                    make_double2(a[ci][0] * invs, a[ci][1] * invs);
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv * invs;
+        a[ci][0] = rs0;
+        a[ci][1] = rs1;
+        s = ldexp_d(s * pv, -ep);
+        ep = fexp_d(pv) - 1;
+    }
+}
+
+__device__ void elim_v7(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    int *ex = (int *)RINV;  // 64 per-row half exponents (equilibration)
+    if (tid < 64) ex[tid] = (fexp_d(T[tid][tid]) - 1) >> 1;
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? ldexp_d(T[row][col], -(ex[row] + ex[col]))
+                                 : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    for (int c = 0; c < r0; ++c) {
+        while (*vc <= c) {
+        }
+        asm volatile("" ::: "memory");
+        const double2 v = *(const double2 *)&ROWS[c][c0];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[64 + (c >> 1)][(c & 1) * 64 + r0 + i];
+            a[i][0] = __builtin_fma(-mm.x, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-mm.x, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-mm.y, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-mm.y, v.y, a[i + 1][1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v7<0>(a, ROWS, piv, vc); break;
+        case 1: produce_v7<1>(a, ROWS, piv, vc); break;
+        case 2: produce_v7<2>(a, ROWS, piv, vc); break;
+        case 3: produce_v7<3>(a, ROWS, piv, vc); break;
+        case 4: produce_v7<4>(a, ROWS, piv, vc); break;
+        case 5: produce_v7<5>(a, ROWS, piv, vc); break;
+        case 6: produce_v7<6>(a, ROWS, piv, vc); break;
+        default: produce_v7<7>(a, ROWS, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+    __syncthreads();
+    // W = What S^-1: row i = normalised row * sqrt(pivot), column c scaled by 2^-ex[c]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pt = piv[r0 + i];
+        const double sq = pt / sqrt(pt);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = ldexp_d(a[i][q] * sq, -ex[c0 + q - 64]);
+    }
+    __syncthreads();
+}
+
 // ---------------- V5: D-only elimination (1 column per lane), no W ----------------
 template <int W>
 __device__ __forceinline__ void produce_v5(double (&a)[8], double (*ROWS)[128], double *RINV,
@@ -531,6 +639,7 @@ __global__ __launch_bounds__(512) void k_elim(const double *A, double *W, double
         else if (V == 5) elim_v5(T, ROWS, RINV, piv, &cnt);
         else if (V == 6) elim_v6(T, ROWS, RINV, piv, &cnt);
         else if (V == 2) elim_v1<1>(T, PUB, RINV, piv, &cnt);
+        else if (V == 7) elim_v7(T, ROWS, RINV, piv, &cnt);
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         tot += t1 - t0;
     }
@@ -589,13 +698,13 @@ int main() {
     double *dA, *dW, *dP;
     unsigned long long *dt;
     hipMalloc(&dA, 64 * 64 * 8);
-    hipMalloc(&dW, 64 * 64 * 8 * 7);
-    hipMalloc(&dP, 64 * 8 * 7);
+    hipMalloc(&dW, 64 * 64 * 8 * 8);
+    hipMalloc(&dP, 64 * 8 * 8);
     hipMalloc(&dt, 8);
     hipMemcpy(dA, h.data(), 64 * 64 * 8, hipMemcpyHostToDevice);
-    std::vector<double> W[7], P[7];
+    std::vector<double> W[8], P[8];
     const int reps = 200;
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < 8; ++v) {
         unsigned long long t = 0;
         for (int rep = 0; rep < 2; ++rep) {
             if (v == 0) k_elim<0><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
@@ -605,6 +714,7 @@ int main() {
             if (v == 4) k_elim<4><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             if (v == 5) k_elim<5><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             if (v == 6) k_elim<6><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 7) k_elim<7><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
         }
         W[v].resize(4096);
@@ -639,7 +749,7 @@ int main() {
         }
     }
     // check: W = U^-T satisfies W A W' = I (lower W)
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < 8; ++v) {
         if (v == 5) continue;
         double err = 0, dw = 0;
         for (int i = 0; i < 64; ++i)
