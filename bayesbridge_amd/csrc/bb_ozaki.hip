@@ -618,12 +618,19 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
     const int ntiles = nt * (nt + 1) / 2;
     const int noff = nt * (nt - 1) / 2, npair = (nt + 1) / 2;
     const int nper = noff + npair;
-    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    // persistent: workgroup b (one per CU, b -> XCD b % 8) takes virtual blocks b, b + grid,
+    // ... so every round of a unit's tiles runs on the XCD whose L2 holds its row blocks;
+    // the tile slot rotates by 4 per round so each workgroup gets its share of diagonal pairs
+    const int xcd = blockIdx.x & 7, q0 = blockIdx.x >> 3, qs = gridDim.x >> 3;
+    const int nunits = kOzMods * nsplit;
+    for (int rnd = 0;; ++rnd) {
+    const int q = q0 + rnd * qs;
     const int u = xcd + 8 * (q / nper);
-    const int local = q % nper;
+    if (u >= nunits) break;
+    const int local = (q % nper + 4 * rnd) % nper;
     const int mod = u % kOzMods;
     const int split = u / kOzMods;
-    if (split >= nsplit) return;
+    if (rnd > 0) __syncthreads();  // the previous tile's LDS ring is drained
     const int per = (nkc + nsplit - 1) / nsplit;
     const int c0 = split * per;
     const int nch = max(0, min(nkc, c0 + per) - c0);
@@ -657,6 +664,7 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
             oz_diag_pass<dbg, true>(smem, bA, bB, kstride, c0, nch, wid, slot, out, C.m[mod],
                                     C.inv_m[mod]);
     }
+    }
 }
 
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
@@ -666,7 +674,17 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
     const OzConsts &C = oz_consts();
     // per (modulus, split) unit -- kOzMods * nsplit units, a multiple of 8 (unit u -> XCD
     // u % 8) -- the off-diagonal tiles and the diagonal pairs in one launch
-    const unsigned gu = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
+    const unsigned gu0 = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
+    // one workgroup per CU (128 KB of LDS each), a multiple of 8 (the XCD count)
+    static const unsigned cus8 = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v < 8)
+            v = 256;
+        return (unsigned)(v / 8 * 8);
+    }();
+    const unsigned gu = gu0 < cus8 ? gu0 : cus8;
     switch (dbg) {  // dbg != 0: timing ablations of bb_bench_ozaki only (results meaningless)
         case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
         case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
