@@ -114,25 +114,14 @@ int oz_rows(int n_pad) { return (n_pad + kOzT - 1) / kOzT * kOzT; }
 
 int oz_splits_for(int n_oz, int nkc) {
     const int nt = n_oz / kOzT;
-    const int tiles = nt * (nt + 1) / 2;
-    // grid = tiles x kOzMods x S workgroups, one per CU at a time: pick the S (power of two,
-    // >= 16 chunks per split) with the best last-round fill over 256 CUs
-    // (at most 4: the CRT is specialised for 1, 2 and 4 splits, and every split adds a
-    // partial plane per modulus that it must read)
-    int best = 1;
-    double best_eff = 0.0;
-    for (int S = 1; S <= 4; S *= 2) {
-        if (S > 1 && nkc / S < 16) break;
-        const double wg = (double)tiles * kOzMods * S;
-        const double rounds = std::ceil(wg / 256.0);
-        double eff = wg / (rounds * 256.0);
-        // more splits cost partial traffic; prefer fewer unless clearly fuller
-        if (eff > best_eff + 0.05) {
-            best_eff = eff;
-            best = S;
-        }
-    }
-    return best;
+    const int nper = nt * (nt - 1) / 2 + (nt + 1) / 2;  // workgroups per (modulus, split) unit
+    // the persistent GEMM runs one workgroup per CU over kOzMods * S units: take the fewest
+    // K splits (each adds a partial plane per modulus for the GEMM to write and the CRT to
+    // read) that give every CU a workgroup, at most 4 (the CRT's specialisations) and with
+    // >= 16 chunks per split
+    int S = 1;
+    while (S < 4 && nper * kOzMods * S < 256 && nkc / (2 * S) >= 16) S *= 2;
+    return S;
 }
 
 size_t oz_residue_bytes(int n_oz, int p_pad) { return (size_t)kOzMods * n_oz * p_pad; }
