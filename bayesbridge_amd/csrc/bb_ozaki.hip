@@ -112,6 +112,9 @@ int oz_bits_for(int K) {
 
 int oz_rows(int n_pad) { return (n_pad + kOzT - 1) / kOzT * kOzT; }
 
+// 2^31 / (123^2 * 64) = 2217.9: chunks per split with exact int32 accumulation
+constexpr int kOzMaxSplitChunks = 2217;
+
 int oz_splits_for(int n_oz, int nkc) {
     const int nt = n_oz / kOzT;
     const int nper = nt * (nt - 1) / 2 + (nt + 1) / 2;  // workgroups per (modulus, split) unit
@@ -121,6 +124,9 @@ int oz_splits_for(int n_oz, int nkc) {
     // >= 16 chunks per split
     int S = 1;
     while (S < 4 && nper * kOzMods * S < 256 && nkc / (2 * S) >= 16) S *= 2;
+    // exactness: a split's int32 sums of products of balanced residues (|r| <= 123) must stay
+    // below 2^31, i.e. at most kOzMaxSplitChunks 64-deep chunks per split
+    while ((nkc + S - 1) / S > kOzMaxSplitChunks) S *= 2;
     return S;
 }
 
