@@ -191,10 +191,13 @@ void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, c
 // their columns j lie in row c's support J_c: the workgroup stages D[J_c] in LDS once and
 // the pairs carry 16-bit positions into J_c instead of 32-bit column indices -- the
 // per-pair D gathers become LDS reads and the pair stream shrinks to 10 bytes.  The same
-// pass forms the diagonal sum_j X_cj^2 D_j and (X u)_c.  Entries keep k_sp_gram's lane
-// groups and per-lane order (kSpLpe lanes per entry, lane q sums pairs q, q + kSpLpe, ...),
-// with kSpDepth pairs per lane in flight.  Heaviest columns (largest c) launch first.
-constexpr int kSpDepth = 8;
+// pass forms the diagonal sum_j X_cj^2 D_j and (X u)_c.  kSpColLpe lanes per entry, lane q
+// sums pairs q, q + kSpColLpe, ... in order, kSpDepth pairs per lane in flight, then a fixed
+// xor tree.  Heaviest columns (largest c) launch first.  Measured at C5 (~20 pairs per
+// entry): 8 lanes x 4 deep 0.74 ms, 8 x 2..16 0.74-0.77, 4 x 8 (the first version) 0.80,
+// 16 x 4 0.84, 2 x 16 1.10 ms.
+constexpr int kSpColLpe = 8;
+constexpr int kSpDepth = 4;
 
 __global__ __launch_bounds__(256) void k_sp_gram_col(
     const int *__restrict__ rowptr, const int *__restrict__ colidx,
@@ -227,27 +230,27 @@ __global__ __launch_bounds__(256) void k_sp_gram_col(
         if (xu) xu[c] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
     }
     const size_t e0 = tri_index(0, c);
-    const int g = tid / kSpLpe, q = tid % kSpLpe;
-    for (int r0 = 0; r0 < c; r0 += 256 / kSpLpe) {
+    const int g = tid / kSpColLpe, q = tid % kSpColLpe;
+    for (int r0 = 0; r0 < c; r0 += 256 / kSpColLpe) {
         const int r = r0 + g;
         double s = 0.0;
         if (r < c) {
             const unsigned en = estart[e0 + r + 1];
-            for (unsigned k = estart[e0 + r] + q; k < en; k += kSpDepth * kSpLpe) {
+            for (unsigned k = estart[e0 + r] + q; k < en; k += kSpDepth * kSpColLpe) {
                 double pv[kSpDepth];
                 unsigned short iv[kSpDepth];
 #pragma unroll
                 for (int i = 0; i < kSpDepth; ++i) {
-                    const unsigned kk = k + i * kSpLpe;
+                    const unsigned kk = k + i * kSpColLpe;
                     pv[i] = kk < en ? prod[kk] : 0.0;
                     iv[i] = kk < en ? pidx[kk] : (unsigned short)0;
                 }
 #pragma unroll
                 for (int i = 0; i < kSpDepth; ++i)
-                    if (k + i * kSpLpe < en) s += pv[i] * Dl[iv[i]];
+                    if (k + i * kSpColLpe < en) s += pv[i] * Dl[iv[i]];
             }
         }
-        s = group_sum<kSpLpe>(s);
+        s = group_sum<kSpColLpe>(s);
         if (q == 0 && r < c) tri[e0 + r] = s;
     }
 }
