@@ -198,8 +198,8 @@ typedef struct bb_config {
     int trace_capacity; /* number of trace slots kept on device (>= 1) */
     uint64_t seed, stream;
     int device;
-    int gram_mode;      /* Woodbury Gram: 0 fp64 MFMA, 1 Ozaki-II on int8 MFMA (fp64-accurate);
-                           default 1 */
+    int gram_mode;      /* Woodbury Gram X diag(D) X' and the logistic X'Omega X: 0 fp64 MFMA,
+                           1 Ozaki-II on int8 MFMA (fp64-accurate); default 1 */
     int betaburn;       /* triangle method: rtnorm_gibbs passes per sweep - 1 */
 } bb_config;
 
