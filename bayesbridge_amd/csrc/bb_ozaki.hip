@@ -614,15 +614,17 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
     const int noff = nt * (nt - 1) / 2, npair = (nt + 1) / 2;
     const int nper = noff + npair;
     // persistent: workgroup b (one per CU, b -> XCD b % 8) takes virtual blocks b, b + grid,
-    // ... so every round of a unit's tiles runs on the XCD whose L2 holds its row blocks;
-    // the tile slot rotates by 4 per round so each workgroup gets its share of diagonal pairs
+    // ... so every round of a unit's tiles runs on the XCD whose L2 holds its row blocks
     const int xcd = blockIdx.x & 7, q0 = blockIdx.x >> 3, qs = gridDim.x >> 3;
     const int nunits = kOzMods * nsplit;
     for (int rnd = 0;; ++rnd) {
     const int q = q0 + rnd * qs;
     const int u = xcd + 8 * (q / nper);
     if (u >= nunits) break;
-    const int local = (q % nper + 4 * rnd) % nper;
+    // tile slot rotated per unit (a permutation of the unit's slots, so every tile is done
+    // exactly once whatever nper and the grid are); when a round is one unit per XCD (C3)
+    // each workgroup takes one diagonal pair in eight rounds
+    const int local = (q % nper + 4 * (q / nper)) % nper;
     const int mod = u % kOzMods;
     const int split = u / kOzMods;
     if (rnd > 0) __syncthreads();  // the previous tile's LDS ring is drained

@@ -116,13 +116,16 @@ def test_gram_ozaki_exact_on_integers(gpu_lib):
     """Integer Y, square-integer w: the Ozaki-II Gram is exact (every scaled input
     sqrt(w_j) Y_ij is an integer times a power of two, the CRT recovers the exact integer product), so it must equal the int64
     product bit for bit -- this also pins the int8 MFMA operand and C/D lane maps, the tile
-    decode and the split-K / XCD grouping (n not a multiple of the 256 tile, ragged k)."""
+    decode and the split-K / XCD grouping (n not a multiple of the 256 tile, ragged k).
+    (1500, 700) and (1100, 2500) have more virtual blocks than the persistent GEMM's grid
+    with a unit's tiles straddling its rounds (18 and 13 workgroups per unit, 32 per XCD)."""
     bb = gpu_lib
     rng = np.random.default_rng(17)
-    for n, k in [(300, 1000), (77, 5000), (600, 333)]:
+    for n, k in [(300, 1000), (77, 5000), (600, 333), (1500, 700), (1100, 2500)]:
         Yi = rng.integers(-60, 61, size=(n, k))
         wi = rng.choice([0, 1, 4, 9], size=k)  # perfect squares: sqrt(w) Y stays integral
-        ref = (Yi * wi) @ Yi.T
+        # every partial sum is an integer below 2^53, so the fp64 BLAS product is exact
+        ref = (Yi * wi).astype(np.float64) @ Yi.T.astype(np.float64)
         C = bb.gram(Yi.astype(np.float64), wi.astype(np.float64), mode=bb.GRAM_OZAKI)
         assert np.array_equal(C, ref.astype(np.float64)), (n, k)
 
