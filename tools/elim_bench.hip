@@ -543,6 +543,177 @@ __device__ void elim_v7(double (*T)[65], double (*ROWS)[128], double *RINV, doub
     __syncthreads();
 }
 
+// ---------------- V8: the product's diag_eliminate (round 2), for a like-for-like baseline ----
+template <int W>
+__device__ __forceinline__ void produce_v8(double (&a)[8][2], double (*ROWS)[128],
+                                          double (*MUL)[64], double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(-m, rs0, a[i][0]);
+            a[i][1] = __builtin_fma(-m, rs1, a[i][1]);
+        }
+        if (W < 7) {
+            *(double2 *)&ROWS[c][c0] = make_double2(rs0, rs1);
+            if (lane < 32) *(double2 *)&MUL[c][c0] = make_double2(a[ci][0], a[ci][1]);
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ void elim_v8(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    double(*MUL)[64] = (double(*)[64]) & T[0][0];
+    double a[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = r0 + i, col = c0 + q;
+            a[i][q] = (col < 64) ? T[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+        }
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    int avail = 0;
+    for (int c = 0; c < r0; ++c) {
+        if (c >= avail) {
+            while ((avail = *vc) <= c) {
+            }
+            asm volatile("" ::: "memory");
+        }
+        const double2 v = *(const double2 *)&ROWS[c][c0];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&MUL[c][r0 + i];
+            a[i][0] = __builtin_fma(-mm.x, v.x, a[i][0]);
+            a[i][1] = __builtin_fma(-mm.x, v.y, a[i][1]);
+            a[i + 1][0] = __builtin_fma(-mm.y, v.x, a[i + 1][0]);
+            a[i + 1][1] = __builtin_fma(-mm.y, v.y, a[i + 1][1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v8<0>(a, ROWS, MUL, piv, vc); break;
+        case 1: produce_v8<1>(a, ROWS, MUL, piv, vc); break;
+        case 2: produce_v8<2>(a, ROWS, MUL, piv, vc); break;
+        case 3: produce_v8<3>(a, ROWS, MUL, piv, vc); break;
+        case 4: produce_v8<4>(a, ROWS, MUL, piv, vc); break;
+        case 5: produce_v8<5>(a, ROWS, MUL, piv, vc); break;
+        case 6: produce_v8<6>(a, ROWS, MUL, piv, vc); break;
+        default: produce_v8<7>(a, ROWS, MUL, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pv = piv[r0 + i];
+        double r = __builtin_amdgcn_rsq(pv);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            if (c0 + q >= 64) T[r0 + i][c0 + q - 64] = a[i][q] * r;
+    }
+    __syncthreads();
+}
+
+// ---------------- V9: A-only elimination (one column per lane) with V8's consumer; U rows
+// into T (no W: the inverse would be a separate blocked MFMA step) ----------------
+template <int W>
+__device__ __forceinline__ void produce_v9(double (&a)[8], double (*ROWS)[128], double *piv,
+                                          volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci], c);
+        const double inv = fast_rcp(pv);
+        const double rs = a[ci] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci], 8 * W + i);
+            a[i] = __builtin_fma(-m, rs, a[i]);
+        }
+        if (W < 7) {
+            ROWS[c][lane] = rs;
+            ROWS[c][64 + lane] = a[ci];
+            asm volatile("" ::: "memory");
+            if (lane == 0) *vc = c + 1;
+        }
+        if (lane == 0) piv[c] = pv;
+    }
+}
+
+__device__ void elim_v9(double (*T)[65], double (*ROWS)[128], double *RINV, double *piv,
+                        int *cnt) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8;
+    double a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = T[r0 + i][lane];
+    if (tid == 0) *cnt = 0;
+    __syncthreads();
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)cnt;
+    int avail = 0;
+    for (int c = 0; c < r0; ++c) {
+        if (c >= avail) {
+            while ((avail = *vc) <= c) {
+            }
+            asm volatile("" ::: "memory");
+        }
+        const double v = ROWS[c][lane];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            const double2 mm = *(const double2 *)&ROWS[c][64 + r0 + i];
+            a[i] = __builtin_fma(-mm.x, v, a[i]);
+            a[i + 1] = __builtin_fma(-mm.y, v, a[i + 1]);
+        }
+    }
+    const unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_setprio(3);
+    switch (wid) {
+        case 0: produce_v9<0>(a, ROWS, piv, vc); break;
+        case 1: produce_v9<1>(a, ROWS, piv, vc); break;
+        case 2: produce_v9<2>(a, ROWS, piv, vc); break;
+        case 3: produce_v9<3>(a, ROWS, piv, vc); break;
+        case 4: produce_v9<4>(a, ROWS, piv, vc); break;
+        case 5: produce_v9<5>(a, ROWS, piv, vc); break;
+        case 6: produce_v9<6>(a, ROWS, piv, vc); break;
+        default: produce_v9<7>(a, ROWS, piv, vc); break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const unsigned long long tg1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) { g_ts[2 * wid] = tg0; g_ts[2 * wid + 1] = tg1; }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double pv = piv[r0 + i];
+        double r = __builtin_amdgcn_rsq(pv);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+        r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+        T[r0 + i][lane] = lane >= r0 + i ? a[i] * r : 0.0;
+    }
+    __syncthreads();
+}
+
 // ---------------- V5: D-only elimination (1 column per lane), no W ----------------
 template <int W>
 __device__ __forceinline__ void produce_v5(double (&a)[8], double (*ROWS)[128], double *RINV,
@@ -640,6 +811,8 @@ __global__ __launch_bounds__(512) void k_elim(const double *A, double *W, double
         else if (V == 6) elim_v6(T, ROWS, RINV, piv, &cnt);
         else if (V == 2) elim_v1<1>(T, PUB, RINV, piv, &cnt);
         else if (V == 7) elim_v7(T, ROWS, RINV, piv, &cnt);
+        else if (V == 8) elim_v8(T, ROWS, RINV, piv, &cnt);
+        else if (V == 9) elim_v9(T, ROWS, RINV, piv, &cnt);
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         tot += t1 - t0;
     }
@@ -698,13 +871,13 @@ int main() {
     double *dA, *dW, *dP;
     unsigned long long *dt;
     hipMalloc(&dA, 64 * 64 * 8);
-    hipMalloc(&dW, 64 * 64 * 8 * 8);
-    hipMalloc(&dP, 64 * 8 * 8);
+    hipMalloc(&dW, 64 * 64 * 8 * 10);
+    hipMalloc(&dP, 64 * 8 * 10);
     hipMalloc(&dt, 8);
     hipMemcpy(dA, h.data(), 64 * 64 * 8, hipMemcpyHostToDevice);
-    std::vector<double> W[8], P[8];
+    std::vector<double> W[10], P[10];
     const int reps = 200;
-    for (int v = 0; v < 8; ++v) {
+    for (int v = 0; v < 10; ++v) {
         unsigned long long t = 0;
         for (int rep = 0; rep < 2; ++rep) {
             if (v == 0) k_elim<0><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
@@ -715,6 +888,8 @@ int main() {
             if (v == 5) k_elim<5><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             if (v == 6) k_elim<6><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             if (v == 7) k_elim<7><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 8) k_elim<8><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
+            if (v == 9) k_elim<9><<<1, 512>>>(dA, dW + v * 4096, dP + v * 64, dt, reps);
             hipMemcpy(&t, dt, 8, hipMemcpyDeviceToHost);
         }
         W[v].resize(4096);
@@ -749,8 +924,8 @@ int main() {
         }
     }
     // check: W = U^-T satisfies W A W' = I (lower W)
-    for (int v = 0; v < 8; ++v) {
-        if (v == 5) continue;
+    for (int v = 0; v < 10; ++v) {
+        if (v == 5 || v == 9) continue;
         double err = 0, dw = 0;
         for (int i = 0; i < 64; ++i)
             for (int j = 0; j < 64; ++j) {
