@@ -549,14 +549,19 @@ __global__ __launch_bounds__(256) void k_scalars(const double *red1, int nbS, co
                                                  Key key, uint64_t t, double *tau_tr,
                                                  double *sig2_tr, double *alpha_tr, int tau_only,
                                                  uint32_t *err) {
-    __shared__ double sh[4];
+    __shared__ double sh[5];
     const double *xb = red1 + nbS;
     double v = 0.0;
     for (int i = threadIdx.x; i < n; i += 256) {
         const double r = y[i] - xb[i];
         v += r * r;
     }
-    const double rss = block_sum<256>(v, sh);
+    const double rss0 = block_sum<256>(v, sh);
+    if (threadIdx.x == 0) sh[4] = rss0;
+    __syncthreads();
+    const double rss = sh[4];
+    // tau (wave 0) and sig2 (wave 1) are independent draws on their own counters: one lane
+    // of each wave, concurrently
     if (threadIdx.x == 0) {
         double S = 0.0;
         for (int q = 0; q < nbS; ++q) S += red1[q];
@@ -567,16 +572,17 @@ __global__ __launch_bounds__(256) void k_scalars(const double *red1, int nbS, co
             const double nu = gamma1(shape, key, t, KIND_TAU, err) / rate;
             sc->tau = exp(-1.0 * log(nu) / alpha);
         }
+        sc->s_abs_pow = S;
+        sc->rss = rss;
+        if (tau_tr) *tau_tr = sc->tau;
+        if (alpha_tr) *alpha_tr = alpha;
+    } else if (threadIdx.x == 64) {
         if (!tau_only && !hy.know_sig2) {
             const double shape = hy.sig2_shape + 0.5 * (double)n;
             const double scale = hy.sig2_scale + 0.5 * rss;
             sc->sig2 = scale / gamma1(shape, key, t, KIND_SIG2, err);
         }
-        sc->s_abs_pow = S;
-        sc->rss = rss;
-        if (tau_tr) *tau_tr = sc->tau;
         if (sig2_tr) *sig2_tr = sc->sig2;
-        if (alpha_tr) *alpha_tr = sc->alpha;
     }
 }
 
