@@ -286,7 +286,7 @@ struct bb_engine {
     // Ozaki-II Gram (gram_mode 1)
     int n_oz = 0, oz_b = 0, oz_S = 1;
     double *oz_xmax = nullptr, *oz_rscale = nullptr;
-    unsigned long long *oz_rowbits = nullptr;
+    double *oz_rowmax = nullptr;  // per chunk-group row maxima (launch_oz_scale scratch)
     int *oz_escale = nullptr;
     int8_t *oz_R = nullptr, *oz_P = nullptr;
     // logistic: X' resident for X'Omega X, omega, kappa = y - 1/2, the per-sweep Gram
@@ -408,7 +408,7 @@ struct bb_engine {
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
             if (cfg.gram_mode == 1) {
                 mark(PH_OZPREP);
-                launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowbits, oz_rscale,
+                launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowmax, oz_rscale,
                                 oz_escale);
                 // the residue pass over X also forms the X u partials
                 launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R, u,
@@ -438,7 +438,7 @@ struct bb_engine {
                 // X'Omega X = Y Y', Y = X' diag(sqrt(omega)): the Ozaki-II Gram of the
                 // resident transpose (rows = coefficients, K = observations)
                 mark(PH_OZPREP);
-                launch_oz_scale(stream, omega, n_pad, oz_xmax, n_oz, oz_b, oz_rowbits, oz_rscale,
+                launch_oz_scale(stream, omega, n_pad, oz_xmax, n_oz, oz_b, oz_rowmax, oz_rscale,
                                 oz_escale);
                 launch_oz_residues(stream, Xt, p_pad, p_pad, n_oz, n_pad, omega, oz_rscale, oz_R,
                                    nullptr, nullptr);
@@ -789,7 +789,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->oz_b = oz_bits_for(p_pad);
             e->oz_S = oz_splits_for(e->n_oz, nkc);
             e->oz_xmax = dalloc<double>((size_t)nkc * e->n_oz, o);
-            e->oz_rowbits = dalloc<unsigned long long>(e->n_oz, o);
+            e->oz_rowmax = dalloc<double>((size_t)oz_bound_groups(p_pad) * e->n_oz, o);
             e->oz_rscale = dalloc<double>(e->n_oz, o);
             e->oz_escale = dalloc<int>(e->n_oz, o);
             e->oz_R = dalloc<int8_t>(oz_residue_bytes(e->n_oz, p_pad), o);
@@ -824,7 +824,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->oz_b = oz_bits_for(n_pad);
             e->oz_S = oz_splits_for(e->n_oz, nkc);
             e->oz_xmax = dalloc<double>((size_t)nkc * e->n_oz, o);
-            e->oz_rowbits = dalloc<unsigned long long>(e->n_oz, o);
+            e->oz_rowmax = dalloc<double>((size_t)oz_bound_groups(n_pad) * e->n_oz, o);
             e->oz_rscale = dalloc<double>(e->n_oz, o);
             e->oz_escale = dalloc<int>(e->n_oz, o);
             e->oz_R = dalloc<int8_t>(oz_residue_bytes(e->n_oz, n_pad), o);
@@ -1852,7 +1852,7 @@ int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
         const int b = oz_bits_for(k_pad);
         const int S = oz_splits_for(n_oz, nkc);
         double *xmax = dalloc<double>((size_t)nkc * n_oz, owned);
-        unsigned long long *rowbits = dalloc<unsigned long long>(n_oz, owned);
+        double *rowmax = dalloc<double>((size_t)oz_bound_groups(k_pad) * n_oz, owned);
         double *rscale = dalloc<double>(n_oz, owned);
         int *escale = dalloc<int>(n_oz, owned);
         int8_t *R = dalloc<int8_t>(oz_residue_bytes(n_oz, k_pad), owned);
@@ -1860,7 +1860,7 @@ int bb_gram_ozaki(double *C, const double *Yh, const double *wh, int n, int k) {
         const size_t stride = (size_t)n_pad * n_pad;
         double *red = dalloc<double>(stride + n_pad, owned);
         launch_oz_xmax(0, dY, n_pad, n_pad, n_oz, k_pad, xmax);
-        launch_oz_scale(0, dw, k_pad, xmax, n_oz, b, rowbits, rscale, escale);
+        launch_oz_scale(0, dw, k_pad, xmax, n_oz, b, rowmax, rscale, escale);
         launch_oz_residues(0, dY, n_pad, n_pad, n_oz, k_pad, dw, rscale, R);
         launch_oz_gemm(0, R, n_oz, k_pad, S, P);
         launch_oz_crt(0, P, S, n_oz, n_pad, escale, nullptr, 0, red);

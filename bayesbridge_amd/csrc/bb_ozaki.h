@@ -44,10 +44,11 @@ size_t oz_partial_bytes(int n_oz, int nsplit);
 void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                     double *xmax);
 // Per sweep: row exponents from the bound max_c xmax[c][i] * max_{j in c} sqrt(D_j):
-// rscale[i] = 2^(b - e_i), escale[i] = e_i - b.  rowbits: n_oz words of scratch, zero on
-// entry and left zero.
+// rscale[i] = 2^(b - e_i), escale[i] = e_i - b.  part: scratch of
+// oz_bound_groups(p_pad) * n_oz doubles (per chunk-group row maxima).
+int oz_bound_groups(int p_pad);
 void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
-                     int b, unsigned long long *rowbits, double *rscale, int *escale);
+                     int b, double *part, double *rscale, int *escale);
 // Residues r = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8), plane k, 64-column chunk c,
 // stored as [16-row block][16-byte unit 0..3][row in block][16 B].  When u is
 // given, the same pass writes the X.u partials xu_part[g * n_pad + i] (g = 256-column group,
