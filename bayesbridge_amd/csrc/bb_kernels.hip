@@ -20,7 +20,6 @@
 #include <unordered_map>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstring>
 
 #include "bb_kernels.h"
@@ -153,6 +152,44 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
     }
 }
 
+// Small batches (p_loc <= kLamSpecMax): one wave per coefficient with outer-attempt
+// speculation (stable_spec_draw<64, 8>: 8 outer attempts of 8 inner attempts per round, the
+// sequential loop's draw) instead of k_lambda's 64 lanes on 64 inner attempts of one outer
+// attempt.  Such a launch is as long as its slowest draw, and 8 outer attempts per round cut
+// the slowest draw's rounds: C4 (p = 1000) lambda 49 -> 39 us.  At p = 5000 and 6250 it
+// measured equal to k_lambda with G = 8 (75 vs 73 us, 78 vs 77 us), so larger p keep that.
+constexpr int kLamSpecMax = 1024;
+
+__global__ __launch_bounds__(256) void k_lambda_spec(const double *beta, int p_loc, int p_pad,
+                                                     uint64_t j0, const DevScalars *sc, Key key,
+                                                     uint64_t t, int mode, double *lam, double *D,
+                                                     double *u, double *lam_trace,
+                                                     uint32_t *err) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+    const bool active = i < p_loc;
+    const double tau = sc->tau;
+    const double b = active ? beta[i] : 0.0;
+    const double x = stable_spec_draw<64, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
+                                             key, t, j0 + (uint64_t)i, err);
+    if ((threadIdx.x & 63) != 0 || i >= p_pad) return;
+    if (active) {
+        const double l = 2 * x;
+        lam[i] = l;
+        if (lam_trace) lam_trace[i] = l;
+        if (mode == LAMBDA_WOODBURY) {
+            const double d = (tau * tau) / l;
+            D[i] = d;
+            u[i] = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
+        }
+    } else {
+        lam[i] = 1.0;
+        if (mode == LAMBDA_WOODBURY) {
+            D[i] = 0.0;
+            u[i] = 0.0;
+        }
+    }
+}
+
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
 // as long as its slowest wave, and a wave is as long as the slowest of its G-lane groups'
 // draws; here each workgroup owns a contiguous range of coefficients and a group that has
@@ -279,6 +316,11 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     long threads = (long)p_pad * group;
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
+    if (p_loc <= kLamSpecMax) {
+        k_lambda_spec<<<(p_pad + 3) / 4, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode,
+                                                      lam, D, u, lam_trace, err);
+        return;
+    }
     if (ni && group == 8) {
         // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy)
         const int nwg = std::max(1, std::min(4 * device_cus_lam(), (p_pad + 31) / 32));
