@@ -152,26 +152,32 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
     }
 }
 
-// Small batches (p_loc <= kLamSpecMax): one wave per coefficient with outer-attempt
-// speculation (stable_spec_draw<64, 8>: 8 outer attempts of 8 inner attempts per round, the
-// sequential loop's draw) instead of k_lambda's 64 lanes on 64 inner attempts of one outer
-// attempt.  Such a launch is as long as its slowest draw, and 8 outer attempts per round cut
-// the slowest draw's rounds: C4 (p = 1000) lambda 49 -> 39 us.  At p = 5000 and 6250 it
-// measured equal to k_lambda with G = 8 (75 vs 73 us, 78 vs 77 us), so larger p keep that.
-constexpr int kLamSpecMax = 1024;
+// p_loc <= kLamSpecMax: L lanes per coefficient with outer-attempt speculation
+// (stable_spec_draw<L, 8>: L/8 outer attempts of 8 inner attempts per round, the sequential
+// loop's draw) instead of inner-only speculation (k_lambda: G lanes on G inner attempts of
+// one outer attempt).  A launch is as long as its slowest draw, and the outer segments cut
+// the slowest draw's rounds.  Measured lambda phase (bench, alpha = 0.5):
+//   p = 1000 (C4):   L = 64  40 us, L = 32 43, L = 16 47, k_lambda G = 64 49 us;
+//   p = 5000 (C2):   L = 16  58 us, L = 32 60, L = 64 75, k_lambda G = 8 74 us;
+//   p = 6250 / 12500 / 25000 / 50000:  L = 16  58 / 76 / 111 / 202 us against
+//                    k_lambda(_cb) 76 / 101 / 141 / 216 us;
+//   p = 200000 (C5, alpha = 0.3):      L = 16 0.61 ms against k_lambda_cb 0.42 ms.
+constexpr int kLamSpecWide = 1024;  // L = 64 up to here, L = 16 above
+constexpr int kLamSpecMax = 50000;
 
+template <int L>
 __global__ __launch_bounds__(256) void k_lambda_spec(const double *beta, int p_loc, int p_pad,
                                                      uint64_t j0, const DevScalars *sc, Key key,
                                                      uint64_t t, int mode, double *lam, double *D,
                                                      double *u, double *lam_trace,
                                                      uint32_t *err) {
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform
+    const int i = blockIdx.x * (256 / L) + (threadIdx.x / L);  // group-uniform
     const bool active = i < p_loc;
     const double tau = sc->tau;
     const double b = active ? beta[i] : 0.0;
-    const double x = stable_spec_draw<64, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
-                                             key, t, j0 + (uint64_t)i, err);
-    if ((threadIdx.x & 63) != 0 || i >= p_pad) return;
+    const double x = stable_spec_draw<L, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
+                                            key, t, j0 + (uint64_t)i, err);
+    if ((threadIdx.x % L) != 0 || i >= p_pad) return;
     if (active) {
         const double l = 2 * x;
         lam[i] = l;
@@ -317,8 +323,12 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
     if (p_loc <= kLamSpecMax) {
-        k_lambda_spec<<<(p_pad + 3) / 4, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode,
-                                                      lam, D, u, lam_trace, err);
+        if (p_loc <= kLamSpecWide)
+            k_lambda_spec<64><<<(p_pad + 3) / 4, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
+                                                              mode, lam, D, u, lam_trace, err);
+        else
+            k_lambda_spec<16><<<(p_pad + 15) / 16, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
+                                                                mode, lam, D, u, lam_trace, err);
         return;
     }
     if (ni && group == 8) {
