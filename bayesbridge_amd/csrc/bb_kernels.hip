@@ -678,23 +678,35 @@ void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stri
                                                              xu_part, nxu, red2, packed);
 }
 
+// One thread per upper-triangle entry (packed index e -> (r, c): consecutive threads walk a
+// column, so the red2 reads and the M writes are both contiguous), then one per entry of the
+// right-hand-side block columns.  (The first version ran a thread per entry of the full
+// n_pad x (n_pad + 64) matrix, half of them idle: C3 13.3 -> 11.6 us, C5 57 -> 45 us.)
 __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n_pad,
                                                 const double *y, const DevScalars *sc, Key key,
                                                 uint64_t t, double *M, int ldm, int rhs_col) {
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const size_t tot = (size_t)n_pad * (n_pad + kNB);
-    if (idx >= tot) return;
-    const int r = (int)(idx % n_pad), c = (int)(idx / n_pad);
+    const size_t ntri = tri_count(n_pad);
     const double sig2 = sc->sig2;
+    if (idx < ntri) {
+        // c = floor((sqrt(8 e + 1) - 1) / 2), corrected by one either way
+        int c = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
+        while ((size_t)c * (c + 1) / 2 > idx) --c;
+        while ((size_t)(c + 1) * (c + 2) / 2 <= idx) ++c;
+        const int r = (int)(idx - (size_t)c * (c + 1) / 2);
+        M[(size_t)r + (size_t)c * ldm] = red2[idx] / sig2 + (r == c ? 1.0 : 0.0);
+        return;
+    }
+    const size_t e = idx - ntri;
+    if (e >= (size_t)n_pad * kNB) return;
+    const int r = (int)(e % n_pad), c = n_pad + (int)(e / n_pad);
     double *dst = M + (size_t)r + (size_t)c * ldm;
-    if (c < n_pad) {
-        if (r <= c) *dst = red2[tri_index(r, c)] / sig2 + (r == c ? 1.0 : 0.0);
-    } else if (c == rhs_col) {
+    if (c == rhs_col) {
         double v = 0.0;
         if (r < n) {
             const double sig = sqrt(sig2);
             const double delta = normal_at(key, t, KIND_DELTA, (uint64_t)r);
-            const double xu = red2[tri_count(n_pad) + r];
+            const double xu = red2[ntri + r];
             v = y[r] / sig - (xu / sig + delta);
         }
         *dst = v;
@@ -706,7 +718,7 @@ __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n
 void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,
                    const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *M,
                    int ldm, int rhs_col) {
-    const size_t tot = (size_t)n_pad * (n_pad + kNB);
+    const size_t tot = tri_count(n_pad) + (size_t)n_pad * kNB;
     k_form_m<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(red2, n, n_pad, y, sc, Key{k0, k1}, t,
                                                            M, ldm, rhs_col);
 }
