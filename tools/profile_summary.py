@@ -9,6 +9,9 @@ wide coalesced streaming read (MI355X_MICROARCH.md HBM section), so read bytes a
 which streams X exactly once with known bytes, is reported beside it as an in-run
 calibration of that factor.
 Usage: python tools/profile_summary.py r01 [n] [p]
+The workload (n, p, design) is read from the profiled bench line (kt_bench.json) when it is
+there, so `ROUND=r02c5 bash tools/profile_round.sh --workload c5` followed by
+`python tools/profile_summary.py r02c5` summarises C5 (bench.py picks the file by n, p).
 """
 import csv
 import glob
@@ -47,6 +50,16 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 2000
     p = int(sys.argv[3]) if len(sys.argv) > 3 else 50000
     src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    bench, cfg = {}, {}
+    try:  # the bench line the kernel-trace pass printed
+        line = [l for l in open(os.path.join(src, "kt_bench.json")) if l.startswith("{")][-1]
+        bench = json.loads(line)
+        cfg = bench.get("config", {})
+        n, p = int(cfg.get("n", n)), int(cfg.get("p", p))
+    except (OSError, IndexError, ValueError):
+        pass
+    wl = cfg.get("workload", "")
+    logit, sparse = "logistic" in wl, "sparse" in wl
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     ks = one(os.path.join(src, "kt", "**", "*kernel_stats.csv"))
@@ -54,7 +67,7 @@ def main():
     rows = list(csv.DictReader(open(ks)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"# rocprofv3 --kernel-trace --stats of: python3 bench.py --steps 10 --warmup 2 "
-             f"--no-cpu-baseline (n={n}, p={p}, 1 GPU)",
+             f"--no-cpu-baseline ({wl or f'n={n}, p={p}'}, 1 GPU)",
              f"{'kernel':48s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'tot_ms':>9s}  share"]
     avg_us = {}
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
@@ -91,12 +104,17 @@ def main():
             break
     # the Gram GEMM kernels: fp64 k_gram reads X (+D) and writes n_pad^2 partials per split;
     # k_oz_gemm reads the 16 int8 residue planes (16 n_oz p_pad bytes) and writes partials
-    n_oz = -(-n_pad // 256) * 256
+    # (the logistic Gram X' diag(omega) X has rows = coefficients and K = observations)
+    rows_pad, k_pad = (p_pad, n_pad) if logit else (n_pad, p_pad)
+    n_oz = -(-rows_pad // 256) * 256
     algo = {"bb::k_gram": x_bytes + 8.0 * p_pad + 8.0 * n_pad ** 2,
-            "bb::k_oz_residues": x_bytes + 16.0 * n_oz * p_pad}
+            "bb::k_oz_residues": x_bytes + 16.0 * n_oz * k_pad}
     for k in out["kernels"]:  # production GEMM instantiation(s): dbg = 0
         if k.startswith("bb::k_oz_gemm") and "<0" in k:
-            algo[k] = 16.0 * n_oz * p_pad
+            algo[k] = 16.0 * n_oz * k_pad
+    if sparse:  # the pair-list Gram's algorithmic bytes as bench.py counts them
+        algo = {"bb::k_sp_gram_col": bench["roofline"]["algorithmic_bytes_per_launch"]}
+    out["workload"]["name"] = wl or None
     out["gram_kernels"] = {}
     for k, a in algo.items():
         if k in out["kernels"]:
