@@ -148,7 +148,7 @@ def test_gram_ozaki_fp64_accuracy(gpu_lib, n, k):
     assert e_oz < 4 * max(e_64, 1e-16), (e_oz, e_64)
 
 
-@pytest.mark.parametrize("m,nrhs", [(20, 1), (64, 2), (130, 1), (700, 2)])
+@pytest.mark.parametrize("m,nrhs", [(20, 1), (64, 2), (130, 1), (700, 2), (3500, 2)])
 def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
     bb = gpu_lib
     rng = np.random.default_rng(m)
