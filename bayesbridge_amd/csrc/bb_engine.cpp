@@ -365,7 +365,7 @@ struct bb_engine {
             nparts = 1;
         } else {
             launch_xv(stream, X, n_pad, beta, p_loc, n_pad, xb_part);
-            nparts = xv_chunks(p_loc);
+            nparts = xv_chunks(p_loc, n_pad);
         }
     }
 
@@ -426,7 +426,7 @@ struct bb_engine {
                 launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
                               oz_xu_parts(p_pad), red2);
             else
-                launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad),
+                launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
                                 red2, 1);
         } else if (method == 6) {
             launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
@@ -770,9 +770,11 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     e->u = dalloc<double>(p_pad, o);
     e->sc = dalloc<DevScalars>(1, o);
     e->err = dalloc<uint32_t>(4, o);
-    e->nparts = xv_chunks(p_pad);
+    e->nparts = xv_chunks(p_pad, n_pad);
     e->xb_part = dalloc<double>(
-        (size_t)std::max(xv_chunks(p_pad), beta_xb_parts(c.p_local)) * n_pad, o);
+        (size_t)std::max(e->method == 5 ? 1 : xv_chunks_max(p_pad), beta_xb_parts(c.p_local)) *
+            n_pad,
+        o);
     e->nbS = pre_blocks_s(c.p_local);
     e->red1 = dalloc<double>((size_t)e->nbS + n_pad, o);
     e->group = stable_group_for(c.p_local);
@@ -800,7 +802,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->slab_stride = (size_t)n_pad * n_pad;
             e->slabs = dalloc<double>(e->slab_stride * e->S, o);
         }
-        e->xu_part = dalloc<double>((size_t)xv_chunks(p_pad) * n_pad, o);
+        e->xu_part = dalloc<double>((size_t)xv_chunks_max(p_pad) * n_pad, o);
     }
     if (e->woodbury()) {
         e->red2 = dalloc<double>(tri_count(n_pad) + n_pad, o);

@@ -25,7 +25,8 @@ struct Hyper {
 constexpr int kGramTile = 128;  // Gram output tile (rows of X per tile)
 constexpr int kGramBK = 16;     // Gram K step
 constexpr int kNB = 64;         // Cholesky block
-constexpr int kXvCols = 256;    // columns per block of the X.v partial-sum kernel
+constexpr int kXvCols = 256;    // columns per block of the X.v partial-sum kernel (at most)
+constexpr int kXvMinCols = 32;  // ... and at least (small grids split the columns finer)
 constexpr int kXvRows = 512;    // rows per block of the X.v partial-sum kernel
 constexpr int kTriMaxP = 2048;  // triangle-mixture sampler: coefficients in one workgroup
 
@@ -60,7 +61,8 @@ void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n
                  int S, double *slabs, int ldo, size_t slab_stride);
 
 // part[cb * n_pad + r] = sum over columns j of chunk cb of X[r, j] * v[j].
-int xv_chunks(int ncols);
+int xv_chunks(int ncols, int n_pad);  // X.v partials launch_xv writes (= k_pre's nparts)
+int xv_chunks_max(int ncols);         // upper bound over n_pad, for allocation
 void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
                double *part);
 

@@ -506,11 +506,11 @@ void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_xv(const double *__restrict__ X, int ldx,
                                             const double *__restrict__ v, int ncols, int n_pad,
-                                            double *__restrict__ part) {
+                                            int cols, double *__restrict__ part) {
     __shared__ double vs[kXvCols];
     const int cb = blockIdx.x, rb = blockIdx.y;
-    const int c0 = cb * kXvCols;
-    const int nc = min(kXvCols, ncols - c0);
+    const int c0 = cb * cols;
+    const int nc = min(cols, ncols - c0);
     for (int i = threadIdx.x; i < kXvCols; i += 256) vs[i] = (i < nc) ? v[c0 + i] : 0.0;
     __syncthreads();
     const int r = rb * kXvRows + 2 * threadIdx.x;
@@ -540,12 +540,27 @@ __global__ __launch_bounds__(256) void k_xv(const double *__restrict__ X, int ld
     *(double2 *)(part + (size_t)cb * n_pad + r) = make_double2(ax, ay);
 }
 
-int xv_chunks(int ncols) { return (ncols + kXvCols - 1) / kXvCols; }
+// Columns per partial: kXvCols, halved (down to 32) until the launch has >= 1024 workgroups
+// -- at C4 (n = 10 000, p = 1000) 256 columns gave 80 workgroups and 2.2 TB/s
+static int xv_cols(int ncols, int n_pad) {
+    const long rb = (n_pad + kXvRows - 1) / kXvRows;
+    int c = kXvCols;
+    while (c > kXvMinCols && (long)((ncols + c - 1) / c) * rb < 1024) c >>= 1;
+    return c;
+}
+
+int xv_chunks(int ncols, int n_pad) {
+    const int c = xv_cols(ncols, n_pad);
+    return (ncols + c - 1) / c;
+}
+
+int xv_chunks_max(int ncols) { return (ncols + kXvMinCols - 1) / kXvMinCols; }
 
 void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
                double *part) {
-    dim3 grid(xv_chunks(ncols), (n_pad + kXvRows - 1) / kXvRows);
-    k_xv<<<grid, 256, 0, s>>>(X, ldx, v, ncols, n_pad, part);
+    const int cols = xv_cols(ncols, n_pad);
+    dim3 grid((ncols + cols - 1) / cols, (n_pad + kXvRows - 1) / kXvRows);
+    k_xv<<<grid, 256, 0, s>>>(X, ldx, v, ncols, n_pad, cols, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -604,9 +619,22 @@ __global__ __launch_bounds__(256) void k_scalars(const double *red1, int nbS, co
     __shared__ double sh[5];
     const double *xb = red1 + nbS;
     double v = 0.0;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        const double r = y[i] - xb[i];
-        v += r * r;
+    // the residual sum of squares (sig2 only: the logistic sweep skips it), eight loads of
+    // y and X.beta per thread in flight at a time -- a one-load-pair loop paid the memory
+    // latency once per iteration (21 us at n = 10 000)
+    for (int i0 = tau_only ? n : (int)threadIdx.x; i0 < n; i0 += 256 * 8) {
+        double yv[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * 256;
+            yv[u] = i < n ? y[i] : 0.0;
+            xv[u] = i < n ? xb[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const double r = yv[u] - xv[u];
+            v += r * r;
+        }
     }
     const double rss0 = block_sum<256>(v, sh);
     if (threadIdx.x == 0) sh[4] = rss0;
