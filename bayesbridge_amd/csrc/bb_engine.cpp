@@ -424,7 +424,7 @@ struct bb_engine {
             mark(PH_REDUCE);
             if (cfg.gram_mode == 1)
                 launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
-                              oz_xu_parts(p_pad), red2);
+                              oz_xu_parts(p_pad, n_oz), red2);
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
                                 red2, 1);

@@ -53,7 +53,7 @@ void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xm
 // stored as [16-row block][16-byte unit 0..3][row in block][16 B].  When u is
 // given, the same pass writes the X.u partials xu_part[g * n_pad + i] (g = 256-column group,
 // oz_xu_parts(p_pad) of them; rows < n_pad).
-int oz_xu_parts(int p_pad);
+int oz_xu_parts(int p_pad, int n_oz);  // X.u partials of launch_oz_residues (<= p_pad / 64)
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R,
                         const double *u = nullptr, double *xu_part = nullptr);

@@ -237,12 +237,12 @@ __device__ __forceinline__ double oz_readlane_d(double v, int lane) {
 }
 
 constexpr int kOzResCols = 32;   // columns per wave (half a chunk): keeps occupancy >= 4
-constexpr int kOzResChunks = 4;  // 64-column chunks per workgroup (= one kXvCols X.u partial)
+constexpr int kOzResChunks = 4;  // 64-column chunks per workgroup, at most (oz_res_cpw)
 
-// Workgroup = kOzResChunks 64-column chunks x 256 rows (8 waves: 4 row slices x 2 column
+// Workgroup = cpw (<= kOzResChunks) 64-column chunks x 256 rows (8 waves: 4 row slices x 2 column
 // halves), so the X reads are 2 KB contiguous per column and each modulus plane is written
 // as one 16 KB contiguous block per chunk.  The same pass over X also forms the X.u partial
-// sums of the Woodbury draw (u = sqrt(D) z): part[g][row] over the 256 columns of group g,
+// sums of the Woodbury draw (u = sqrt(D) z): part[g][row] over the cpw * 64 columns of group g,
 // summed per lane in column order, then the two column halves -- so the separate X.u pass
 // (k_xv) disappears from the Ozaki sweep.
 __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ X, int ldx,
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
                                                      const double *__restrict__ rscale,
                                                      int8_t *__restrict__ R, OzConsts C,
                                                      const double *__restrict__ u,
-                                                     double *__restrict__ xu_part) {
+                                                     double *__restrict__ xu_part, int cpw) {
     __shared__ double xu_half[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int half = w & 1;
@@ -260,8 +260,8 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
     // rows >= n_pad (tile padding) load a valid row and are zeroed through rs = 0
     const double rsl = row < n_pad ? rs : 0.0;
     double xu = 0.0;
-    for (int cc = 0; cc < kOzResChunks; ++cc) {
-        const int kc = blockIdx.x * kOzResChunks + cc;
+    for (int cc = 0; cc < cpw; ++cc) {
+        const int kc = blockIdx.x * cpw + cc;
         if (kc >= nkc) break;
         const int col0 = kc * kOzKC + half * kOzResCols;
         const int cl = col0 + (lane & (kOzResCols - 1));
@@ -326,15 +326,26 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
         xu_part[(size_t)blockIdx.x * n_pad + row] = xu + xu_half[w >> 1][lane];
 }
 
-int oz_xu_parts(int p_pad) { return (p_pad / kOzKC + kOzResChunks - 1) / kOzResChunks; }
+// Chunks per workgroup: kOzResChunks, halved (down to 1) until the launch has >= 1024
+// workgroups -- at C2 (K = 5120, 1024 rows) four chunks gave 80 workgroups
+static int oz_res_cpw(int nkc, int n_oz) {
+    int c = kOzResChunks;
+    while (c > 1 && (long)((nkc + c - 1) / c) * (n_oz / 256) < 1024) c >>= 1;
+    return c;
+}
+
+int oz_xu_parts(int p_pad, int n_oz) {
+    const int nkc = p_pad / kOzKC, c = oz_res_cpw(nkc, n_oz);
+    return (nkc + c - 1) / c;
+}
 
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R, const double *u,
                         double *xu_part) {
-    const int nkc = p_pad / kOzKC;
-    dim3 grid(oz_xu_parts(p_pad), n_oz / 256);
+    const int nkc = p_pad / kOzKC, cpw = oz_res_cpw(nkc, n_oz);
+    dim3 grid((nkc + cpw - 1) / cpw, n_oz / 256);
     k_oz_residues<<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts(), u,
-                                       xu_part);
+                                       xu_part, cpw);
 }
 
 // ---------------------------------------------------------------------------
