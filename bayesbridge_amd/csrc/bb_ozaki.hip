@@ -740,8 +740,18 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
         const int t = threadIdx.x & 7;
         const long r = ((long)blockIdx.x * 256 + threadIdx.x) >> 3;
         double v = 0.0;
-        if (r < n_pad)
-            for (int q = t; q < nxu; q += 8) v += xu_part[(size_t)q * n_pad + r];
+        if (r < n_pad) {
+            // eight loads in flight, summed in the same order as one at a time
+            int q = t;
+            for (; q + 56 < nxu; q += 64) {
+                double x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = xu_part[(size_t)(q + 8 * u) * n_pad + r];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v += x[u];
+            }
+            for (; q < nxu; q += 8) v += xu_part[(size_t)q * n_pad + r];
+        }
         // fixed-order combine of the 8 lane sums
         v += __shfl_xor(v, 4, 8);
         v += __shfl_xor(v, 2, 8);
