@@ -429,11 +429,15 @@ struct bb_engine {
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
                                 red2, 1);
         } else if (method == 6) {
-            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
-                          group, lam, nullptr, nullptr, trl, err);
-            mark(PH_PG);
-            // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums)
-            launch_pg(stream, red1 + nbS, n, n_pad, cfg.seed, cfg.stream, t, omega, err);
+            // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums): drawn in the
+            // lambda launch (trailing workgroups) when that is the speculative kernel
+            if (!launch_lambda_pg(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t,
+                                  group, lam, trl, red1 + nbS, n, n_pad, omega, err)) {
+                launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t,
+                              LAMBDA_ONLY, group, lam, nullptr, nullptr, trl, err);
+                mark(PH_PG);
+                launch_pg(stream, red1 + nbS, n, n_pad, cfg.seed, cfg.stream, t, omega, err);
+            }
             if (cfg.gram_mode == 1) {
                 // X'Omega X = Y Y', Y = X' diag(sqrt(omega)): the Ozaki-II Gram of the
                 // resident transpose (rows = coefficients, K = observations)

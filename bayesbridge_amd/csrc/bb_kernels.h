@@ -45,6 +45,12 @@ void launch_retstable_batch(hipStream_t s, double *x, const double *alpha, const
                             const double *h, int num, uint64_t k0, uint64_t k1, uint64_t t,
                             int group, uint32_t *err);
 
+// lambda (LAMBDA_ONLY) and omega ~ PG(1, psi) in one launch when p_loc takes the
+// speculative lambda kernel; false (nothing launched) otherwise
+bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int group,
+                      double *lam, double *lam_trace, const double *psi, int n, int n_pad,
+                      double *omega, uint32_t *err);
 void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                    const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int mode,
                    int group, double *lam, double *D, double *u, double *lam_trace,

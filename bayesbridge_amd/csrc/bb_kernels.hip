@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "bb_kernels.h"
+#include "bb_pg.h"
 #include "bb_sampler.h"
 
 namespace bb {
@@ -165,12 +166,26 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
 constexpr int kLamSpecWide = 1024;  // L = 64 up to here, L = 16 above
 constexpr int kLamSpecMax = 50000;
 
+// PgTail: the logistic sweep's omega ~ PG(1, psi) draws (independent of lambda: psi = X beta
+// is known before tau) ride in the same launch as trailing workgroups -- 10 000 draws are
+// only 157 waves, which alone leave most of the chip idle for the draw's latency.
+struct PgTail {
+    const double *psi = nullptr;
+    int n = 0, n_pad = 0;
+    double *omega = nullptr;
+};
+
 template <int L>
 __global__ __launch_bounds__(256) void k_lambda_spec(const double *beta, int p_loc, int p_pad,
                                                      uint64_t j0, const DevScalars *sc, Key key,
                                                      uint64_t t, int mode, double *lam, double *D,
                                                      double *u, double *lam_trace,
-                                                     uint32_t *err) {
+                                                     uint32_t *err, int lam_blocks, PgTail pgt) {
+    if ((int)blockIdx.x >= lam_blocks) {
+        pg_draw_at(((int)blockIdx.x - lam_blocks) * 256 + (int)threadIdx.x, pgt.psi, pgt.n,
+                   pgt.n_pad, key, t, pgt.omega, err);
+        return;
+    }
     const int i = blockIdx.x * (256 / L) + (threadIdx.x / L);  // group-uniform
     const bool active = i < p_loc;
     const double tau = sc->tau;
@@ -314,6 +329,29 @@ __global__ __launch_bounds__(kLamCbWG) void k_lambda_cb(const double *beta, int 
     if (have) atomicOr(err, 2u);  // bounded: a draw that never finished is flagged
 }
 
+bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int group,
+                      double *lam, double *lam_trace, const double *psi, int n, int n_pad,
+                      double *omega, uint32_t *err) {
+    if (p_loc > kLamSpecMax) return false;  // the caller launches k_pg itself
+    const Key key{k0, k1};
+    const PgTail pgt{psi, n, n_pad, omega};
+    const int pgb = (n_pad + 255) / 256;
+    (void)group;
+    if (p_loc <= kLamSpecWide) {
+        const int lb = (p_pad + 3) / 4;
+        k_lambda_spec<64><<<lb + pgb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
+                                                   LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
+                                                   err, lb, pgt);
+    } else {
+        const int lb = (p_pad + 15) / 16;
+        k_lambda_spec<16><<<lb + pgb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
+                                                   LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
+                                                   err, lb, pgt);
+    }
+    return true;
+}
+
 void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                    const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int mode,
                    int group, double *lam, double *D, double *u, double *lam_trace,
@@ -323,12 +361,15 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
     if (p_loc <= kLamSpecMax) {
-        if (p_loc <= kLamSpecWide)
-            k_lambda_spec<64><<<(p_pad + 3) / 4, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
-                                                              mode, lam, D, u, lam_trace, err);
-        else
-            k_lambda_spec<16><<<(p_pad + 15) / 16, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
-                                                                mode, lam, D, u, lam_trace, err);
+        if (p_loc <= kLamSpecWide) {
+            const int lb = (p_pad + 3) / 4;
+            k_lambda_spec<64><<<lb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,
+                                                 u, lam_trace, err, lb, PgTail{});
+        } else {
+            const int lb = (p_pad + 15) / 16;
+            k_lambda_spec<16><<<lb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,
+                                                 u, lam_trace, err, lb, PgTail{});
+        }
         return;
     }
     if (ni && group == 8) {
