@@ -66,6 +66,7 @@ EXPORTED_SYMBOLS = [
     "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
     "bb_pg_batch", "bb_group_create_rccl", "bb_group_sync", "bb_set_device_count",
     "bb_set_trace_budget", "bb_debug_interrupt_after", "bb_last_call_info",
+    "bb_engine_set_timed_phase",
 ]
 
 
@@ -110,6 +111,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_gram_mode.argtypes = [c.c_void_p]
     L.bb_engine_enable_timing.argtypes = [c.c_void_p, c.c_int]
     L.bb_engine_reset_timing.argtypes = [c.c_void_p]
+    L.bb_engine_set_timed_phase.argtypes = [c.c_void_p, c.c_int]
     L.bb_engine_kernel_times.argtypes = [c.c_void_p, _dp, _dp, _ip]
     L.bb_engine_error_flags.argtypes = [c.c_void_p, c.POINTER(c.c_uint32)]
     L.bb_retstable_batch.argtypes = [_dp, _dp, _dp, _dp, c.c_int, c.c_uint64, c.c_uint64,
@@ -985,10 +987,15 @@ class Engine:
         _check(library().bb_engine_set_state(self._h, _p(beta), tau, sig2, alpha),
                "bb_engine_set_state")
 
-    def enable_timing(self, on: bool = True, phases: bool = True):
+    def enable_timing(self, on: bool = True, phases: bool = True, timed_phase: str = "gram"):
         """HIP-event timing on the engine stream: every phase start (phases=True) or only
-        the Gram kernel's bracket (two events per sweep, used inside timed loops)."""
-        library().bb_engine_enable_timing(self._h, (2 if phases else 1) if on else 0)
+        the bracket of `timed_phase` (a bb_phase_name, two events per sweep, used inside
+        timed loops; kernel_times()[0] is its average)."""
+        L = library()
+        names = [L.bb_phase_name(i).decode() for i in range(L.bb_phase_count())]
+        _check(L.bb_engine_set_timed_phase(self._h, names.index(timed_phase)),
+               "bb_engine_set_timed_phase")
+        L.bb_engine_enable_timing(self._h, (2 if phases else 1) if on else 0)
 
     def reset_timing(self):
         library().bb_engine_reset_timing(self._h)
@@ -1027,9 +1034,10 @@ class Engine:
 
 
 class ShardGroup:
-    """Column shards of one chain driven by one host thread.  rccl=False: engines on ONE
-    device exchanging through on-device sums (the sharded decomposition on a single GPU);
-    rccl=True: engines on distinct devices exchanging with RCCL (ncclCommInitAll) -- the
+    """Column shards of one chain driven from one process.  rccl=False: engines on ONE
+    device, one host thread, exchanges through on-device sums (the sharded decomposition on
+    a single GPU); rccl=True: engines on distinct devices exchanging with RCCL
+    (ncclCommInitAll), each member's sweeps enqueued by its own host thread -- the
     single-process multi-GPU path of the .C entry points."""
 
     def __init__(self, engines, rccl=False):

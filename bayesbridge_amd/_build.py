@@ -42,7 +42,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return SO_PATH
     objs = []
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-             "-Wall", "-Wno-unused-result", f"-I{os.path.join(ROOT, 'include')}"]
+             "-Wall", "-Wno-unused-result", "-pthread", f"-I{os.path.join(ROOT, 'include')}"]
     procs = []
     for src in SOURCES:  # translation units compile in parallel
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
@@ -56,7 +56,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise subprocess.CalledProcessError(1, failed[0])
     tmp = SO_PATH + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
-           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-ldl"]
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-ldl", "-pthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -16,6 +16,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bayesbridge.h"
@@ -122,6 +123,23 @@ void next_call_key(uint64_t *k0, uint64_t *k1) {
 // Sparse design (CSC input): CSC + CSR copies on the device and the Gram pair list
 // (bb_sparse.h).  Built once at setup; X is constant over a chain.
 // ---------------------------------------------------------------------------
+// The canonical dgCMatrix form every CSC entry point requires (colptr[0] = 0,
+// non-decreasing, rows in [0, n), strictly increasing within a column); throws otherwise.
+// Both .C CSC paths (sparse engine and densified dense path) run it, so a malformed matrix
+// is refused the same way whichever path its shape selects.
+static void csc_validate(int n, int p, const int *cp, const int *ri) {
+    if (cp[0] != 0) throw HipError("CSC: colptr[0] must be 0");
+    for (int j = 0; j < p; ++j) {
+        if (cp[j + 1] < cp[j]) throw HipError("CSC: colptr must be non-decreasing");
+        for (int q = cp[j]; q < cp[j + 1]; ++q) {
+            if (ri[q] < 0 || ri[q] >= n) throw HipError("CSC: row index out of range");
+            if (q > cp[j] && ri[q] <= ri[q - 1])
+                throw HipError("CSC: row indices must be strictly increasing within a "
+                               "column (canonical dgCMatrix form)");
+        }
+    }
+}
+
 struct SparseDesign {
     int n = 0, n_pad = 0, p = 0;
     long nnz = 0;
@@ -142,16 +160,7 @@ struct SparseDesign {
         n = n_;
         n_pad = n_pad_;
         p = p_;
-        if (cp[0] != 0) throw HipError("CSC: colptr[0] must be 0");
-        for (int j = 0; j < p; ++j) {
-            if (cp[j + 1] < cp[j]) throw HipError("CSC: colptr must be non-decreasing");
-            for (int q = cp[j]; q < cp[j + 1]; ++q) {
-                if (ri[q] < 0 || ri[q] >= n) throw HipError("CSC: row index out of range");
-                if (q > cp[j] && ri[q] <= ri[q - 1])
-                    throw HipError("CSC: row indices must be strictly increasing within a "
-                                   "column (canonical dgCMatrix form)");
-            }
-        }
+        csc_validate(n, p, cp, ri);
         nnz = cp[p];
         std::vector<int> rp(n_pad + 1, 0), ci(nnz > 0 ? nnz : 1), pos(nnz > 0 ? nnz : 1);
         std::vector<double> rv(nnz > 0 ? nnz : 1);
@@ -303,23 +312,25 @@ struct bb_engine {
     double *tr_beta = nullptr, *tr_lam = nullptr, *tr_sig2 = nullptr, *tr_tau = nullptr,
            *tr_alpha = nullptr;
     int cap = 1;
-    // communicator
+    // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
     ncclComm_t comm = nullptr;
+    bool own_comm = true;
     // timing: per-sweep event marks at phase starts, on the engine stream
     bool timing = false;
-    int timing_level = 2;  // 1: Gram bracket only, 2: every phase
+    int timing_level = 2;  // 1: one phase's bracket only (timed_phase), 2: every phase
+    int timed_phase = PH_GRAM;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::vector<std::pair<int, int>>> sweep_marks;  // (phase, event)
     size_t ev_next = 0;
 
     void mark(int phase) {
         if (!timing) return;
-        // level 1: only the Gram kernel's bracket (start of PH_GRAM and the next mark), so
-        // a timed run carries two events per sweep instead of one per phase
+        // level 1: only the timed phase's bracket (its start and the next mark), so a timed
+        // run carries two events per sweep instead of one per phase
         if (timing_level == 1) {
             const bool open = !sweep_marks.back().empty() &&
-                              sweep_marks.back().back().first == PH_GRAM;
-            if (phase != PH_GRAM && !open) return;
+                              sweep_marks.back().back().first == timed_phase;
+            if (phase != timed_phase && !open) return;
         }
         int e0 = ev();
         HIPCHECK(hipEventRecord(ev_pool[e0], stream));
@@ -328,7 +339,7 @@ struct bb_engine {
 
     ~bb_engine() {
         if (stream) (void)hipStreamSynchronize(stream);
-        if (comm) ncclCommDestroy(comm);
+        if (comm && own_comm) ncclCommDestroy(comm);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         for (void *q : owned) (void)hipFree(q);
         if (stream) (void)hipStreamDestroy(stream);
@@ -429,15 +440,12 @@ struct bb_engine {
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
                                 red2, 1);
         } else if (method == 6) {
-            // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums): drawn in the
-            // lambda launch (trailing workgroups) when that is the speculative kernel
+            // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums): drawn by
+            // trailing workgroups of the speculative lambda launch.  The logistic engine caps
+            // p at 16384 (engine create), inside that launch's range (kLamSpecMax).
             if (!launch_lambda_pg(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t,
-                                  group, lam, trl, red1 + nbS, n, n_pad, omega, err)) {
-                launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t,
-                              LAMBDA_ONLY, group, lam, nullptr, nullptr, trl, err);
-                mark(PH_PG);
-                launch_pg(stream, red1 + nbS, n, n_pad, cfg.seed, cfg.stream, t, omega, err);
-            }
+                                  group, lam, trl, red1 + nbS, n, n_pad, omega, err))
+                throw HipError("logistic sweep: p beyond the fused lambda / Polya-Gamma launch");
             if (cfg.gram_mode == 1) {
                 // X'Omega X = Y Y', Y = X' diag(sqrt(omega)): the Ozaki-II Gram of the
                 // resident transpose (rows = coefficients, K = observations)
@@ -1268,6 +1276,15 @@ int bb_engine_enable_timing(bb_engine *e, int enable) {
     return 0;
 }
 
+int bb_engine_set_timed_phase(bb_engine *e, int phase) {
+    if (phase < 0 || phase >= PH_END) {
+        set_error("bb_engine_set_timed_phase: phase %d out of range", phase);
+        return -1;
+    }
+    e->timed_phase = phase;
+    return 0;
+}
+
 int bb_engine_reset_timing(bb_engine *e) {
     (void)hipStreamSynchronize(e->stream);
     e->sweep_marks.clear();
@@ -1307,7 +1324,7 @@ int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_a
         int ng = 0;
         for (auto &marks : e->sweep_marks) {
             for (size_t i = 0; i + 1 < marks.size(); ++i)
-                if (marks[i].first == PH_GRAM) {
+                if (marks[i].first == e->timed_phase) {
                     float v = 0;
                     HIPCHECK(hipEventElapsedTime(&v, e->ev_pool[marks[i].second],
                                                  e->ev_pool[marks[i + 1].second]));
@@ -1365,6 +1382,7 @@ struct bb_group {
         for (auto *m : members) {
             (void)hipSetDevice(m->cfg.device);
             (void)hipStreamSynchronize(m->stream);
+            if (rccl) m->comm = nullptr;  // lent by this group
         }
         for (auto c : comms) ncclCommDestroy(c);
         if (!members.empty()) (void)hipSetDevice(members[0]->cfg.device);
@@ -1431,6 +1449,12 @@ bb_group *group_create(bb_engine **engines, int count, bool rccl) {
             for (int i = 0; i < count; ++i) devs[i] = engines[i]->cfg.device;
             g->comms.assign(count, nullptr);
             NCCLCHECK(ncclCommInitAll(g->comms.data(), count, devs.data()));
+            // each member runs whole sweeps on its own host thread (bb_group_run) and
+            // exchanges through its own communicator, as one rank of a multi-process job
+            for (int i = 0; i < count; ++i) {
+                engines[i]->comm = g->comms[i];
+                engines[i]->own_comm = false;
+            }
         } else {
             HIPCHECK(hipSetDevice(engines[0]->cfg.device));
             HIPCHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
@@ -1468,6 +1492,34 @@ void bb_group_destroy(bb_group *g) { delete g; }
 
 int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
                  int mcmc_phase) {
+    if (g->rccl) {
+        // one enqueue thread per device: member i runs its `count` sweeps exactly as rank i
+        // of a one-process-per-GPU job would (phase a, all-reduce, phase b, all-reduce,
+        // phase c on its own stream and communicator), so the host cost per sweep does not
+        // grow with the device count
+        const size_t k = g->members.size();
+        std::vector<std::string> errs(k);
+        std::vector<std::thread> th;
+        th.reserve(k);
+        for (size_t i = 0; i < k; ++i)
+            th.emplace_back([&, i] {
+                bb_engine *m = g->members[i];
+                try {
+                    HIPCHECK(hipSetDevice(m->cfg.device));
+                    m->run(t0, count, first_slot, slot_step, mcmc_phase);
+                    HIPCHECK(hipGetLastError());
+                } catch (std::exception &ex) {
+                    errs[i] = ex.what();
+                }
+            });
+        for (auto &t : th) t.join();
+        for (size_t i = 0; i < k; ++i)
+            if (!errs[i].empty()) {
+                set_error("group member %zu: %s", i, errs[i].c_str());
+                return -1;
+            }
+        return 0;
+    }
     try {
         for (int k = 0; k < count; ++k) {
             const uint64_t t = t0 + (uint64_t)k;
@@ -2321,7 +2373,11 @@ namespace {
 // ---------------------------------------------------------------------------
 // .C drivers: device selection, trace ring with chunked copy-out, interrupt polling.
 // ---------------------------------------------------------------------------
-int g_max_devices = 0;                      // bb_set_device_count (0: every visible device)
+// bb_set_device_count: devices a .C chain may shard over (0: every visible device).  The
+// default is 1: a sharded chain sums its Gram in a different fp64 order than one device, and
+// p > n chains amplify such roundoff, so traces depend on the device count and
+// multi-device sharding is opt-in.
+int g_max_devices = 1;
 size_t g_trace_budget = size_t(1) << 30;   // device bytes of trace ring per engine
 std::atomic<int> g_debug_interrupt{-1};     // bb_debug_interrupt_after (test hook)
 int g_last_devices = 0, g_last_interrupted = 0, g_last_capacity = 0;
@@ -2577,6 +2633,7 @@ Outcome drive_chain(Chain &ch, int nburn, uint64_t t_base, int m, int b, double 
         if (f & ~4u) {
             printf("Error: numerical failure in the device sampler (flags %u)\n", f);
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
         }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -2610,6 +2667,7 @@ Outcome stable_call(const bb_config &c, Create create, int b, double *betap, dou
         if (chain_build(ch, c, 2, create) != 0) {
             printf("Error: %s\n", g_last_error.c_str());
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
             *runtime = 0.0;
             return OUT_ERROR;
         }
@@ -2620,6 +2678,7 @@ Outcome stable_call(const bb_config &c, Create create, int b, double *betap, dou
         if (o == OUT_ERROR) {
             printf("Error: %s\n", g_last_error.c_str());
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
         }
     }
     if (g_verbose && o == OUT_OK) printf("Sampling complete: %g sec. for %i iterations.\n", *runtime, m);
@@ -2692,11 +2751,20 @@ Outcome stable_csc(const bb_config &c, const double *yp, const int *Xcolptr, con
             b, betap, lambdap, sig2p, taup, alphap, runtime, title);
     }
     // p <= n or the orthogonal design: the dense paths of bridge_reg_stable (least-squares
-    // start, p x p Cholesky or ortho draw) on the densified X
+    // start, p x p Cholesky or ortho draw) on the densified X, after the same validation as
+    // the sparse engine's
+    try {
+        csc_validate(n, p, Xcolptr, Xrowidx);
+    } catch (std::exception &ex) {
+        printf("Error: %s\n", ex.what());
+        printf("Aborting Gibbs sampler.\n");
+        fflush(stdout);
+        *runtime = 0.0;
+        return OUT_ERROR;
+    }
     std::vector<double> Xd((size_t)n * p, 0.0);
     for (int j = 0; j < p; ++j)
-        for (int q = Xcolptr[j]; q < Xcolptr[j + 1]; ++q)
-            if (Xrowidx[q] >= 0 && Xrowidx[q] < n) Xd[(size_t)j * n + Xrowidx[q]] = Xval[q];
+        for (int q = Xcolptr[j]; q < Xcolptr[j + 1]; ++q) Xd[(size_t)j * n + Xrowidx[q]] = Xval[q];
     return stable_dense(c, yp, Xd.data(), b, betap, lambdap, sig2p, taup, alphap, runtime, title);
 }
 
@@ -2707,6 +2775,7 @@ Outcome logit_call(bb_config c, const double *yp, const double *Xp, int b, doubl
         if (!(yp[i] == 0.0 || yp[i] == 1.0)) {
             printf("Error: logistic bridge needs y in {0, 1} (y[%d] = %g)\n", i, yp[i]);
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
             *runtime = 0.0;
             return OUT_ERROR;
         }
@@ -2731,6 +2800,7 @@ Outcome tri_call(const bb_config &c, const double *yp, const double *Xp, int b, 
             }) != 0) {
             printf("Error: %s\n", g_last_error.c_str());
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
             *runtime = 0.0;
             return OUT_ERROR;
         }
@@ -2741,6 +2811,7 @@ Outcome tri_call(const bb_config &c, const double *yp, const double *Xp, int b, 
         if (o == OUT_ERROR) {
             printf("Error: %s\n", g_last_error.c_str());
             printf("Aborting Gibbs sampler.\n");
+            fflush(stdout);
         }
     }
     if (g_verbose && o == OUT_OK) printf("Sampling complete: %g sec. for %i iterations.\n", *runtime, m);

@@ -283,6 +283,16 @@ __global__ __launch_bounds__(NT) void k_small_chain(
     }
 }
 
+// Dynamic LDS above the 64 KB default needs a per-kernel opt-in: done once for every
+// instance (thread-safe static init), with the launch error checked by the caller.
+template <int NT, int L, int I>
+static void small_chain_lds_optin() {
+    static const hipError_t rc = hipFuncSetAttribute(
+        (const void *)k_small_chain<NT, L, I>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        kSmallXLds);
+    (void)rc;
+}
+
 void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
                         const double *G, int ldg, const double *cvec, const double *gdiag,
                         int ortho, double *beta, double *lam, DevScalars *sc, Hyper hy,
@@ -293,13 +303,10 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
     const size_t xbytes = (size_t)n * p * sizeof(double);
     const int x_lds = xbytes <= kSmallXLds;
     const size_t shm = x_lds ? xbytes : 0;
+    small_chain_lds_optin<512, 64, 16>();
+    small_chain_lds_optin<512, 32, 8>();
+    small_chain_lds_optin<512, 16, 8>();
     auto go = [&](auto kern, int nt) {
-        static bool attr = false;  // one-time opt-in above the 64 KB default
-        if (!attr) {
-            (void)hipFuncSetAttribute((const void *)kern,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kSmallXLds);
-            attr = true;
-        }
         kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, x_lds, beta, lam, sc,
                                 hy, Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta,
                                 tr_lam, tr_sig2, tr_tau, tr_alpha, err);

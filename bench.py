@@ -187,53 +187,32 @@ def blas_threads(threads):
     return threadpool_limits(limits=threads)
 
 
-def cpu_baseline(n, p, alpha, sweeps, log_every=True, threads=None, literal=False):
-    """Oracle sweeps on the host: the CPU restatement of the reference sweep.  Default: the
-    Woodbury draw, algorithm-matched to the GPU path (reference-literal p x p Cholesky at
-    p=50000 needs a 20 GB Gram and ~4e13 flop per sweep).  literal=True: the reference's own
-    p x p path (BridgeRegression.cpp:24-25 X'X and X'y once, then per sweep
-    :552-575 dpotrf of X'X + diag(lambda sig2 / tau^2) and three triangular solves).
-    threads: BLAS threads (None = the environment's).  Returns (median s per sweep, threads)."""
+def cpu_baseline(n, p, alpha, sweeps, threads=None, literal=False):
+    """The compiled CPU baseline (oracle/bb_cpu_chain.c + scipy's OpenBLAS, no Python in the
+    loop): the stable chain from beta = 0 with the reference-literal p x p Cholesky
+    (literal=True, BridgeRegression.cpp:552-575: X'X once, then dpotrf of
+    X'X + diag(lambda sig2 / tau^2) and three triangular solves per sweep) or the exact
+    Woodbury form the GPU runs (dsyrk + n x n dpotrf + dgemv).  threads: BLAS / OpenMP
+    threads (None: OMP_NUM_THREADS or every CPU).  Returns (s per sweep, threads)."""
     import oracle
-    from oracle import gibbs
 
-    X = make_columns(n, 0, p)
-    y, _ = make_problem_y(n, p)
-    beta = np.zeros(p)
-    tau, sig2 = 1.0, 1.0
-    times = []
-    with blas_threads(threads):
-        if literal:
-            G, c = X.T @ X, X.T @ y
-        for t in range(1, sweeps + 1):
-            t0 = time.perf_counter()
-            tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, 2.0, 2.0, 1, 0,
-                                      t)
-            r = y - X @ beta
-            sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, 1, 0, t)
-            lam = oracle.sample_lambda(beta, alpha, tau, 1, 0, t)
-            z = oracle.normals(p, 1, 0, t, oracle.KIND_BETA_Z)
-            if literal:
-                beta = gibbs.beta_step_chol(G, c, lam, sig2, tau, z)
-            else:
-                d = oracle.normals(n, 1, 0, t, oracle.KIND_DELTA)
-                beta = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
-            times.append(time.perf_counter() - t0)
-            if log_every:
-                log(f"[cpu_baseline] {'literal' if literal else 'woodbury'} "
-                    f"threads={threads or 'env'} sweep {t}: {times[-1]:.3f} s")
-    # first sweep starts from beta = 0 (all lambda draws at h = 0); report the median
-    per = float(np.median(times))
     if threads is None:
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return per, threads
+    X = make_columns(n, 0, p)
+    y, _ = make_problem_y(n, p)
+    r = oracle.cpu_chain(y, X, sweeps + 1, burn=0, alpha=alpha,
+                         method="chol" if literal else "woodbury", seed=0xB4E5B41D6E,
+                         threads=threads, record=False)
+    log(f"[cpu_baseline] {'literal' if literal else 'woodbury'} threads={threads}: "
+        f"{sweeps} sweeps in {r['runtime']:.3f} s")
+    return r["runtime"] / sweeps, threads
 
 
 def pmc_traffic(n, p, world, kernel):
-    """HBM bytes per k_gram launch from the newest committed PMC summary of this workload
-    (profiles/rNN_pmc.json, written by tools/profile_round.sh + tools/profile_summary.py:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 read correction).  None if absent or
-    for a different workload / world size."""
+    """HBM bytes per launch of `kernel` (exact name or template prefix) from the newest
+    committed PMC summary of this workload (profiles/rNN_pmc.json, written by
+    tools/profile_round.sh + tools/profile_summary.py: separate FETCH_SIZE / WRITE_SIZE
+    passes, gfx950 x2 read correction).  None if absent or for another workload / world."""
     import glob
 
     best = None
@@ -243,13 +222,104 @@ def pmc_traffic(n, p, world, kernel):
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        gk = d.get("gram_kernels", {})
         if w.get("n") != n or w.get("p") != p or world != 1:
             continue
-        for k in gk:  # exact name, or the prefix of a template instantiation
-            if k == kernel or k.startswith(kernel + "<"):
-                best = (gk[k]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+        for k, v in d.get("kernels", {}).items():
+            if (k == kernel or k.startswith(kernel + "<")) and v.get("hbm_bytes") == v.get(
+                    "hbm_bytes"):  # skip NaN (kernel missing from one of the passes)
+                best = (v["hbm_bytes"], os.path.relpath(f, ROOT))
     return best
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+# Phases whose bracket (HIP events at phase starts) covers exactly one kernel launch, in the
+# engine's per-sweep order (bb_engine.cpp phase_b / phase_c): the candidates for the
+# `roofline` kernel.  "ozprep" (k_oz_bound + k_oz_finalize + k_oz_residues) is not a single
+# kernel and is reported through phases_ms only.
+SINGLE_KERNEL_PHASES = ("lambda", "gram", "reduce", "chol", "solve", "beta")
+CHOL_NB = 64  # k_chol_persistent block size (bb_kernels.hip kNB)
+
+
+def roofline_for(phase, ms, ctx, traffic_world):
+    """Roofline object of the kernel behind `phase`, given its average launch time `ms`.
+    ctx: dict(n, p, p_loc, kind, gram_mode, eng, bb).  Formulas: DESIGN.md s5 / s8."""
+    bb, eng, kind = ctx["bb"], ctx["eng"], ctx["kind"]
+    n, p, p_loc = ctx["n"], ctx["p"], ctx["p_loc"]
+    gram_mode = ctx["gram_mode"]
+    logit, sparse = kind == "logit", kind == "sparse"
+    sec = ms * 1e-3
+    out = {"phase": phase, "kernel_ms_avg": ms}
+    if phase == "gram":
+        n_pad = -(-n // 128) * 128
+        ntri = n_pad * (n_pad + 1) // 2
+        if sparse:
+            # pair-list Gram by output column, per launch: 8 B product + 2 B row position per
+            # pair, 4 B segment start + 8 B packed entry per triangle entry, the CSR rows
+            # (12 B per non-zero) and D, u (8 B each per column)
+            si = eng.sparse_info()
+            if si["col_mode"]:
+                byts = 10.0 * si["pairs"] + 12.0 * ntri + 12.0 * si["nnz"] + 16.0 * p_loc
+                kname, kfull = "k_sp_gram_col (pair-list Gram by output column)", "bb::k_sp_gram_col"
+            else:
+                byts = 12.0 * si["pairs"] + 12.0 * ntri + 8.0 * p_loc
+                kname, kfull = "k_sp_gram (pair-list Gram)", "bb::k_sp_gram"
+            out.update(bound="hbm", kernel=kname, achieved=byts / sec / 1e9, peak=8000.0,
+                       unit="GB/s", algorithmic_bytes_per_launch=byts,
+                       # SURVEY 8(d)'s definition: 12 B per non-zero per pass over X
+                       survey_8d_bytes_per_pass=12.0 * si["nnz"],
+                       survey_8d_rate_GBps=12.0 * si["nnz"] / sec / 1e9)
+        elif gram_mode == bb.GRAM_OZAKI:
+            rows, kdim = (p, n) if logit else (n, p_loc)
+            ops = 16.0 * rows * (rows + 1) * kdim  # 16 exact int8 Grams (lower triangle, 2/MAC)
+            kfull = "bb::k_oz_gemm16u"
+            out.update(bound="mfma", kernel=("k_oz_gemm16u X'Omega X" if logit else "k_oz_gemm16u")
+                       + " (v_mfma_i32_16x16x64_i8)", achieved=ops / sec / 1e12,
+                       peak=INT8_MFMA_PEAK_TOPS, unit="TOP/s", ops_per_launch=ops,
+                       algorithmic_bytes_per_launch=16.0 * rows * kdim)
+        else:
+            flops = float(n) * p * (p + 1) if logit else float(n) * (n + 1) * p_loc
+            kfull = "bb::k_gram"
+            out.update(bound="mfma", kernel="k_gram (v_mfma_f64_16x16x4_f64)",
+                       achieved=flops / sec / 1e12, peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                       ops_per_launch=flops,
+                       algorithmic_bytes_per_launch=8.0 * (p if logit else n) * (n if logit else p_loc))
+    elif phase == "chol":
+        # the per-sweep Cholesky of the n x n Woodbury system (p x p for the logistic path):
+        # m^3/3 algorithmic flops; its time is set by the chain of m_pad/64 dependent block
+        # steps (DESIGN.md s5.2), reported as the latency model beside the flop rate
+        m = p if logit else n
+        m_pad = -(-m // 256) * 256 if logit else -(-n // 128) * 128
+        flops = m ** 3 / 3.0
+        steps = m_pad // CHOL_NB
+        kfull = "bb::k_chol_persistent"
+        out.update(bound="mfma", kernel="k_chol_persistent (fp64 MFMA, one launch per factor)",
+                   achieved=flops / sec / 1e12, peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                   ops_per_launch=flops, algorithmic_bytes_per_launch=8.0 * m_pad * m_pad,
+                   latency_model={"system": m, "system_padded": m_pad, "block": CHOL_NB,
+                                  "dependent_block_steps": steps,
+                                  "us_per_step": ms * 1e3 / steps,
+                                  "model": "time = steps x (in-LDS elimination of the 64-block "
+                                           "+ W = U_kk^-T + U_k,k+1 + next diagonal update) "
+                                           "(DESIGN.md s5.2)"})
+    else:
+        kfull = {"lambda": "bb::k_lambda", "reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve",
+                 "beta": "bb::k_beta"}[phase]
+        out.update(bound="latency", kernel=kfull, achieved=None, peak=None, unit=None)
+    out["frac"] = (out["achieved"] / out["peak"]) if out.get("peak") else None
+    tr = pmc_traffic(n, p, traffic_world, kfull)
+    out["traffic"] = tr[0] if tr else None
+    out["traffic_unit"] = "HBM bytes per launch (rocprofv3 PMC)"
+    out["traffic_source"] = tr[1] if tr else None
+    return out
+
+
+def fail(msg, code=2):
+    log(f"bench.py: ERROR: {msg}")
+    raise SystemExit(code)
 
 
 def main():
@@ -265,107 +335,172 @@ def main():
     ap.add_argument("--alpha", type=float, default=None)
     ap.add_argument("--cpu-sweeps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the N > 1 pre-timing check of the sharded chain against one "
+                         "device holding the whole problem")
     ap.add_argument("--single-process", action="store_true",
                     help="drive --gpus N devices from ONE process through an RCCL shard group "
-                         "(ncclCommInitAll) -- the path the .C entry points use under R")
+                         "(ncclCommInitAll) -- the path the .C entry points use under R; the "
+                         "default for --gpus N > 1 without a torch.distributed launcher")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
                     help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: the "
                          "library default, Ozaki)")
     args = ap.parse_args()
     wn, wp, walpha, kind = WORKLOADS[args.workload]
-    sparse, logit = kind == "sparse", kind == "logit"
     n = args.rows or wn
     p = args.cols or wp
     alpha = args.alpha or walpha
-    cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
-        (2 if sparse else 20 if logit else 5)
-
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        fail("--gpus must be >= 1")
+    if world_env > 1 and world_env != args.gpus:
+        fail(f"launched with WORLD_SIZE={world_env} but --gpus={args.gpus}")
+    if kind in ("small", "logit") and args.gpus > 1:
+        fail(f"workload {args.workload} does not shard (p <= n: replicas only, DESIGN.md s7); "
+             f"run it with --gpus 1")
     if kind == "small":
         return small_chain(args, n, p, alpha)
-    if args.single_process:
-        return single_process(args, n, p, alpha, kind)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # noqa: F811
+    if world_env > 1:
+        mode = "ranks"  # one process per GPU (torch.distributed launcher), RCCL per rank
+    elif args.gpus > 1 or args.single_process:
+        mode = "group"  # one process drives every GPU (the .C entry points' path)
+    else:
+        mode = "single"
+    return run_chain(args, n, p, alpha, kind, mode)
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
+def shard_bounds(p, world, r):
+    per = (p + world - 1) // world
+    j0 = min(p, r * per)
+    return j0, min(p, j0 + per)
+
+
+def make_design(kind, n, p, j0, j1):
+    if kind == "sparse":
+        return make_sparse_columns(n, j0, j1)
+    if kind == "logit":
+        return make_logit_problem(n, p)[0]
+    return make_columns(n, j0, j1)
+
+
+def make_y(kind, n, p):
+    if kind == "sparse":
+        return make_sparse_problem_y(n, p)[0]
+    if kind == "logit":
+        return make_logit_problem(n, p)[1]
+    return make_problem_y(n, p)[0]
+
+
+def run_chain(args, n, p, alpha, kind, mode):
+    """C2-C5: one chain of the p > n Woodbury sampler (or the logistic p <= n sampler) on
+    --gpus devices.  mode "single": one engine on one GPU; "ranks": this process is rank
+    RANK of a torch.distributed job, one GPU and one column shard per rank, RCCL
+    all-reduces between ranks; "group": this process drives N GPUs through an RCCL shard
+    group, one enqueue thread per device (bb_group_run).  Timing: W warm-up sweeps, then K
+    sweeps between barrier + synchronize fences on every device, max over ranks."""
     import torch
 
     import bayesbridge_amd as bb
 
-    # every rank drives its own GPU; torch's current device must match for the
-    # torch.cuda.synchronize() fences of the timing protocol
-    ndev = max(1, torch.cuda.device_count())
-    device = local_rank % ndev
-    torch.cuda.set_device(device)
+    sparse, logit = kind == "sparse", kind == "logit"
+    cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
+        (2 if sparse else 20 if logit else 5)
+    world = args.gpus
+    rank = int(os.environ.get("RANK", "0")) if mode == "ranks" else 0
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) if mode == "ranks" else 0
+    ndev = torch.cuda.device_count()
+    need = world if mode == "group" else local_rank + 1
+    if ndev < need:
+        fail(f"--gpus {world} ({mode} mode) needs {need} visible GPU(s), found {ndev}; "
+             f"refusing to measure fewer GPUs than requested")
+    dist = None
+    if mode == "ranks":
+        import torch.distributed as dist  # noqa: F811
 
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    devices = list(range(world)) if mode == "group" else [local_rank]
+    torch.cuda.set_device(devices[0])
     bb.set_verbose(0)
-    per = (p + world - 1) // world
-    j0 = min(p, rank * per)
-    j1 = min(p, j0 + per)
-    p_loc = j1 - j0
+    gram_mode = None if args.gram is None else (bb.GRAM_OZAKI if args.gram == "ozaki"
+                                                else bb.GRAM_FP64)
+    shard_world = 1 if mode == "single" else world
+    my_ranks = list(range(world)) if mode == "group" else [rank]
+
+    def make_engine(r, dev, cap, world_=None, stream=0):
+        w_ = shard_world if world_ is None else world_
+        j0, j1 = shard_bounds(p, w_, r)
+        X = make_design(kind, n, p, j0, j1)
+        cfg = bb.EngineConfig(n=n, p=p, p_local=(p if logit else j1 - j0), j0=j0, rank=r,
+                              world=w_, true_alpha=alpha, method=6 if logit else 2,
+                              trace_capacity=cap, seed=0xB4E5B41D6E, stream=stream,
+                              device=dev, gram_mode=gram_mode)
+        return bb.Engine(cfg, X, y)
+
     t_setup0 = time.perf_counter()
-    if logit and world > 1:
-        raise SystemExit("the logistic workload runs on one GPU (replicas only)")
-    if sparse:
-        X = make_sparse_columns(n, j0, j1)
-        y, _ = make_sparse_problem_y(n, p)
-        nnz_loc = int(X.nnz)
-    elif logit:
-        X, y, _ = make_logit_problem(n, p)
-        nnz_loc = n * p
-    else:
-        X = make_columns(n, j0, j1)
-        y, _ = make_problem_y(n, p)
-        nnz_loc = n * p_loc
-    cfg = bb.EngineConfig(n=n, p=p, p_local=p_loc, j0=j0, rank=rank, world=world,
-                          true_alpha=alpha, method=6 if logit else 2,
-                          trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
-                          stream=0, device=device,
-                          gram_mode=None if args.gram is None else
-                          (bb.GRAM_OZAKI if args.gram == "ozaki" else bb.GRAM_FP64))
-    eng = bb.Engine(cfg, X, y)
-    del X
-    force_rccl = os.environ.get("BB_FORCE_RCCL", "0") == "1"
-    if world > 1:
-        if rank == 0:
-            uid = bb.Engine.comm_unique_id()
-            obj = [uid]
-        else:
-            obj = [None]
+    y = make_y(kind, n, p)
+    cap = max(1, min(args.steps, 1000))
+    engines = [make_engine(r, devices[i], cap) for i, r in enumerate(my_ranks)]
+    eng = engines[0]
+    grp = None
+    if mode == "group":
+        grp = bb.ShardGroup(engines, rccl=True)
+    elif mode == "ranks":
+        obj = [bb.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0])
-    elif force_rccl:
-        # exercise the RCCL exchange path on one GPU (1-rank communicator)
-        eng.comm_init(bb.Engine.comm_unique_id())
-    eng.init_state()
+    elif os.environ.get("BB_FORCE_RCCL", "0") == "1":
+        eng.comm_init(bb.Engine.comm_unique_id())  # 1-rank communicator (testing)
+    runner = grp or eng
+    runner.init_state()
     setup_s = time.perf_counter() - t_setup0
-    log(f"[rank {rank}] setup {setup_s:.2f} s  (workload={args.workload}, n={n}, p={p}, "
-        f"p_local={p_loc}, method={eng.method()})")
+    p_loc = eng.p_local
+    log(f"[rank {rank}] setup {setup_s:.2f} s  (workload={args.workload}, mode={mode}, n={n}, "
+        f"p={p}, p_local={p_loc}, devices={devices}, method={eng.method()})")
+
+    def sync_all():
+        runner.sync()
+        for d in devices:
+            torch.cuda.synchronize(d)
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    parity = None
+    if world > 1 and not args.no_parity_check:
+        parity = shard_parity_check(bb, dist, rank, engines, my_ranks, runner, make_engine,
+                                    devices[0], p, world)
+        if not parity["ok"]:
+            if rank == 0:
+                log(f"bench.py: ERROR: sharded chain differs from the one-device engine: "
+                    f"{json.dumps(parity)}")
+            raise SystemExit(3)
+        runner.init_state()  # restart the chain from the reference start after the check
 
     t = 1
-    eng.run(t, args.warmup, first_slot=-1)
+    runner.run(t, args.warmup, first_slot=-1)
     t += args.warmup
-    eng.sync()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    # inside the timed region only the Gram kernel is bracketed by HIP events (two per sweep)
-    eng.enable_timing(True, phases=False)
+    sync_all()
+    # per-phase breakdown (untimed, an event at every phase start of rank 0's sweeps): it
+    # also picks the dominant single-kernel phase, whose launches the timed loop brackets
+    nph = max(1, min(args.steps, 20))
+    eng.enable_timing(True, phases=True)
+    eng.reset_timing()
+    runner.run(t, nph, first_slot=-1)
+    t += nph
+    sync_all()
+    phases = eng.phase_times()
+    _, sweep_ms_phases, _ = eng.kernel_times()
+    dom = max((ph for ph in SINGLE_KERNEL_PHASES if ph in phases), key=lambda k: phases[k])
+    barrier()
+    eng.enable_timing(True, phases=False, timed_phase=dom)
     eng.reset_timing()
     t0 = time.perf_counter()
     # the timed loop records every sweep's beta / lambda / sig2 / tau into the device trace
     # ring, as the reference's MCMC loop writes its output slots (BridgeWrapper.cpp:287-298)
-    eng.run(t, args.steps, first_slot=0)
-    eng.sync()
-    torch.cuda.synchronize()
+    runner.run(t, args.steps, first_slot=0)
+    sync_all()
     elapsed = time.perf_counter() - t0
     t += args.steps
     if dist:
@@ -373,149 +508,48 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    gram_ms, _, nsamp = eng.kernel_times()
-    # per-phase breakdown from a short untimed run with an event at every phase start
-    eng.enable_timing(True, phases=True)
-    eng.reset_timing()
-    nph = max(1, min(args.steps, 20))
-    eng.run(t, nph, first_slot=-1)
-    eng.sync()
-    t += nph
-    phases = eng.phase_times()
-    _, sweep_ms, _ = eng.kernel_times()
+    dom_ms, _, _ = eng.kernel_times()
     eng.enable_timing(False)
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
         log(f"[rank {rank}] WARNING: state tau={st['tau']} sig2={st['sig2']} flags={flags}")
 
-    value = args.steps / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
-    gram_mode = eng.gram_mode()
-    gram_flops = float(n) * (n + 1) * p_loc
-    n_pad = -(-n // 128) * 128
-    ntri = n_pad * (n_pad + 1) // 2
-    if sparse:
-        # Dominant kernel = the pair-list sparse Gram, HBM-bound.  By-column
-        # kernel, per launch: the pair stream (8 B product + 2 B row position per pair), the
-        # segment starts (4 B per packed entry) and the packed triangle written (8 B per
-        # entry), the CSR rows (4 B index + 8 B value per non-zero) and D, u (8 B each per
-        # column).  The general kernel streams 4 B column indices instead and gathers D.
-        si = eng.sparse_info()
-        pairs = si["pairs"]
-        if si["col_mode"]:
-            kernel_bytes = 10.0 * pairs + 12.0 * ntri + 12.0 * si["nnz"] + 16.0 * p_loc
-            kname = "k_sp_gram_col (pair-list Gram by output column)"
-            kfull = "bb::k_sp_gram_col"
-        else:
-            kernel_bytes = 12.0 * pairs + 12.0 * ntri + 8.0 * p_loc
-            kname = "k_sp_gram (pair-list Gram)"
-            kfull = "bb::k_sp_gram"
-        achieved = kernel_bytes / (gram_ms * 1e-3) / 1e9 if gram_ms > 0 else 0.0
-        peak, unit, bound = 8000.0, "GB/s", "hbm"
-        kernel_ops = kernel_bytes
-        alg_bytes = kernel_bytes
-        traffic = pmc_traffic(n, p, world, kfull)
-    elif logit and gram_mode == bb.GRAM_OZAKI:
-        # Dominant kernel = the per-sweep X'Omega X as the Ozaki-II int8 Gram of X' diag(omega)
-        # (rows = coefficients, K = observations): kOzMods x p(p+1) n int8 ops per launch
-        kernel_ops = 16.0 * p * (p + 1) * n
-        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-        peak, unit, kname, bound = (INT8_MFMA_PEAK_TOPS, "TOP/s",
-                                    "k_oz_gemm16u X'Omega X (v_mfma_i32_16x16x64_i8)", "mfma")
-        alg_bytes = 16.0 * n * p
-        traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u")
-    elif logit:
-        # Dominant kernel = the per-sweep X'Omega X (fp64 MFMA k_gram over K = n rows):
-        # n p (p + 1) algorithmic flops per launch (path p <= n, C4)
-        kernel_ops = float(n) * p * (p + 1)
-        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-        peak, unit, kname, bound = (FP64_MFMA_PEAK_TFLOPS, "TFLOP/s",
-                                    "k_gram X'Omega X (v_mfma_f64_16x16x4_f64)", "mfma")
-        alg_bytes = 8.0 * n * p
-        traffic = pmc_traffic(n, p, world, "bb::k_gram")
-    elif gram_mode == bb.GRAM_OZAKI:
-        # Dominant kernel = the Gram GEMM: algorithmic int8 ops of one k_oz_gemm launch,
-        # kOzMods x n(n+1) p_local (16 exact symmetric int8 Grams).
-        kernel_ops = 16.0 * n * (n + 1) * p_loc
-        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-        peak, unit, kname, bound = (INT8_MFMA_PEAK_TOPS, "TOP/s",
-                                    "k_oz_gemm16u (v_mfma_i32_16x16x64_i8)", "mfma")
-        alg_bytes = 16.0 * n * p_loc
-        traffic = pmc_traffic(n, p, world, "bb::k_oz_gemm16u")
-    else:
-        # fp64 path: algorithmic fp64 flops of one k_gram launch, n(n+1) p_local
-        kernel_ops = gram_flops
-        achieved = kernel_ops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-        peak, unit, kname, bound = (FP64_MFMA_PEAK_TFLOPS, "TFLOP/s",
-                                    "k_gram (v_mfma_f64_16x16x4_f64)", "mfma")
-        alg_bytes = 8.0 * n * p_loc
-        traffic = pmc_traffic(n, p, world, "bb::k_gram")
-    gram_total_ms = gram_ms + phases.get("ozprep", 0.0) + phases.get("reduce", 0.0)
-    # the dense Gram's fp64-equivalent rate (meaningless for the sparse design)
-    if logit:
-        gram_flops = float(n) * p * (p + 1)
-    fp64_equiv = (gram_flops / (gram_total_ms * 1e-3) / 1e12
-                  if gram_total_ms > 0 and kind in ("dense", "logit") else None)
+    ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode())
+    traffic_world = 1 if mode == "single" else world
+    roof = roofline_for(dom, dom_ms, ctx, traffic_world)
+    roof["timing"] = "HIP events on rank 0's engine stream around every timed launch"
+    secondary = None
+    if dom != "gram" and "gram" in phases:
+        secondary = roofline_for("gram", phases["gram"], ctx, traffic_world)
+        secondary["timing"] = f"HIP events at phase starts, {nph} untimed sweeps"
+    gram_total_ms = sum(phases.get(k, 0.0) for k in ("ozprep", "gram", "reduce"))
 
-    cpu = None
+    cpu = cpu_more = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_sweeps > 0:
-        log(f"[cpu_baseline] timing {cpu_sweeps} oracle sweeps at n={n}, p={p} ...")
-        if sparse:
-            per_sweep, threads = cpu_baseline_sparse(n, p, alpha, cpu_sweeps)
-            what = "scipy SpGEMM + LAPACK"
-        elif logit:
-            per_sweep, threads = cpu_baseline_logit(n, p, alpha, cpu_sweeps)
-            what = "numpy X'Omega X + LAPACK + C Polya-Gamma sampler"
-        else:
-            per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps)
-            what = "numpy/OpenBLAS"
-        cpu = {"value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads, "kind": "port",
-               "sample": f"{cpu_sweeps} {'logistic' if logit else 'Woodbury'} sweeps of the "
-                         f"oracle ({what}, "
-                         f"{threads} threads, + C tilted-stable sampler) at n={n}, p={p}; "
-                         f"median sweep {per_sweep:.3f} s"}
+        cpu, cpu_more = cpu_baselines(args, n, p, alpha, kind, cpu_sweeps)
 
-    # C2: the CPU baseline at 1 core and all cores, for the Woodbury port and
-    # for the reference-literal p x p path (dpotrf at p = 5000)
-    cpu_more = None
-    if (cpu is not None and args.workload == "c2" and p <= 8000):
-        cpu_more = []
-        for lit in (False, True):
-            for th in (1, None):
-                if not lit and th is None:
-                    per_sweep, threads = 1.0 / cpu["value"], cpu["cores"]
-                else:
-                    per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps, threads=th,
-                                                      literal=lit)
-                cpu_more.append({
-                    "value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads,
-                    "kind": "port",
-                    "path": ("reference-literal p x p Cholesky (dpotrf p=%d)" % p if lit
-                             else "Woodbury (algorithm-matched to the GPU)"),
-                    "sample": f"{cpu_sweeps} sweeps, median {per_sweep:.3f} s"})
-
+    value = args.steps / elapsed
     if rank == 0:
-        wl = {"c1": "C1 Gaussian bridge", "c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
+        wl = {"c2": "C2 Gaussian bridge", "c3": "C3 Gaussian bridge",
               "c4": "C4 logistic bridge (Polya-Gamma)",
               "c5": f"C5 sparse CSC Gaussian bridge (density {SPARSE_DENSITY})"}[args.workload]
-        config = {"workload": f"{wl} n={n} p={p} alpha={alpha}",
-                  "rccl": bool(world > 1 or force_rccl),
-                  "n": n, "p": p, "alpha": alpha,
+        par = {"single": "one GPU",
+               "ranks": f"column-shard x{world}, one process per GPU, RCCL all-reduce",
+               "group": f"column-shard x{world}, one process (RCCL shard group, "
+                        f"ncclCommInitAll, one enqueue thread per GPU)"}[mode]
+        config = {"workload": f"{wl} n={n} p={p} alpha={alpha}", "n": n, "p": p,
+                  "alpha": alpha, "mode": mode, "parallelism": par,
                   "beta_step": ("p x p Cholesky of X'Omega X + diag(lambda/tau^2)" if logit
-                                else "woodbury (exact, p > n)"),
-                  "parallelism": f"column-shard x{world}" + (" + RCCL all-reduce"
-                                                             if world > 1 else "")}
+                                else "woodbury (exact, p > n)")}
         if sparse:
             si = eng.sparse_info()
             config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
                           nnz_local=si["nnz"], pairs_local=si["pairs"], max_row_nnz=si["max_row"])
-        elif logit:
-            config["gram"] = ("X'Omega X ozaki-II int8 (fp64-accurate)"
-                              if gram_mode == bb.GRAM_OZAKI else "X'Omega X fp64 mfma")
         else:
-            config["gram"] = ("ozaki-II int8 (fp64-accurate)" if gram_mode == bb.GRAM_OZAKI
-                              else "fp64 mfma")
+            config["gram"] = (("X'Omega X " if logit else "") +
+                              ("ozaki-II int8 (fp64-accurate)"
+                               if eng.gram_mode() == bb.GRAM_OZAKI else "fp64 mfma"))
         rec = {
             "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
             "value": value,
@@ -523,7 +557,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": 1000.0 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -531,28 +565,125 @@ def main():
             "data": ("synthetic (SURVEY.md 8(d) design, seed 20240501"
                      + (f", Bernoulli({SPARSE_DENSITY}) sparsity)" if sparse else ")")),
             "config": config,
-            "roofline": {"bound": bound, "kernel": kname,
-                         "achieved": achieved, "peak": peak,
-                         "unit": unit, "frac": achieved / peak,
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
-                         "traffic_source": traffic[1] if traffic else None,
-                         "algorithmic_bytes_per_launch": alg_bytes,
-                         "gram_ms_avg": gram_ms,
-                         "sweep_ms_avg_events": sweep_ms,
-                         "ops_per_launch": kernel_ops,
-                         "gram_fp64_equivalent_tflops": fp64_equiv,
-                         "gram_total_ms": gram_total_ms},
+            "roofline": roof,
+            "roofline_secondary": secondary,
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+            "sweep_ms_phase_events": sweep_ms_phases,
+            "gram_total_ms": gram_total_ms,
             "cpu_baseline": cpu,
+            "parity_check": parity,
             "setup_s": setup_s,
         }
         if cpu_more:
             rec["cpu_baselines"] = cpu_more
         print(json.dumps(rec), flush=True)
-    eng.close()
+    if grp:
+        grp.close()
+    for e in engines:
+        e.close()
     if dist:
         dist.destroy_process_group()
+
+
+def shard_parity_check(bb, dist, rank, engines, my_ranks, runner, make_engine, dev0, p, world,
+                       k0=6, sweeps=2):
+    """Before timing an N > 1 run: two teacher-forced sweeps of the sharded chain against ONE
+    engine holding the whole problem on rank 0's device (the same counters, so the only
+    difference is the fp64 summation order of the Gram, S_alpha and X beta).  Start: the
+    one-device chain after k0 sweeps from beta = 0.  Bars as
+    tests/test_gpu_parity.py::test_shard_group_matches_single_engine (beta 1e-9 relative L2,
+    lambda 1e-10 with no decision flips, tau 1e-12, sig2 1e-11).  Returns a dict with the
+    errors and `ok` (the same on every rank)."""
+    ref = None
+    state = None
+    if rank == 0:
+        ref = make_engine(0, dev0, 1, world_=1, stream=0)
+        ref.init_state()
+        ref.run(1, k0, first_slot=-1)
+        ref.sync()
+        state = ref.state()
+    errs = {"beta_rel_l2": 0.0, "lambda_max_rel": 0.0, "lambda_flips": 0, "tau_rel": 0.0,
+            "sig2_rel": 0.0}
+    for s in range(sweeps):
+        if dist:
+            obj = [state]
+            dist.broadcast_object_list(obj, src=0)
+            state = obj[0]
+        t = 1_000_000 + s  # counters of their own: the check is not part of the chain
+        for e, r in zip(engines, my_ranks):
+            j0, j1 = shard_bounds(p, world, r)
+            e.set_state(state["beta"][j0:j1], state["tau"], state["sig2"], state["alpha"])
+        runner.run(t, 1, first_slot=-1)
+        runner.sync()
+        parts = [(r, e.state()) for e, r in zip(engines, my_ranks)]
+        if dist:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, parts)
+            parts = [x for g in gathered for x in g]
+        if rank == 0:
+            parts.sort(key=lambda q: q[0])
+            bg = np.concatenate([q[1]["beta"] for q in parts])
+            lg = np.concatenate([q[1]["lambda"] for q in parts])
+            ref.set_state(state["beta"], state["tau"], state["sig2"], state["alpha"])
+            ref.run(t, 1, first_slot=-1)
+            ref.sync()
+            r1 = ref.state()
+            lr = np.abs(lg - r1["lambda"]) / np.maximum(np.abs(r1["lambda"]), 1e-300)
+            e0 = parts[0][1]
+            errs["beta_rel_l2"] = max(errs["beta_rel_l2"], rel_l2(bg, r1["beta"]))
+            errs["lambda_max_rel"] = max(errs["lambda_max_rel"], float(lr.max()))
+            errs["lambda_flips"] += int(np.sum(lr > 1e-6))
+            errs["tau_rel"] = max(errs["tau_rel"], abs(e0["tau"] - r1["tau"]) / r1["tau"])
+            errs["sig2_rel"] = max(errs["sig2_rel"], abs(e0["sig2"] - r1["sig2"]) / r1["sig2"])
+            state = r1
+    ok = None
+    if rank == 0:
+        ok = (errs["beta_rel_l2"] <= 1e-9 and errs["lambda_max_rel"] <= 1e-10
+              and errs["lambda_flips"] == 0 and errs["tau_rel"] <= 1e-12
+              and errs["sig2_rel"] <= 1e-11)
+        ref.close()
+    if dist:
+        obj = [(ok, errs)]
+        dist.broadcast_object_list(obj, src=0)
+        ok, errs = obj[0]
+    return dict(ok=bool(ok), sweeps=sweeps, start=f"one-device chain after {k0} sweeps",
+                against="one engine holding all p columns on rank 0's device", **errs)
+
+
+def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
+    """The cpu_baseline leg (rank 0, N = 1 only), timed on this host."""
+    sparse, logit = kind == "sparse", kind == "logit"
+    log(f"[cpu_baseline] timing {cpu_sweeps} CPU sweeps at n={n}, p={p} ...")
+    if sparse:
+        per_sweep, threads = cpu_baseline_sparse(n, p, alpha, cpu_sweeps)
+        what = ("oracle Woodbury sweeps (scipy SpGEMM + LAPACK, numpy, + C tilted-stable "
+                "sampler)")
+    elif logit:
+        per_sweep, threads = cpu_baseline_logit(n, p, alpha, cpu_sweeps)
+        what = "oracle logistic sweeps (numpy X'Omega X + LAPACK + C Polya-Gamma sampler)"
+    else:
+        per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps)
+        what = ("compiled C Woodbury chain (oracle/bb_cpu_chain.c: dsyrk + dpotrf + dgemv, "
+                "scipy OpenBLAS, OpenMP lambda draws)")
+    cpu = {"value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads, "kind": "port",
+           "sample": f"{cpu_sweeps} {what} at n={n}, p={p}, {threads} threads; "
+                     f"{per_sweep:.3f} s per sweep"}
+    # SURVEY.md 8(d): the CPU baseline at 1 core and all cores, for the algorithm-matched
+    # Woodbury chain and (p <= 8000) the reference-literal p x p path
+    cpu_more = None
+    if kind == "dense":
+        cpu_more = [dict(cpu, path="Woodbury (algorithm-matched to the GPU)")]
+        variants = [(False, 1, max(1, min(cpu_sweeps, 3)))]
+        if p <= 8000:
+            variants += [(True, None, 3), (True, 1, 2)]
+        for lit, th, ns in variants:
+            per_sweep, threads = cpu_baseline(n, p, alpha, ns, threads=th, literal=lit)
+            cpu_more.append({
+                "value": 1.0 / per_sweep, "unit": "sweeps/s", "cores": threads, "kind": "port",
+                "path": ("reference-literal p x p Cholesky (dpotrf p=%d)" % p if lit
+                         else "Woodbury (algorithm-matched to the GPU)"),
+                "sample": f"{ns} sweeps of the compiled C chain, {per_sweep:.3f} s per sweep"})
+    return cpu, cpu_more
 
 
 def small_chain(args, n, p, alpha):
@@ -577,17 +708,16 @@ def small_chain(args, n, p, alpha):
     value = args.steps / runtime
     cpu = None
     if not args.no_cpu_baseline:
-        from oracle import gibbs
+        import oracle
 
-        ns = args.cpu_sweeps if args.cpu_sweeps is not None else 2000
-        with blas_threads(1):
-            t0 = time.perf_counter()
-            gibbs.bridge_regression_stable(y, X, ns, burn=0, alpha=alpha, seed=1, stream=0,
-                                           method="chol")
-            per = (time.perf_counter() - t0) / ns
+        ns = args.cpu_sweeps if args.cpu_sweeps is not None else 20000
+        r = oracle.cpu_chain(y, X, ns + 1, burn=0, alpha=alpha, method="chol",
+                             seed=0xB4E5B41D6E, threads=1, record=False)
+        per = r["runtime"] / ns
         cpu = {"value": 1.0 / per, "unit": "sweeps/s", "cores": 1, "kind": "port",
-               "sample": f"{ns} sweeps of the oracle's reference-literal chain (numpy/LAPACK "
-                         f"p x p Cholesky + C samplers, 1 thread) at n={n}, p={p}"}
+               "sample": f"{ns} sweeps of the compiled C reference-literal chain "
+                         f"(oracle/bb_cpu_chain.c: p x p dpotrf + dtrsm, scipy OpenBLAS, "
+                         f"1 thread) at n={n}, p={p}"}
     # the p x p path's algorithmic flops per sweep (path p <= n):
     # p^3/3 + 3 p^2 + 2 n p; the fused chain is latency-bound, far from any roofline
     flops = p ** 3 / 3.0 + 3.0 * p * p + 2.0 * n * p
@@ -609,65 +739,6 @@ def small_chain(args, n, p, alpha):
         "cpu_baseline": cpu, "call_wall_s": wall,
     }
     print(json.dumps(rec), flush=True)
-
-
-def single_process(args, n, p, alpha, kind):
-    """--single-process: the .C entry points' multi-GPU path -- one host thread, one engine
-    per device holding a column shard, exchanges through an RCCL group (bb_group_create_rccl,
-    ncclCommInitAll).  Same workload, timing protocol and JSON line as the default mode."""
-    import torch
-
-    import bayesbridge_amd as bb
-
-    if kind == "logit":
-        raise SystemExit("the logistic workload runs on one GPU")
-    ndev = args.gpus
-    if ndev > max(1, torch.cuda.device_count()):
-        raise SystemExit(f"--single-process --gpus {ndev}: only {torch.cuda.device_count()} visible")
-    bb.set_verbose(0)
-    per = (p + ndev - 1) // ndev
-    y = make_sparse_problem_y(n, p)[0] if kind == "sparse" else make_problem_y(n, p)[0]
-    t_setup0 = time.perf_counter()
-    engines = []
-    for r in range(ndev):
-        j0, j1 = r * per, min(p, (r + 1) * per)
-        X = make_sparse_columns(n, j0, j1) if kind == "sparse" else make_columns(n, j0, j1)
-        cfg = bb.EngineConfig(n=n, p=p, p_local=j1 - j0, j0=j0, rank=r, world=ndev,
-                              true_alpha=alpha, method=2,
-                              trace_capacity=max(1, min(args.steps, 1000)), seed=0xB4E5B41D6E,
-                              stream=0, device=r)
-        engines.append(bb.Engine(cfg, X, y))
-        del X
-    grp = bb.ShardGroup(engines, rccl=ndev > 1) if ndev > 1 else None
-    (grp or engines[0]).init_state()
-    setup_s = time.perf_counter() - t_setup0
-    runner = grp or engines[0]
-    runner.run(1, args.warmup, first_slot=-1)
-    runner.sync()
-    engines[0].enable_timing(True, phases=False)
-    engines[0].reset_timing()
-    t0 = time.perf_counter()
-    runner.run(1 + args.warmup, args.steps, first_slot=0)
-    runner.sync()
-    elapsed = time.perf_counter() - t0
-    gram_ms, _, _ = engines[0].kernel_times()
-    rec = {
-        "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
-        "value": args.steps / elapsed, "unit": "sweeps/s", "n_gpus": ndev,
-        "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (SURVEY.md 8(d) design, seed 20240501)",
-        "config": {"workload": f"{args.workload} n={n} p={p} alpha={alpha}", "n": n, "p": p,
-                   "alpha": alpha, "parallelism": f"column-shard x{ndev}, one process, "
-                                                  "RCCL group (ncclCommInitAll)"},
-        "roofline": None, "cpu_baseline": None, "gram_ms_rank0": gram_ms, "setup_s": setup_s,
-    }
-    print(json.dumps(rec), flush=True)
-    if grp:
-        grp.close()
-    for e in engines:
-        e.close()
 
 
 if __name__ == "__main__":

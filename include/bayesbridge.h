@@ -263,10 +263,14 @@ int bb_engine_set_state(bb_engine *e, const double *beta, double tau, double sig
                         double alpha);
 
 /*
- * Shard group: `count` engines on ONE device with cfg.rank = 0..count-1 and
- * cfg.world = count, each holding a column shard, driven by one host thread with the
- * per-sweep exchanges done as on-device sums.  Exercises the sharded decomposition on a
- * single GPU (RCCL cannot place two ranks on one device).  p > n path only.
+ * Shard group: `count` engines with cfg.rank = 0..count-1 and cfg.world = count, each
+ * holding a column shard of one p > n chain.  Two kinds share the type:
+ *   - bb_group_create: every member on ONE device, driven by one host thread, the per-sweep
+ *     exchanges done as on-device sums (the sharded decomposition on a single GPU; RCCL
+ *     cannot place two ranks on one device);
+ *   - bb_group_create_rccl: members on DISTINCT devices, communicators from
+ *     ncclCommInitAll lent to the members, each member's sweeps enqueued by its own host
+ *     thread inside bb_group_run (the single-process multi-GPU path of the .C entry points).
  */
 typedef struct bb_group bb_group;
 /* Batch of truncated draws (mode 0..5 = rtnorm_left, rtnorm_both, rtnorm,
@@ -293,10 +297,9 @@ int bb_engine_get_tri_basis(bb_engine *e, double *tV, double *a, double *d);
 int bb_engine_set_tri_state(bb_engine *e, const double *u);
 
 int bb_group_create(bb_engine **engines, int count, bb_group **out);
-/* The same group over engines on DISTINCT devices, exchanging with RCCL: communicators from
- * ncclCommInitAll, each exchange an ncclGroupStart / ncclAllReduce per member / ncclGroupEnd
- * on the members' streams.  This is the single-process multi-GPU path the .C entry points
- * use (R calls .C from one process). */
+/* The group over engines on DISTINCT devices, exchanging with RCCL (see above).  R calls .C
+ * from one process, so this is the multi-GPU path of the .C entry points; bb_group_run
+ * starts one enqueue thread per member and joins them before it returns. */
 int bb_group_create_rccl(bb_engine **engines, int count, bb_group **out);
 void bb_group_destroy(bb_group *g);
 int bb_group_init_state(bb_group *g);
@@ -305,10 +308,11 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
 int bb_group_sync(bb_group *g);
 
 /*
- * .C driver controls.  bridge_reg_stable / bridge_reg_stable_csc shard the columns of a
- * p > n (Woodbury, alpha known, non-ortho) problem over the visible devices in one process
- * (>= 4096 columns per device, an RCCL group); bb_set_device_count(k) caps that at k devices
- * (0: all).  Traces live on the device in a ring of at most `bytes` per engine (default
+ * .C driver controls.  bb_set_device_count(k) lets bridge_reg_stable / bridge_reg_stable_csc
+ * shard the columns of a p > n (Woodbury, alpha known, non-ortho) problem over up to k
+ * visible devices in one process (>= 4096 columns per device, an RCCL group; 0: every
+ * visible device).  The default is 1 (opt-in): a sharded chain sums its Gram in another
+ * fp64 order, and p > n chains amplify roundoff, so a trace depends on the device count.  Traces live on the device in a ring of at most `bytes` per engine (default
  * 1 GiB), copied out to the caller's P x M buffers whenever it fills, so M is not bounded by
  * HBM.  Every 10 sweeps the driver polls R's interrupt (R_CheckUserInterrupt under
  * R_ToplevelExec, as BridgeWrapper.cpp:273-275 polls), stops, releases the device, returns
@@ -330,9 +334,12 @@ int bb_engine_get_omega(bb_engine *e, double *omega);
 int bb_engine_gram_mode(const bb_engine *e);
 
 /* Per-kernel timing with HIP events on the engine's stream.  enable: 0 off, 1 only the
- * Gram kernel is bracketed (two events per sweep, for timed runs), 2 every phase start.
- * kernel_times: average ms of the Gram kernel and of the event-covered part of a sweep. */
+ * timed phase is bracketed (two events per sweep, for timed runs), 2 every phase start.
+ * kernel_times: average ms of the timed phase (first output) and of the event-covered part
+ * of a sweep.  The timed phase is the Gram GEMM unless bb_engine_set_timed_phase chose
+ * another (an index 0 .. bb_phase_count()-2 of bb_phase_name). */
 int bb_engine_enable_timing(bb_engine *e, int enable);
+int bb_engine_set_timed_phase(bb_engine *e, int phase);
 int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
                            int *samples);
 int bb_engine_reset_timing(bb_engine *e);
@@ -404,7 +411,7 @@ int bb_bridge_em(double *beta, const double *y, const double *X, int n, int p, d
                  double alpha, double lambda_max, double tol, int max_iter, int use_cg);
 
 /* trace.beta on the device: bridge EM (direct solves) for every ratio of a grid in ONE
- * launch, a workgroup per ratio, for 1 <= p <= 64.  beta: count x p (row r for ratios[r]),
+ * launch, a workgroup per ratio, for 1 <= p <= 128.  beta: count x p (row r for ratios[r]),
  * solves: count (bb_bridge_em's return per ratio).  Returns 0 or -1 (bb_last_error()). */
 int bb_bridge_em_batch(double *beta, int *solves, const double *y, const double *X, int n,
                        int p, const double *ratios, const double *lambda_max, int count,

@@ -249,3 +249,52 @@ def pg_batch(psi, seed, stream, t):
     if fails:
         raise ValueError(f"pg_batch: {fails} failed draws")
     return om
+
+
+# ---------------------------------------------------------------------------
+# Compiled reference-literal CPU chain (bb_cpu_chain.c + scipy's OpenBLAS): bench.py's
+# cpu_baseline.  Test infrastructure only, like the rest of this package.
+# ---------------------------------------------------------------------------
+_CPU_LIB_PATH = os.path.join(_HERE, "build", "libbbcpu.so")
+_cpu = None
+CPU_METHODS = {"chol": 0, "woodbury": 1, "ortho": 2}
+
+
+def cpu_lib():
+    global _cpu
+    if _cpu is None:
+        srcs = [os.path.join(_HERE, f) for f in ("bb_cpu_chain.c", "bb_oracle.c", "Makefile")]
+        if (not os.path.exists(_CPU_LIB_PATH)) or any(
+                os.path.getmtime(_CPU_LIB_PATH) < os.path.getmtime(s) for s in srcs):
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = ctypes.CDLL(_CPU_LIB_PATH)
+        d, i = ctypes.c_double, ctypes.c_int
+        L.bbc_stable_chain.argtypes = [i, _dp, _dp, i, i, d, d, d, d, d, d, i, i,
+                                       ctypes.c_uint64, ctypes.c_uint64, i, _dp, _dp, _dp]
+        L.bbc_stable_chain.restype = d
+        _cpu = L
+    return _cpu
+
+
+def cpu_chain(y, X, nsamp, burn=500, alpha=0.5, method="auto", sig2_shape=0.0, sig2_scale=0.0,
+              nu_shape=2.0, nu_rate=2.0, true_sig2=0.0, seed=0, stream=0, threads=1,
+              record=True):
+    """The stable chain (alpha known) in compiled C: bridge_regression_stable's driver with
+    the reference-literal p x p Cholesky ("chol"), the exact Woodbury form ("woodbury") or
+    the orthogonal design ("ortho"); "auto" = chol if p <= n else woodbury.  Same counters
+    as oracle/gibbs.py.  Returns dict(beta P x M, tau, sig2, runtime = post-burn seconds)."""
+    X = np.asfortranarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    n, p = X.shape
+    if method == "auto":
+        method = "chol" if p <= n else "woodbury"
+    M = int(nsamp)
+    beta = np.zeros((p, M), order="F") if record else None
+    tau, sig2 = np.zeros(M), np.zeros(M)
+    rt = cpu_lib().bbc_stable_chain(CPU_METHODS[method], _ptr(X), _ptr(y), n, p, alpha,
+                                    nu_shape, nu_rate, sig2_shape, sig2_scale, true_sig2,
+                                    int(burn), M, seed, stream, int(threads),
+                                    _ptr(beta) if record else None, _ptr(tau), _ptr(sig2))
+    if rt < 0:
+        raise RuntimeError(f"bbc_stable_chain failed ({rt})")
+    return dict(beta=beta, tau=tau, sig2=sig2, runtime=rt, method=method)

@@ -1,0 +1,76 @@
+"""bench.py dispatch, as the driver invokes it (no GPU needed).
+
+`python bench.py --gpus N` without a torch.distributed launcher drives N GPUs from one
+process (the .C entry points' RCCL shard group); with fewer than N visible GPUs it must exit
+non-zero with a clear message instead of silently measuring one GPU.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, env_extra=None):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    if env_extra:
+        env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args],
+                          capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
+
+
+def _visible_gpus():
+    import torch
+
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_visible_gpus() >= 2, reason="needs a host with fewer than 2 GPUs")
+def test_gpus_2_without_launcher_refuses_one_gpu():
+    r = run_bench("--gpus", "2", "--steps", "2", "--warmup", "0", "--no-cpu-baseline",
+                  "--rows", "64", "--cols", "300")
+    assert r.returncode != 0
+    assert "refusing to measure fewer GPUs than requested" in r.stderr, r.stderr[-2000:]
+    assert not r.stdout.strip(), "no JSON line may be printed"
+
+
+def test_world_size_mismatch_is_an_error():
+    r = run_bench("--gpus", "4", "--steps", "2", "--warmup", "0",
+                  env_extra={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus=4" in r.stderr
+
+
+@pytest.mark.parametrize("workload", ["c1", "c4"])
+def test_unsharded_workloads_refuse_multi_gpu(workload):
+    r = run_bench("--workload", workload, "--gpus", "2", "--steps", "2", "--warmup", "0")
+    assert r.returncode != 0
+    assert "does not shard" in r.stderr
+
+
+def test_dominant_phase_roofline_formulas():
+    """roofline_for: the Cholesky entry's flop rate and latency model follow DESIGN.md s8
+    (m^3/3 flop per launch, m_pad/64 dependent block steps)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class FakeBB:
+        GRAM_OZAKI, GRAM_FP64 = 1, 0
+
+    ctx = dict(bb=FakeBB, eng=None, kind="dense", n=1000, p=5000, p_loc=5000, gram_mode=1)
+    r = bench.roofline_for("chol", 0.25, ctx, 1)
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s"
+    assert abs(r["achieved"] - 1000 ** 3 / 3 / 0.25e-3 / 1e12) < 1e-9
+    assert r["latency_model"]["dependent_block_steps"] == 1024 // 64
+    assert abs(r["frac"] - r["achieved"] / bench.FP64_MFMA_PEAK_TFLOPS) < 1e-15
+    g = bench.roofline_for("gram", 0.05, ctx, 1)
+    assert abs(g["achieved"] - 16.0 * 1000 * 1001 * 5000 / 0.05e-3 / 1e12) < 1e-6
+    lg = dict(ctx, kind="logit", n=10000, p=1000, p_loc=1000)
+    r = bench.roofline_for("chol", 0.25, lg, 1)
+    assert r["latency_model"]["system"] == 1000
+    assert r["latency_model"]["system_padded"] == 1024

@@ -115,17 +115,19 @@ def test_one_member_group_equals_single_engine(gpu_lib, mode):
 
 
 def test_c_entry_device_count_control(gpu_lib):
+    """Sharding a .C chain over devices is opt-in: the default is one device (ADVICE r2);
+    bb_set_device_count(0) allows every visible device (>= 4096 columns each)."""
     bb = gpu_lib
     X, y, _ = synthetic_problem(50, 9000, seed=7)
-    bb.set_device_count(1)
+    bb.set_seed(SEED + 3)
+    a = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
+    assert bb.last_call_info()["devices"] == 1
+    bb.set_device_count(0)
     try:
         bb.set_seed(SEED + 3)
-        a = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
-        assert bb.last_call_info()["devices"] == 1
+        b = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
+        assert bb.last_call_info()["devices"] == min(bb.device_count(), 9000 // 4096)
     finally:
-        bb.set_device_count(0)
-    bb.set_seed(SEED + 3)
-    b = bb.bridge_reg_stb(y, X, nsamp=6, burn=2)
-    assert bb.last_call_info()["devices"] == min(bb.device_count(), 9000 // 4096)
+        bb.set_device_count(1)
     if bb.device_count() == 1:
         _same(a, b)

@@ -45,16 +45,19 @@ def test_pg_batch_matches_oracle(gpu_lib):
 
 @pytest.mark.parametrize("n,p,kw", [(500, 40, {}), (1500, 300, dict(alpha=0.3)),
                                     (300, 25, dict(true_tau=0.7)),
-                                    (1500, 300, dict(gram_mode=0))])
+                                    (1500, 300, dict(gram_mode=0)),
+                                    (3000, 2000, dict(sweeps=6))])
 def test_logit_teacher_forced(gpu_lib, n, p, kw):
     """25 teacher-forced sweeps; X'Omega X on the Ozaki-II int8 Gram (the default) and on the
-    fp64 MFMA Gram (gram_mode=0)."""
+    fp64 MFMA Gram (gram_mode=0).  p = 2000 > 1024 runs the 16-lane speculative lambda
+    kernel with the Polya-Gamma draws as its trailing workgroups."""
     bb = gpu_lib
     X, y, _ = logit_problem(n, p, n + p)
     alpha = kw.get("alpha", 0.5)
     true_tau = kw.get("true_tau", 0.0)
     seed, stream = SEED + 31, 2
-    o = gibbs.bridge_regression_logit(y, X, 25, burn=0, alpha=alpha, true_tau=true_tau,
+    o = gibbs.bridge_regression_logit(y, X, kw.get("sweeps", 25), burn=0, alpha=alpha,
+                                      true_tau=true_tau,
                                       seed=seed, stream=stream, record_state=True)
     e = bb.Engine(bb.EngineConfig(n=n, p=p, method=6, seed=seed, stream=stream,
                                   true_alpha=alpha, true_tau=true_tau,

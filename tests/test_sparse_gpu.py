@@ -278,3 +278,40 @@ def test_teacher_forced_c5_workload(gpu_lib):
         beta = b
     assert e.error_flags() == 0
     e.close()
+
+
+@pytest.mark.parametrize("n,p", [(40, 12), (12, 40)])
+@pytest.mark.parametrize("defect", ["unsorted", "duplicate", "out_of_range"])
+def test_csc_entry_rejects_malformed_on_both_paths(gpu_lib, capfd, n, p, defect):
+    """.C("bridge_reg_stable_csc") refuses a non-canonical dgCMatrix the same way whether the
+    shape selects the densified dense path (p <= n) or the sparse engine (p > n): the usual
+    'Error: ... Aborting Gibbs sampler.' and no samples."""
+    import ctypes
+    bb = gpu_lib
+    L = bb.library()
+    rng = np.random.default_rng(4)
+    colptr = np.arange(0, 2 * p + 1, 2, dtype=np.int32)
+    rowidx = np.concatenate([[0, 1 + (j % (n - 1))] for j in range(p)]).astype(np.int32)
+    if defect == "unsorted":
+        rowidx[2], rowidx[3] = rowidx[3], 0
+    elif defect == "duplicate":
+        rowidx[3] = rowidx[2]
+    else:
+        rowidx[5] = n
+    val = rng.standard_normal(2 * p)
+    y = rng.standard_normal(n)
+    M = 4
+    beta, lam = np.zeros((p, M), order="F"), np.zeros((p, M), order="F")
+    sig2, tau, alph = np.zeros(M), np.zeros(M), np.zeros(M)
+    d = lambda v: ctypes.byref(ctypes.c_double(float(v)))  # noqa: E731
+    i = lambda v: ctypes.byref(ctypes.c_int(int(v)))  # noqa: E731
+    rt = ctypes.c_double(0.0)
+    ip = ctypes.POINTER(ctypes.c_int)
+    capfd.readouterr()
+    L.bridge_reg_stable_csc(bb._p(beta), bb._p(lam), bb._p(sig2), bb._p(tau), bb._p(alph),
+                            bb._p(y), colptr.ctypes.data_as(ip), rowidx.ctypes.data_as(ip),
+                            bb._p(val), d(0), d(0), d(2), d(2), d(1), d(1), d(0), d(0), d(0.5),
+                            i(p), i(n), i(M), i(2), ctypes.byref(rt), i(0))
+    out = capfd.readouterr().out
+    assert "CSC:" in out and "Aborting Gibbs sampler." in out, out
+    assert not beta.any() and not sig2.any()

@@ -1,0 +1,141 @@
+"""The reference's published benchmark, replicated like for like.
+
+Protocol (Notes/bbnotes.tex:893-965, Code/R/PublicBenchmark.R:140-310): for each design and
+method, 10 simulations of 100 000 samples after 10 000 burn-in sweeps, alpha = 0.5, sig2
+Jeffreys, nu = tau^-alpha ~ Ga(2, rate = 2); per simulation the coda effectiveSize of every
+beta_j (sum.stat, :112-134); per coefficient the median over the simulations (table.info,
+:276-305, `apply(info$stb.stat[,colnum,], 1, median)`); the table reports min / median /
+max / sd of those per-coefficient values and the median runtime.  ESR = ESS / runtime.
+
+Designs (the reference's data(diabetes), man/diabetes.Rd:22: "x has been standardized to
+have unit L2 norm in each column and zero mean"):
+  DB   = sklearn's load_diabetes(scaled=True) -- the same Efron et al. data, columns centred
+         and scaled to unit L2 norm -- and y = the raw target, centred (:331-341);
+  DBI  = x2: the 10 columns of DB, their 45 pairwise products and the 9 squares (sex is
+         binary), each centred and scaled to unit L2 norm (lars' quadratic model);
+  orth = Q of the QR of the centred design, qr.Q(qr(X)) (unit columns, :485-488), run with
+         ortho = TRUE.
+The Boston Housing designs need mlbench's data, absent offline, so only DB / DBI are
+compared with the published ESS.
+
+Beside each GPU row: the compiled CPU chain (oracle/bb_cpu_chain.c, reference-literal
+p x p dpotrf / the ortho draw, scipy OpenBLAS, 1 thread) on the same design, one simulation
+of CPU_SAMPLES samples, for sweeps/s side by side.  Output: one JSON document on stdout.
+Usage: python tools/published_ess.py [> profiles/r03_published_ess.json]
+"""
+import itertools
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bayesbridge_amd as bb  # noqa: E402
+from bayesbridge_amd.diagnostics import effective_size  # noqa: E402
+
+# Notes/bbnotes.tex:901-925 (general design) and :946-978 (orthogonal design):
+# (time s, ESS min, med, max, sd)
+PUBLISHED = {
+    ("DB", "tri"): (1.51, 9744.17, 16583.07, 45168.14, 10901.50),
+    ("DB", "stable"): (4.80, 28727.55, 54360.66, 98428.62, 24566.58),
+    ("DBI", "tri"): (45.12, 227.78, 674.99, 1582.25, 232.56),
+    ("DBI", "stable"): (68.68, 17924.24, 60873.07, 91261.17, 18936.41),
+    ("DB", "tri_orth"): (1.20, 56884.02, 67798.11, 95013.04, 11393.50),
+    ("DB", "stable_orth"): (4.06, 64337.74, 83198.38, 97460.85, 10473.23),
+    ("DBI", "tri_orth"): (8.69, 20692.11, 66531.77, 100000.0, 24770.91),
+    ("DBI", "stable_orth"): (25.30, 32037.12, 76789.69, 100000.0, 20687.61),
+}
+
+
+def unit_l2(Z):
+    Z = Z - Z.mean(axis=0)
+    return Z / np.linalg.norm(Z, axis=0)
+
+
+def designs():
+    from sklearn.datasets import load_diabetes
+    d = load_diabetes(scaled=True)  # centred, unit L2 columns: the lars diabetes$x
+    X = unit_l2(d.data)
+    y = d.target - d.target.mean()
+    cols = [X[:, i] for i in range(10)]
+    cols += [X[:, i] * X[:, j] for i, j in itertools.combinations(range(10), 2)]
+    cols += [X[:, i] ** 2 for i in range(10) if i != 1]  # sex is binary: no square
+    X2 = unit_l2(np.column_stack(cols))
+    assert X2.shape == (442, 64)
+    return {"DB": (X, y), "DBI": (X2, y)}
+
+
+def qr_q(X):
+    return np.linalg.qr(X)[0]
+
+
+def gpu_run(X, y, method, nsamp, burn, seed):
+    bb.set_seed(seed)
+    orth = method.endswith("_orth")
+    if method.startswith("tri"):
+        out = bb.bridge_reg_tri(y, X, nsamp=nsamp, burn=burn, ortho=orth)
+    else:
+        out = bb.bridge_reg_stb(y, X, nsamp=nsamp, burn=burn, ortho=orth)
+    return out["beta"], out["runtime"]
+
+
+def cpu_run(X, y, method, nsamp, burn):
+    import oracle
+    if method.startswith("tri"):
+        return None
+    r = oracle.cpu_chain(y, X, nsamp, burn=burn, method="ortho" if method.endswith("_orth")
+                         else "chol", seed=1, threads=1, record=False)
+    return nsamp / r["runtime"]
+
+
+def main():
+    nsamp = int(os.environ.get("NSAMP", "100000"))
+    burn = int(os.environ.get("BURN", "10000"))
+    nsim = int(os.environ.get("NSIM", "10"))
+    cpu_samples = int(os.environ.get("CPU_SAMPLES", "20000"))
+    only_m = os.environ.get("METHODS", "stable,tri,stable_orth,tri_orth").split(",")
+    bb.set_verbose(0)
+    rows = []
+    for name, (X0, y) in designs().items():
+        for method in only_m:
+            X = qr_q(X0) if method.endswith("_orth") else X0
+            ess, rts = [], []
+            for s in range(nsim):
+                t0 = time.perf_counter()
+                beta, rt = gpu_run(X, y, method, nsamp, burn, seed=1000 + s)
+                ess.append(effective_size(beta))
+                rts.append(rt)
+                print(f"[{name} {method}] sim {s}: runtime {rt:.2f} s (wall "
+                      f"{time.perf_counter() - t0:.1f} s), ESS median {np.median(ess[-1]):.0f}",
+                      file=sys.stderr, flush=True)
+            per_coef = np.median(np.array(ess), axis=0)  # table.info: median over simulations
+            rt = float(np.median(rts))
+            rec = {"design": name, "method": method, "n": X.shape[0], "p": X.shape[1],
+                   "simulations": nsim, "nsamp": nsamp, "burn": burn,
+                   "runtime_s": rt, "sweeps_per_s": nsamp / rt,
+                   "ess": {"min": float(per_coef.min()), "median": float(np.median(per_coef)),
+                           "max": float(per_coef.max()), "sd": float(np.std(per_coef, ddof=1))},
+                   "esr_median": float(np.median(per_coef)) / rt}
+            pub = PUBLISHED.get((name, method))
+            if pub:
+                rec["published"] = {"runtime_s": pub[0], "sweeps_per_s": 100000 / pub[0],
+                                    "ess": dict(zip(("min", "median", "max", "sd"), pub[1:])),
+                                    "source": "Notes/bbnotes.tex:901-978 (2011 laptop)"}
+            cpu = cpu_run(X, y, method, cpu_samples, min(burn, cpu_samples // 10))
+            if cpu:
+                rec["cpu_compiled_1core_sweeps_per_s"] = cpu
+            rows.append(rec)
+            print(json.dumps(rec), file=sys.stderr, flush=True)
+    print(json.dumps({"protocol": f"{nsim} simulations x {nsamp} samples after {burn} burn-in, "
+                                  "alpha = 0.5, sig2 Jeffreys, nu ~ Ga(2, 2) "
+                                  "(Notes/bbnotes.tex:893-965)",
+                      "ess": "coda effectiveSize per beta_j, median over simulations; "
+                             "min / median / max / sd over coefficients",
+                      "results": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
