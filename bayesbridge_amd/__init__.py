@@ -66,7 +66,7 @@ EXPORTED_SYMBOLS = [
     "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
     "bb_pg_batch", "bb_group_create_rccl", "bb_group_sync", "bb_set_device_count",
     "bb_set_trace_budget", "bb_debug_interrupt_after", "bb_last_call_info",
-    "bb_engine_set_timed_phase",
+    "bb_engine_set_timed_phase", "bb_set_chol_version",
 ]
 
 
@@ -126,6 +126,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_group_create_rccl.argtypes = [c.POINTER(c.c_void_p), c.c_int, c.POINTER(c.c_void_p)]
     L.bb_group_sync.argtypes = [c.c_void_p]
     L.bb_set_device_count.argtypes = [c.c_int]
+    L.bb_set_chol_version.argtypes = [c.c_int]
     L.bb_set_trace_budget.argtypes = [c.c_longlong]
     L.bb_debug_interrupt_after.argtypes = [c.c_int]
     L.bb_last_call_info.argtypes = [_ip, _ip, _ip]
@@ -220,6 +221,11 @@ def set_verbose(v: int) -> None:
 def set_device_count(k: int) -> None:
     """Cap the devices a .C sampler call may shard over (0: every visible device)."""
     library().bb_set_device_count(int(k))
+
+
+def set_chol_version(version: int) -> None:
+    """Device Cholesky chain variant: 2 (pipelined, default) or 1 (round-2 chain)."""
+    _check(library().bb_set_chol_version(int(version)), "bb_set_chol_version")
 
 
 def set_trace_budget(nbytes: int) -> None:

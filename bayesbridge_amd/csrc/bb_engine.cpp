@@ -270,6 +270,9 @@ static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "o
 struct bb_engine {
     bb_config cfg{};
     int n = 0, p = 0, p_loc = 0, n_pad = 0, p_pad = 0;
+    // p x p systems (methods 1, 6): factored at round_up(p, 64) inside the p_pad-strided
+    // buffers, so a p = 64 design is one block step, not p_pad / 64 = 4
+    int chol_m = 0;
     int method = 0;  // 1 chol, 2 woodbury, 3 ortho, 4 triangle mixture, 5 sparse woodbury,
                      // 6 logistic (Polya-Gamma)
     int group = 1;
@@ -509,15 +512,16 @@ struct bb_engine {
         } else if (method == 1 || method == 6) {
             // logistic: A = X'Omega X + diag(lambda / tau^2) (sig2 = 1), c = X'kappa
             mark(PH_FORM);
-            launch_form_a(stream, method == 6 ? Gw : G, p_pad, lam, sc, cvec, p, p_pad, A, p_pad,
-                          p_pad, method == 6 && cfg.gram_mode == 1);
+            const int m = chol_m;  // round_up(p, 64) <= p_pad
+            launch_form_a(stream, method == 6 ? Gw : G, p_pad, lam, sc, cvec, p, m, A, p_pad, m,
+                          method == 6 && cfg.gram_mode == 1);
             mark(PH_CHOL);
-            chol_factor(stream, A, p_pad, p_pad, 1, err, Wd, flags);
+            chol_factor(stream, A, p_pad, m, 1, err, Wd, flags);
             mark(PH_SOLVE);
-            launch_chol_rhs(stream, A, p_pad, p_pad, p, p_pad, cfg.seed, cfg.stream, t, Y2);
-            chol_bsolve(stream, A, p_pad, p_pad, Wd, Y2, W2, 2, flags, err);
+            launch_chol_rhs(stream, A, p_pad, m, p, m, cfg.seed, cfg.stream, t, Y2);
+            chol_bsolve(stream, A, p_pad, m, Wd, Y2, W2, 2, flags, err);
             mark(PH_BETA);
-            launch_beta_chol(stream, W2, p_pad, sc, p, beta, trb);
+            launch_beta_chol(stream, W2, m, sc, p, beta, trb);
         } else if (method == 3) {
             mark(PH_BETA);
             launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta, trb);
@@ -550,7 +554,8 @@ struct bb_engine {
                 mark(PH_BETA);
             }
             if (method == 4)
-                launch_tri_chain(stream, X, n_pad, n, p, y, tVc, tVr, tri_a, tri_d, beta, u, lam,
+                launch_tri_chain(stream, X, n_pad, n, p, y, tVc, tVr, tri_a, tri_d, tri_G, cvec,
+                                 cfg.ortho, beta, u, lam,
                                  D, sc, hy, cfg.betaburn, cfg.seed, cfg.stream, t0, count,
                                  first_slot, slot_step, cap, tr_beta, tr_u, tr_lam, tr_shape,
                                  tr_sig2, tr_tau, tr_alpha, err);
@@ -733,6 +738,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     e->p_loc = c.p_local;
     e->n_pad = round_up(c.n, kGramTile);
     e->p_pad = round_up(c.p_local, 256);
+    e->chol_m = round_up(c.p_local, kNB);
     e->cap = c.trace_capacity < 1 ? 1 : c.trace_capacity;
     e->hy = Hyper{c.sig2_shape, c.sig2_scale, c.nu_shape, c.nu_rate, c.alpha_a, c.alpha_b,
                   c.true_tau > 0, c.true_sig2 > 0, c.true_alpha > 0};
@@ -900,8 +906,9 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     // small p, one device, alpha known: whole sweeps in one single-workgroup launch
     e->fused = (e->method == 1 || e->method == 3) && c.p <= kSmallChainMaxP && c.world == 1 &&
                e->hy.know_alpha && e->cvec && e->gdiag && (e->method == 3 || e->G);
-    if (e->method == 4)  // bb_tri.hip k_tri_chain: non-orthogonal design only
-        e->fused = !c.ortho && c.p <= kTriChainMaxP && c.world == 1 && e->hy.know_alpha;
+    if (e->method == 4)  // bb_tri.hip k_tri_chain (general and orthogonal designs)
+        e->fused = c.p <= kTriChainMaxP && c.world == 1 && e->hy.know_alpha &&
+                   (!c.ortho || (e->tri_G && e->cvec));
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -911,12 +918,13 @@ void engine_init_state_local(bb_engine *e) {
     bool ls_ok = false;
     if (e->G != nullptr) {
         e->clear_err();
-        launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, e->p_pad, e->A,
-                      e->p_pad, e->p_pad);
-        chol_factor(e->stream, e->A, e->p_pad, e->p_pad, 1, e->err, e->Wd, e->flags);
-        HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)e->p_pad * e->p_pad,
-                                e->p_pad * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
-        chol_bsolve(e->stream, e->A, e->p_pad, e->p_pad, e->Wd, e->Y2, e->W2, 1, e->flags, e->err);
+        const int m = e->chol_m ? e->chol_m : e->p_pad;
+        launch_form_a(e->stream, e->G, e->p_pad, nullptr, e->sc, e->cvec, e->p, m, e->A,
+                      e->p_pad, m);
+        chol_factor(e->stream, e->A, e->p_pad, m, 1, e->err, e->Wd, e->flags);
+        HIPCHECK(hipMemcpyAsync(e->Y2, e->A + (size_t)m * e->p_pad, m * sizeof(double),
+                                hipMemcpyDeviceToDevice, e->stream));
+        chol_bsolve(e->stream, e->A, e->p_pad, m, e->Wd, e->Y2, e->W2, 1, e->flags, e->err);
         uint32_t f = e->read_err();
         ls_ok = (f & 8u) == 0;
         if (ls_ok) {
@@ -2703,6 +2711,12 @@ Outcome stable_dense(const bb_config &c, const double *yp, const double *Xp, int
 extern "C" {
 
 void bb_set_device_count(int count) { g_max_devices = count < 0 ? 0 : count; }
+
+int bb_set_chol_version(int version) {
+    if (version != 1 && version != 2) return -1;
+    g_chol_version = version;
+    return 0;
+}
 void bb_set_trace_budget(long long bytes) {
     g_trace_budget = bytes > 0 ? (size_t)bytes : (size_t(1) << 30);
 }

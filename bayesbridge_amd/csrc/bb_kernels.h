@@ -121,6 +121,8 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 size_t chol_flag_words(int m_pad, int nrhs_blocks);
 // doubles of the Wd buffer chol_factor needs (W_k blocks + scratch tiles)
 size_t chol_wd_words(int m_pad);
+// k_chol_persistent chain variant: 2 (pipelined, default) or 1 (round-2 chain), for A/B
+extern int g_chol_version;
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *Wd, unsigned int *flags, unsigned long long *trace = nullptr);
 
@@ -212,7 +214,7 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
 constexpr int kTriChainMaxP = 32;
 void launch_tri_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
                       const double *tVc, const double *tVr, const double *a, const double *d,
-                      double *beta, double *u, double *omega, double *shape, DevScalars *sc,
+                      const double *Gf, const double *c, int ortho, double *beta, double *u, double *omega, double *shape, DevScalars *sc,
                       Hyper hy, int betaburn, uint64_t k0, uint64_t k1, uint64_t t0, int count,
                       int first_slot, int slot_step, int cap, double *tr_beta, double *tr_u,
                       double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,

@@ -1433,14 +1433,324 @@ __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[1
     __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// Chain v2 (round 3): the post-elimination products leave the critical path.
+// v1 runs, per 64-block step, elimination (10.9 us at m = 2048) -> W pass -> U_{k,k+1} =
+// W_k A_{k,k+1} (1.8 us) -> D_{k+1} = A_{k+1,k+1} - U'U (2.0 us) -> publish: ~17 us.  Here:
+//   - the pivot rows are published without the separate multiplier array (consumers take the
+//     multiplier from the scaled row and rescale the row by p_c), which frees the LDS for the
+//     hand-off tile S = A_{k,k+1} and the U rows during the elimination;
+//   - W_k rows go to global memory from the producing wave's registers as soon as its group
+//     is done; W_k is published when the last wave's stores have drained;
+//   - once S has arrived (the hand-off lands ~7.5 us after W_{k-1}) and row blocks 0-2 are
+//     eliminated, waves 0-5 form U rows 0..47 (U = W_k S = sqrt(p) ROWS_I S, fp64 MFMA) and
+//     the partial D_{k+1} = A_{k+1,k+1} - sum_{s < 48} U_s' U_s of the 10 upper 16x16 blocks,
+//     while waves 6-7 are still pivoting;
+//   - after the last pivot only U row block 3 (waves 4-7, 16 MFMAs each) and the last four
+//     K steps of D_{k+1} remain: the next elimination starts ~0.5 us after the last pivot.
+// Same flags, tiles and owners as v1; U_{k,k+1} is published by the last of its storing waves.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_wait_ge(const volatile __attribute__((address_space(3))) int *p,
+                                            int v, uint32_t *err) {
+    for (unsigned spins = 0; *p < v;) {
+        if (++spins > (1u << 22)) {  // bounded: a broken hand-off flags, never hangs
+            if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 16u);
+            break;
+        }
+    }
+    asm volatile("" ::: "memory");
+}
+
+// lane 0 adds 1 to an LDS counter; returns the value before (uniform across the wave)
+__device__ __forceinline__ int lds_bump(int *p) {
+    int old = 0;
+    asm volatile("" ::: "memory");
+    if ((threadIdx.x & 63) == 0)  // release: this wave's earlier LDS / drained stores first
+        old = __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(old);
+}
+
+template <int W>
+__device__ __forceinline__ void elim_produce2(double (&a)[8][2], double (*ROWS)[128], double *piv,
+                                             volatile __attribute__((address_space(3))) int *vc) {
+    const int lane = threadIdx.x & 63, c0 = lane * 2;
+#pragma unroll
+    for (int ci = 0; ci < 8; ++ci) {
+        const int c = 8 * W + ci;
+        const double pv = readlane_d(a[ci][ci & 1], 4 * W + (ci >> 1));
+        const double inv = fast_rcp(pv);
+        const double rs0 = a[ci][0] * inv, rs1 = a[ci][1] * inv;
+#pragma unroll
+        for (int i = ci + 1; i < 8; ++i) {
+            const double m = readlane_d(a[ci][i & 1], 4 * W + (i >> 1));
+            a[i][0] = __builtin_fma(-m, rs0, a[i][0]);
+            a[i][1] = __builtin_fma(-m, rs1, a[i][1]);
+        }
+        *(double2 *)&ROWS[c][c0] = make_double2(rs0, rs1);
+        if (lane == 0) piv[c] = pv;
+        asm volatile("" ::: "memory");
+        if (lane == 0) *vc = c + 1;
+    }
+}
+
+// U block (by, bx) of U = W S, W = diag(sqrt p) ROWS_I (lower triangular: K steps < 4 by + 4)
+__device__ __forceinline__ v4d u_block2(const double (*ROWS)[128], const double (*S)[65],
+                                        const double *piv, int by, int bx) {
+    const int lane = threadIdx.x & 63, ry = by * 16 + (lane & 15), cx = bx * 16 + (lane & 15);
+    v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = a0;
+    const int nk = 4 * by + 4;
+    for (int kk = 0; kk < nk; kk += 2) {
+        const int s0 = 4 * kk + (lane >> 4);
+        a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(ROWS[ry][64 + s0], S[s0][cx], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ROWS[ry][68 + s0], S[s0 + 4][cx], a1, 0, 0, 0);
+    }
+    v4d u = a0 + a1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) u[r] *= sqrt(piv[by * 16 + (lane >> 4) + 4 * r]);
+    return u;
+}
+
+// U block -> LDS rows (T) and the (k, k+1) tile of A (write-through, for the owners)
+__device__ __forceinline__ void u_put2(double (*T)[65], double *A, int lda, int k, int by, int bx,
+                                       const v4d &u) {
+    const int lane = threadIdx.x & 63, x = bx * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int y = by * 16 + (lane >> 4) + 4 * r;
+        T[y][x] = u[r];
+        st_sc1(&A[(size_t)(k * kNB + y) + (size_t)((k + 1) * kNB + x) * lda], u[r]);
+    }
+}
+
+// acc += sum_{s in [4 k0, 4 k1)} U[s][16 by + .]' U[s][16 bx + .]
+__device__ __forceinline__ void dprime_acc2(const double (*T)[65], int by, int bx, int k0, int k1,
+                                            v4d &acc) {
+    const int lane = threadIdx.x & 63, cy = by * 16 + (lane & 15), cx = bx * 16 + (lane & 15);
+    for (int kk = k0; kk < k1; ++kk) {
+        const int s0 = 4 * kk + (lane >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(T[s0][cy], T[s0][cx], acc, 0, 0, 0);
+    }
+}
+
+__device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
+                              const CholFlags &F, uint32_t *err, unsigned long long *trace,
+                              double *L) {
+    double(*T)[65] = (double(*)[65])L;                 // U_{k,k+1} rows
+    double(*S)[65] = (double(*)[65])(L + 4160);        // hand-off A_{k,k+1}
+    double(*ROWS)[128] = (double(*)[128])(L + 8320);   // published pivot rows [A | I] / p
+    double(*Dn)[65] = (double(*)[65])(L + 8320);       // next diagonal block (aliases ROWS)
+    __shared__ double piv[64];
+    __shared__ int cnt, s_ready, ua_cnt, w_drain, u_drain;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int r0 = wid * 8, c0 = lane * 2;
+    volatile __attribute__((address_space(3))) int *vc =
+        (volatile __attribute__((address_space(3))) int *)&cnt;
+    auto vlds = [](int *p) {
+        return (volatile __attribute__((address_space(3))) int *)p;
+    };
+    // D_{k+1} blocks of this wave (waves 0-5; upper blocks in order (0,0) (0,1) (1,1) (0,2)
+    // (1,2) (2,2) (0,3) (1,3) (2,3) (3,3)): waves 0-3 take blocks w and w + 4, waves 4-5
+    // blocks 8 and 9
+    auto bxy = [](int blk, int &by, int &bx) {
+        bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
+        by = blk - bx * (bx + 1) / 2;
+    };
+    const int nd = wid < 4 ? 2 : wid < 6 ? 1 : 0;
+    int dby[2] = {0, 0}, dbx[2] = {0, 0};
+    if (wid < 4) {
+        bxy(wid, dby[0], dbx[0]);
+        bxy(wid + 4, dby[1], dbx[1]);
+    } else if (wid < 6) {
+        bxy(wid + 4, dby[0], dbx[0]);
+    }
+#define CHAIN2_TS(slot)                                                                 \
+    do {                                                                                \
+        if (trace && lane == 0) trace[k * 32 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+    tile_load(Dn, A, lda, 0, 0, true);
+    for (int k = 0; k < nblk; ++k) {
+        __syncthreads();  // Dn (the diagonal block) complete
+        double a[8][2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int row = r0 + i, col = c0 + q;
+                a[i][q] = (col < 64) ? Dn[row][col] : ((col - 64 == row) ? 1.0 : 0.0);
+            }
+        if (tid == 0) cnt = s_ready = ua_cnt = w_drain = u_drain = 0;
+        __syncthreads();  // a[][] in registers: ROWS (= Dn) may be overwritten
+        if (wid == 0) CHAIN2_TS(0);
+        // ---- apply the earlier groups' pivot rows as they are published ----
+        int avail = 0;
+        for (int c = 0; c < r0; ++c) {
+            if (c >= avail) {
+                for (unsigned spins = 0; (avail = *vc) <= c;) {
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0) atomicOr(err, 16u);
+                        avail = r0;
+                        break;
+                    }
+                }
+                asm volatile("" ::: "memory");
+            }
+            const double2 v = *(const double2 *)&ROWS[c][c0];
+            const double pc = piv[c];
+            const double vx = v.x * pc, vy = v.y * pc;  // the unscaled pivot row
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                const double2 mm = *(const double2 *)&ROWS[c][r0 + i];  // multipliers / p_c
+                a[i][0] = __builtin_fma(-mm.x, vx, a[i][0]);
+                a[i][1] = __builtin_fma(-mm.x, vy, a[i][1]);
+                a[i + 1][0] = __builtin_fma(-mm.y, vx, a[i + 1][0]);
+                a[i + 1][1] = __builtin_fma(-mm.y, vy, a[i + 1][1]);
+            }
+        }
+        // ---- my group: 8 pivots in-wave ----
+        __builtin_amdgcn_s_setprio(3);
+        switch (wid) {
+            case 0: elim_produce2<0>(a, ROWS, piv, vc); break;
+            case 1: elim_produce2<1>(a, ROWS, piv, vc); break;
+            case 2: elim_produce2<2>(a, ROWS, piv, vc); break;
+            case 3: elim_produce2<3>(a, ROWS, piv, vc); break;
+            case 4: elim_produce2<4>(a, ROWS, piv, vc); break;
+            case 5: elim_produce2<5>(a, ROWS, piv, vc); break;
+            case 6: elim_produce2<6>(a, ROWS, piv, vc); break;
+            default: elim_produce2<7>(a, ROWS, piv, vc); break;
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (wid == 7) CHAIN2_TS(1);
+        // ---- my rows of W_k = U_kk^-T (the I part / sqrt p) to global memory ----
+        double *Wk = Wd + (size_t)k * kNB * kNB;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double pv = piv[r0 + i];
+            if (lane == 0 && !(pv > 0.0)) atomicOr(err, 8u);
+            double r = __builtin_amdgcn_rsq(pv);
+            r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+            r = r * __builtin_fma(-0.5 * pv * r, r, 1.5);
+            if (lane >= 32) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    st_sc1(&Wk[(size_t)(c0 + q - 64) * kNB + r0 + i], a[i][q] * r);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lds_bump(&w_drain) == 7 && lane == 0)
+            __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k + 1 == nblk) break;
+        // ---- the hand-off tile S = A_{k,k+1} (updated by its owner through step k-1) ----
+        if (wid < 4) {
+            const unsigned int *f1 = &F.R[2 * k + 1];
+            for (unsigned spins = 0;;) {
+                const unsigned int v1 = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane((int)(v1 == F.ep))) break;
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 25)) {
+                    if (lane == 0) atomicOr(err, 16u);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double *t1 = A + (size_t)k * kNB + (size_t)(k + 1) * kNB * lda;
+            double h[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int e = tid + q * 256, y = e & 63, x = e >> 6;
+                h[q] = ld_sc1(&t1[(size_t)y + (size_t)x * lda]);
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int e = tid + q * 256, y = e & 63, x = e >> 6;
+                S[y][x] = h[q];
+            }
+            asm volatile("" ::: "memory");
+            lds_bump(&s_ready);
+        }
+        v4d dacc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+        double qv[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+        if (wid < 6) {
+            // ---- phase a: U rows 0..47 and the partial next diagonal block ----
+            lds_wait_ge(vc, 48, err);
+            lds_wait_ge(vlds(&s_ready), 4, err);
+            if (wid < 4) {
+                const v4d u2 = u_block2(ROWS, S, piv, 2, wid);
+                u_put2(T, A, lda, k, 2, wid, u2);
+                const v4d u0 = u_block2(ROWS, S, piv, 0, wid);
+                u_put2(T, A, lda, k, 0, wid, u0);
+            } else {
+                const int b0 = 2 * (wid - 4);
+                const v4d ua = u_block2(ROWS, S, piv, 1, b0);
+                u_put2(T, A, lda, k, 1, b0, ua);
+                const v4d ub = u_block2(ROWS, S, piv, 1, b0 + 1);
+                u_put2(T, A, lda, k, 1, b0 + 1, ub);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_bump(&ua_cnt);
+            lds_bump(&u_drain);
+            // the (k+1, k+1) hand-off: this wave's D blocks of A_{k+1,k+1}
+            const unsigned int *f2 = &F.R[2 * (k + 1)];
+            for (unsigned spins = 0;;) {
+                const unsigned int v2 = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane((int)(v2 == F.ep))) break;
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 25)) {
+                    if (lane == 0) atomicOr(err, 16u);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double *t2 = A + (size_t)(k + 1) * kNB + (size_t)(k + 1) * kNB * lda;
+            for (int d = 0; d < nd; ++d)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int y = dby[d] * 16 + (lane >> 4) + 4 * r, x = dbx[d] * 16 + (lane & 15);
+                    qv[d][r] = ld_sc1(&t2[(size_t)y + (size_t)x * lda]);
+                }
+            lds_wait_ge(vlds(&ua_cnt), 6, err);
+            for (int d = 0; d < nd; ++d) dprime_acc2(T, dby[d], dbx[d], 0, 12, dacc[d]);
+        }
+        if (wid >= 4) {
+            // ---- phase b: U row block 3, once every pivot is published ----
+            lds_wait_ge(vc, 64, err);
+            lds_wait_ge(vlds(&s_ready), 4, err);
+            const v4d u3 = u_block2(ROWS, S, piv, 3, wid - 4);
+            u_put2(T, A, lda, k, 3, wid - 4, u3);
+        }
+        __syncthreads();  // U complete in T; every read of ROWS and S done
+        if (wid == 0) CHAIN2_TS(5);
+        for (int d = 0; d < nd; ++d) {
+            dprime_acc2(T, dby[d], dbx[d], 12, 16, dacc[d]);
+            const int by = dby[d], bx = dbx[d];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int y = by * 16 + (lane >> 4) + 4 * r, x = bx * 16 + (lane & 15);
+                Dn[y][x] = (y <= x) ? qv[d][r] - dacc[d][r] : 0.0;
+                if (by != bx) Dn[x][y] = 0.0;  // the mirrored lower block
+            }
+        }
+        if (wid >= 4) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lds_bump(&u_drain) == 9 && lane == 0)
+                __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (wid == 0) CHAIN2_TS(7);
+    }
+#undef CHAIN2_TS
+}
+
+template <int V>
 __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int nblk, int ncb,
                                                          double *Wd, CholFlags F,
                                                          uint32_t *err,
                                                          unsigned long long *trace) {
     // T: tile being updated / the chain's diagonal block -> W; S: staging U_ki / the chain's
     // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
-    // During the chain's elimination S and Q together hold the published pivot rows.
-    __shared__ __attribute__((aligned(16))) double Lb[3][64][65];
+    // During the v1 chain's elimination S and Q together hold the published pivot rows; the
+    // v2 chain (chol_chain_v2) lays out U rows, S and the pivot rows side by side.
+    __shared__ __attribute__((aligned(16))) double Lraw[V == 2 ? 16512 : 3 * 64 * 65];
+    double(*Lb)[64][65] = (double(*)[64][65])Lraw;
     __shared__ double piv[64];
     __shared__ int cnt;
     __shared__ int pre_ready;  // owner: the next update's panels are published
@@ -1451,6 +1761,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     v4d acc[2];
     if (blockIdx.x == 0) {
         // ------------------------------ the chain ------------------------------
+        if constexpr (V == 2) {
+            chol_chain_v2(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
+            return;
+        }
         const int lane = tid & 63, wid = tid >> 6;
         double(*ROWS)[128] = (double(*)[128]) & Lb[1][0][0];
         tile_load(T, A, lda, 0, 0, true);
@@ -1793,6 +2107,10 @@ static int device_cus() {
     return n;
 }
 
+// chain variant of k_chol_persistent (1: round-2 chain, 2: pipelined chain, the default);
+// bb_set_chol_version switches it for A/B measurements
+int g_chol_version = 2;
+
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *Wd, unsigned int *flags, unsigned long long *trace) {
     const int nblk = m_pad / kNB;
@@ -1803,7 +2121,10 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
                 flags + bsolve_flag_offset(m_pad, nrhs_blocks) + nblk, ncb, ep};
     const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
     const int grid = std::min(device_cus(), 1 + ntiles);
-    k_chol_persistent<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+    if (g_chol_version == 1)
+        k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+    else
+        k_chol_persistent<2><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
 }
 
 

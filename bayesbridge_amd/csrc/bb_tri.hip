@@ -479,7 +479,8 @@ __device__ __forceinline__ void tc_variate(TcVariates &v, int e, int p, double t
 __global__ __launch_bounds__(kTcNT) void k_tri_chain(
     const double *__restrict__ X, int ldx, int n, int p, const double *__restrict__ y,
     const double *__restrict__ tVc, const double *__restrict__ tVr,
-    const double *__restrict__ av, const double *__restrict__ dv, int x_lds, double *beta,
+    const double *__restrict__ av, const double *__restrict__ dv, const double *__restrict__ Gf,
+    const double *__restrict__ cv, int ortho, int x_lds, double *beta,
     double *u, double *omega, double *shape, DevScalars *sc, Hyper hy, int betaburn, Key key,
     uint64_t t0, int count, int first_slot, int slot_step, int cap, double *tr_beta,
     double *tr_u, double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,
@@ -491,9 +492,10 @@ __global__ __launch_bounds__(kTcNT) void k_tri_chain(
     __shared__ double red[2][kTcNT / 64];
     __shared__ double s_tau, s_sig2;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // orthogonal design: sTc holds the full symmetric Gram X'X (row j contiguous) instead
     for (int e = tid; e < p * p; e += kTcNT) {
-        sTc[e] = tVc[e];
-        sTr[e] = tVr[e];
+        sTc[e] = ortho ? Gf[e] : tVc[e];
+        if (!ortho) sTr[e] = tVr[e];
     }
     if (x_lds)
         for (int e = tid; e < n * p; e += kTcNT) sX[e] = X[(size_t)(e % n) + (size_t)(e / n) * ldx];
@@ -504,8 +506,8 @@ __global__ __launch_bounds__(kTcNT) void k_tri_chain(
     if (tid < p) {
         sb[tid] = beta[tid];
         uj = u[tid];
-        aj_c = av[tid];
-        dj_c = dv[tid];
+        aj_c = ortho ? cv[tid] : av[tid];          // ortho: c_j = (X'y)_j
+        dj_c = ortho ? Gf[(size_t)tid * p + tid] : dv[tid];  //        G_jj
     }
     if (tid == 0) {
         s_tau = sc->tau;
@@ -587,6 +589,31 @@ __global__ __launch_bounds__(kTcNT) void k_tri_chain(
                     tr_u[(size_t)slot * p + lane] = uj;
                 }
             }
+            if (ortho) {
+                // sample_beta_ortho (BridgeRegression.cpp:362-403), one coordinate pass as
+                // k_tri_update's: m_j = (c_j - sum_{k != j} G_jk beta_k) / G_jj, sd
+                // sqrt(sig2 / G_jj), truncated to |beta_j| <= b_j; attempts 0..kTcK-1 of
+                // every coordinate precomputed by waves 1..7 during the previous sweep
+                double bl = act ? sb[lane] : 0.0;
+                for (int j = 0; j < p; ++j) {
+                    const double prod = (act && lane != j) ? sTc[j * p + lane] * bl : 0.0;
+                    const double xb = wave_sum64(prod);  // xor butterfly: the same bits in
+                                                          // every lane
+                    const double gjj = readlane_d(dj_c, j), bnd = readlane_d(bj, j);
+                    const double m = (readlane_d(aj_c, j) - xb) / gjj;
+                    const double sd = sqrt(sig2 / gjj);
+                    const int ka = lane < kTcK ? lane : 0;
+                    const double zn = tnorm_par<kTcK>(-1.0 * bnd, bnd, m, sd, v.r[j][ka][0],
+                                                      v.r[j][ka][1], v.x[j][ka], key, t,
+                                                      (uint64_t)j, 0, err);
+                    if (lane == j) bl = zn;
+                }
+                if (act) {
+                    sb[lane] = bl;
+                    if (slot >= 0) tr_beta[(size_t)slot * p + lane] = bl;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else {
             // conditional mean a_i / d_i^2 and sd sigma / d_i of coordinate i (lane i)
             const bool ok = dj_c > 1e-16;
             const double ci = ok ? aj_c / (dj_c * dj_c) : 0.0;
@@ -653,6 +680,7 @@ __global__ __launch_bounds__(kTcNT) void k_tri_chain(
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // sb read by other lanes next
             }
             if (act && slot >= 0) tr_beta[(size_t)slot * p + lane] = sb[lane];
+            }
         }
         __syncthreads();
     }
@@ -814,7 +842,7 @@ void launch_tri_update(hipStream_t s, double *beta, double *u, double *omega, do
 
 void launch_tri_chain(hipStream_t s, const double *X, int ldx, int n, int p, const double *y,
                       const double *tVc, const double *tVr, const double *a, const double *d,
-                      double *beta, double *u, double *omega, double *shape, DevScalars *sc,
+                      const double *Gf, const double *c, int ortho, double *beta, double *u, double *omega, double *shape, DevScalars *sc,
                       Hyper hy, int betaburn, uint64_t k0, uint64_t k1, uint64_t t0, int count,
                       int first_slot, int slot_step, int cap, double *tr_beta, double *tr_u,
                       double *tr_omega, double *tr_shape, double *tr_sig2, double *tr_tau,
@@ -822,14 +850,11 @@ void launch_tri_chain(hipStream_t s, const double *X, int ldx, int n, int p, con
     if (count <= 0 || p < 1 || p > kTriChainMaxP) return;  // the engine checks p at setup
     const size_t xbytes = (size_t)n * p * sizeof(double);
     const int x_lds = xbytes <= kTcXLds;
-    static bool attr = false;  // one-time opt-in above the 64 KB default
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void *)k_tri_chain,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcXLds);
-        attr = true;
-    }
+    static const hipError_t attr = hipFuncSetAttribute(  // one-time opt-in above 64 KB
+        (const void *)k_tri_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTcXLds);
+    (void)attr;
     k_tri_chain<<<1, kTcNT, x_lds ? xbytes : 0, s>>>(
-        X, ldx, n, p, y, tVc, tVr, a, d, x_lds, beta, u, omega, shape, sc, hy, betaburn,
+        X, ldx, n, p, y, tVc, tVr, a, d, Gf, c, ortho, x_lds, beta, u, omega, shape, sc, hy, betaburn,
         Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta, tr_u, tr_omega, tr_shape,
         tr_sig2, tr_tau, tr_alpha, err);
 }

@@ -686,13 +686,32 @@ def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
     return cpu, cpu_more
 
 
+def small_phase_model(n, p):
+    """The in-kernel phase split of the fused small-p sweep for this (n, p) from the committed
+    tools/small_phase_bench output (profiles/r*_c1_small_phases.txt), or None."""
+    import glob
+    import re
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c1_small_phases.txt"))):
+        for line in open(f):
+            m = re.match(r"n=(\d+) p=(\d+) ortho=0: ([\d.]+) us/sweep \(rss ([\d.]+), "
+                         r"tau/sig2 ([\d.]+), lambda ([\d.]+), beta ([\d.]+) us\)", line)
+            if m and int(m.group(1)) == n and int(m.group(2)) == p:
+                v = [float(m.group(i)) for i in range(3, 8)]
+                best = {"source": os.path.relpath(f, ROOT), "us_per_sweep_in_kernel": v[0],
+                        "phases_us": {"S_alpha_rss": v[1], "tau_sig2": v[2], "lambda": v[3],
+                                      "beta_chol_solves": v[4]}}
+    return best
+
+
 def small_chain(args, n, p, alpha):
     """C1 (BASELINE configs[0], p <= n): the reference-literal p x p path, run as the .C
     driver runs it -- one bridge_reg_stable call, W burn-in and K recorded sweeps; with p <= 32
     every block of sweeps is one single-workgroup launch.  `value` is K / the
-    call's post-burn runtime.  The CPU baseline is the oracle's reference-literal chain
-    (gibbs.bridge_regression_stable, method "chol": numpy/LAPACK p x p Cholesky + the C
-    samplers, one BLAS thread) over a bounded number of sweeps."""
+    call's post-burn runtime.  The CPU baseline is the compiled reference-literal chain
+    (oracle/bb_cpu_chain.c: p x p dpotrf + dtrsm on scipy's OpenBLAS + the C samplers, one
+    thread) over a bounded number of sweeps."""
     import torch  # noqa: F401  (device init on the same footing as the other workloads)
 
     import bayesbridge_amd as bb
@@ -718,10 +737,15 @@ def small_chain(args, n, p, alpha):
                "sample": f"{ns} sweeps of the compiled C reference-literal chain "
                          f"(oracle/bb_cpu_chain.c: p x p dpotrf + dtrsm, scipy OpenBLAS, "
                          f"1 thread) at n={n}, p={p}"}
-    # the p x p path's algorithmic flops per sweep (path p <= n):
-    # p^3/3 + 3 p^2 + 2 n p; the fused chain is latency-bound, far from any roofline
-    flops = p ** 3 / 3.0 + 3.0 * p * p + 2.0 * n * p
-    achieved = flops * value / 1e12
+    # The fused chain is one workgroup running dependent draws: no flop or byte roofline
+    # bounds it (p^3/3 + 3p^2 + 2np = 8e3 flop per sweep at C1).  Its bound is latency: the
+    # per-sweep chain of S_alpha/rss -> tau, sig2 -> lambda (p rejection draws in parallel,
+    # the slowest decides) -> the p x p Cholesky and solves, measured in-kernel by
+    # tools/small_phase_bench (profiles/r03_c1_small_phases.txt, s_memrealtime per phase).
+    lat = small_phase_model(n, p)
+    roof = {"bound": "latency", "kernel": "k_small_chain (whole sweeps in one workgroup)",
+            "achieved": 1e6 / value, "unit": "us per sweep", "peak": None, "frac": None,
+            "traffic": None, "latency_model": lat}
     rec = {
         "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
         "value": value, "unit": "sweeps/s", "n_gpus": 1, "steps": args.steps,
@@ -732,10 +756,7 @@ def small_chain(args, n, p, alpha):
                    "alpha": alpha, "beta_step": "p x p Cholesky (reference-literal)",
                    "parallelism": "replicas only (p <= n)",
                    "kernel": "k_small_chain (whole sweeps in one workgroup)"},
-        "roofline": {"bound": "mfma", "kernel": "k_small_chain", "achieved": achieved,
-                     "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "note": "latency-bound: one workgroup, a chain of dependent draws"},
+        "roofline": roof,
         "cpu_baseline": cpu, "call_wall_s": wall,
     }
     print(json.dumps(rec), flush=True)

@@ -160,6 +160,29 @@ def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
     assert rel_err(x, ref) < 1e-10 * np.linalg.cond(A) ** 0.5
 
 
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("m", [40, 64, 128, 200, 1000, 2048, 5000])
+def test_chol_chain_versions_match_numpy(gpu_lib, m, version):
+    """Both chain variants of k_chol_persistent (2: pipelined, the default; 1: round 2), from
+    one block (m <= 64) to 79 block steps, on an ill-conditioned SPD system."""
+    bb = gpu_lib
+    rng = np.random.default_rng(m + 7)
+    B = rng.standard_normal((m, m)) * np.exp(rng.uniform(-6, 6, m))
+    A = B @ B.T + 1e-3 * np.eye(m)
+    b = rng.standard_normal((m, 1))
+    bb.set_chol_version(version)
+    try:
+        x = bb.chol_solve(A, b)
+    finally:
+        bb.set_chol_version(2)
+    ref = np.linalg.solve(A, b)
+    cond = np.linalg.cond(A)
+    # backward error of the solve against A (normwise), and the forward error
+    res = np.linalg.norm(A @ x - b) / (np.linalg.norm(A, 2) * np.linalg.norm(x))
+    assert res < 1e-13, res
+    assert rel_err(x, ref) < 1e-12 * cond, (rel_err(x, ref), cond)
+
+
 def test_chol_solve_detects_non_spd(gpu_lib):
     bb = gpu_lib
     A = np.array([[1.0, 2.0], [2.0, 1.0]])

@@ -1,12 +1,19 @@
 """Parity at the chain's steady state.
 
 The full-size teacher-forced tests elsewhere start near the truth (beta_true + noise).  Here
-the GPU chain first runs FREE for 150 sweeps from the reference start (beta0 = 0,
+the GPU chain first runs FREE for thousands of sweeps from the reference start (beta0 = 0,
 BridgeWrapper.cpp:242-244 with p > n), so lambda, tau, sig2 and the prior variances
 D = tau^2 / lambda are wherever the sampler itself takes them; from that state three sweeps
 are teacher-forced against the oracle (the Woodbury restatement of BridgeRegression.cpp:
 552-575 over numpy / scipy.sparse, the C tilted-stable sampler), each from the oracle's
 previous output.
+
+Two regimes (oracle chains at C2, /tmp-free measurement recorded in DESIGN.md s6): from
+beta0 = 0 the chain first sits near beta = 0 with tau tiny and sig2 ~ var(y), where
+M = I + X D X' / sig2 is the identity to 1e-8 (C3 after 120 sweeps: cond(M) - 1 = 2e-8);
+after ~700 sweeps (C2) it moves to the fitted regime (sig2 ~ 0.01, D over 9 decades,
+cond(M) ~ 1e5).  The free-run lengths below are chosen to end in the second regime where
+the chain gets there within a few seconds of GPU time; the regime reached is printed.
 
 Bars: beta 1e-9 relative L2, lambda / tau / sig2 1e-11 relative with no accept/reject
 decision flips.  The state reached is printed (tau, sig2, the span of D and the condition
@@ -64,8 +71,8 @@ def m_condition(X, lam, tau, sig2):
     return float(ev[-1] / ev[0]), span
 
 
-@pytest.mark.parametrize("name", ["c2", "c3", "c5"])
-def test_steady_state_teacher_forced(gpu_lib, name, capsys):
+@pytest.mark.parametrize("name,free", [("c2", 2000), ("c3", 2500), ("c5", 1500)])
+def test_steady_state_teacher_forced(gpu_lib, name, free, capsys):
     bb = gpu_lib
     X, y, alpha = workload(name)
     n, p = X.shape
@@ -73,7 +80,7 @@ def test_steady_state_teacher_forced(gpu_lib, name, capsys):
                                   trace_capacity=1), X, y)
     assert e.method() in (2, 5)
     e.init_state()
-    e.run(1, 150, first_slot=-1)  # free-running from beta0 = 0
+    e.run(1, free, first_slot=-1)  # free-running from beta0 = 0
     e.sync()
     s = e.state()
     beta, tau, sig2 = s["beta"], s["tau"], s["sig2"]
@@ -87,7 +94,7 @@ def test_steady_state_teacher_forced(gpu_lib, name, capsys):
         if t == 1001:
             cond, span = m_condition(X, lam, tau, sig2)
             with capsys.disabled():
-                print(f"\n[{name} steady state after 150 free sweeps] tau={tau:.4g} "
+                print(f"\n[{name} state after {free} free sweeps] tau={tau:.4g} "
                       f"sig2={sig2:.4g} |beta|>1e-3: {int(np.sum(np.abs(beta) > 1e-3))} "
                       f"D span 10^{span:.1f} cond(M)={cond:.3g}")
         assert flips(g["lambda"], lam) == 0, t

@@ -69,10 +69,10 @@ def test_engine_basis_ill_conditioned(gpu_lib):
     assert np.allclose(np.abs(tV @ W), np.eye(p), atol=1e-6)
 
 
-# (n, p, betaburn).  Non-orthogonal designs with alpha known and p <= 32 run the fused
-# single-launch chain (bb_tri.hip k_tri_chain); "betaburn" (p = 33), "unknown_alpha" and
-# "ortho" the general per-sweep path.  "x_in_hbm": n p 8 bytes above the fused kernel's LDS
-# staging limit, so X is read from HBM.
+# (n, p, betaburn).  Designs with alpha known and p <= 32 run the fused single-launch chain
+# (bb_tri.hip k_tri_chain; "ortho" its orthogonal-design coordinate pass, round 3);
+# "betaburn" (p = 33), "unknown_alpha" and ("ortho", 800, 600) the general per-sweep path.
+# "x_in_hbm": n p 8 bytes above the fused kernel's LDS staging limit, so X is read from HBM.
 SHAPES = {"c1": (100, 20, 0), "unknown_alpha": (100, 20, 0), "betaburn": (80, 33, 2),
           "betaburn_fused": (80, 24, 2), "x_in_hbm": (400, 32, 0),
           "known_tau_sig2": (100, 20, 0), "ortho": (100, 20, 0)}

@@ -11,8 +11,10 @@ Designs (the reference's data(diabetes), man/diabetes.Rd:22: "x has been standar
 have unit L2 norm in each column and zero mean"):
   DB   = sklearn's load_diabetes(scaled=True) -- the same Efron et al. data, columns centred
          and scaled to unit L2 norm -- and y = the raw target, centred (:331-341);
-  DBI  = x2: the 10 columns of DB, their 45 pairwise products and the 9 squares (sex is
-         binary), each centred and scaled to unit L2 norm (lars' quadratic model);
+  DBI  = x2: the 10 columns of DB, the 9 squares (sex is binary) and the 45 pairwise
+         products, in lars' column order (main effects, squares, interactions), each
+         centred and scaled to unit L2 norm (lars' quadratic model).  The order matters only
+         for the orthogonalised runs (Q of the QR depends on it);
   orth = Q of the QR of the centred design, qr.Q(qr(X)) (unit columns, :485-488), run with
          ortho = TRUE.
 The Boston Housing designs need mlbench's data, absent offline, so only DB / DBI are
@@ -21,7 +23,8 @@ compared with the published ESS.
 Beside each GPU row: the compiled CPU chain (oracle/bb_cpu_chain.c, reference-literal
 p x p dpotrf / the ortho draw, scipy OpenBLAS, 1 thread) on the same design, one simulation
 of CPU_SAMPLES samples, for sweeps/s side by side.  Output: one JSON document on stdout.
-Usage: python tools/published_ess.py [> profiles/r03_published_ess.json]
+Usage: python tools/published_ess.py OUT.json  (the library's .C drivers print to stdout,
+so the document is written to the file named on the command line)
 """
 import itertools
 import json
@@ -61,8 +64,8 @@ def designs():
     X = unit_l2(d.data)
     y = d.target - d.target.mean()
     cols = [X[:, i] for i in range(10)]
-    cols += [X[:, i] * X[:, j] for i, j in itertools.combinations(range(10), 2)]
     cols += [X[:, i] ** 2 for i in range(10) if i != 1]  # sex is binary: no square
+    cols += [X[:, i] * X[:, j] for i, j in itertools.combinations(range(10), 2)]
     X2 = unit_l2(np.column_stack(cols))
     assert X2.shape == (442, 64)
     return {"DB": (X, y), "DBI": (X2, y)}
@@ -97,9 +100,12 @@ def main():
     nsim = int(os.environ.get("NSIM", "10"))
     cpu_samples = int(os.environ.get("CPU_SAMPLES", "20000"))
     only_m = os.environ.get("METHODS", "stable,tri,stable_orth,tri_orth").split(",")
+    only_d = os.environ.get("DESIGNS", "DB,DBI").split(",")
     bb.set_verbose(0)
     rows = []
     for name, (X0, y) in designs().items():
+        if name not in only_d:
+            continue
         for method in only_m:
             X = qr_q(X0) if method.endswith("_orth") else X0
             ess, rts = [], []
@@ -129,12 +135,14 @@ def main():
                 rec["cpu_compiled_1core_sweeps_per_s"] = cpu
             rows.append(rec)
             print(json.dumps(rec), file=sys.stderr, flush=True)
-    print(json.dumps({"protocol": f"{nsim} simulations x {nsamp} samples after {burn} burn-in, "
+    out = sys.argv[1] if len(sys.argv) > 1 else "/dev/stdout"
+    with open(out, "w") as fh:
+        fh.write(json.dumps({"protocol": f"{nsim} simulations x {nsamp} samples after {burn} burn-in, "
                                   "alpha = 0.5, sig2 Jeffreys, nu ~ Ga(2, 2) "
                                   "(Notes/bbnotes.tex:893-965)",
                       "ess": "coda effectiveSize per beta_j, median over simulations; "
                              "min / median / max / sd over coefficients",
-                      "results": rows}, indent=1))
+                      "results": rows}, indent=1) + "\n")
 
 
 if __name__ == "__main__":
