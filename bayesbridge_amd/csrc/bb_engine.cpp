@@ -287,6 +287,7 @@ struct bb_engine {
     DevScalars *sc = nullptr;
     uint32_t *err = nullptr;
     double *xb_part = nullptr, *red1 = nullptr;
+    double *red3 = nullptr;  // sharded alpha MH: [S(alpha_new), S(alpha_old)]
     int nparts = 0, nbS = 0;
     bool xb_stale = false;  // a fused run left the X beta partials behind beta
     // woodbury
@@ -475,7 +476,7 @@ struct bb_engine {
                               slot_ptr(tr_beta, slot, p_loc), slot_ptr(tr_u, slot, p_loc), trl,
                               slot_ptr(tr_shape, slot, p_loc), err);
         } else {
-            launch_lambda(stream, beta, p_loc, p_pad, 0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
+            launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream, t, LAMBDA_ONLY,
                           group, lam, nullptr, nullptr, trl, err);
         }
     }
@@ -524,22 +525,39 @@ struct bb_engine {
             launch_beta_chol(stream, W2, m, sc, p, beta, trb);
         } else if (method == 3) {
             mark(PH_BETA);
-            launch_beta_ortho(stream, gdiag, cvec, lam, sc, p, cfg.seed, cfg.stream, t, beta, trb);
+            launch_beta_ortho(stream, gdiag, cvec, lam, sc, p_loc, (uint64_t)cfg.j0, cfg.seed,
+                              cfg.stream, t, beta, trb);
         }
         if (!xb_fused) {
             mark(PH_XB);
             xbeta();
         }
         if (!hy.know_alpha) {
+            mark(PH_ALPHA);
+            if (cfg.world > 1) {
+                // a column shard: this shard's two sums, exchanged (red3) before phase_d
+                launch_alpha_sums(stream, beta, p_loc, sc, cfg.seed, cfg.stream, t, red3);
+                return;
+            }
             // BridgeWrapper.cpp:272 (burn-in: alpha_a, alpha_b), :294 (MCMC: alpha_b, alpha_b
             // -- reference quirk kept), ortho :499/:519 (alpha_a, alpha_b).
-            mark(PH_ALPHA);
-            // triangle driver: (alpha_a, alpha_b) in both loops (BridgeWrapper.cpp:146,173)
-            const double pr_a =
-                ((method <= 2 || method == 5) && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
-            launch_alpha_mh(stream, beta, p, sc, pr_a, hy.alpha_b, cfg.seed, cfg.stream, t,
-                            slot_ptr(tr_alpha, slot, 1));
+            launch_alpha_mh(stream, beta, p, sc, alpha_prior_a(mcmc_phase), hy.alpha_b, cfg.seed,
+                            cfg.stream, t, slot_ptr(tr_alpha, slot, 1));
         }
+        mark(PH_END);
+    }
+
+    // triangle driver: (alpha_a, alpha_b) in both loops (BridgeWrapper.cpp:146,173)
+    double alpha_prior_a(int mcmc_phase) const {
+        return ((method <= 2 || method == 5) && mcmc_phase) ? hy.alpha_b : hy.alpha_a;
+    }
+    // a sharded chain with alpha unknown exchanges the MH sums between phase_c and phase_d
+    bool alpha_exchange() const { return !hy.know_alpha && cfg.world > 1; }
+
+    void phase_d(uint64_t t, int slot, int mcmc_phase) {
+        if (!alpha_exchange()) return;
+        launch_alpha_decide(stream, red3, p, sc, alpha_prior_a(mcmc_phase), hy.alpha_b, cfg.seed,
+                            cfg.stream, t, slot_ptr(tr_alpha, slot, 1));
         mark(PH_END);
     }
 
@@ -580,6 +598,10 @@ struct bb_engine {
         phase_b(t, slot);
         if (woodbury()) allreduce(red2, red2_count());
         phase_c(t, slot, mcmc_phase);
+        if (alpha_exchange()) {
+            allreduce(red3, 2);
+            phase_d(t, slot, mcmc_phase);
+        }
     }
 
     uint32_t read_err() {
@@ -758,10 +780,11 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     else if (c.ortho) e->method = 3;
     else if (c.method == 1 || (c.method == 0 && c.p <= c.n)) e->method = 1;
     else e->method = 2;
-    if (c.world > 1 && !e->woodbury())
-        throw HipError("column sharding (world > 1) is implemented for the Woodbury path only");
-    if (c.world > 1 && !e->hy.know_alpha)
-        throw HipError("unknown alpha with world > 1 is not supported");
+    // column shards: the p > n Woodbury draws (dense, sparse) and the orthogonal design
+    // (per-coefficient draws, p > n); alpha known or unknown (the MH sums are exchanged)
+    if (c.world > 1 && !e->woodbury() && !(e->method == 3 && c.p > c.n))
+        throw HipError("column sharding (world > 1) is implemented for the p > n paths only "
+                       "(Woodbury, sparse Woodbury, orthogonal design)");
     if (e->method == 4 && (c.p > c.n || c.p > kTriMaxP))
         throw HipError("triangle sampler needs p <= n and p <= 2048");
     if (e->method == 1 && c.p > 16384) throw HipError("p x p Cholesky path limited to p <= 16384");
@@ -795,6 +818,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         o);
     e->nbS = pre_blocks_s(c.p_local);
     e->red1 = dalloc<double>((size_t)e->nbS + n_pad, o);
+    e->red3 = dalloc<double>(2, o);
     e->group = stable_group_for(c.p_local);
     e->tr_beta = dalloc<double>((size_t)c.p_local * e->cap, o);
     e->tr_lam = dalloc<double>((size_t)c.p_local * e->cap, o);
@@ -1546,6 +1570,13 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
             for (auto *m : g->members) {
                 g->on(m);
                 m->phase_c(t, slot, mcmc_phase);
+            }
+            if (g->members[0]->alpha_exchange()) {
+                g->reduce(&bb_engine::red3, 2);
+                for (auto *m : g->members) {
+                    g->on(m);
+                    m->phase_d(t, slot, mcmc_phase);
+                }
             }
         }
         HIPCHECK(hipGetLastError());
@@ -2466,12 +2497,13 @@ int ring_capacity(int m, int p_local, int ntr) {
     return (int)std::min<size_t>(cap, (size_t)(m < 1 ? 1 : m));
 }
 
-// Devices for a column-sharded chain: 1 unless p > n on the Woodbury path with alpha known
-// and more than one device visible; at least 4096 columns per device.
+// Devices for a column-sharded chain: 1 unless p > n (the Woodbury path, or the orthogonal
+// design; alpha known or unknown) and sharding was enabled (bb_set_device_count); at least
+// 4096 columns per device.
 int chain_devices(const bb_config &c) {
     const int nvis = bb_device_count();
     int k = g_max_devices > 0 ? std::min(g_max_devices, nvis) : nvis;
-    if (c.p <= c.n || c.ortho || c.true_alpha <= 0 || (c.method != 0 && c.method != 2)) return 1;
+    if (c.p <= c.n || (c.method != 0 && c.method != 2 && c.method != 3)) return 1;
     k = std::min(k, std::max(1, c.p / 4096));
     return std::max(1, k);
 }
@@ -2713,7 +2745,7 @@ extern "C" {
 void bb_set_device_count(int count) { g_max_devices = count < 0 ? 0 : count; }
 
 int bb_set_chol_version(int version) {
-    if (version != 1 && version != 2) return -1;
+    if (version < 1 || version > 3) return -1;
     g_chol_version = version;
     return 0;
 }

@@ -158,12 +158,18 @@ void launch_beta_chol(hipStream_t s, const double *W2, int p_pad, const DevScala
 
 // Orthogonal design: beta_i ~ N(c_i/u_i, sig2/u_i), u_i = G_ii + lambda_i sig2/tau^2.
 void launch_beta_ortho(hipStream_t s, const double *gdiag, const double *c, const double *lam,
-                       const DevScalars *sc, int p, uint64_t k0, uint64_t k1, uint64_t t,
-                       double *beta, double *beta_trace);
+                       const DevScalars *sc, int p, uint64_t j0, uint64_t k0, uint64_t k1,
+                       uint64_t t, double *beta, double *beta_trace);
 
 // alpha | beta, tau random-walk MH (world == 1).
 void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, double pr_a,
                      double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr);
+// the alpha MH step of a column-sharded chain: per-shard sums, then (after the exchange of
+// the two sums) the decision with the global p
+void launch_alpha_sums(hipStream_t s, const double *beta, int p_loc, const DevScalars *sc,
+                       uint64_t k0, uint64_t k1, uint64_t t, double *sums);
+void launch_alpha_decide(hipStream_t s, const double *sums, int p, DevScalars *sc, double pr_a,
+                         double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr);
 
 // Triangle-mixture update (bb_tri.hip): omega, u and the rtnorm_gibbs beta passes of one
 // sweep of bridge.reg.tri, given sc->tau, sig2, alpha; ortho != 0: the orthogonal-design

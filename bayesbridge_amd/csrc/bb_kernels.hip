@@ -1450,9 +1450,17 @@ __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[1
 //     K steps of D_{k+1} remain: the next elimination starts ~0.5 us after the last pivot.
 // Same flags, tiles and owners as v1; U_{k,k+1} is published by the last of its storing waves.
 // ---------------------------------------------------------------------------
+// pivot-row stride: 128 + 2 doubles, so the 16 rows an MFMA A-operand read touches (rows
+// 16 by + (lane & 15), one column) fall in distinct LDS banks (a 128-double stride put them
+// all in one bank: 16-way conflicts on every U operand); 16-byte aligned for the double2
+// row stores
+constexpr int kRowsLd = 130;
+
 __device__ __forceinline__ void lds_wait_ge(const volatile __attribute__((address_space(3))) int *p,
                                             int v, uint32_t *err) {
     for (unsigned spins = 0; *p < v;) {
+        __builtin_amdgcn_s_sleep(1);  // a waiting wave leaves the LDS and issue slots to the
+                                      // producers it waits for
         if (++spins > (1u << 22)) {  // bounded: a broken hand-off flags, never hangs
             if ((threadIdx.x & 63) == 0 && err) atomicOr(err, 16u);
             break;
@@ -1471,7 +1479,7 @@ __device__ __forceinline__ int lds_bump(int *p) {
 }
 
 template <int W>
-__device__ __forceinline__ void elim_produce2(double (&a)[8][2], double (*ROWS)[128], double *piv,
+__device__ __forceinline__ void elim_produce2(double (&a)[8][2], double (*ROWS)[kRowsLd], double *piv,
                                              volatile __attribute__((address_space(3))) int *vc) {
     const int lane = threadIdx.x & 63, c0 = lane * 2;
 #pragma unroll
@@ -1494,7 +1502,7 @@ __device__ __forceinline__ void elim_produce2(double (&a)[8][2], double (*ROWS)[
 }
 
 // U block (by, bx) of U = W S, W = diag(sqrt p) ROWS_I (lower triangular: K steps < 4 by + 4)
-__device__ __forceinline__ v4d u_block2(const double (*ROWS)[128], const double (*S)[65],
+__device__ __forceinline__ v4d u_block2(const double (*ROWS)[kRowsLd], const double (*S)[65],
                                         const double *piv, int by, int bx) {
     const int lane = threadIdx.x & 63, ry = by * 16 + (lane & 15), cx = bx * 16 + (lane & 15);
     v4d a0 = {0.0, 0.0, 0.0, 0.0}, a1 = a0;
@@ -1532,12 +1540,17 @@ __device__ __forceinline__ void dprime_acc2(const double (*T)[65], int by, int b
     }
 }
 
+// V = 2: phase a on waves 0-5, U row block 3 on waves 4-7; V = 3: phase a on waves
+// {0, 1, 4, 5} (SIMDs 0, 1: the last two producers, waves 6 and 7, keep SIMDs 2, 3 to
+// themselves), U row block 3 on waves 0-3, and no wave waits for its global stores to drain
+// before the work that follows them.
+template <int V>
 __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                               const CholFlags &F, uint32_t *err, unsigned long long *trace,
                               double *L) {
     double(*T)[65] = (double(*)[65])L;                 // U_{k,k+1} rows
     double(*S)[65] = (double(*)[65])(L + 4160);        // hand-off A_{k,k+1}
-    double(*ROWS)[128] = (double(*)[128])(L + 8320);   // published pivot rows [A | I] / p
+    double(*ROWS)[kRowsLd] = (double(*)[kRowsLd])(L + 8320);  // pivot rows [A | I] / p
     double(*Dn)[65] = (double(*)[65])(L + 8320);       // next diagonal block (aliases ROWS)
     __shared__ double piv[64];
     __shared__ int cnt, s_ready, ua_cnt, w_drain, u_drain;
@@ -1555,13 +1568,22 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
         bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
         by = blk - bx * (bx + 1) / 2;
     };
-    const int nd = wid < 4 ? 2 : wid < 6 ? 1 : 0;
-    int dby[2] = {0, 0}, dbx[2] = {0, 0};
-    if (wid < 4) {
-        bxy(wid, dby[0], dbx[0]);
-        bxy(wid + 4, dby[1], dbx[1]);
-    } else if (wid < 6) {
-        bxy(wid + 4, dby[0], dbx[0]);
+    // V = 3: wave q in {0, 1, 4, 5} (qi = 0..3) holds blocks qi, qi + 4 and qi + 8 (< 10)
+    const bool pa = V == 2 ? wid < 6 : (wid & 2) == 0;  // a phase-a wave
+    const int qi = (wid & 1) | ((wid >> 1) & 2);
+    int nd = 0;
+    int dby[3] = {0, 0, 0}, dbx[3] = {0, 0, 0};
+    if (V == 2) {
+        nd = wid < 4 ? 2 : wid < 6 ? 1 : 0;
+        if (wid < 4) {
+            bxy(wid, dby[0], dbx[0]);
+            bxy(wid + 4, dby[1], dbx[1]);
+        } else if (wid < 6) {
+            bxy(wid + 4, dby[0], dbx[0]);
+        }
+    } else if (pa) {
+        nd = qi < 2 ? 3 : 2;
+        for (int d = 0; d < nd; ++d) bxy(qi + 4 * d, dby[d], dbx[d]);
     }
 #define CHAIN2_TS(slot)                                                                 \
     do {                                                                                \
@@ -1635,10 +1657,13 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                     st_sc1(&Wk[(size_t)(c0 + q - 64) * kNB + r0 + i], a[i][q] * r);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lds_bump(&w_drain) == 7 && lane == 0)
-            __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k + 1 == nblk) break;
+        if (k + 1 == nblk) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lds_bump(&w_drain) == 7 && lane == 0)
+                __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        // (the W stores drain behind this wave's U work; W_k is released before the barrier)
         // ---- the hand-off tile S = A_{k,k+1} (updated by its owner through step k-1) ----
         if (wid < 4) {
             const unsigned int *f1 = &F.R[2 * k + 1];
@@ -1667,13 +1692,18 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
             asm volatile("" ::: "memory");
             lds_bump(&s_ready);
         }
-        v4d dacc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-        double qv[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-        if (wid < 6) {
+        v4d dacc[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+        double qv[3][4] = {};
+        if (pa) {
             // ---- phase a: U rows 0..47 and the partial next diagonal block ----
             lds_wait_ge(vc, 48, err);
             lds_wait_ge(vlds(&s_ready), 4, err);
-            if (wid < 4) {
+            if (V == 3) {
+                for (int by = 2; by >= 0; --by) {
+                    const v4d u = u_block2(ROWS, S, piv, by, qi);
+                    u_put2(T, A, lda, k, by, qi, u);
+                }
+            } else if (wid < 4) {
                 const v4d u2 = u_block2(ROWS, S, piv, 2, wid);
                 u_put2(T, A, lda, k, 2, wid, u2);
                 const v4d u0 = u_block2(ROWS, S, piv, 0, wid);
@@ -1685,9 +1715,13 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                 const v4d ub = u_block2(ROWS, S, piv, 1, b0 + 1);
                 u_put2(T, A, lda, k, 1, b0 + 1, ub);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_bump(&ua_cnt);
-            lds_bump(&u_drain);
+            lds_bump(&ua_cnt);  // this wave's U rows are in T (LDS, in order)
+            if (V == 2) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // W rows and U blocks
+                lds_bump(&u_drain);
+                if (lds_bump(&w_drain) == 7 && lane == 0)
+                    __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             // the (k+1, k+1) hand-off: this wave's D blocks of A_{k+1,k+1}
             const unsigned int *f2 = &F.R[2 * (k + 1)];
             for (unsigned spins = 0;;) {
@@ -1707,15 +1741,22 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                     const int y = dby[d] * 16 + (lane >> 4) + 4 * r, x = dbx[d] * 16 + (lane & 15);
                     qv[d][r] = ld_sc1(&t2[(size_t)y + (size_t)x * lda]);
                 }
-            lds_wait_ge(vlds(&ua_cnt), 6, err);
+            lds_wait_ge(vlds(&ua_cnt), V == 2 ? 6 : 4, err);
             for (int d = 0; d < nd; ++d) dprime_acc2(T, dby[d], dbx[d], 0, 12, dacc[d]);
         }
-        if (wid >= 4) {
+        const bool pb = V == 2 ? wid >= 4 : wid < 4;  // a U-row-block-3 wave
+        if (pb) {
             // ---- phase b: U row block 3, once every pivot is published ----
             lds_wait_ge(vc, 64, err);
             lds_wait_ge(vlds(&s_ready), 4, err);
-            const v4d u3 = u_block2(ROWS, S, piv, 3, wid - 4);
-            u_put2(T, A, lda, k, 3, wid - 4, u3);
+            const int bx = V == 2 ? wid - 4 : wid;
+            const v4d u3 = u_block2(ROWS, S, piv, 3, bx);
+            u_put2(T, A, lda, k, 3, bx, u3);
+            if (V == 2 && wid >= 6) {  // waves 6-7 have not released their W rows yet
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lds_bump(&w_drain) == 7 && lane == 0)
+                    __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();  // U complete in T; every read of ROWS and S done
         if (wid == 0) CHAIN2_TS(5);
@@ -1729,11 +1770,25 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                 if (by != bx) Dn[x][y] = 0.0;  // the mirrored lower block
             }
         }
-        if (wid >= 4) {
+        if (V == 2) {
+            if (wid >= 4) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lds_bump(&u_drain) == 9 && lane == 0)
+                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            // every wave's W rows, and the U blocks of the phase-a and phase-b waves, have
+            // been issued; each wave drains its own stores and counts in, the last one
+            // releases W_k (8 waves) and U_{k,k+1} (its 8 storing passes)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lds_bump(&u_drain) == 9 && lane == 0)
-                __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (lds_bump(&w_drain) == 7 && lane == 0)
+                __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int ub = (pa ? 1 : 0) + (pb ? 1 : 0);
+            for (int b = 0; b < ub; ++b)
+                if (lds_bump(&u_drain) == 7 && lane == 0)
+                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         }
         if (wid == 0) CHAIN2_TS(7);
     }
@@ -1749,7 +1804,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
     // During the v1 chain's elimination S and Q together hold the published pivot rows; the
     // v2 chain (chol_chain_v2) lays out U rows, S and the pivot rows side by side.
-    __shared__ __attribute__((aligned(16))) double Lraw[V == 2 ? 16512 : 3 * 64 * 65];
+    __shared__ __attribute__((aligned(16))) double Lraw[V >= 2 ? 8320 + 64 * 130 : 3 * 64 * 65];
     double(*Lb)[64][65] = (double(*)[64][65])Lraw;
     __shared__ double piv[64];
     __shared__ int cnt;
@@ -1761,8 +1816,8 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     v4d acc[2];
     if (blockIdx.x == 0) {
         // ------------------------------ the chain ------------------------------
-        if constexpr (V == 2) {
-            chol_chain_v2(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
+        if constexpr (V >= 2) {
+            chol_chain_v2<V>(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
             return;
         }
         const int lane = tid & 63, wid = tid >> 6;
@@ -1971,6 +2026,9 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             const int k = merge ? i - 1 : i - 2;
             OWN_TS(0);
             flag_acquire2(&F.W[k], &F.H[k], F.ep, err);
+            // merge also reads the chain's U_{k,i} (i = k + 1): the v2 chain publishes W_k
+            // as soon as the elimination ends, before U_{k,k+1} (v1 released both together)
+            if (merge) flag_acquire2(&F.P[k * F.ncb + i], nullptr, F.ep, err);
             OWN_TS(1);
             const double *Wk = Wd + (size_t)k * kNB * kNB;
             double vw[8], va[8], vu[8];
@@ -2123,8 +2181,10 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
     const int grid = std::min(device_cus(), 1 + ntiles);
     if (g_chol_version == 1)
         k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
-    else
+    else if (g_chol_version == 2)
         k_chol_persistent<2><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+    else
+        k_chol_persistent<3><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
 }
 
 
@@ -2480,23 +2540,24 @@ void launch_beta_chol(hipStream_t s, const double *W2, int p_pad, const DevScala
 
 __global__ __launch_bounds__(256) void k_beta_ortho(const double *gdiag, const double *cvec,
                                                     const double *lam, const DevScalars *sc,
-                                                    int p, Key key, uint64_t t, double *beta,
-                                                    double *trace) {
+                                                    int p, uint64_t j0, Key key, uint64_t t,
+                                                    double *beta, double *trace) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= p) return;
     const double sig2 = sc->sig2, tau = sc->tau;
     const double uu = gdiag[i] + lam[i] * sig2 / (tau * tau);
     const double sd = sqrt(sig2 / uu);
     const double m = cvec[i] / uu;
-    const double b = m + sd * normal_at(key, t, KIND_BETA_Z, (uint64_t)i);
+    // z_j on the GLOBAL column index (j0 = a column shard's first column)
+    const double b = m + sd * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
     beta[i] = b;
     if (trace) trace[i] = b;
 }
 
 void launch_beta_ortho(hipStream_t s, const double *gdiag, const double *c, const double *lam,
-                       const DevScalars *sc, int p, uint64_t k0, uint64_t k1, uint64_t t,
-                       double *beta, double *beta_trace) {
-    k_beta_ortho<<<(p + 255) / 256, 256, 0, s>>>(gdiag, c, lam, sc, p, Key{k0, k1}, t, beta,
+                       const DevScalars *sc, int p, uint64_t j0, uint64_t k0, uint64_t k1,
+                       uint64_t t, double *beta, double *beta_trace) {
+    k_beta_ortho<<<(p + 255) / 256, 256, 0, s>>>(gdiag, c, lam, sc, p, j0, Key{k0, k1}, t, beta,
                                                  beta_trace);
 }
 
@@ -2542,6 +2603,75 @@ __global__ __launch_bounds__(1024) void k_alpha_mh(const double *beta, int p, De
 void launch_alpha_mh(hipStream_t s, const double *beta, int p, DevScalars *sc, double pr_a,
                      double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr) {
     k_alpha_mh<<<1, 1024, 0, s>>>(beta, p, sc, pr_a, pr_b, Key{k0, k1}, t, alpha_tr);
+}
+
+// The same MH step for a column-sharded chain, split around an exchange: k_alpha_sums writes
+// this shard's [S(alpha_new), S(alpha_old)], S(a) = sum_j exp(a log|beta_j / tau|) (the
+// proposal comes from the shared counter, so every shard proposes the same alpha_new); the
+// caller sums the pairs over shards; k_alpha_decide evaluates llh_alpha_marg with the
+// GLOBAL p and accepts or rejects (BridgeRegression.cpp:469-503).  One shard gives the bits
+// of k_alpha_mh (same loop, tree and expressions).
+__device__ __forceinline__ double alpha_proposal(double a_old, Key key, uint64_t t, double &u1) {
+    const U4 u = uniforms(key, t, KIND_ALPHA, 0, 0, 0);
+    u1 = u.r[1];
+    const double ep = 0.1;
+    const double l_new = fmax(0.0, a_old - ep);
+    const double r_new = fmin(1.0, a_old + ep);
+    return l_new + (r_new - l_new) * u.r[0];
+}
+
+__global__ __launch_bounds__(1024) void k_alpha_sums(const double *beta, int p_loc,
+                                                     const DevScalars *sc, Key key, uint64_t t,
+                                                     double *sums) {
+    __shared__ double sh[16];
+    const double tau = sc->tau, a_old = sc->alpha;
+    double u1;
+    const double a_new = alpha_proposal(a_old, key, t, u1);
+    double sn = 0.0, so = 0.0;
+    for (int i = threadIdx.x; i < p_loc; i += 1024) {
+        const double si = log(fabs(beta[i] / tau));
+        sn += exp(a_new * si);
+        so += exp(a_old * si);
+    }
+    const double Sn = block_sum<1024>(sn, sh);
+    const double So = block_sum<1024>(so, sh);
+    if (threadIdx.x == 0) {
+        sums[0] = Sn;
+        sums[1] = So;
+    }
+}
+
+__global__ void k_alpha_decide(const double *sums, int p, DevScalars *sc, double pr_a,
+                               double pr_b, Key key, uint64_t t, double *alpha_tr) {
+    if (threadIdx.x != 0) return;
+    const double a_old = sc->alpha, ep = 0.1;
+    double u1;
+    const double a_new = alpha_proposal(a_old, key, t, u1);
+    const double d_new = fmin(1.0, a_old + ep) - fmax(0.0, a_old - ep);
+    const double pp = (double)p;
+    const double llh_new = pp * log(a_new) - pp * lgamma(1.0 / a_new) - sums[0];
+    const double llh_old = pp * log(a_old) - pp * lgamma(1.0 / a_old) - sums[1];
+    const double lbc = lgamma(pr_a) + lgamma(pr_b) - lgamma(pr_a + pr_b);
+    const double ldb_new = (pr_a - 1.0) * log(a_new) + (pr_b - 1.0) * log(1.0 - a_new) - lbc;
+    const double ldb_old = (pr_a - 1.0) * log(a_old) + (pr_b - 1.0) * log(1.0 - a_old) - lbc;
+    const double l_old = fmax(0.0, a_new - ep);
+    const double r_old = fmin(1.0, a_new + ep);
+    const double d_old = r_old - l_old;
+    const double log_accept = llh_new - llh_old + ldb_new - ldb_old + log(d_old) - log(d_new);
+    double an = a_new;
+    if (u1 > exp(log_accept)) an = a_old;
+    sc->alpha = an;
+    if (alpha_tr) *alpha_tr = an;
+}
+
+void launch_alpha_sums(hipStream_t s, const double *beta, int p_loc, const DevScalars *sc,
+                       uint64_t k0, uint64_t k1, uint64_t t, double *sums) {
+    k_alpha_sums<<<1, 1024, 0, s>>>(beta, p_loc, sc, Key{k0, k1}, t, sums);
+}
+
+void launch_alpha_decide(hipStream_t s, const double *sums, int p, DevScalars *sc, double pr_a,
+                         double pr_b, uint64_t k0, uint64_t k1, uint64_t t, double *alpha_tr) {
+    k_alpha_decide<<<1, 64, 0, s>>>(sums, p, sc, pr_a, pr_b, Key{k0, k1}, t, alpha_tr);
 }
 
 __global__ void k_record_scalars(const DevScalars *sc, double *tau_tr, double *sig2_tr,

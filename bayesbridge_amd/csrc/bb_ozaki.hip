@@ -428,10 +428,14 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
 #pragma unroll
         for (int g = 0; g < 8; ++g) glds_one(kc, stage, g);
     };
-    v4i acc[8][8], accv[8];
+    // accv: D2's diagonal blocks 0..3 (DIAGQ waves) or 4..7 (the off-diagonal waves, which
+    // read the same slot fragments): 68 MFMAs per chunk on every wave instead of 64 / 72, so
+    // the pair's chunk step (one barrier per chunk) is 6 % rather than 12.5 % longer than an
+    // off-diagonal tile's and the pair lags its unit's tiles half as much
+    v4i acc[8][8], accv[4];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        accv[i] = (v4i){0, 0, 0, 0};
+        if (i < 4) accv[i] = (v4i){0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
     }
@@ -461,6 +465,7 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
                 if (!(dbg & 2)) fb_n[g] = frag(it + 1, g);
 #pragma unroll
                 for (int j = 3; j < 8; ++j) oz_mfma16(acc[g][j], fb_c[j], fa_c[g]);
+                if (g >= 4) oz_mfma16v(accv[g - 4], fa_c[g], fa_c[g]);
             } else {
                 // D1 (fb x fb) block (g, j <= g); D2 (fa x fa) block (g, j < g) in acc[j][g]
                 // and its diagonal block in accv[g]
@@ -471,7 +476,7 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
                 if (!(dbg & 2)) fa_n[g] = frag(it + 1, 8 + g);
 #pragma unroll
                 for (int j = 0; j < g; ++j) oz_mfma16(acc[j][g], fa_c[j], fa_c[g]);
-                oz_mfma16v(accv[g], fa_c[g], fa_c[g]);
+                if (g < 4) oz_mfma16v(accv[g], fa_c[g], fa_c[g]);
                 if (!(dbg & 2)) fb_n[g] = frag(it + 1, g);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -517,6 +522,8 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j) store(128 + 16 * i + rl, 16 * j + cl, acc[i][j]);
+#pragma unroll
+        for (int i = 4; i < 8; ++i) store(128 + 16 * i + rl, 128 + 16 * i + cl, accv[i - 4]);
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -524,7 +531,7 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
             for (int j = 0; j <= i; ++j) store(16 * i + rl, 16 * j + cl, acc[i][j]);
 #pragma unroll
             for (int j = 0; j < i; ++j) store(128 + 16 * i + rl, 128 + 16 * j + cl, acc[j][i]);
-            store(128 + 16 * i + rl, 128 + 16 * i + cl, accv[i]);
+            if (i < 4) store(128 + 16 * i + rl, 128 + 16 * i + cl, accv[i]);
         }
     }
 }
@@ -669,6 +676,7 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
                           kstride, c0, nch, wid, P0 + (size_t)tile * (kOzT * kOzT), C.m[mod],
                           C.inv_m[mod]);
     } else {
+        if (dbg & 16) continue;  // ablation: the diagonal pairs idle (traffic probe)
         const int pr = local - noff;
         const int I1 = 2 * pr, I2 = min(2 * pr + 1, nt - 1);  // odd nt: the last tile twice
         const int slot = wid & 1;
@@ -710,6 +718,7 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
         case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
         case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
         case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
+        case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
         default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
     }
 }

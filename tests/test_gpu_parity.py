@@ -160,7 +160,7 @@ def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
     assert rel_err(x, ref) < 1e-10 * np.linalg.cond(A) ** 0.5
 
 
-@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("version", [1, 2, 3])
 @pytest.mark.parametrize("m", [40, 64, 128, 200, 1000, 2048, 5000])
 def test_chol_chain_versions_match_numpy(gpu_lib, m, version):
     """Both chain variants of k_chol_persistent (2: pipelined, the default; 1: round 2), from
@@ -392,32 +392,39 @@ def test_teacher_forced_bench_workload(gpu_lib):
     e.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_shard_group_matches_single_engine(gpu_lib, world):
-    """The column-sharded sweep (two exchanges per sweep) on one GPU vs the unsharded
-    engine, teacher-forced from identical states for several sweeps."""
+@pytest.mark.parametrize("world,kind", [(2, "known"), (3, "known"), (2, "alpha"), (3, "alpha"),
+                                        (2, "ortho")])
+def test_shard_group_matches_single_engine(gpu_lib, world, kind):
+    """The column-sharded sweep (two exchanges per sweep; a third, of the two alpha MH sums,
+    when alpha is unknown) on one GPU vs the unsharded engine, teacher-forced from identical
+    states for several sweeps.  "ortho": the orthogonal-design draw for p > n, sharded."""
     bb = gpu_lib
     n, p = 200, 1100
     X, y, btrue = synthetic_problem(n, p, seed=21)
     seed, stream = SEED + 9, 0
-    single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, method=2), X, y)
+    ta = 0.0 if kind == "alpha" else 0.5
+    ortho = kind == "ortho"
+    single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, true_alpha=ta,
+                                       ortho=ortho), X, y)
     single.init_state()
+    assert single.method() == (3 if ortho else 2)
     per = (p + world - 1) // world
     shards = []
     for r in range(world):
         j0, j1 = r * per, min(p, (r + 1) * per)
         cfg = bb.EngineConfig(n=n, p=p, p_local=j1 - j0, j0=j0, rank=r, world=world, seed=seed,
-                              stream=stream, method=2)
+                              stream=stream, true_alpha=ta, ortho=ortho)
         shards.append(bb.Engine(cfg, np.asfortranarray(X[:, j0:j1]), y))
     grp = bb.ShardGroup(shards)
     grp.init_state()
     rng = np.random.default_rng(3)
     beta = btrue + 0.05 * rng.standard_normal(p)
-    tau, sig2 = 0.9, 1.1
-    for t in range(1, 6):
-        single.set_state(beta, tau, sig2, 0.5)
+    tau, sig2, alpha = 0.9, 1.1, 0.5
+    naccept = 0
+    for t in range(1, 9):
+        single.set_state(beta, tau, sig2, alpha)
         for r, e in enumerate(shards):
-            e.set_state(beta[r * per:min(p, (r + 1) * per)], tau, sig2, 0.5)
+            e.set_state(beta[r * per:min(p, (r + 1) * per)], tau, sig2, alpha)
         single.run(t, 1)
         grp.run(t, 1)
         grp.sync()
@@ -428,11 +435,15 @@ def test_shard_group_matches_single_engine(gpu_lib, world):
         for q in parts:
             assert abs(q["tau"] - s1["tau"]) <= 1e-13 * s1["tau"]
             assert abs(q["sig2"] - s1["sig2"]) <= 1e-12 * s1["sig2"]
+            assert abs(q["alpha"] - s1["alpha"]) <= 1e-14, (t, q["alpha"], s1["alpha"])
+        naccept += s1["alpha"] != alpha
         # same counters; tau differs only by the summation order of S_alpha
         assert flips(lg, s1["lambda"]) == 0
         assert np.max(np.abs(lg - s1["lambda"]) / s1["lambda"]) < 1e-11
         assert rel_err(bg, s1["beta"]) < 1e-10, (t, rel_err(bg, s1["beta"]))
-        beta, tau, sig2 = s1["beta"], s1["tau"], s1["sig2"]
+        beta, tau, sig2, alpha = s1["beta"], s1["tau"], s1["sig2"], s1["alpha"]
+    if kind == "alpha":
+        assert naccept > 0  # the MH step moved alpha at least once
     grp.close()
     single.close()
 
