@@ -233,6 +233,34 @@ def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stre
     return u + D * (Xk.T @ w) / sig, lam, tau, sig2
 
 
+def alpha_mh_sharded(a_old, beta_k, p, tau, pr_a, pr_b, seed, stream, t, allreduce, ep=0.1):
+    """The alpha MH step (BridgeRegression.cpp:469-503) on a column shard: every shard draws
+    the same proposal from the shared counter, sums exp(a log|beta_j / tau|) over its own
+    columns for a_new and a_old, the two sums are all-reduced, and the decision uses the
+    GLOBAL p -- the engine's k_alpha_sums / exchange / k_alpha_decide."""
+    from . import KIND_ALPHA, uniforms
+
+    u = uniforms(seed, stream, t, KIND_ALPHA, 0)
+    l_new, r_new = max(0.0, a_old - ep), min(1.0, a_old + ep)
+    d_new = r_new - l_new
+    a_new = l_new + d_new * u[0]
+    sl = np.log(np.abs(beta_k / tau))
+    S = allreduce(np.array([np.exp(a_new * sl).sum(), np.exp(a_old * sl).sum()]))
+    lg = __import__("math").lgamma
+
+    def llh(a, Sa):
+        return p * np.log(a) - p * lg(1.0 / a) - Sa
+
+    def ldb(x):
+        return (pr_a - 1.0) * np.log(x) + (pr_b - 1.0) * np.log(1.0 - x) - (
+            lg(pr_a) + lg(pr_b) - lg(pr_a + pr_b))
+
+    d_old = min(1.0, a_new + ep) - max(0.0, a_new - ep)
+    log_accept = (llh(a_new, S[0]) - llh(a_old, S[1]) + ldb(a_new) - ldb(a_old) +
+                  np.log(d_old) - np.log(d_new))
+    return a_old if u[1] > np.exp(log_accept) else a_new
+
+
 def bridge_regression_tri(y, X, nsamp, basis, burn=500, alpha=0.5, sig2_shape=0.0,
                           sig2_scale=0.0, nu_shape=2.0, nu_rate=2.0, alpha_a=1.0, alpha_b=1.0,
                           true_sig2=0.0, true_tau=0.0, true_alpha=None, betaburn=0, seed=0,

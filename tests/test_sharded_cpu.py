@@ -95,3 +95,48 @@ def test_sharded_sweep_equals_dense_woodbury_step():
     d = oracle.normals(30, 7, 0, 3, oracle.KIND_DELTA)
     b2 = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
     np.testing.assert_allclose(b1, b2, rtol=1e-11, atol=1e-13)
+
+
+def _alpha_worker(rank, world, port, p, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(9)
+    beta = rng.standard_normal(p) * np.exp(rng.uniform(-4, 1, p))
+    per = (p + world - 1) // world
+    j0, j1 = rank * per, min(p, (rank + 1) * per)
+
+    def allreduce(v):
+        t = torch.from_numpy(np.ascontiguousarray(v))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    out = []
+    a = 0.5
+    for t in range(1, 40):
+        a = gibbs.alpha_mh_sharded(a, beta[j0:j1], p, 0.7, 1.0, 1.0, 13, 2, t, allreduce)
+        out.append(a)
+    if rank == 0:
+        np.save(out_path, np.array(out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_alpha_mh_matches_unsharded(tmp_path, world):
+    """The alpha MH step on column shards (its two sums all-reduced, the global p in the
+    likelihood) walks the same alpha path as the unsharded oracle step."""
+    import oracle
+
+    p = 500
+    out = str(tmp_path / "alpha.npy")
+    mp.spawn(_alpha_worker, args=(world, _free_port(), p, out), nprocs=world, join=True)
+    got = np.load(out)
+    rng = np.random.default_rng(9)
+    beta = rng.standard_normal(p) * np.exp(rng.uniform(-4, 1, p))
+    a, ref = 0.5, []
+    for t in range(1, 40):
+        a = oracle.alpha_mh(a, beta, 0.7, 1.0, 1.0, 13, 2, t)
+        ref.append(a)
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0)
+    assert len(set(np.round(ref, 12))) > 3  # the walk moves
