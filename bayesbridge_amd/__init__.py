@@ -224,7 +224,7 @@ def set_device_count(k: int) -> None:
 
 
 def set_chol_version(version: int) -> None:
-    """Device Cholesky chain variant: 2 (pipelined, default) or 1 (round-2 chain)."""
+    """Device Cholesky chain variant: 1 (default) or the pipelined 2 / 3 (A/B only)."""
     _check(library().bb_set_chol_version(int(version)), "bb_set_chol_version")
 
 

@@ -1540,10 +1540,10 @@ __device__ __forceinline__ void dprime_acc2(const double (*T)[65], int by, int b
     }
 }
 
-// V = 2: phase a on waves 0-5, U row block 3 on waves 4-7; V = 3: phase a on waves
-// {0, 1, 4, 5} (SIMDs 0, 1: the last two producers, waves 6 and 7, keep SIMDs 2, 3 to
-// themselves), U row block 3 on waves 0-3, and no wave waits for its global stores to drain
-// before the work that follows them.
+// Phase a on waves 0-5, U row block 3 on waves 4-7.  V = 2 drains stores and releases W_k /
+// U_{k,k+1} through LDS counters as they complete; V = 3 forms the partial next diagonal
+// block before polling the (k+1, k+1) hand-off and drains every store once, before the
+// step's closing barrier, releasing both flags after it (v1's release).
 template <int V>
 __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                               const CholFlags &F, uint32_t *err, unsigned long long *trace,
@@ -1568,22 +1568,14 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
         bx = blk < 1 ? 0 : blk < 3 ? 1 : blk < 6 ? 2 : 3;
         by = blk - bx * (bx + 1) / 2;
     };
-    // V = 3: wave q in {0, 1, 4, 5} (qi = 0..3) holds blocks qi, qi + 4 and qi + 8 (< 10)
-    const bool pa = V == 2 ? wid < 6 : (wid & 2) == 0;  // a phase-a wave
-    const int qi = (wid & 1) | ((wid >> 1) & 2);
-    int nd = 0;
+    const bool pa = wid < 6;  // a phase-a wave
+    int nd = wid < 4 ? 2 : wid < 6 ? 1 : 0;
     int dby[3] = {0, 0, 0}, dbx[3] = {0, 0, 0};
-    if (V == 2) {
-        nd = wid < 4 ? 2 : wid < 6 ? 1 : 0;
-        if (wid < 4) {
-            bxy(wid, dby[0], dbx[0]);
-            bxy(wid + 4, dby[1], dbx[1]);
-        } else if (wid < 6) {
-            bxy(wid + 4, dby[0], dbx[0]);
-        }
-    } else if (pa) {
-        nd = qi < 2 ? 3 : 2;
-        for (int d = 0; d < nd; ++d) bxy(qi + 4 * d, dby[d], dbx[d]);
+    if (wid < 4) {
+        bxy(wid, dby[0], dbx[0]);
+        bxy(wid + 4, dby[1], dbx[1]);
+    } else if (wid < 6) {
+        bxy(wid + 4, dby[0], dbx[0]);
     }
 #define CHAIN2_TS(slot)                                                                 \
     do {                                                                                \
@@ -1591,7 +1583,7 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
     } while (0)
     tile_load(Dn, A, lda, 0, 0, true);
     for (int k = 0; k < nblk; ++k) {
-        __syncthreads();  // Dn (the diagonal block) complete
+        if (V != 3 || k == 0) __syncthreads();  // Dn (the diagonal block) complete
         double a[8][2];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -1657,6 +1649,7 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                     st_sc1(&Wk[(size_t)(c0 + q - 64) * kNB + r0 + i], a[i][q] * r);
             }
         }
+        if (wid == 7) CHAIN2_TS(2);
         if (k + 1 == nblk) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lds_bump(&w_drain) == 7 && lane == 0)
@@ -1698,12 +1691,7 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
             // ---- phase a: U rows 0..47 and the partial next diagonal block ----
             lds_wait_ge(vc, 48, err);
             lds_wait_ge(vlds(&s_ready), 4, err);
-            if (V == 3) {
-                for (int by = 2; by >= 0; --by) {
-                    const v4d u = u_block2(ROWS, S, piv, by, qi);
-                    u_put2(T, A, lda, k, by, qi, u);
-                }
-            } else if (wid < 4) {
+            if (wid < 4) {
                 const v4d u2 = u_block2(ROWS, S, piv, 2, wid);
                 u_put2(T, A, lda, k, 2, wid, u2);
                 const v4d u0 = u_block2(ROWS, S, piv, 0, wid);
@@ -1721,6 +1709,11 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                 lds_bump(&u_drain);
                 if (lds_bump(&w_drain) == 7 && lane == 0)
                     __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                // V = 3: the partial next diagonal block needs only U rows 0..47, not the
+                // (k+1, k+1) hand-off (subtracted at the end)
+                lds_wait_ge(vlds(&ua_cnt), 6, err);
+                for (int d = 0; d < nd; ++d) dprime_acc2(T, dby[d], dbx[d], 0, 12, dacc[d]);
             }
             // the (k+1, k+1) hand-off: this wave's D blocks of A_{k+1,k+1}
             const unsigned int *f2 = &F.R[2 * (k + 1)];
@@ -1741,17 +1734,22 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                     const int y = dby[d] * 16 + (lane >> 4) + 4 * r, x = dbx[d] * 16 + (lane & 15);
                     qv[d][r] = ld_sc1(&t2[(size_t)y + (size_t)x * lda]);
                 }
-            lds_wait_ge(vlds(&ua_cnt), V == 2 ? 6 : 4, err);
-            for (int d = 0; d < nd; ++d) dprime_acc2(T, dby[d], dbx[d], 0, 12, dacc[d]);
+            if (wid == 0) CHAIN2_TS(6);
+            if (wid == 4) CHAIN2_TS(4);
+            if (V == 2) {
+                lds_wait_ge(vlds(&ua_cnt), 6, err);
+                for (int d = 0; d < nd; ++d) dprime_acc2(T, dby[d], dbx[d], 0, 12, dacc[d]);
+            }
         }
-        const bool pb = V == 2 ? wid >= 4 : wid < 4;  // a U-row-block-3 wave
+        const bool pb = wid >= 4;  // a U-row-block-3 wave
         if (pb) {
             // ---- phase b: U row block 3, once every pivot is published ----
             lds_wait_ge(vc, 64, err);
             lds_wait_ge(vlds(&s_ready), 4, err);
-            const int bx = V == 2 ? wid - 4 : wid;
+            const int bx = wid - 4;
             const v4d u3 = u_block2(ROWS, S, piv, 3, bx);
             u_put2(T, A, lda, k, 3, bx, u3);
+            if (wid == 7) CHAIN2_TS(3);
             if (V == 2 && wid >= 6) {  // waves 6-7 have not released their W rows yet
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lds_bump(&w_drain) == 7 && lane == 0)
@@ -1778,17 +1776,16 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         } else {
-            // every wave's W rows, and the U blocks of the phase-a and phase-b waves, have
-            // been issued; each wave drains its own stores and counts in, the last one
-            // releases W_k (8 waves) and U_{k,k+1} (its 8 storing passes)
+            // V = 3: every wave drains its own W-row and U-block stores (long issued for all
+            // but the last producers) before the step's closing barrier; W_k and U_{k,k+1} are
+            // then released together by one thread after it (as v1 releases them)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lds_bump(&w_drain) == 7 && lane == 0)
+            __syncthreads();
+            if (tid == 0) {
                 __hip_atomic_store(&F.W[k], F.ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int ub = (pa ? 1 : 0) + (pb ? 1 : 0);
-            for (int b = 0; b < ub; ++b)
-                if (lds_bump(&u_drain) == 7 && lane == 0)
-                    __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&F.P[k * F.ncb + k + 1], F.ep, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (wid == 0) CHAIN2_TS(7);
     }
@@ -1954,12 +1951,14 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         const int nupd = diag ? i - 1 : i;  // (i,i): updates 0..i-2, the chain applies i-1
         const int nstd = (merge || dmerge) ? nupd - 1 : nupd;
         bool pub = false;  // merge: U_{k,j} (in Q) is published with the hand-off
-        // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1)
+        // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1),
+        // D = the diagonal hand-off (kt+1, kt+1)
         constexpr int kt = 6;
         unsigned long long *otr = nullptr;
         if (trace && nblk > kt + 1) {
             if (i == kt && j == kt + 1) otr = trace + (size_t)nblk * 32 + 8;
             if (i == kt - 1 && j == kt + 1) otr = trace + (size_t)nblk * 32;
+            if (i == kt + 1 && j == kt + 1) otr = trace + (size_t)nblk * 32 + 16;
         }
 #define OWN_TS(slot)                                                                \
     do {                                                                            \
@@ -2165,9 +2164,9 @@ static int device_cus() {
     return n;
 }
 
-// chain variant of k_chol_persistent (1: round-2 chain, 2: pipelined chain, the default);
-// bb_set_chol_version switches it for A/B measurements
-int g_chol_version = 2;
+// chain variant of k_chol_persistent (1: the default; 2, 3: the pipelined chains, measured
+// slower -- DESIGN.md §5.2); bb_set_chol_version switches it for A/B measurements
+int g_chol_version = 1;
 
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *Wd, unsigned int *flags, unsigned long long *trace) {

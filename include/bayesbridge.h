@@ -319,8 +319,9 @@ int bb_group_sync(bb_group *g);
  * the samples drawn so far and re-raises the interrupt in R.
  */
 void bb_set_device_count(int count);
-/* Chain variant of the device Cholesky (k_chol_persistent): 2 = pipelined chain (default),
- * 1 = the round-2 chain; for A/B measurements.  Returns 0, or -1 for another value. */
+/* Chain variant of the device Cholesky (k_chol_persistent): 1 = the default chain, 2 and 3 =
+ * the pipelined chains (measured slower); for A/B measurements.  Returns 0,
+ * or -1 for another value. */
 int bb_set_chol_version(int version);
 void bb_set_trace_budget(long long bytes);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

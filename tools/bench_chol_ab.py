@@ -1,6 +1,7 @@
 """A/B of the device Cholesky chain variants (bb_set_chol_version): factor + solve times at
-the system sizes of the BASELINE configs (C2/C4 m = 1024, C3 2048, C5 5120) and the v2
-chain's per-step stamps at m = 2048 (slot 0 step start, 1 last pivot, 5 U complete, 7 end).
+the system sizes of the BASELINE configs (C2/C4 m = 1024, C3 2048, C5 5120) and the v2 /
+v3 chains' per-step stamps at m = 2048 (slot 0 step start, 1 last pivot; the rest relative
+to the last pivot).
 Usage: python tools/bench_chol_ab.py"""
 import json
 import os
@@ -21,26 +22,41 @@ for m in (512, 1024, 2048, 4096, 5120):
         row[f"v{v}_solve_us"] = s * 1e3
     out[m] = row
     print(m, json.dumps({k: round(x, 1) for k, x in row.items()}), flush=True)
+NAMES = {2: "wave7 W stored", 3: "wave7 U rb3 put", 4: "wave4 Q loaded", 5: "U complete (B1)",
+         6: "wave0 Q loaded", 7: "step end"}
 for v in (2, 3):
     bb.set_chol_version(v)
     f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
     t = ts[:-1, :8].astype(np.int64) * 0.01
     steps = np.diff(t[:, 0])
     lp = t[:-1, 1] - t[:-1, 0]
-    u5 = t[:-1, 5] - t[:-1, 1]
-    en = t[:-1, 7] - t[:-1, 5]
-    print(f"v{v} m=2048 step median {np.median(steps):.2f} us: start->last pivot "
-          f"{np.median(lp[1:-1]):.2f}, last pivot->U done {np.median(u5[1:-1]):.2f}, "
-          f"U->end {np.median(en[1:-1]):.2f}")
-bb.set_chol_version(2)
-if False:
+    rel = {NAMES[j]: round(float(np.median((t[:-1, j] - t[:-1, 1])[1:-1])), 2) for j in NAMES}
+    print(f"v{v} m=2048 step median {np.median(steps):.2f} us, start->last pivot "
+          f"{np.median(lp[1:-1]):.2f}; after the last pivot (us): {json.dumps(rel)}", flush=True)
+bb.set_chol_version(1)
+
+# the step-6 hand-offs against the chain: owner stamps of tiles A = (5, 7) (stored tile,
+# slots 0-3 its last standard update, 4 flag), B = (6, 7) (merge: 0 start, 1 W_5 / H_5 seen,
+# 2 U_{5,7} formed, 3 merged, 4 released) and D = (7, 7) (dmerge, same slots), relative to
+# the start of chain step 6 (us)
+kt = 6
+for v in (1, 3):
+    bb.set_chol_version(v)
     f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
-t = ts[:-1, :8].astype(np.int64) * 0.01
-steps = np.diff(t[:, 0])
-print("v2 m=2048 step us (start-to-start):", np.round(steps[:8], 2).tolist(), "... median",
-      round(float(np.median(steps)), 2))
-lp = t[:-1, 1] - t[:-1, 0]
-u5 = t[:-1, 5] - t[:-1, 1]
-en = t[:-1, 7] - t[:-1, 5]
-print("  start->last pivot %.2f  last pivot->U done %.2f  U->end %.2f (medians, us)" %
-      (np.median(lp[1:-1]), np.median(u5[1:-1]), np.median(en[1:-1])))
+    t0 = int(ts[kt, 0])
+    rel = lambda x: round((int(x) - t0) * 0.01, 2) if x else None  # noqa: E731
+    own = ts[-1]
+    print(f"v{v} step {kt}: prev step end {rel(ts[kt - 1, 7])}, last pivot {rel(ts[kt, 1])}, "
+          f"end {rel(ts[kt, 7])}; A {[rel(x) for x in own[0:5]]} B {[rel(x) for x in own[8:13]]} "
+          f"D {[rel(x) for x in own[16:21]]}", flush=True)
+bb.set_chol_version(1)
+
+# v1 elimination: producer-group start / end stamps (trace slots 16-23 / 24-31) relative to
+# the step start, medians over the steps (us)
+bb.set_chol_version(1)
+f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
+t = ts[1:-2].astype(np.int64)
+st = np.median((t[:, 16:24] - t[:, [0]]) * 0.01, axis=0)
+en = np.median((t[:, 24:32] - t[:, [0]]) * 0.01, axis=0)
+print("v1 groups start", np.round(st, 2).tolist(), "end", np.round(en, 2).tolist(),
+      "last pivot", round(float(np.median((t[:, 1] - t[:, 0]) * 0.01)), 2), flush=True)
