@@ -113,7 +113,9 @@ def main():
         if k.startswith("bb::k_oz_gemm") and "<0" in k:
             algo[k] = 16.0 * n_oz * k_pad
     if sparse:  # the pair-list Gram's algorithmic bytes as bench.py counts them
-        algo = {"bb::k_sp_gram_col": bench["roofline"]["algorithmic_bytes_per_launch"]}
+        rf = bench["roofline"] if bench["roofline"].get("phase") == "gram" else \
+            bench.get("roofline_secondary", {})
+        algo = {"bb::k_sp_gram_col": rf.get("algorithmic_bytes_per_launch")}
     out["workload"]["name"] = wl or None
     out["gram_kernels"] = {}
     for k, a in algo.items():
