@@ -228,6 +228,11 @@ def set_chol_version(version: int) -> None:
     _check(library().bb_set_chol_version(int(version)), "bb_set_chol_version")
 
 
+def chol_version() -> int:
+    """The device Cholesky chain variant in use (bb_set_chol_version(0) reports it)."""
+    return int(library().bb_set_chol_version(0))
+
+
 def set_trace_budget(nbytes: int) -> None:
     """Device bytes of the trace ring per engine (<= 0 restores the 1 GiB default)."""
     library().bb_set_trace_budget(int(nbytes))

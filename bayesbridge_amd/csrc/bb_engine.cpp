@@ -1567,9 +1567,17 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
             }
             if (g->members[0]->woodbury())
                 g->reduce(&bb_engine::red2, g->members[0]->red2_count());
-            for (auto *m : g->members) {
+            // phase c holds the persistent Cholesky / backward-solve kernels, which need every
+            // workgroup of their grid resident at once: two members' launches on the shared
+            // device must not overlap (two C3-sized factorisations side by side each hold part
+            // of the CUs and wait on tiles owned by workgroups that cannot start), so the
+            // members' phase c run one after another
+            for (size_t i = 0; i < g->members.size(); ++i) {
+                bb_engine *m = g->members[i];
                 g->on(m);
+                if (i > 0) HIPCHECK(hipStreamWaitEvent(m->stream, g->mev[i - 1], 0));
                 m->phase_c(t, slot, mcmc_phase);
+                if (i + 1 < g->members.size()) HIPCHECK(hipEventRecord(g->mev[i], m->stream));
             }
             if (g->members[0]->alpha_exchange()) {
                 g->reduce(&bb_engine::red3, 2);
@@ -2077,9 +2085,20 @@ int bb_bench_ozaki(int n, int k, int nsplit, int dbg, int reps, double *ms) {
         hipEvent_t e0, e1;
         HIPCHECK(hipEventCreate(&e0));
         HIPCHECK(hipEventCreate(&e1));
-        launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg);
+        // dbg 999: production kernel without K rotation; 1000 + L: with pair lead L / 1000;
+        // 1000000 + 1000 T + L: lead L / 1000 and late shift T / 1000
+        int lead = kOzLeadDefault, late = -1;
+        if (dbg == 999 || (dbg >= 1000 && dbg < 2000)) {
+            lead = dbg == 999 ? -1 : dbg - 1000;
+            dbg = 0;
+        } else if (dbg >= 1000000) {
+            lead = dbg % 1000;
+            late = (dbg / 1000) % 1000;
+            dbg = 0;
+        }
+        launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg, lead, late);
         HIPCHECK(hipEventRecord(e0, 0));
-        for (int r = 0; r < reps; ++r) launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg);
+        for (int r = 0; r < reps; ++r) launch_oz_gemm(0, R, n_oz, k_pad, S, P, dbg, lead, late);
         HIPCHECK(hipEventRecord(e1, 0));
         HIPCHECK(hipEventSynchronize(e1));
         float t = 0;
@@ -2745,6 +2764,7 @@ extern "C" {
 void bb_set_device_count(int count) { g_max_devices = count < 0 ? 0 : count; }
 
 int bb_set_chol_version(int version) {
+    if (version == 0) return g_chol_version;  // query
     if (version < 1 || version > 3) return -1;
     g_chol_version = version;
     return 0;

@@ -1801,7 +1801,8 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
     // During the v1 chain's elimination S and Q together hold the published pivot rows; the
     // v2 chain (chol_chain_v2) lays out U rows, S and the pivot rows side by side.
-    __shared__ __attribute__((aligned(16))) double Lraw[V >= 2 ? 8320 + 64 * 130 : 3 * 64 * 65];
+    constexpr bool kV2 = V >= 2;  // the pipelined chains
+    __shared__ __attribute__((aligned(16))) double Lraw[kV2 ? 8320 + 64 * 130 : 3 * 64 * 65];
     double(*Lb)[64][65] = (double(*)[64][65])Lraw;
     __shared__ double piv[64];
     __shared__ int cnt;
@@ -1813,7 +1814,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     v4d acc[2];
     if (blockIdx.x == 0) {
         // ------------------------------ the chain ------------------------------
-        if constexpr (V >= 2) {
+        if constexpr (kV2) {
             chol_chain_v2<V>(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
             return;
         }

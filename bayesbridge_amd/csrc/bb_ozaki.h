@@ -58,8 +58,13 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
                         const double *D, const double *rscale, int8_t *R,
                         const double *u = nullptr, double *xu_part = nullptr);
 // P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
+// lead_pm: the diagonal pairs' K lead in 1/1000 of the pass (kOzLeadDefault: the tuned
+// value; < 0: no K rotation at all, every pass from chunk 0); late_pm: the start shift per
+// earlier pair round in 1/1000 of the pass (< 0: the tuned value).  Results do not depend on
+// either.
+constexpr int kOzLeadDefault = -1000000;
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
-                    int dbg = 0);
+                    int dbg = 0, int lead_pm = kOzLeadDefault, int late_pm = -1);
 // red2[tri_index(r, c)] (r <= c < n_pad) = G(r, c); red2[tri_count(n_pad) + r] = sum_q
 // xu_part[q][r].
 void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,

@@ -415,10 +415,16 @@ __device__ __forceinline__ void oz_mfma16v(v4i &acc, const v4i &a, const v4i &b)
 template <int dbg, bool DIAGQ>
 __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
                                              const int8_t *baseB, size_t kstride, int c0,
-                                             int nch, int wid, int slot, int8_t *out, int m,
-                                             double im) {
+                                             int nch, int cs, int wid, int slot, int8_t *out,
+                                             int m, double im) {
     const int lane = threadIdx.x & 63;
     const int voff = wid * 4096 + lane * 16;
+    // chunk of K step i: the pass starts at chunk cs of its split and wraps (exact integer
+    // sums, so the order does not change a bit of the result)
+    auto kat = [&](int i) {
+        const int q = cs + i;
+        return c0 + (q >= nch ? q - nch : q);
+    };
     auto glds_one = [&](int kc, int stage, int g) {
         int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
         const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
@@ -451,7 +457,7 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
             __builtin_amdgcn_s_barrier();
         }
         asm volatile("" ::: "memory");
-        const int kc_next = c0 + min(it + kOzStages, nch - 1);
+        const int kc_next = kat(min(it + kOzStages, nch - 1));
         const int st_next = (it + kOzStages) % kOzStages;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -485,11 +491,11 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
     v4i fa0[8], fb0[8], fa1[8], fb1[8];
     if (nch > 0) {
 #pragma unroll
-        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        for (int st = 0; st < kOzStages - 1; ++st) issue(kat(min(st, nch - 1)), st);
         oz_wait_vm<16>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
+        issue(kat(min(kOzStages - 1, nch - 1)), kOzStages - 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             fa0[i] = frag(0, 8 + i);
@@ -541,10 +547,15 @@ __device__ __forceinline__ void oz_diag_pass(int8_t *smem, const int8_t *baseA,
 template <int dbg>
 __device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
                                              const int8_t *baseB, size_t kstride, int c0,
-                                             int nch, int wid, int8_t *out, int m, double im) {
+                                             int nch, int cs, int wid, int8_t *out, int m,
+                                             double im) {
     const int lane = threadIdx.x & 63;
     const int wr = wid >> 1, wc = wid & 1;
     const int voff = wid * 4096 + lane * 16;
+    auto kat = [&](int i) {  // as in oz_diag_pass
+        const int q = cs + i;
+        return c0 + (q >= nch ? q - nch : q);
+    };
     auto glds_one = [&](int kc, int stage, int g) {
         int8_t *sb = smem + stage * kOzStageBytes + (g >> 2) * kOzOpBytes;
         const int8_t *src = ((g >> 2) ? baseB : baseA) + (size_t)kc * kstride + (g & 3) * 1024;
@@ -574,7 +585,7 @@ __device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
             __builtin_amdgcn_s_barrier();
         }
         asm volatile("" ::: "memory");
-        const int kc_next = c0 + min(it + kOzStages, nch - 1);
+        const int kc_next = kat(min(it + kOzStages, nch - 1));
         const int st_next = (it + kOzStages) % kOzStages;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -592,11 +603,11 @@ __device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
     v4i fa0[8], fb0[8], fa1[8], fb1[8];
     if (nch > 0) {
 #pragma unroll
-        for (int st = 0; st < kOzStages - 1; ++st) issue(c0 + min(st, nch - 1), st);
+        for (int st = 0; st < kOzStages - 1; ++st) issue(kat(min(st, nch - 1)), st);
         oz_wait_vm<16>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue(c0 + min(kOzStages - 1, nch - 1), kOzStages - 1);
+        issue(kat(min(kOzStages - 1, nch - 1)), kOzStages - 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             fa0[i] = frag_a(0, i);
@@ -633,10 +644,24 @@ __device__ __forceinline__ void oz_full_pass(int8_t *smem, const int8_t *baseA,
 // ceil(nt/2) diagonal pairs, all of one unit on one XCD (block b -> XCD b % 8) so that the
 // pairs share their row blocks in L2 with the unit's off-diagonal tiles running beside them
 // (launched alone, the pairs stream their rows from HBM).
+// K rotation (round 3): a unit's row blocks are shared through the XCD's 4 MB L2, which
+// spans ~32 chunk steps of the unit (8 row blocks x 16 KB per step), so a workgroup that runs
+// more than ~32 chunks behind the rest reads from HBM.  The diagonal pairs do 68 MFMAs per
+// wave per chunk against 64 and used to fall ~47 chunks behind over a C3 tile, and the
+// workgroups that ran a pair in one round start the next round that much late: the pairs
+// alone missed L2 for 1.2 GB per launch (profiles/r03_ozaki_pairs_l2.json).  Each pass now
+// starts at the chunk its unit is expected to be at and wraps around the split: a workgroup
+// that ran pairs in earlier rounds starts 1/16 of a pass further per such round, and a
+// diagonal pair starts a further `lead` ahead, half its expected lag, so it is ahead of the
+// unit for the first half of the pass and behind it for the second.  (A progress word
+// published from the chunk loop measured 3.5x slower: the store in the loop makes the
+// compiler wait out every LDS-DMA piece.)  The integer sums are exact: any order gives the
+// same bits.  lead < 0: every pass starts at chunk 0 (the round-2 order, for A/B).
 template <int dbg>
 __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict__ R, int n_oz,
                                                        int nkc, int nsplit,
-                                                       int8_t *__restrict__ P, OzConsts C) {
+                                                       int8_t *__restrict__ P, int lead_pm,
+                                                       int late_pm, OzConsts C) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
     const int nt = n_oz / kOzT;
     const int ntiles = nt * (nt + 1) / 2;
@@ -656,10 +681,24 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
     const int local = (q % nper + 4 * (q / nper)) % nper;
     const int mod = u % kOzMods;
     const int split = u / kOzMods;
-    if (rnd > 0) __syncthreads();  // the previous tile's LDS ring is drained
     const int per = (nkc + nsplit - 1) / nsplit;
     const int c0 = split * per;
     const int nch = max(0, min(nkc, c0 + per) - c0);
+    if (rnd > 0) __syncthreads();  // the previous tile's LDS ring is drained
+    const bool is_pair = local >= noff;
+    // this workgroup's K start (see above): a pair pass takes ~68/64 of an off-diagonal
+    // one, so every earlier round spent on a pair delays the start by late_pm / 1000 of a pass
+    int cs = 0;
+    if (nch > 0 && lead_pm >= 0) {
+        int late = 0;  // earlier rounds of this workgroup that ran a diagonal pair
+        for (int r0 = 0; r0 < rnd; ++r0) {
+            const int q_ = q0 + r0 * qs;
+            late += ((q_ % nper + 4 * (q_ / nper)) % nper) >= noff;
+        }
+        const long shift =
+            ((long)nch * late * late_pm + (is_pair ? (long)nch * lead_pm : 0)) / 1000;
+        cs = (int)(shift % nch);
+    }
     const size_t kstride = (size_t)n_oz * kOzKC;
     const int8_t *plane = R + (size_t)mod * nkc * kstride;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -673,8 +712,8 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
         const int K = local - I * (I - 1) / 2;
         const int tile = I * (I + 1) / 2 + K;
         oz_full_pass<dbg>(smem, plane + (size_t)I * kOzT * kOzKC, plane + (size_t)K * kOzT * kOzKC,
-                          kstride, c0, nch, wid, P0 + (size_t)tile * (kOzT * kOzT), C.m[mod],
-                          C.inv_m[mod]);
+                          kstride, c0, nch, cs, wid, P0 + (size_t)tile * (kOzT * kOzT),
+                          C.m[mod], C.inv_m[mod]);
     } else {
         if (dbg & 16) continue;  // ablation: the diagonal pairs idle (traffic probe)
         const int pr = local - noff;
@@ -685,20 +724,22 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
         const int8_t *bA = plane + (size_t)I1 * kOzT * kOzKC;
         const int8_t *bB = plane + (size_t)I2 * kOzT * kOzKC;
         if (wid < 2)
-            oz_diag_pass<dbg, false>(smem, bA, bB, kstride, c0, nch, wid, slot, out, C.m[mod],
-                                     C.inv_m[mod]);
+            oz_diag_pass<dbg, false>(smem, bA, bB, kstride, c0, nch, cs, wid, slot, out,
+                                     C.m[mod], C.inv_m[mod]);
         else
-            oz_diag_pass<dbg, true>(smem, bA, bB, kstride, c0, nch, wid, slot, out, C.m[mod],
-                                    C.inv_m[mod]);
+            oz_diag_pass<dbg, true>(smem, bA, bB, kstride, c0, nch, cs, wid, slot, out,
+                                    C.m[mod], C.inv_m[mod]);
     }
     }
 }
 
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
-                    int dbg) {
+                    int dbg, int lead_pm, int late_pm) {
     const int nt = n_oz / kOzT;
     const int nkc = p_pad / kOzKC;
     const OzConsts &C = oz_consts();
+    if (lead_pm == kOzLeadDefault) lead_pm = 30;  // (68 - 64) / 68 / 2 of the pass
+    if (late_pm < 0) late_pm = 62;                // (68 - 64) / 64 of the pass
     // per (modulus, split) unit -- kOzMods * nsplit units, a multiple of 8 (unit u -> XCD
     // u % 8) -- the off-diagonal tiles and the diagonal pairs in one launch
     const unsigned gu0 = (unsigned)(nt * (nt - 1) / 2 + (nt + 1) / 2) * kOzMods * nsplit;
@@ -713,13 +754,13 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
     }();
     const unsigned gu = gu0 < cus8 ? gu0 : cus8;
     switch (dbg) {  // dbg != 0: timing ablations of bb_bench_ozaki only (results meaningless)
-        case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C); break;
-        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, C);
+        case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
+        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C);
     }
 }
 

@@ -320,8 +320,8 @@ int bb_group_sync(bb_group *g);
  */
 void bb_set_device_count(int count);
 /* Chain variant of the device Cholesky (k_chol_persistent): 1 = the default chain, 2 and 3 =
- * the pipelined chains (measured slower); for A/B measurements.  Returns 0,
- * or -1 for another value. */
+ * the pipelined chains (measured slower); for A/B measurements.  Returns 0, or -1 for another value; version 0
+ * changes nothing and returns the variant in use. */
 int bb_set_chol_version(int version);
 void bb_set_trace_budget(long long bytes);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
@@ -387,7 +387,10 @@ int bb_bench_chol(int m, int reps, double *ms_factor, double *ms_solve,
 int bb_gram(double *C, const double *Y, const double *w, int n, int k);
 
 /* Microbenchmark of the Ozaki int8 GEMM alone on random residues (n x k, nsplit K splits, 0 =
- * automatic); dbg != 0 selects timing ablations (results then meaningless). */
+ * automatic); dbg != 0 selects timing ablations (results then meaningless), except dbg = 999
+ * (the production kernel with every pass from K chunk 0), dbg = 1000 + L (the production
+ * kernel with the diagonal pairs' K lead set to L / 1000 of the pass) and dbg = 1000000 +
+ * 1000 T + L (lead L / 1000, start shift T / 1000 of a pass per earlier diagonal-pair round). */
 int bb_bench_ozaki(int n, int k, int nsplit, int dbg, int reps, double *ms);
 
 /* The same Gram through the Ozaki-II int8 path (w >= 0): exact integer Gram of the

@@ -163,18 +163,20 @@ def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
 @pytest.mark.parametrize("version", [1, 2, 3])
 @pytest.mark.parametrize("m", [40, 64, 128, 200, 1000, 2048, 5000])
 def test_chol_chain_versions_match_numpy(gpu_lib, m, version):
-    """Both chain variants of k_chol_persistent (2: pipelined, the default; 1: round 2), from
-    one block (m <= 64) to 79 block steps, on an ill-conditioned SPD system."""
+    """Every chain variant of k_chol_persistent (1: the default; 2, 3: pipelined), from one
+    block (m <= 64) to 79 block steps, on an ill-conditioned SPD system.  The variant in use
+    before the test is restored afterwards."""
     bb = gpu_lib
     rng = np.random.default_rng(m + 7)
     B = rng.standard_normal((m, m)) * np.exp(rng.uniform(-6, 6, m))
     A = B @ B.T + 1e-3 * np.eye(m)
     b = rng.standard_normal((m, 1))
+    default = bb.chol_version()
     bb.set_chol_version(version)
     try:
         x = bb.chol_solve(A, b)
     finally:
-        bb.set_chol_version(2)
+        bb.set_chol_version(default)
     ref = np.linalg.solve(A, b)
     cond = np.linalg.cond(A)
     # backward error of the solve against A (normwise), and the forward error

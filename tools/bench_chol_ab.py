@@ -13,9 +13,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bayesbridge_amd as bb  # noqa: E402
 
 out = {}
+VERSIONS = tuple(int(v) for v in os.environ.get("CHOL_VERSIONS", "1,2,3").split(","))
 for m in (512, 1024, 2048, 4096, 5120):
     row = {}
-    for v in (1, 2, 3):
+    for v in VERSIONS:
         bb.set_chol_version(v)
         f, s = bb.bench_chol(m, reps=10)
         row[f"v{v}_factor_us"] = f * 1e3
@@ -24,7 +25,7 @@ for m in (512, 1024, 2048, 4096, 5120):
     print(m, json.dumps({k: round(x, 1) for k, x in row.items()}), flush=True)
 NAMES = {2: "wave7 W stored", 3: "wave7 U rb3 put", 4: "wave4 Q loaded", 5: "U complete (B1)",
          6: "wave0 Q loaded", 7: "step end"}
-for v in (2, 3):
+for v in [v for v in VERSIONS if v in (2, 3)]:
     bb.set_chol_version(v)
     f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
     t = ts[:-1, :8].astype(np.int64) * 0.01
@@ -40,7 +41,7 @@ bb.set_chol_version(1)
 # 2 U_{5,7} formed, 3 merged, 4 released) and D = (7, 7) (dmerge, same slots), relative to
 # the start of chain step 6 (us)
 kt = 6
-for v in (1, 3):
+for v in VERSIONS:
     bb.set_chol_version(v)
     f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
     t0 = int(ts[kt, 0])
@@ -51,12 +52,16 @@ for v in (1, 3):
           f"D {[rel(x) for x in own[16:21]]}", flush=True)
 bb.set_chol_version(1)
 
-# v1 elimination: producer-group start / end stamps (trace slots 16-23 / 24-31) relative to
-# the step start, medians over the steps (us)
+# v1 elimination: producer-group start / end stamps (trace slots 16-23 / 24-31)
+# relative to the step start, medians over the steps (us)
+for v in [v for v in VERSIONS if v == 1]:
+    bb.set_chol_version(v)
+    f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
+    t = ts[1:-2].astype(np.int64)
+    st = np.median((t[:, 16:24] - t[:, [0]]) * 0.01, axis=0)
+    en = np.median((t[:, 24:32] - t[:, [0]]) * 0.01, axis=0)
+    steps = np.diff(ts[:-1, 0].astype(np.int64)) * 0.01
+    print(f"v{v} groups start", np.round(st, 2).tolist(), "end", np.round(en, 2).tolist(),
+          "last pivot", round(float(np.median((t[:, 1] - t[:, 0]) * 0.01)), 2),
+          "step median", round(float(np.median(steps)), 2), flush=True)
 bb.set_chol_version(1)
-f, s, ts = bb.bench_chol(2048, reps=3, trace=True)
-t = ts[1:-2].astype(np.int64)
-st = np.median((t[:, 16:24] - t[:, [0]]) * 0.01, axis=0)
-en = np.median((t[:, 24:32] - t[:, [0]]) * 0.01, axis=0)
-print("v1 groups start", np.round(st, 2).tolist(), "end", np.round(en, 2).tolist(),
-      "last pivot", round(float(np.median((t[:, 1] - t[:, 0]) * 0.01)), 2), flush=True)

@@ -20,6 +20,10 @@ import bench  # noqa: E402
 import bayesbridge_amd as bb  # noqa: E402
 
 
+def note(msg):
+    print(f"[enqueue_probe] {msg}", file=sys.stderr, flush=True)
+
+
 def probe(engines, runner, sweeps):
     runner.run(1, 3, first_slot=-1)
     runner.sync()
@@ -37,6 +41,7 @@ def main():
     members = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     sweeps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
     bb.set_verbose(0)
+    note(f"n={n} p={p} members={members}: building data")
     y, _ = bench.make_problem_y(n, p)
     out = {"n": n, "p": p, "sweeps": sweeps, "results": []}
     per = (p + members - 1) // members
@@ -46,9 +51,12 @@ def main():
         cfg = bb.EngineConfig(n=n, p=p, p_local=j1 - j0, j0=j0, rank=r, world=members,
                               true_alpha=0.5, method=2, seed=0xB4E5B41D6E)
         engines.append(bb.Engine(cfg, bench.make_columns(n, j0, j1), y))
+        note(f"engine {r} created")
     grp = bb.ShardGroup(engines)
     grp.init_state()
+    note("on-device group ready")
     h, d = probe(engines, grp, sweeps)
+    note(f"on-device group: host {h:.3f} ms, device {d:.3f} ms per sweep")
     out["results"].append({"config": f"on-device group, {members} members, one host thread",
                            "host_enqueue_ms_per_sweep": h, "device_ms_per_sweep": d})
     grp.close()
@@ -58,7 +66,9 @@ def main():
     e = bb.Engine(cfg, bench.make_columns(n, 0, p), y)
     g1 = bb.ShardGroup([e], rccl=True)
     g1.init_state()
+    note("RCCL group ready")
     h, d = probe([e], g1, sweeps)
+    note(f"RCCL group: host {h:.3f} ms, device {d:.3f} ms per sweep")
     out["results"].append({"config": "RCCL group, 1 member (its own enqueue thread)",
                            "host_enqueue_ms_per_sweep": h, "device_ms_per_sweep": d})
     g1.close()
