@@ -1973,7 +1973,12 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         // (at m = 5120 the owners, not the chain, set the pace through the middle third).
         // The updates sum in the MFMA accumulators, T -= sum once at the end: no LDS
         // read-modify-write of T and one barrier fewer per update.
+        // Round 3: a catching-up owner checked the next panel's flags once per update (one
+        // serial L2 round trip per update, issued by thread 0 before the barrier); now wave 0
+        // checks up to eight upcoming panels at once and the owner remembers how far they are
+        // published (ready_to), so most updates of a catch-up skip the check.
         bool have = false;  // S (and Q) already hold panel k
+        int ready_to = -1;  // panels <= ready_to are known to be published (uniform)
         acc[0] = acc[1] = (v4d){0.0, 0.0, 0.0, 0.0};
         for (int k = 0; k < nstd; ++k) {
             if (k == nupd - 1) OWN_TS(0);
@@ -1983,18 +1988,27 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
                 if (k == nupd - 1) OWN_TS(1);
                 tile_load(S, A, lda, k, i, false);
                 if (!diag) tile_load(Q, A, lda, k, j, false);
+                if (ready_to < k) ready_to = k;
             }
-            if (tid == 0) {
-                bool rdy = k + 1 < nstd;
-                if (rdy)
-                    rdy = __hip_atomic_load(&F.P[(k + 1) * F.ncb + i], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT) == F.ep &&
-                          (diag || __hip_atomic_load(&F.P[(k + 1) * F.ncb + j], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) == F.ep);
-                pre_ready = rdy;
+            if (k + 1 < nstd && k + 1 > ready_to) {
+                if (tid < 64) {
+                    const int kk = k + 1 + (int)tid;
+                    bool ok = false;
+                    if (tid < 8 && kk < nstd)
+                        ok = __hip_atomic_load(&F.P[kk * F.ncb + i], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) == F.ep &&
+                             (diag || __hip_atomic_load(&F.P[kk * F.ncb + j], __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) == F.ep);
+                    // the published prefix k+1 .. k+n (lanes >= 8 count as unpublished)
+                    const unsigned long long bad = __ballot(!ok);
+                    if (tid == 0) pre_ready = k + (int)__builtin_ctzll(bad);
+                }
+            } else if (tid == 0) {
+                pre_ready = ready_to;
             }
             __syncthreads();
-            const bool pre = pre_ready;
+            ready_to = pre_ready;
+            const bool pre = k + 1 < nstd && k + 1 <= ready_to;
             if (k == nupd - 1) OWN_TS(2);
             double vs[8], vq[8];
             if (pre) {
