@@ -448,6 +448,45 @@ def test_shard_group_matches_single_engine(gpu_lib, world, kind):
     single.close()
 
 
+def test_shard_group_cu_filling_system(gpu_lib):
+    """An on-device shard group whose n x n system fills every CU with its persistent
+    Cholesky (n = 1600: 25 block rows, 350 tiles > CUs): the members' factorisations must
+    run one after another (bb_group_run chains their phase c; overlapped, each held part of
+    the CUs while waiting on tiles owned by workgroups that could not start).  Two
+    teacher-forced sweeps against the unsharded engine, no error flags."""
+    bb = gpu_lib
+    n, p, world = 1600, 4000, 2
+    X, y, btrue = synthetic_problem(n, p, seed=23)
+    seed, stream = SEED + 11, 0
+    single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, true_alpha=0.5), X, y)
+    single.init_state()
+    per = p // world
+    shards = [bb.Engine(bb.EngineConfig(n=n, p=p, p_local=per, j0=r * per, rank=r, world=world,
+                                        seed=seed, stream=stream, true_alpha=0.5),
+                        np.asfortranarray(X[:, r * per:(r + 1) * per]), y) for r in range(world)]
+    grp = bb.ShardGroup(shards)
+    grp.init_state()
+    beta = btrue + 0.05 * np.random.default_rng(5).standard_normal(p)
+    tau, sig2 = 0.9, 1.1
+    for t in (1, 2):
+        single.set_state(beta, tau, sig2, 0.5)
+        for r, e in enumerate(shards):
+            e.set_state(beta[r * per:(r + 1) * per], tau, sig2, 0.5)
+        single.run(t, 1)
+        grp.run(t, 1)
+        grp.sync()
+        s1 = single.state()
+        bg = np.concatenate([e.state()["beta"] for e in shards])
+        assert rel_err(bg, s1["beta"]) < 1e-9, (t, rel_err(bg, s1["beta"]))
+        beta, tau, sig2 = s1["beta"], s1["tau"], s1["sig2"]
+    assert single.error_flags() == 0
+    assert all(e.error_flags() == 0 for e in shards)
+    grp.close()
+    single.close()
+    for e in shards:
+        e.close()
+
+
 def test_gpu_matches_golden_vectors(gpu_lib):
     """The HIP path against the committed fixtures (tests/golden/oracle_vectors.npz)."""
     import os
