@@ -1954,7 +1954,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         bool pub = false;  // merge: U_{k,j} (in Q) is published with the hand-off
         // owner trace (bb_bench_chol): hop B = hand-off tile (kt, kt+1), hop A = (kt-1, kt+1),
         // D = the diagonal hand-off (kt+1, kt+1)
-        constexpr int kt = 6;
+        const int kt = nblk >= 48 ? nblk / 2 : 6;  // the middle step for large m
         unsigned long long *otr = nullptr;
         if (trace && nblk > kt + 1) {
             if (i == kt && j == kt + 1) otr = trace + (size_t)nblk * 32 + 8;
@@ -1966,6 +1966,7 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
         if (otr && tid == 0) otr[slot] = __builtin_amdgcn_s_memrealtime();          \
     } while (0)
         tile_load(T, A, lda, i, j, diag);
+        OWN_TS(6);  // traced hand-off tiles: when the owner started the tile
         __syncthreads();
         // An owner that lags the chain finds the next panels already published: their loads
         // (into registers) are issued before this update's MFMAs and land in S / Q after
