@@ -66,7 +66,7 @@ EXPORTED_SYMBOLS = [
     "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
     "bb_pg_batch", "bb_group_create_rccl", "bb_group_sync", "bb_set_device_count",
     "bb_set_trace_budget", "bb_debug_interrupt_after", "bb_last_call_info",
-    "bb_engine_set_timed_phase", "bb_set_chol_version",
+    "bb_engine_set_timed_phase", "bb_set_chol_version", "bb_set_tuning",
 ]
 
 
@@ -127,6 +127,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_group_sync.argtypes = [c.c_void_p]
     L.bb_set_device_count.argtypes = [c.c_int]
     L.bb_set_chol_version.argtypes = [c.c_int]
+    L.bb_set_tuning.argtypes = [c.c_int, c.c_int]
     L.bb_set_trace_budget.argtypes = [c.c_longlong]
     L.bb_debug_interrupt_after.argtypes = [c.c_int]
     L.bb_last_call_info.argtypes = [_ip, _ip, _ip]
@@ -226,6 +227,12 @@ def set_device_count(k: int) -> None:
 def set_chol_version(version: int) -> None:
     """Device Cholesky chain variant: 1 (default) or the pipelined 2 / 3 (A/B only)."""
     _check(library().bb_set_chol_version(int(version)), "bb_set_chol_version")
+
+
+def set_tuning(key: int, value: int) -> int:
+    """A/B tuning knob (bb_set_tuning): key 1 = non-temporal Ozaki residue stores.  Returns
+    the previous value."""
+    return int(library().bb_set_tuning(int(key), int(value)))
 
 
 def chol_version() -> int:

@@ -2769,6 +2769,21 @@ int bb_set_chol_version(int version) {
     g_chol_version = version;
     return 0;
 }
+int bb_set_tuning(int key, int value) {
+    switch (key) {
+        case 1: {
+            const int old = g_oz_res_nt;
+            if (value >= 0) g_oz_res_nt = value > 2 ? 2 : value;
+            return old;
+        }
+        case 2: {
+            const int old = g_bxb_nt;
+            if (value >= 0) g_bxb_nt = value ? 1 : 0;
+            return old;
+        }
+        default: return -1;
+    }
+}
 void bb_set_trace_budget(long long bytes) {
     g_trace_budget = bytes > 0 ? (size_t)bytes : (size_t(1) << 30);
 }

@@ -2423,7 +2423,7 @@ void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, co
 // sweep.  NR = n_pad / 128 <= 16.
 constexpr int kBxbWaves = 4;
 
-template <int NR>
+template <int NR, bool NTL>
 __global__ __launch_bounds__(64 * kBxbWaves, 1) void k_beta_wb_xb(
     const double *__restrict__ X, int ldx, int n_pad, const double *__restrict__ w,
     const double *__restrict__ u, const double *__restrict__ D, const DevScalars *sc, int p_loc,
@@ -2444,7 +2444,15 @@ __global__ __launch_bounds__(64 * kBxbWaves, 1) void k_beta_wb_xb(
         const int jj = min(j, p_loc - 1);
         const double *col = X + (size_t)jj * ldx + 2 * lane;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) xv[i] = *(const double2 *)(col + 128 * i);
+        for (int i = 0; i < NR; ++i) {
+            if constexpr (NTL) {
+                typedef double v2d_ __attribute__((ext_vector_type(2)));
+                const v2d_ t2 = __builtin_nontemporal_load((const v2d_ *)(col + 128 * i));
+                xv[i] = make_double2(t2.x, t2.y);
+            } else {
+                xv[i] = *(const double2 *)(col + 128 * i);
+            }
+        }
         ud = make_double2(u[jj], D[jj]);
     };
     // consume column j from xc, then refill xc with column j + 3 nw
@@ -2507,6 +2515,10 @@ int beta_xb_parts(int p_loc) {
 
 bool beta_xb_supported(int n_pad) { return n_pad % 128 == 0 && n_pad <= 2048; }
 
+// non-temporal X loads in the fused beta pass (X is streamed once per sweep, larger than
+// every cache): C3 beta 0.151 -> 0.138 ms (tools/res_nt_ab.py); bb_set_tuning(2, v) for A/B
+int g_bxb_nt = 1;
+
 void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,
                              const double *u, const double *D, const DevScalars *sc, int p_loc,
                              double *beta, double *beta_trace, double *part) {
@@ -2514,8 +2526,12 @@ void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad,
     switch (n_pad / 128) {
 #define BXB(NR)                                                                             \
     case NR:                                                                                \
-        k_beta_wb_xb<NR><<<g, 64 * kBxbWaves, 0, s>>>(X, ldx, n_pad, w, u, D, sc, p_loc, beta,  \
-                                                      beta_trace, part);                   \
+        if (g_bxb_nt)                                                                       \
+            k_beta_wb_xb<NR, true><<<g, 64 * kBxbWaves, 0, s>>>(X, ldx, n_pad, w, u, D, sc,     \
+                                                               p_loc, beta, beta_trace, part); \
+        else                                                                                \
+            k_beta_wb_xb<NR, false><<<g, 64 * kBxbWaves, 0, s>>>(X, ldx, n_pad, w, u, D, sc,    \
+                                                                p_loc, beta, beta_trace, part); \
         break;
         BXB(1) BXB(2) BXB(3) BXB(4) BXB(5) BXB(6) BXB(7) BXB(8)
         BXB(9) BXB(10) BXB(11) BXB(12) BXB(13) BXB(14) BXB(15) BXB(16)

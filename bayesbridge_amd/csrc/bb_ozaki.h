@@ -58,6 +58,7 @@ void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int 
                         const double *D, const double *rscale, int8_t *R,
                         const double *u = nullptr, double *xu_part = nullptr);
 // P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
+extern int g_oz_res_nt;  // residue-plane stores non-temporal (bb_set_tuning key 1)
 // lead_pm: the diagonal pairs' K lead in 1/1000 of the pass (kOzLeadDefault: the tuned
 // value; < 0: no K rotation at all, every pass from chunk 0); late_pm: the start shift per
 // earlier pair round in 1/1000 of the pass (< 0: the tuned value).  Results do not depend on

@@ -245,6 +245,7 @@ constexpr int kOzResChunks = 4;  // 64-column chunks per workgroup, at most (oz_
 // sums of the Woodbury draw (u = sqrt(D) z): part[g][row] over the cpw * 64 columns of group g,
 // summed per lane in column order, then the two column halves -- so the separate X.u pass
 // (k_xv) disappears from the Ozaki sweep.
+template <bool NT, bool NTL>
 __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ X, int ldx,
                                                      int n_pad, int n_oz, int nkc,
                                                      const double *__restrict__ D,
@@ -270,7 +271,8 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
         const double *xp = X + (size_t)min(row, n_pad - 1) + (size_t)col0 * ldx;
         double v[kOzResCols];
 #pragma unroll
-        for (int j = 0; j < kOzResCols; ++j) v[j] = xp[(size_t)j * ldx];
+        for (int j = 0; j < kOzResCols; ++j)
+            v[j] = NTL ? __builtin_nontemporal_load(xp + (size_t)j * ldx) : xp[(size_t)j * ldx];
         if (u) {
 #pragma unroll
             for (int j = 0; j < kOzResCols; ++j) xu += v[j] * oz_readlane_d(ul, j);
@@ -314,8 +316,9 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
                     const unsigned int hi = __builtin_amdgcn_perm(b4[3], b4[2], 0x0c0c0400u);
                     wd[d] = lo | (hi << 16);
                 }
-                *(v4i *)(dst + q * 256) =
-                    (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+                const v4i val = (v4i){(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+                if constexpr (NT) __builtin_nontemporal_store(val, (v4i *)(dst + q * 256));
+                else *(v4i *)(dst + q * 256) = val;
             }
         }
     }
@@ -339,13 +342,26 @@ int oz_xu_parts(int p_pad, int n_oz) {
     return (nkc + c - 1) / c;
 }
 
+// residue-plane stores and X loads (round 3, tools/res_nt_ab.py, C3 ozprep on three boxes):
+// 0 ordinary, 1 non-temporal stores, 2 (the default) non-temporal stores and X loads.
+// Box A: 0.68 / 0.53 / -- ms (ordinary stores slow there); box B: 0.457 / 0.463 / 0.405 ms;
+// box C: 0.458 / 0.465 / 0.461 ms.  bb_set_tuning(1, v) for A/B
+int g_oz_res_nt = 2;
+
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R, const double *u,
                         double *xu_part) {
     const int nkc = p_pad / kOzKC, cpw = oz_res_cpw(nkc, n_oz);
     dim3 grid((nkc + cpw - 1) / cpw, n_oz / 256);
-    k_oz_residues<<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R, oz_consts(), u,
-                                       xu_part, cpw);
+    if (g_oz_res_nt == 2)
+        k_oz_residues<true, true><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R,
+                                                       oz_consts(), u, xu_part, cpw);
+    else if (g_oz_res_nt)
+        k_oz_residues<true, false><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R,
+                                                        oz_consts(), u, xu_part, cpw);
+    else
+        k_oz_residues<false, false><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale,
+                                                         R, oz_consts(), u, xu_part, cpw);
 }
 
 // ---------------------------------------------------------------------------
