@@ -2781,6 +2781,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_bxb_nt = value ? 1 : 0;
             return old;
         }
+        case 3: {
+            const int old = g_sp_nt;
+            if (value >= 0) g_sp_nt = value ? 1 : 0;
+            return old;
+        }
         default: return -1;
     }
 }

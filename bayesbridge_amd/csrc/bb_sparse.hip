@@ -199,6 +199,7 @@ void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, c
 constexpr int kSpColLpe = 8;
 constexpr int kSpDepth = 4;
 
+template <bool NTL>
 __global__ __launch_bounds__(256) void k_sp_gram_col(
     const int *__restrict__ rowptr, const int *__restrict__ colidx,
     const double *__restrict__ rval, const unsigned *__restrict__ estart,
@@ -242,8 +243,13 @@ __global__ __launch_bounds__(256) void k_sp_gram_col(
 #pragma unroll
                 for (int i = 0; i < kSpDepth; ++i) {
                     const unsigned kk = k + i * kSpColLpe;
-                    pv[i] = kk < en ? prod[kk] : 0.0;
-                    iv[i] = kk < en ? pidx[kk] : (unsigned short)0;
+                    if constexpr (NTL) {  // the pair list is streamed once per sweep
+                        pv[i] = kk < en ? __builtin_nontemporal_load(prod + kk) : 0.0;
+                        iv[i] = kk < en ? __builtin_nontemporal_load(pidx + kk) : (unsigned short)0;
+                    } else {
+                        pv[i] = kk < en ? prod[kk] : 0.0;
+                        iv[i] = kk < en ? pidx[kk] : (unsigned short)0;
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < kSpDepth; ++i)
@@ -257,13 +263,20 @@ __global__ __launch_bounds__(256) void k_sp_gram_col(
 
 int sp_col_max_row() { return kSpColMaxRow; }
 
+// non-temporal pair-list loads (bb_set_tuning key 3)
+int g_sp_nt = 0;
+
 void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                         const unsigned *estart, const double *prod, const unsigned short *pidx,
                         const double *D, const double *u, int n_pad, int max_row, double *tri,
                         double *xu) {
     const size_t lds = (size_t)(max_row > 0 ? max_row : 1) * sizeof(double);
-    k_sp_gram_col<<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad,
-                                          tri, xu);
+    if (g_sp_nt)
+        k_sp_gram_col<true><<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D,
+                                                    u, n_pad, tri, xu);
+    else
+        k_sp_gram_col<false><<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D,
+                                                     u, n_pad, tri, xu);
 }
 
 // One wave per row c of X (CSR), lanes strided over the row's entries, fixed tree.
