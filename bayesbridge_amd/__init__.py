@@ -657,6 +657,11 @@ def bridge_em(y, X, alpha=0.5, ratio=1.0, lambda_max=None, tol=1e-9, max_iter=30
     return beta
 
 
+# Above this p a single workgroup's p x p factorisations are slower than the per-ratio
+# loop over the whole-device Cholesky (bridge_em), so trace_beta loops there.
+EM_BATCH_MAX_P = 2048
+
+
 def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=False):
     """trace.beta (Code/R/bridge-trace.R:22-54) without the plot: bridge.EM over a grid of
     ratios with lambda.max = ratio / tol.  Returns {"beta" (L x P), "grid", "log.grid"}."""
@@ -667,7 +672,7 @@ def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=F
     if X.ndim == 1:
         X = X[:, None]
     P = X.shape[1]
-    if 1 <= P <= 128 and not use_cg:
+    if 1 <= P <= EM_BATCH_MAX_P and not use_cg:
         # the whole grid in one device launch (a workgroup per ratio)
         beta, _ = bridge_em_batch(y, X, ratio_grid, alpha=alpha,
                                   lambda_max=ratio_grid / tol, tol=tol, max_iter=max_iter)
@@ -680,7 +685,8 @@ def trace_beta(y, X, alpha=0.5, ratio_grid=None, tol=1e-9, max_iter=30, use_cg=F
 
 
 def bridge_em_batch(y, X, ratios, alpha=0.5, lambda_max=None, tol=1e-9, max_iter=30):
-    """bridge.EM (direct solves) for every ratio in one device launch, p <= 128.
+    """bridge.EM (direct solves) for every ratio in one device launch (a workgroup per
+    ratio; the system in LDS for p <= 128, a tiled Cholesky over global memory above).
     Returns (beta (len(ratios) x P), solves (len(ratios)))."""
     L = library()
     _require_gpu()

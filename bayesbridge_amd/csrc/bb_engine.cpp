@@ -2295,8 +2295,10 @@ int bb_bridge_em(double *beta_out, const double *yh, const double *Xh, int n, in
     return ret;
 }
 
-// Batched EM over `count` ratios (trace.beta) for p <= 128, direct solves: X'X and X'y
-// once, then one launch in which a workgroup per ratio runs the whole EM (k_em_batch).
+// Batched EM over `count` ratios (trace.beta), direct solves: X'X and X'y once, then one
+// launch in which a workgroup per ratio runs the whole EM -- k_em_batch (system in LDS) for
+// p <= 128, k_em_batch_tiled (system in a global scratch slice per ratio, tiled Cholesky)
+// above, the ratios in chunks whose scratch fits min(free / 2, 16 GiB).
 // beta: count x p (row r = ratio r); solves: count (as bb_bridge_em returns, -1 on a
 // non positive-definite system).  Returns 0, or -1 with bb_last_error().
 int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double *Xh, int n,
@@ -2305,7 +2307,7 @@ int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double
     std::vector<void *> owned;
     int rc = 0;
     try {
-        if (p < 1 || p > 128) throw HipError("bb_bridge_em_batch: needs 1 <= p <= 128");
+        if (p < 1) throw HipError("bb_bridge_em_batch: needs p >= 1");
         if (count < 1) throw HipError("bb_bridge_em_batch: empty ratio grid");
         HIPCHECK(hipSetDevice(g_device));
         const int n_pad = round_up(n, kGramTile), p_pad = round_up(p, 256);
@@ -2334,8 +2336,27 @@ int bb_bridge_em_batch(double *beta, int *solves, const double *yh, const double
         HIPCHECK(hipMemcpy(dl, lambda_max, count * sizeof(double), hipMemcpyHostToDevice));
         double *db = dalloc<double>((size_t)count * p, owned);
         int *ds = dalloc<int>(count, owned);
-        launch_em_batch(0, G, p_pad, bvec, p, dr, dl, count, alpha, tol, max_iter, db, ds);
-        HIPCHECK(hipGetLastError());
+        if (p <= 128) {
+            launch_em_batch(0, G, p_pad, bvec, p, dr, dl, count, alpha, tol, max_iter, db, ds);
+            HIPCHECK(hipGetLastError());
+        } else {
+            const int pe = round_up(p, em_tile());
+            const size_t per = (size_t)pe * pe * sizeof(double);
+            size_t fr = 0, tot = 0;
+            HIPCHECK(hipMemGetInfo(&fr, &tot));
+            const size_t budget = std::min(fr / 2, (size_t)16 << 30);
+            const int chunk = (int)std::max<size_t>(1, std::min<size_t>(count, budget / per));
+            if (per > fr) throw HipError("bb_bridge_em_batch: p x p system does not fit");
+            double *scr = dalloc<double>((size_t)chunk * pe * pe, owned);
+            double *vec = dalloc<double>((size_t)chunk * 3 * pe, owned);
+            int *msk = dalloc<int>((size_t)chunk * pe, owned);
+            for (int r0 = 0; r0 < count; r0 += chunk) {
+                launch_em_batch_tiled(0, G, p_pad, bvec, p, pe, dr, dl, r0,
+                                      std::min(chunk, count - r0), alpha, tol, max_iter, scr, vec,
+                                      msk, db, ds);
+                HIPCHECK(hipGetLastError());
+            }
+        }
         HIPCHECK(hipMemcpy(beta, db, (size_t)count * p * sizeof(double), hipMemcpyDeviceToHost));
         HIPCHECK(hipMemcpy(solves, ds, count * sizeof(int), hipMemcpyDeviceToHost));
     } catch (std::exception &ex) {

@@ -107,6 +107,14 @@ void launch_em_cg(hipStream_t s, const double *A, int lda, int n, const double *
 void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, int p,
                      const double *ratios, const double *lambda_max, int count, double alpha,
                      double tol, int max_iter, double *beta_out, int *solves_out);
+// The same EM for any p: a workgroup per ratio r0 .. r0 + count - 1, each with a p_pad x
+// p_pad system in scratch (count slices; p_pad a multiple of em_tile()), vecs: 3 p_pad
+// doubles and masks: p_pad ints per workgroup.  Tiled Cholesky over LDS tiles.
+void launch_em_batch_tiled(hipStream_t s, const double *G, int ldg, const double *b, int p,
+                           int p_pad, const double *ratios, const double *lambda_max, int r0,
+                           int count, double alpha, double tol, int max_iter, double *scratch,
+                           double *vecs, int *masks, double *beta_out, int *solves_out);
+int em_tile();
 // packed != 0: G is the packed upper triangle (tri_index, as k_oz_crt writes it)
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,

@@ -1077,6 +1077,276 @@ void launch_em_batch(hipStream_t s, const double *G, int ldg, const double *b, i
                                               max_iter, beta_out, solves_out);
 }
 
+// Batched bridge EM for p > 128 (trace.beta at any p): the EM loop of k_em_batch, one
+// workgroup per ratio, with the ratio's p_pad x p_pad system (lower triangle, column-major)
+// in a global scratch slice instead of LDS.  Tiled right-looking Cholesky over 64 x 64 tiles
+// staged in LDS: the diagonal tile factored in place (two barriers per pivot), its
+// triangular inverse formed by one wave (a lane per column), the panel tiles multiplied by
+// it, the trailing tiles updated by 64^3 products (4 x 4 outputs per thread, in m order);
+// substitution tile by tile, the off-diagonal part as matvecs over LDS tiles (four fixed
+// partial sums per row) and the diagonal part on one wave with shuffles.  Every sum has a
+// fixed order, so a ratio's result does not depend on the batch it runs in.
+constexpr int kEmTile = 64, kEmLd = kEmTile + 1;
+
+namespace {
+
+// t[m * kEmLd + r] = A(r0 + r, c0 + m): a tile column is a contiguous LDS row
+__device__ __forceinline__ void em_tile_load(const double *A, int lda, int r0, int c0,
+                                             double *t) {
+    for (int e = threadIdx.x; e < kEmTile * kEmTile; e += 256) {
+        const int r = e & (kEmTile - 1), m = e / kEmTile;
+        t[m * kEmLd + r] = A[(size_t)(r0 + r) + (size_t)(c0 + m) * lda];
+    }
+}
+
+// tile (r0, c0) of A = [A -] sum_m a[m][r] b[m][c]; thread owns rows (tid & 15) + 16 ii
+// and columns (tid >> 4) + 16 jj (a wave stores 4 columns x 128 contiguous bytes)
+template <bool SUB>
+__device__ __forceinline__ void em_tile_mm(const double *a, const double *b, double *A, int lda,
+                                           int r0, int c0) {
+    const int tr = threadIdx.x & 15, tc = threadIdx.x >> 4;
+    double acc[4][4] = {};
+    for (int m = 0; m < kEmTile; ++m) {
+        double av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[i] = a[m * kEmLd + tr + 16 * i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j] = b[m * kEmLd + tc + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fma(av[i], bv[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double *cp = A + (size_t)(r0 + tr + 16 * i) + (size_t)(c0 + tc + 16 * j) * lda;
+            *cp = SUB ? *cp - acc[i][j] : acc[i][j];
+        }
+}
+
+// In-place lower Cholesky of the p_pad x p_pad matrix (T tiles a side).  false (uniformly
+// across the workgroup) on a pivot that is not > 0.
+__device__ bool em_chol_tiled(double *A, int lda, int T, double *ta, double *tb) {
+    const int tid = threadIdx.x;
+    for (int k = 0; k < T; ++k) {
+        const int k0 = k * kEmTile;
+        __syncthreads();
+        em_tile_load(A, lda, k0, k0, ta);
+        for (int c = 0; c < kEmTile; ++c) {
+            __syncthreads();
+            const double piv = ta[c * kEmLd + c];
+            if (!(piv > 0.0)) return false;
+            const double d = sqrt(piv);
+            __syncthreads();
+            if (tid < kEmTile) {
+                if (tid > c) ta[c * kEmLd + tid] /= d;
+                else if (tid == c) ta[c * kEmLd + c] = d;
+            }
+            __syncthreads();
+            const int w = kEmTile - 1 - c;  // columns j = c + 1 .. 63, rows r >= j
+            for (int e = tid; e < w * kEmTile; e += 256) {
+                const int j = c + 1 + e / kEmTile, r = e & (kEmTile - 1);
+                if (r >= j) ta[j * kEmLd + r] -= ta[c * kEmLd + r] * ta[c * kEmLd + j];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < kEmTile * kEmTile; e += 256) {
+            const int r = e & (kEmTile - 1), m = e / kEmTile;
+            if (r >= m) A[(size_t)(k0 + r) + (size_t)(k0 + m) * lda] = ta[m * kEmLd + r];
+        }
+        if (k + 1 == T) break;
+        // Linv = L_kk^-1 (lower), stored tb[m][c] = Linv(c, m): lane cc forms column cc
+        if (tid < kEmTile) {
+            const int cc = tid;
+            for (int r = 0; r < kEmTile; ++r) {
+                double s = (r == cc) ? 1.0 : 0.0;
+                for (int m = cc; m < r; ++m) s -= ta[m * kEmLd + r] * tb[cc * kEmLd + m];
+                tb[cc * kEmLd + r] = (r >= cc) ? s / ta[r * kEmLd + r] : 0.0;
+            }
+        }
+        // panel: L_ik = A_ik L_kk^-T
+        for (int i = k + 1; i < T; ++i) {
+            __syncthreads();
+            em_tile_load(A, lda, i * kEmTile, k0, ta);
+            __syncthreads();
+            em_tile_mm<false>(ta, tb, A, lda, i * kEmTile, k0);
+        }
+        // trailing: A_ij -= L_ik L_jk^T, j <= i
+        for (int j = k + 1; j < T; ++j) {
+            __syncthreads();
+            em_tile_load(A, lda, j * kEmTile, k0, tb);
+            for (int i = j; i < T; ++i) {
+                __syncthreads();
+                em_tile_load(A, lda, i * kEmTile, k0, ta);
+                __syncthreads();
+                em_tile_mm<true>(ta, tb, A, lda, i * kEmTile, j * kEmTile);
+            }
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// v <- L^-T L^-1 v with the factor em_chol_tiled left in A
+__device__ void em_solve_tiled(const double *A, int lda, int T, double *v, double *ta,
+                               double *red) {
+    const int tid = threadIdx.x, i = tid & (kEmTile - 1), q = tid / kEmTile;
+    for (int k = 0; k < T; ++k) {  // L y = v
+        const int k0 = k * kEmTile;
+        double s = 0.0;
+        __syncthreads();
+        for (int j = 0; j < k; ++j) {
+            __syncthreads();
+            em_tile_load(A, lda, k0, j * kEmTile, ta);
+            __syncthreads();
+            for (int m = q * 16; m < q * 16 + 16; ++m) s += ta[m * kEmLd + i] * v[j * kEmTile + m];
+        }
+        red[tid] = s;
+        __syncthreads();
+        em_tile_load(A, lda, k0, k0, ta);
+        __syncthreads();
+        if (tid < kEmTile) {
+            double val = v[k0 + i] - (((red[i] + red[64 + i]) + red[128 + i]) + red[192 + i]);
+            for (int c = 0; c < kEmTile; ++c) {
+                const double yc = __shfl(val, c, 64) / ta[c * kEmLd + c];
+                if (i > c) val -= ta[c * kEmLd + i] * yc;
+                else if (i == c) val = yc;
+            }
+            v[k0 + i] = val;
+        }
+    }
+    for (int k = T - 1; k >= 0; --k) {  // L' x = y
+        const int k0 = k * kEmTile;
+        double s = 0.0;
+        __syncthreads();
+        for (int j = k + 1; j < T; ++j) {
+            __syncthreads();
+            em_tile_load(A, lda, j * kEmTile, k0, ta);  // ta[m][r] = L(j0 + r, k0 + m)
+            __syncthreads();
+            for (int r = q * 16; r < q * 16 + 16; ++r) s += ta[i * kEmLd + r] * v[j * kEmTile + r];
+        }
+        red[tid] = s;
+        __syncthreads();
+        em_tile_load(A, lda, k0, k0, ta);
+        __syncthreads();
+        if (tid < kEmTile) {
+            double val = v[k0 + i] - (((red[i] + red[64 + i]) + red[128 + i]) + red[192 + i]);
+            for (int c = kEmTile - 1; c >= 0; --c) {
+                const double zc = __shfl(val, c, 64) / ta[c * kEmLd + c];
+                if (i < c) val -= ta[i * kEmLd + c] * zc;
+                else if (i == c) val = zc;
+            }
+            v[k0 + i] = val;
+        }
+    }
+    __syncthreads();
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_em_batch_tiled(
+    const double *__restrict__ G, int ldg, const double *__restrict__ bvec, int p, int p_pad,
+    const double *__restrict__ ratios, const double *__restrict__ lambda_max, int r0,
+    double alpha, double tol, int max_iter, double *__restrict__ scratch,
+    double *__restrict__ vecs, int *__restrict__ masks, double *__restrict__ beta_out,
+    int *__restrict__ solves_out) {
+    __shared__ double ta[kEmTile * kEmLd], tb[kEmTile * kEmLd];
+    __shared__ double red[256];
+    __shared__ int cnt[4];
+    __shared__ double dsh;
+    const int tid = threadIdx.x, T = p_pad / kEmTile, r = r0 + (int)blockIdx.x;
+    double *A = scratch + (size_t)blockIdx.x * p_pad * p_pad;
+    double *x = vecs + (size_t)blockIdx.x * 3 * p_pad, *old = x + p_pad, *lam = old + p_pad;
+    int *mask = masks + (size_t)blockIdx.x * p_pad;
+    const double tau = ratios[r], sig = 1.0, lmax = lambda_max[r];
+    const double c1 = alpha * exp((2 - alpha) * (log(tau) - log(sig)));
+    const double c2 = exp(-2 * (log(tau) - log(sig)));
+    double *out = beta_out + (size_t)r * p;
+    for (int i = tid; i < p_pad; i += 256) {
+        mask[i] = i < p;
+        lam[i] = 0.0;
+    }
+    auto form = [&](bool with_lam) {
+        __syncthreads();
+        for (int j = tid / 64; j < p_pad; j += 4)
+            for (int i = j + (tid & 63); i < p_pad; i += 64) {
+                double v;
+                if (i < p && mask[i] && mask[j])  // j <= i < p
+                    v = G[(size_t)j + (size_t)i * ldg] + (with_lam && i == j ? c2 * lam[i] : 0.0);
+                else
+                    v = (i == j) ? 1.0 : 0.0;
+                A[(size_t)i + (size_t)j * p_pad] = v;
+            }
+        for (int i = tid; i < p_pad; i += 256) x[i] = (i < p && mask[i]) ? bvec[i] : 0.0;
+        __syncthreads();
+    };
+    auto fail = [&]() {
+        for (int i = tid; i < p; i += 256) out[i] = 0.0;
+        if (tid == 0) solves_out[r] = -1;
+    };
+    form(false);
+    if (!em_chol_tiled(A, p_pad, T, ta, tb)) return fail();
+    em_solve_tiled(A, p_pad, T, x, ta, red);
+    long total = p;
+    double dist = tol + 1.0;
+    int it = 0;
+    while (dist > tol && it < max_iter) {
+        // expectation step: lambda_j and the active set, coordinate j on thread j % 256
+        int keep = 0;
+        for (int i = tid; i < p; i += 256) {
+            if (!mask[i]) continue;
+            const double l = c1 * exp((alpha - 2) * log(fabs(x[i])));
+            if (l < lmax) {
+                lam[i] = l;
+                old[i] = x[i];
+                ++keep;
+            } else {
+                mask[i] = 0;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) keep += __shfl_xor(keep, o, 64);
+        if ((tid & 63) == 0) cnt[tid >> 6] = keep;
+        __syncthreads();
+        const int num = ((cnt[0] + cnt[1]) + cnt[2]) + cnt[3];
+        if (num == 0) {
+            for (int i = tid; i < p; i += 256) out[i] = 0.0;
+            if (tid == 0) solves_out[r] = it;
+            return;
+        }
+        form(true);
+        if (!em_chol_tiled(A, p_pad, T, ta, tb)) return fail();
+        em_solve_tiled(A, p_pad, T, x, ta, red);
+        total += num;
+        // distance over the active set, summed in coordinate order (as the host loop)
+        if (tid == 0) {
+            double d2 = 0.0;
+            for (int j = 0; j < p; ++j)
+                if (mask[j]) d2 += (x[j] - old[j]) * (x[j] - old[j]);
+            dsh = d2;
+        }
+        __syncthreads();
+        dist = sqrt(dsh);
+        ++it;
+        __syncthreads();
+    }
+    for (int i = tid; i < p; i += 256) out[i] = mask[i] ? x[i] : 0.0;
+    if (tid == 0) solves_out[r] = (int)total;
+}
+
+void launch_em_batch_tiled(hipStream_t s, const double *G, int ldg, const double *b, int p,
+                           int p_pad, const double *ratios, const double *lambda_max, int r0,
+                           int count, double alpha, double tol, int max_iter, double *scratch,
+                           double *vecs, int *masks, double *beta_out, int *solves_out) {
+    k_em_batch_tiled<<<count, 256, 0, s>>>(G, ldg, b, p, p_pad, ratios, lambda_max, r0, alpha,
+                                           tol, max_iter, scratch, vecs, masks, beta_out,
+                                           solves_out);
+}
+
+int em_tile() { return kEmTile; }
+
 void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
                    const DevScalars *sc, const double *c, int p, int p_pad, double *A, int lda,
                    int rhs_col, int packed) {

@@ -423,8 +423,10 @@ int bb_chol_solve(double *x, const double *A, const double *b, int m, int nrhs);
 int bb_bridge_em(double *beta, const double *y, const double *X, int n, int p, double ratio,
                  double alpha, double lambda_max, double tol, int max_iter, int use_cg);
 
-/* trace.beta on the device: bridge EM (direct solves) for every ratio of a grid in ONE
- * launch, a workgroup per ratio, for 1 <= p <= 128.  beta: count x p (row r for ratios[r]),
+/* trace.beta on the device (Code/R/bridge-trace.R:25-54): bridge EM (direct solves) for
+ * every ratio of a grid in ONE launch, a workgroup per ratio (the system in LDS for
+ * p <= 128, in a per-ratio global slice with a tiled Cholesky above; the ratios then run in
+ * chunks that fit half the free device memory, at most 16 GiB).  beta: count x p (row r for ratios[r]),
  * solves: count (bb_bridge_em's return per ratio).  Returns 0 or -1 (bb_last_error()). */
 int bb_bridge_em_batch(double *beta, int *solves, const double *y, const double *X, int n,
                        int p, const double *ratios, const double *lambda_max, int count,

@@ -598,6 +598,32 @@ def test_bridge_em_batch_matches_oracle(gpu_lib, n, p):
     assert np.array_equal(tr["beta"], beta)
 
 
+@pytest.mark.parametrize("n,p", [(400, 129), (500, 200), (700, 300)])
+def test_bridge_em_batch_tiled_matches_oracle(gpu_lib, n, p):
+    """trace.beta's grid for p > 128 (a workgroup per ratio, the p x p system in global
+    memory, tiled Cholesky over LDS tiles) against the EM oracle ratio by ratio: same
+    active sets and solve counts, estimates to 1e-9; trace_beta takes the batched path."""
+    from oracle import em
+    bb = gpu_lib
+    X, y = _em_case(n, p, 11 * p)
+    tol = 1e-9
+    grid = np.exp(np.arange(-6.0, 6.01, 1.0))
+    beta, solves = bb.bridge_em_batch(y, X, grid, alpha=0.5, lambda_max=grid / tol, tol=tol,
+                                      max_iter=30)
+    for r, ratio in enumerate(grid):
+        o, s = em.bridge_em(y, X, ratio, 0.5, ratio / tol, tol, 30)
+        assert solves[r] == s, (ratio, solves[r], s)
+        assert np.array_equal(beta[r] == 0, o == 0), ratio
+        scale = max(np.max(np.abs(o)), 1e-300)
+        assert np.max(np.abs(beta[r] - o)) <= 1e-9 * scale, ratio
+    tr = bb.trace_beta(y, X, ratio_grid=grid)
+    assert np.array_equal(tr["beta"], beta)
+    # a ratio's result does not depend on the batch it runs in
+    b1, s1 = bb.bridge_em_batch(y, X, grid[3:4], alpha=0.5, lambda_max=grid[3:4] / tol,
+                                tol=tol, max_iter=30)
+    assert np.array_equal(b1[0], beta[3]) and s1[0] == solves[3]
+
+
 # ---------------------------------------------------------------------------------------
 # The Ozaki-II Gram on the prior variances the chain actually produces, and a long
 # free-running p > n chain against an independent oracle chain (statistical parity).

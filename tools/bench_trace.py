@@ -1,6 +1,6 @@
-"""trace.beta timing: the default 401-ratio grid (bridge-trace.R) on a 442 x 10 design,
-one device launch (bb_bridge_em_batch) against the per-ratio bridge_EM loop, plus the
-numpy oracle loop (oracle/em.py) for scale."""
+"""trace.beta timing: the default 401-ratio grid (bridge-trace.R) on a 442 x 10 design (or
+n x p: `python tools/bench_trace.py [p [n]]`), one device launch (bb_bridge_em_batch)
+against the per-ratio bridge_EM loop, plus the numpy oracle loop (oracle/em.py) for scale."""
 import os
 import sys
 import time
@@ -12,9 +12,15 @@ import bayesbridge_amd as bb  # noqa: E402
 from oracle import em  # noqa: E402
 
 rng = np.random.default_rng(4)
-n, p = 442, 10
+p = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+n = int(sys.argv[2]) if len(sys.argv) > 2 else max(442, 2 * p)
 X = rng.standard_normal((n, p))
-y = X @ np.array([3, -2, 1.5, 0, 0, 0.5, 0, 0, -1, 0.0]) + rng.standard_normal(n)
+if p == 10:
+    b = np.array([3, -2, 1.5, 0, 0, 0.5, 0, 0, -1, 0.0])
+else:
+    b = np.zeros(p)
+    b[:max(3, p // 10)] = rng.uniform(0.5, 3, max(3, p // 10))
+y = X @ b + rng.standard_normal(n)
 grid = np.exp(np.arange(-20.0, 20.0 + 1e-9, 0.1))
 tol = 1e-9
 bb.set_verbose(0)
