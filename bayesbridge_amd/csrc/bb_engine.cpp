@@ -2804,7 +2804,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 3: {
             const int old = g_sp_nt;
-            if (value >= 0) g_sp_nt = value ? 1 : 0;
+            if (value >= 0) g_sp_nt = value > 3 ? 3 : value;
             return old;
         }
         default: return -1;

@@ -61,6 +61,6 @@ void launch_sp_beta(hipStream_t s, const int *colptr, const int *rowidx, const d
                     int p_loc, const double *w, const double *u, const double *D,
                     const DevScalars *sc, double *beta, double *beta_trace);
 
-extern int g_sp_nt;  // non-temporal pair-list loads in k_sp_gram_col (bb_set_tuning key 3)
+extern int g_sp_nt;  // sparse Gram variant (bb_set_tuning key 3, bb_sparse.hip)
 
 }  // namespace bb

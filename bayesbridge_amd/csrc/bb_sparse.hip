@@ -186,8 +186,8 @@ void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, c
     k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out);
 }
 
-// Gram by output column (the production kernel when every row of X has at most
-// kSpColMaxRow non-zeros).  All pairs of the entries (r, c), r < c, share row c of X, so
+// Gram by output column (used when every row of X has at most kSpColMaxRow non-zeros;
+// k_sp_gram_flat below is the default form).  All pairs of the entries (r, c), r < c, share row c of X, so
 // their columns j lie in row c's support J_c: the workgroup stages D[J_c] in LDS once and
 // the pairs carry 16-bit positions into J_c instead of 32-bit column indices -- the
 // per-pair D gathers become LDS reads and the pair stream shrinks to 10 bytes.  The same
@@ -261,17 +261,143 @@ __global__ __launch_bounds__(256) void k_sp_gram_col(
     }
 }
 
+// The same Gram with the pair stream read flat (the production kernel since round 3):
+// the workgroup of column c walks its pair range [estart(0, c), estart(c, c)) in chunks of
+// 256 x kSpFlatV pairs, lane t loading pairs t, t + 256, ... (full-width coalesced loads;
+// the next chunk is requested as soon as the current one is staged), stages the products
+// prod_k D[J_c(idx_k)] in LDS, and one thread per entry intersecting the chunk sums its
+// pairs left to right, an entry that runs past the chunk carrying its partial sum into the
+// next one.  Deterministic: every entry is a plain left-to-right sum of its pairs.
+// Measured at C5 (`tools/sp_nt_ab.py`, same box, alternating): 16 pairs per lane 0.66-0.69
+// ms against 0.71-0.74 for k_sp_gram_col, 8 per lane 0.70-0.73; two chunks in flight per
+// workgroup no faster, and 4 consecutive pairs per lane (16-byte loads) 0.75.
+template <int kSpFlatV>
+__global__ __launch_bounds__(256) void k_sp_gram_flat(
+    const int *__restrict__ rowptr, const int *__restrict__ colidx,
+    const double *__restrict__ rval, const unsigned *__restrict__ estart,
+    const double *__restrict__ prod, const unsigned short *__restrict__ pidx,
+    const double *__restrict__ D, const double *__restrict__ u, int n_pad,
+    double *__restrict__ tri, double *__restrict__ xu) {
+    extern __shared__ double Dl[];  // D over row c's support
+    constexpr int kSpFlatCap = 256 * kSpFlatV;
+    __shared__ double vals[kSpFlatCap];
+    __shared__ double red[2][4];
+    __shared__ double carry_s[2];
+    __shared__ int next_s[2];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = n_pad - 1 - (int)blockIdx.x;
+    const int k0 = rowptr[c], nk = rowptr[c + 1] - k0;
+    double sd = 0.0, su = 0.0;
+    // row c's support, 4 entries per thread in flight (the same per-thread sum order)
+    for (int l0 = tid; l0 < nk; l0 += 4 * 256) {
+        int jv[4];
+        double xv[4], dv[4], uv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int l = l0 + q * 256;
+            jv[q] = l < nk ? colidx[k0 + l] : 0;
+            xv[q] = l < nk ? rval[k0 + l] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            dv[q] = l0 + q * 256 < nk ? D[jv[q]] : 0.0;
+            uv[q] = u && l0 + q * 256 < nk ? u[jv[q]] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (l0 + q * 256 < nk) {
+                Dl[l0 + q * 256] = dv[q];
+                sd += xv[q] * xv[q] * dv[q];
+                if (u) su += xv[q] * uv[q];
+            }
+        }
+    }
+    sd = group_sum<64>(sd);
+    su = group_sum<64>(su);
+    if (lane == 0) {
+        red[0][wid] = sd;
+        red[1][wid] = su;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        tri[tri_index(c, c)] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        if (xu) xu[c] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+    const size_t e0 = tri_index(0, c);
+    const unsigned P0 = estart[e0], P1 = estart[e0 + c];
+    // the next chunk is requested as soon as this one is staged
+    double pv[kSpFlatV];
+    unsigned short iv[kSpFlatV];
+#pragma unroll
+    for (int q = 0; q < kSpFlatV; ++q) {
+        const unsigned k = P0 + q * 256 + tid;
+        pv[q] = k < P1 ? prod[k] : 0.0;
+        iv[q] = k < P1 ? pidx[k] : (unsigned short)0;
+    }
+    int ra = 0, par = 0;
+    double carry = 0.0;
+    unsigned pa = P0;
+    if (tid == 0) next_s[0] = next_s[1] = c;  // (every chunk overwrites its slot)
+    while (pa < P1) {
+        const unsigned pb = min(pa + (unsigned)kSpFlatCap, P1);
+#pragma unroll
+        for (int q = 0; q < kSpFlatV; ++q)
+            vals[q * 256 + tid] = pa + q * 256 + tid < pb ? pv[q] * Dl[iv[q]] : 0.0;
+#pragma unroll
+        for (int q = 0; q < kSpFlatV; ++q) {
+            const unsigned k = pa + kSpFlatCap + q * 256 + tid;
+            pv[q] = k < P1 ? prod[k] : 0.0;
+            iv[q] = k < P1 ? pidx[k] : (unsigned short)0;
+        }
+        __syncthreads();
+        for (int r = ra + tid; r < c; r += 256) {
+            const unsigned st = estart[e0 + r];
+            if (st >= pb) break;
+            const unsigned en = estart[e0 + r + 1];
+            const unsigned lo = st < pa ? pa : st, hi = en < pb ? en : pb;
+            double s = st < pa ? carry : 0.0;
+            unsigned k = lo;
+            for (; k + 4 <= hi; k += 4) {  // 4 LDS reads in flight, adds in order
+                const double v0 = vals[k - pa], v1 = vals[k + 1 - pa], v2 = vals[k + 2 - pa],
+                             v3 = vals[k + 3 - pa];
+                s += v0;
+                s += v1;
+                s += v2;
+                s += v3;
+            }
+            for (; k < hi; ++k) s += vals[k - pa];
+            if (en <= pb) tri[e0 + r] = s;
+            if (en >= pb) {  // the chunk's last entry (exactly one: st < pb <= en)
+                next_s[par] = en > pb ? r : r + 1;  // it runs on: carry its partial sum
+                carry_s[par] = s;
+            }
+        }
+        __syncthreads();  // (parity slots: the ones written here were last read two chunks ago)
+        carry = carry_s[par];  // used only if entry ra continues (starts before pb)
+        ra = next_s[par];
+        pa = pb;
+        par ^= 1;
+    }
+    for (int r = ra + tid; r < c; r += 256) tri[e0 + r] = 0.0;  // empty entries past P1
+}
+
 int sp_col_max_row() { return kSpColMaxRow; }
 
-// non-temporal pair-list loads (bb_set_tuning key 3)
-int g_sp_nt = 0;
+// sparse Gram variant (bb_set_tuning key 3): 0 lanes per entry (k_sp_gram_col), 1 the same
+// with non-temporal pair-list loads, 2 / 3 (the default) the flat chunked stream
+// (k_sp_gram_flat) with 8 / 16 pairs per lane per chunk
+int g_sp_nt = 3;
 
 void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                         const unsigned *estart, const double *prod, const unsigned short *pidx,
                         const double *D, const double *u, int n_pad, int max_row, double *tri,
                         double *xu) {
     const size_t lds = (size_t)(max_row > 0 ? max_row : 1) * sizeof(double);
-    if (g_sp_nt)
+    if (g_sp_nt >= 2) {
+        auto kern = g_sp_nt == 2 ? k_sp_gram_flat<8> : k_sp_gram_flat<16>;
+        kern<<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad, tri,
+                                     xu);
+    } else if (g_sp_nt)
         k_sp_gram_col<true><<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D,
                                                     u, n_pad, tri, xu);
     else

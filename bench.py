@@ -263,7 +263,12 @@ def roofline_for(phase, ms, ctx, traffic_world):
             si = eng.sparse_info()
             if si["col_mode"]:
                 byts = 10.0 * si["pairs"] + 12.0 * ntri + 12.0 * si["nnz"] + 16.0 * p_loc
-                kname, kfull = "k_sp_gram_col (pair-list Gram by output column)", "bb::k_sp_gram_col"
+                if bb.set_tuning(3, -1) >= 2:  # the flat chunked stream (the default)
+                    kname, kfull = ("k_sp_gram_flat (pair-list Gram by output column, flat "
+                                    "stream)", "bb::k_sp_gram_flat")
+                else:
+                    kname, kfull = ("k_sp_gram_col (pair-list Gram by output column)",
+                                    "bb::k_sp_gram_col")
             else:
                 byts = 12.0 * si["pairs"] + 12.0 * ntri + 8.0 * p_loc
                 kname, kfull = "k_sp_gram (pair-list Gram)", "bb::k_sp_gram"

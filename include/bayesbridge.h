@@ -327,7 +327,8 @@ void bb_set_trace_budget(long long bytes);
 /* A/B tuning knobs (measurement tools only).  key 1: the Ozaki residue-plane stores
  * non-temporal (value 1), ordinary (0), or non-temporal stores and X loads (2, the default);
  * key 2: non-temporal X loads in the fused beta / X.beta pass (1, the default) or ordinary (0);
- * key 3: non-temporal pair-list loads in the sparse Gram (1) or ordinary (0).  A negative value changes nothing.  Returns the
+ * key 3: the sparse Gram kernel: lanes per entry (0), the same with non-temporal pair-list
+ * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane.  A negative value changes nothing.  Returns the
  * previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

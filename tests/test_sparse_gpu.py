@@ -33,13 +33,22 @@ def rand_csc(n, p, density, seed, dense_cols=(), empty_rows=()):
     return X
 
 
+@pytest.fixture(params=[0, 2, 3], ids=["lanes", "flat8", "flat16"])
+def sp_variant(request, gpu_lib):
+    """The by-column sparse Gram kernels: lanes per entry (0) and the flat chunked pair
+    stream with 8 or 16 pairs per lane (2, 3 = the production default), bb_set_tuning key 3."""
+    old = gpu_lib.set_tuning(3, request.param)
+    yield request.param
+    gpu_lib.set_tuning(3, old)
+
+
 @pytest.mark.parametrize("n,p,density,extra", [
     (100, 500, 0.05, {}),
     (130, 2000, 0.02, dict(dense_cols=(0, 777), empty_rows=(5, 129))),  # ragged n, edges
     (257, 4000, 0.01, {}),
     (64, 3, 0.5, {}),                                                    # p < 64, tiny
 ])
-def test_sparse_gram_matches_scipy(gpu_lib, n, p, density, extra):
+def test_sparse_gram_matches_scipy(gpu_lib, sp_variant, n, p, density, extra):
     bb = gpu_lib
     X = rand_csc(n, p, density, n + p, **extra)
     rng = np.random.default_rng(3)
@@ -79,7 +88,7 @@ def test_sparse_gram_general_kernel_dense_row(gpu_lib):
     assert np.allclose(xu, X @ u, rtol=1e-12, atol=1e-12)
 
 
-def test_sparse_gram_exact_on_integers(gpu_lib):
+def test_sparse_gram_exact_on_integers(gpu_lib, sp_variant):
     """Integer X and D: every partial sum is an exact integer, so the pair-list Gram must
     equal the int64 product bit for bit (pins the pair placement and segment starts)."""
     bb = gpu_lib
@@ -88,6 +97,27 @@ def test_sparse_gram_exact_on_integers(gpu_lib):
     X = rand_csc(n, p, 0.03, 9, dense_cols=(17,))
     X.data = rng.integers(-50, 51, size=X.data.size).astype(np.float64)
     D = rng.integers(0, 7, size=p).astype(np.float64)
+    C, _ = bb.sparse_gram(X, D)
+    Xi = X.toarray().astype(np.int64)
+    ref = (Xi * D.astype(np.int64)) @ Xi.T
+    assert np.array_equal(C, ref.astype(np.float64))
+
+
+def test_sparse_gram_flat_long_entries(gpu_lib, sp_variant):
+    """Entries with thousands of pairs (two dense-ish rows over many columns) run across
+    several of the flat kernel's 2048-pair chunks, carrying their partial sums; empty
+    entries sit between them.  Integer data: bit-exact."""
+    bb = gpu_lib
+    rng = np.random.default_rng(21)
+    n, p = 200, 12000
+    X = rand_csc(n, p, 0.002, 22).tolil()
+    for r in (3, 150, 151):
+        cols = rng.choice(p, 5000, replace=False)
+        X[r, cols] = rng.integers(1, 9, size=(1, 5000)).astype(np.float64)
+    X = sps.csc_matrix(X)
+    X.data = np.round(X.data * 4)
+    X.eliminate_zeros()
+    D = rng.integers(0, 4, size=p).astype(np.float64)
     C, _ = bb.sparse_gram(X, D)
     Xi = X.toarray().astype(np.int64)
     ref = (Xi * D.astype(np.int64)) @ Xi.T

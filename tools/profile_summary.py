@@ -115,7 +115,8 @@ def main():
     if sparse:  # the pair-list Gram's algorithmic bytes as bench.py counts them
         rf = bench["roofline"] if bench["roofline"].get("phase") == "gram" else \
             bench.get("roofline_secondary", {})
-        algo = {"bb::k_sp_gram_col": rf.get("algorithmic_bytes_per_launch")}
+        algo = {k: rf.get("algorithmic_bytes_per_launch") for k in out["kernels"]
+                if k.startswith("bb::k_sp_gram_col") or k.startswith("bb::k_sp_gram_flat")}
     out["workload"]["name"] = wl or None
     out["gram_kernels"] = {}
     for k, a in algo.items():

@@ -1,6 +1,8 @@
-"""A/B of non-temporal pair-list loads in the sparse Gram (bb_set_tuning key 3) on one C5
-engine (n = 5000, p = 200000, density 0.01); prints the gram phase (HIP events at phase
-starts, 10 sweeps each), alternating.  Usage: python tools/sp_nt_ab.py"""
+"""A/B of the sparse Gram kernels (bb_set_tuning key 3: 0 lanes per entry, 1 the same with
+non-temporal loads, 2 the flat chunked stream) on one C5 engine (n = 5000, p = 200000,
+density 0.01); prints the gram phase (HIP events at phase starts, 10 sweeps each),
+alternating, and the largest difference between the variants' Grams on one D.
+Usage: python tools/sp_nt_ab.py [variants, default 0,2,0,2]"""
 import os
 import sys
 
@@ -18,7 +20,8 @@ t = 1
 e.run(t, 10, first_slot=-1)
 t += 10
 e.sync()
-for nt in (0, 1, 0, 1):
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2,0,2").split(",")]
+for nt in variants:
     bb.set_tuning(3, nt)
     e.enable_timing(True, phases=True)
     e.reset_timing()
@@ -30,3 +33,18 @@ for nt in (0, 1, 0, 1):
           flush=True)
 bb.set_tuning(3, 0)
 e.close()
+import numpy as np  # noqa: E402
+import scipy.sparse as sps  # noqa: E402
+
+Xs = sps.csc_matrix(sps.hstack(X) if isinstance(X, list) else X)
+rng = np.random.default_rng(5)
+D = 10.0 ** rng.uniform(-8, 0, p)
+outs = {}
+for v in sorted(set(variants)):
+    bb.set_tuning(3, v)
+    outs[v] = bb.sparse_gram(Xs, D)[0]
+bb.set_tuning(3, 0)
+base = outs[min(outs)]
+for v, C in outs.items():
+    print(f"variant {v}: max |C - C0| / max|C0| = "
+          f"{np.max(np.abs(C - base)) / np.max(np.abs(base)):.3e}", flush=True)
