@@ -2807,6 +2807,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_sp_nt = value > 3 ? 3 : value;
             return old;
         }
+        case 4: {
+            const int old = g_lam_occ;
+            if (value >= 0) g_lam_occ = value ? 1 : 0;
+            return old;
+        }
         default: return -1;
     }
 }

@@ -176,11 +176,11 @@ struct PgTail {
 };
 
 template <int L>
-__global__ __launch_bounds__(256) void k_lambda_spec(const double *beta, int p_loc, int p_pad,
-                                                     uint64_t j0, const DevScalars *sc, Key key,
-                                                     uint64_t t, int mode, double *lam, double *D,
-                                                     double *u, double *lam_trace,
-                                                     uint32_t *err, int lam_blocks, PgTail pgt) {
+__device__ __forceinline__ void lambda_spec_body(const double *beta, int p_loc, int p_pad,
+                                                 uint64_t j0, const DevScalars *sc, Key key,
+                                                 uint64_t t, int mode, double *lam, double *D,
+                                                 double *u, double *lam_trace, uint32_t *err,
+                                                 int lam_blocks, const PgTail &pgt) {
     if ((int)blockIdx.x >= lam_blocks) {
         pg_draw_at(((int)blockIdx.x - lam_blocks) * 256 + (int)threadIdx.x, pgt.psi, pgt.n,
                    pgt.n_pad, key, t, pgt.omega, err);
@@ -211,6 +211,26 @@ __global__ __launch_bounds__(256) void k_lambda_spec(const double *beta, int p_l
     }
 }
 
+// The sampler needs 157 VGPRs inlined (3 waves per SIMD); the O4 instance is capped at 128
+// (4 waves per SIMD, a few spills to scratch) -- bb_set_tuning key 4 selects it for A/B.
+#define BB_LAMBDA_SPEC_ARGS                                                                  \
+    const double *beta, int p_loc, int p_pad, uint64_t j0, const DevScalars *sc, Key key,    \
+        uint64_t t, int mode, double *lam, double *D, double *u, double *lam_trace,          \
+        uint32_t *err, int lam_blocks, PgTail pgt
+template <int L>
+__global__ __launch_bounds__(256) void k_lambda_spec(BB_LAMBDA_SPEC_ARGS) {
+    lambda_spec_body<L>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
+                        lam_blocks, pgt);
+}
+template <int L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
+    lambda_spec_body<L>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
+                        lam_blocks, pgt);
+}
+#undef BB_LAMBDA_SPEC_ARGS
+int g_lam_occ = 0;  // bb_set_tuning key 4: 1 = the 4-wave instances of the lambda launches
+
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
 // as long as its slowest wave, and a wave is as long as the slowest of its G-lane groups'
 // draws; here each workgroup owns a contiguous range of coefficients and a group that has
@@ -235,13 +255,11 @@ static int device_cus_lam() {
 }
 
 template <int G>
-__global__ __launch_bounds__(kLamCbWG) void k_lambda_cb(const double *beta, int p_loc, int p_pad,
-                                                        int per_wg, uint64_t j0,
-                                                        const DevScalars *sc, Key key, uint64_t t,
-                                                        int mode, double *lam, double *D,
-                                                        double *u, double *lam_trace,
-                                                        uint32_t *err) {
-    __shared__ int s_next;
+__device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, int p_pad,
+                                               int per_wg, uint64_t j0, const DevScalars *sc,
+                                               Key key, uint64_t t, int mode, double *lam,
+                                               double *D, double *u, double *lam_trace,
+                                               uint32_t *err, int &s_next) {
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1), gbase = lane & ~(G - 1);
     const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << (G & 63)) - 1ull);
@@ -329,6 +347,25 @@ __global__ __launch_bounds__(kLamCbWG) void k_lambda_cb(const double *beta, int 
     if (have) atomicOr(err, 2u);  // bounded: a draw that never finished is flagged
 }
 
+#define BB_LAMBDA_CB_ARGS                                                                    \
+    const double *beta, int p_loc, int p_pad, int per_wg, uint64_t j0, const DevScalars *sc, \
+        Key key, uint64_t t, int mode, double *lam, double *D, double *u, double *lam_trace,  \
+        uint32_t *err
+template <int G>
+__global__ __launch_bounds__(kLamCbWG) void k_lambda_cb(BB_LAMBDA_CB_ARGS) {
+    __shared__ int s_next;
+    lambda_cb_body<G>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u, lam_trace,
+                      err, s_next);
+}
+template <int G>
+__global__ __launch_bounds__(kLamCbWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_lambda_cb_o4(BB_LAMBDA_CB_ARGS) {
+    __shared__ int s_next;
+    lambda_cb_body<G>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u, lam_trace,
+                      err, s_next);
+}
+#undef BB_LAMBDA_CB_ARGS
+
 bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                       const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int group,
                       double *lam, double *lam_trace, const double *psi, int n, int n_pad,
@@ -340,14 +377,14 @@ bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, u
     (void)group;
     if (p_loc <= kLamSpecWide) {
         const int lb = (p_pad + 3) / 4;
-        k_lambda_spec<64><<<lb + pgb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
-                                                   LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
-                                                   err, lb, pgt);
+        (g_lam_occ ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb + pgb, 256, 0, s>>>(
+            beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
+            err, lb, pgt);
     } else {
         const int lb = (p_pad + 15) / 16;
-        k_lambda_spec<16><<<lb + pgb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t,
-                                                   LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
-                                                   err, lb, pgt);
+        (g_lam_occ ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb + pgb, 256, 0, s>>>(
+            beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
+            err, lb, pgt);
     }
     return true;
 }
@@ -363,12 +400,14 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     if (p_loc <= kLamSpecMax) {
         if (p_loc <= kLamSpecWide) {
             const int lb = (p_pad + 3) / 4;
-            k_lambda_spec<64><<<lb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,
-                                                 u, lam_trace, err, lb, PgTail{});
+            (g_lam_occ ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb, 256, 0, s>>>(
+                beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
+                PgTail{});
         } else {
             const int lb = (p_pad + 15) / 16;
-            k_lambda_spec<16><<<lb, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D,
-                                                 u, lam_trace, err, lb, PgTail{});
+            (g_lam_occ ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb, 256, 0, s>>>(
+                beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
+                PgTail{});
         }
         return;
     }
@@ -376,7 +415,8 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
         // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy)
         const int nwg = std::max(1, std::min(4 * device_cus_lam(), (p_pad + 31) / 32));
         const int per = (p_pad + nwg - 1) / nwg;
-        k_lambda_cb<8><<<(p_pad + per - 1) / per, kLamCbWG, 0, s>>>(
+        (g_lam_occ ? k_lambda_cb_o4<8> : k_lambda_cb<8>)<<<(p_pad + per - 1) / per, kLamCbWG, 0,
+                                                            s>>>(
             beta, p_loc, p_pad, per, j0, sc, key, t, mode, lam, D, u, lam_trace, err);
         return;
     }

@@ -309,10 +309,12 @@ int bb_group_sync(bb_group *g);
 
 /*
  * .C driver controls.  bb_set_device_count(k) lets bridge_reg_stable / bridge_reg_stable_csc
- * shard the columns of a p > n (Woodbury, alpha known, non-ortho) problem over up to k
- * visible devices in one process (>= 4096 columns per device, an RCCL group; 0: every
- * visible device).  The default is 1 (opt-in): a sharded chain sums its Gram in another
- * fp64 order, and p > n chains amplify roundoff, so a trace depends on the device count.  Traces live on the device in a ring of at most `bytes` per engine (default
+ * shard the columns of a p > n problem (stable mixture: Woodbury or orthogonal design, alpha
+ * known or drawn by MH) over up to k visible devices in one process (>= 4096 columns per
+ * device, an RCCL group; 0: every visible device).  The default is 1 (opt-in): a sharded
+ * chain sums its Gram in another fp64 order, and p > n chains amplify roundoff, so a trace
+ * depends on the device count.  Traces live on the device in a ring of at most `bytes` per
+ * engine (default
  * 1 GiB), copied out to the caller's P x M buffers whenever it fills, so M is not bounded by
  * HBM.  Every 10 sweeps the driver polls R's interrupt (R_CheckUserInterrupt under
  * R_ToplevelExec, as BridgeWrapper.cpp:273-275 polls), stops, releases the device, returns
@@ -328,8 +330,10 @@ void bb_set_trace_budget(long long bytes);
  * non-temporal (value 1), ordinary (0), or non-temporal stores and X loads (2, the default);
  * key 2: non-temporal X loads in the fused beta / X.beta pass (1, the default) or ordinary (0);
  * key 3: the sparse Gram kernel: lanes per entry (0), the same with non-temporal pair-list
- * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane.  A negative value changes nothing.  Returns the
- * previous value, or -1 for an unknown key. */
+ * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane;
+ * key 4: the lambda launches (k_lambda_spec, k_lambda_cb) at their register-minimal 3 waves
+ * per SIMD (0, the default) or capped at 128 VGPRs for 4 waves (1); the draws are the same.
+ * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
 void bb_debug_interrupt_after(int polls);

@@ -1,0 +1,35 @@
+"""The lambda launches' two occupancy instances (bb_set_tuning key 4) draw the same chain.
+
+k_lambda_spec<16> (1024 < p <= 50000) and k_lambda_cb<8> (p > 50000) each exist at their
+register-minimal 3 waves per SIMD and capped at 128 VGPRs for 4 waves per SIMD; both run
+the sequential retstable_LD loop of every coefficient on its own counters
+(retstable.cpp:94-271, BridgeRegression.cpp:506-510), so the traces must be bit-identical."""
+import numpy as np
+import pytest
+
+from tests.conftest import synthetic_problem
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,p", [(200, 3000), (60, 60000)])
+def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(n, p, seed=11, s=10)
+    traces = []
+    old = bb.set_tuning(4, -1)
+    try:
+        for occ in (0, 1):
+            bb.set_tuning(4, occ)
+            e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=6,
+                                          seed=77, stream=0), X, y)
+            e.init_state()
+            e.run(1, 6, first_slot=0)
+            e.sync()
+            assert e.error_flags() == 0
+            traces.append(e.trace(0, 6))
+            e.close()
+    finally:
+        bb.set_tuning(4, old)
+    for k in ("beta", "lambda", "tau", "sig2"):
+        assert np.array_equal(traces[0][k], traces[1][k]), k
