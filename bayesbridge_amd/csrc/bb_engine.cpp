@@ -2809,7 +2809,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 4: {
             const int old = g_lam_occ;
-            if (value >= 0) g_lam_occ = value ? 1 : 0;
+            if (value >= 0) g_lam_occ = value & 3;
             return old;
         }
         default: return -1;

@@ -229,7 +229,10 @@ k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
                         lam_blocks, pgt);
 }
 #undef BB_LAMBDA_SPEC_ARGS
-int g_lam_occ = 0;  // bb_set_tuning key 4: 1 = the 4-wave instances of the lambda launches
+// bb_set_tuning key 4: bit 0 = k_lambda_spec at 4 waves per SIMD, bit 1 = k_lambda_cb at 4.
+// Measured (tools/lambda_occ_ab.py, three alternations): C3 k_lambda_spec<16> 0.200-0.208 ms at
+// either occupancy; C5 k_lambda_cb<8> 0.418-0.428 -> 0.402-0.407 ms at 4 waves.  Default 2.
+int g_lam_occ = 2;
 
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
 // as long as its slowest wave, and a wave is as long as the slowest of its G-lane groups'
@@ -377,12 +380,12 @@ bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, u
     (void)group;
     if (p_loc <= kLamSpecWide) {
         const int lb = (p_pad + 3) / 4;
-        (g_lam_occ ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb + pgb, 256, 0, s>>>(
+        ((g_lam_occ & 1) ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb + pgb, 256, 0, s>>>(
             beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
             err, lb, pgt);
     } else {
         const int lb = (p_pad + 15) / 16;
-        (g_lam_occ ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb + pgb, 256, 0, s>>>(
+        ((g_lam_occ & 1) ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb + pgb, 256, 0, s>>>(
             beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
             err, lb, pgt);
     }
@@ -400,12 +403,12 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     if (p_loc <= kLamSpecMax) {
         if (p_loc <= kLamSpecWide) {
             const int lb = (p_pad + 3) / 4;
-            (g_lam_occ ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb, 256, 0, s>>>(
+            ((g_lam_occ & 1) ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb, 256, 0, s>>>(
                 beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
                 PgTail{});
         } else {
             const int lb = (p_pad + 15) / 16;
-            (g_lam_occ ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb, 256, 0, s>>>(
+            ((g_lam_occ & 1) ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb, 256, 0, s>>>(
                 beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
                 PgTail{});
         }
@@ -415,7 +418,7 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
         // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy)
         const int nwg = std::max(1, std::min(4 * device_cus_lam(), (p_pad + 31) / 32));
         const int per = (p_pad + nwg - 1) / nwg;
-        (g_lam_occ ? k_lambda_cb_o4<8> : k_lambda_cb<8>)<<<(p_pad + per - 1) / per, kLamCbWG, 0,
+        ((g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>)<<<(p_pad + per - 1) / per, kLamCbWG, 0,
                                                             s>>>(
             beta, p_loc, p_pad, per, j0, sc, key, t, mode, lam, D, u, lam_trace, err);
         return;

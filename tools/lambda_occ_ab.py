@@ -1,5 +1,5 @@
 """A/B of the lambda launches' occupancy (bb_set_tuning key 4: 0 = the register-minimal
-instances at 3 waves per SIMD, 1 = capped at 128 VGPRs for 4 waves per SIMD) on the C3
+instances at 3 waves per SIMD, 3 = both capped at 128 VGPRs for 4 waves per SIMD) on the C3
 (k_lambda_spec<16>) and C5 (k_lambda_cb<8>) engines, from a steady state reached after 30
 sweeps; alternates the variants and prints the lambda phase time (HIP events at phase starts,
 20 sweeps each).  It also checks that both variants draw the same chain: one sweep from the
@@ -26,7 +26,7 @@ for wl in sys.argv[1:] or ["c3", "c5"]:
     e.sync()
     st = e.state()
     outs = []
-    for occ in (0, 1):
+    for occ in (0, 3):
         bb.set_tuning(4, occ)
         e.set_state(st["beta"], st["tau"], st["sig2"], st["alpha"])
         e.run(t, 1, first_slot=-1)
@@ -36,7 +36,7 @@ for wl in sys.argv[1:] or ["c3", "c5"]:
     print(f"{wl}: one sweep from the same state, beta bit-identical across variants: {same}",
           flush=True)
     t += 1
-    for occ in (0, 1, 0, 1, 0, 1):
+    for occ in (0, 3, 0, 3, 0, 3):
         bb.set_tuning(4, occ)
         e.enable_timing(True, phases=True)
         e.reset_timing()
@@ -46,7 +46,7 @@ for wl in sys.argv[1:] or ["c3", "c5"]:
         ph = e.phase_times()
         print(f"{wl} occ={occ}: lambda {ph['lambda']:.4f} ms  sweep {sum(ph.values()):.4f} ms",
               flush=True)
-    bb.set_tuning(4, 0)
+    bb.set_tuning(4, 2)
     e.close()
     if not same:
         sys.exit(1)
