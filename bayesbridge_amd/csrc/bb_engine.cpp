@@ -2812,6 +2812,12 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_lam_occ = value & 3;
             return old;
         }
+        case 5: {
+            const int old = g_lam_lanes;
+            if (value == 0 || value == 8 || value == 16 || value == 32 || value == 64)
+                g_lam_lanes = value;
+            return old;
+        }
         default: return -1;
     }
 }

@@ -369,6 +369,32 @@ k_lambda_cb_o4(BB_LAMBDA_CB_ARGS) {
 }
 #undef BB_LAMBDA_CB_ARGS
 
+// One speculative lambda launch with L lanes per coefficient (the draws do not depend on L);
+// pgb trailing workgroups draw the logistic omegas.  g_lam_lanes (bb_set_tuning key 5)
+// overrides the default L for A/B measurements.
+int g_lam_lanes = 0;
+static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p_loc, int p_pad,
+                        uint64_t j0, const DevScalars *sc, Key key, uint64_t t, int mode,
+                        double *lam, double *D, double *u, double *lam_trace, uint32_t *err,
+                        const PgTail &pgt) {
+    if (g_lam_lanes) L = g_lam_lanes;
+    const int per = 256 / L;
+    const int lb = (p_pad + per - 1) / per;
+    const bool o4 = (g_lam_occ & 1) != 0;
+    switch (L) {
+#define BB_SPEC_CASE(LL)                                                                      \
+    case LL:                                                                                  \
+        (o4 ? k_lambda_spec_o4<LL> : k_lambda_spec<LL>)<<<lb + pgb, 256, 0, s>>>(             \
+            beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb, pgt);    \
+        break;
+        BB_SPEC_CASE(8)
+        BB_SPEC_CASE(32)
+        BB_SPEC_CASE(64)
+        default: BB_SPEC_CASE(16)
+#undef BB_SPEC_CASE
+    }
+}
+
 bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                       const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int group,
                       double *lam, double *lam_trace, const double *psi, int n, int n_pad,
@@ -378,17 +404,8 @@ bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, u
     const PgTail pgt{psi, n, n_pad, omega};
     const int pgb = (n_pad + 255) / 256;
     (void)group;
-    if (p_loc <= kLamSpecWide) {
-        const int lb = (p_pad + 3) / 4;
-        ((g_lam_occ & 1) ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb + pgb, 256, 0, s>>>(
-            beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
-            err, lb, pgt);
-    } else {
-        const int lb = (p_pad + 15) / 16;
-        ((g_lam_occ & 1) ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb + pgb, 256, 0, s>>>(
-            beta, p_loc, p_pad, j0, sc, key, t, LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace,
-            err, lb, pgt);
-    }
+    launch_spec(s, p_loc <= kLamSpecWide ? 64 : 16, pgb, beta, p_loc, p_pad, j0, sc, key, t,
+                LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace, err, pgt);
     return true;
 }
 
@@ -401,17 +418,8 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
     if (p_loc <= kLamSpecMax) {
-        if (p_loc <= kLamSpecWide) {
-            const int lb = (p_pad + 3) / 4;
-            ((g_lam_occ & 1) ? k_lambda_spec_o4<64> : k_lambda_spec<64>)<<<lb, 256, 0, s>>>(
-                beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
-                PgTail{});
-        } else {
-            const int lb = (p_pad + 15) / 16;
-            ((g_lam_occ & 1) ? k_lambda_spec_o4<16> : k_lambda_spec<16>)<<<lb, 256, 0, s>>>(
-                beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb,
-                PgTail{});
-        }
+        launch_spec(s, p_loc <= kLamSpecWide ? 64 : 16, 0, beta, p_loc, p_pad, j0, sc, key, t,
+                    mode, lam, D, u, lam_trace, err, PgTail{});
         return;
     }
     if (ni && group == 8) {
