@@ -164,6 +164,10 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
 //                    k_lambda(_cb) 76 / 101 / 141 / 216 us;
 //   p = 200000 (C5, alpha = 0.3):      L = 16 0.61 ms against k_lambda_cb 0.42 ms.
 constexpr int kLamSpecWide = 1024;  // L = 64 up to here, L = 16 above
+// ... and L = 8 above kLamSpecNarrow (round 3, tools/lambda_lanes_ab.py, two alternations from
+// a steady state: C3 p = 50000 L = 8 0.192-0.197 ms, 16 0.205-0.206, 32 0.298-0.300; C2
+// p = 5000 L = 8 0.074-0.079, 16 0.056-0.058, 32 0.057)
+constexpr int kLamSpecNarrow = 40000;
 constexpr int kLamSpecMax = 50000;
 
 // PgTail: the logistic sweep's omega ~ PG(1, psi) draws (independent of lambda: psi = X beta
@@ -373,6 +377,9 @@ k_lambda_cb_o4(BB_LAMBDA_CB_ARGS) {
 // pgb trailing workgroups draw the logistic omegas.  g_lam_lanes (bb_set_tuning key 5)
 // overrides the default L for A/B measurements.
 int g_lam_lanes = 0;
+static int spec_lanes(int p_loc) {
+    return p_loc <= kLamSpecWide ? 64 : p_loc <= kLamSpecNarrow ? 16 : 8;
+}
 static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p_loc, int p_pad,
                         uint64_t j0, const DevScalars *sc, Key key, uint64_t t, int mode,
                         double *lam, double *D, double *u, double *lam_trace, uint32_t *err,
@@ -404,7 +411,7 @@ bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, u
     const PgTail pgt{psi, n, n_pad, omega};
     const int pgb = (n_pad + 255) / 256;
     (void)group;
-    launch_spec(s, p_loc <= kLamSpecWide ? 64 : 16, pgb, beta, p_loc, p_pad, j0, sc, key, t,
+    launch_spec(s, spec_lanes(p_loc), pgb, beta, p_loc, p_pad, j0, sc, key, t,
                 LAMBDA_ONLY, lam, nullptr, nullptr, lam_trace, err, pgt);
     return true;
 }
@@ -418,7 +425,7 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
     if (p_loc <= kLamSpecMax) {
-        launch_spec(s, p_loc <= kLamSpecWide ? 64 : 16, 0, beta, p_loc, p_pad, j0, sc, key, t,
+        launch_spec(s, spec_lanes(p_loc), 0, beta, p_loc, p_pad, j0, sc, key, t,
                     mode, lam, D, u, lam_trace, err, PgTail{});
         return;
     }

@@ -38,9 +38,6 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// LDS written by one lane is read by another lane of the SAME wave after this
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 }  // namespace
 
 // tools/small_phase_bench.cpp builds this file with BB_SMALL_PHASES: thread 0 accumulates

@@ -33,3 +33,29 @@ def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
         bb.set_tuning(4, old)
     for k in ("beta", "lambda", "tau", "sig2"):
         assert np.array_equal(traces[0][k], traces[1][k]), k
+
+
+def test_lambda_lane_counts_same_chain(gpu_lib):
+    """p = 45000 runs k_lambda_spec<8> by default; forcing 16, 32 or 64 lanes per coefficient
+    (bb_set_tuning key 5) must give the same chain bit for bit."""
+    bb = gpu_lib
+    n, p = 40, 45000
+    X, y, _ = synthetic_problem(n, p, seed=12, s=8)
+    traces = []
+    old = bb.set_tuning(5, -1)
+    try:
+        for lanes in (0, 16, 32, 64):
+            bb.set_tuning(5, lanes)
+            e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=5,
+                                          seed=78, stream=0), X, y)
+            e.init_state()
+            e.run(1, 5, first_slot=0)
+            e.sync()
+            assert e.error_flags() == 0
+            traces.append(e.trace(0, 5))
+            e.close()
+    finally:
+        bb.set_tuning(5, old)
+    for tr in traces[1:]:
+        for k in ("beta", "lambda", "tau", "sig2"):
+            assert np.array_equal(traces[0][k], tr[k]), k
