@@ -2814,7 +2814,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 5: {
             const int old = g_lam_lanes;
-            if (value == 0 || value == 8 || value == 16 || value == 32 || value == 64)
+            if (value == 0 || value == 4 || value == 8 || value == 16 || value == 32 || value == 64)
                 g_lam_lanes = value;
             return old;
         }

@@ -179,7 +179,7 @@ struct PgTail {
     double *omega = nullptr;
 };
 
-template <int L>
+template <int L, int I>
 __device__ __forceinline__ void lambda_spec_body(const double *beta, int p_loc, int p_pad,
                                                  uint64_t j0, const DevScalars *sc, Key key,
                                                  uint64_t t, int mode, double *lam, double *D,
@@ -194,7 +194,7 @@ __device__ __forceinline__ void lambda_spec_body(const double *beta, int p_loc, 
     const bool active = i < p_loc;
     const double tau = sc->tau;
     const double b = active ? beta[i] : 0.0;
-    const double x = stable_spec_draw<L, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
+    const double x = stable_spec_draw<L, I>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
                                             key, t, j0 + (uint64_t)i, err);
     if ((threadIdx.x % L) != 0 || i >= p_pad) return;
     if (active) {
@@ -221,15 +221,15 @@ __device__ __forceinline__ void lambda_spec_body(const double *beta, int p_loc, 
     const double *beta, int p_loc, int p_pad, uint64_t j0, const DevScalars *sc, Key key,    \
         uint64_t t, int mode, double *lam, double *D, double *u, double *lam_trace,          \
         uint32_t *err, int lam_blocks, PgTail pgt
-template <int L>
+template <int L, int I = 8>
 __global__ __launch_bounds__(256) void k_lambda_spec(BB_LAMBDA_SPEC_ARGS) {
-    lambda_spec_body<L>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
+    lambda_spec_body<L, I>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
                         lam_blocks, pgt);
 }
-template <int L>
+template <int L, int I = 8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
-    lambda_spec_body<L>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
+    lambda_spec_body<L, I>(beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err,
                         lam_blocks, pgt);
 }
 #undef BB_LAMBDA_SPEC_ARGS
@@ -394,6 +394,10 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
         (o4 ? k_lambda_spec_o4<LL> : k_lambda_spec<LL>)<<<lb + pgb, 256, 0, s>>>(             \
             beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb, pgt);    \
         break;
+        case 4:  // one outer attempt of 4 inner attempts per round (A/B only)
+            (o4 ? k_lambda_spec_o4<4, 4> : k_lambda_spec<4, 4>)<<<lb + pgb, 256, 0, s>>>(
+                beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb, pgt);
+            break;
         BB_SPEC_CASE(8)
         BB_SPEC_CASE(32)
         BB_SPEC_CASE(64)

@@ -1,5 +1,6 @@
 """A/B of the speculative lambda launch's lanes per coefficient (bb_set_tuning key 5: 0 = the
-default policy, L = 64 up to p = 1024 and 16 above; 8 / 16 / 32 / 64 forced) on the C2, C3
+default policy, L = 64 up to p = 1024, 16 up to 40 000, 8 above; 4 / 8 / 16 / 32 / 64
+forced, 4 = one outer attempt of 4 inner attempts per round) on the C2, C3
 and C4 engines from a steady state reached after 30 sweeps.  Alternates the lane counts and
 prints the lambda phase time (HIP events at phase starts, 20 sweeps each), after checking
 that one sweep from the same state draws bit-identical beta under every lane count.
@@ -27,7 +28,7 @@ for wl in sys.argv[1:] or ["c3", "c2", "c4"]:
     t += 30
     e.sync()
     st = e.state()
-    lanes = (64, 32, 16) if logit else (16, 8, 32)
+    lanes = (64, 32, 16) if logit else (8, 4, 16)
     outs = []
     for L in lanes:
         bb.set_tuning(5, L)
