@@ -131,6 +131,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_set_trace_budget.argtypes = [c.c_longlong]
     L.bb_debug_interrupt_after.argtypes = [c.c_int]
     L.bb_last_call_info.argtypes = [_ip, _ip, _ip]
+    L.bb_debug_fail_member.argtypes = [c.c_int, c.c_int]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -255,6 +256,30 @@ def last_call_info():
     d, c, i = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     library().bb_last_call_info(ctypes.byref(d), ctypes.byref(c), ctypes.byref(i))
     return dict(devices=d.value, trace_capacity=c.value, interrupted=bool(i.value))
+
+
+def debug_fail_member(member: int, sweep: int) -> None:
+    """Test hook: member `member` of the next RCCL shard-group run fails before its sweep
+    `sweep` (the group then aborts its communicators and refuses further runs)."""
+    library().bb_debug_fail_member(int(member), int(sweep))
+
+
+def dot_c(name, *args):
+    """R's ``.C(name, ...)`` calling convention, for symbols with no ctypes prototype: each
+    argument is an int or float scalar / sequence (R integer or double vector), passed as a
+    pointer to a fresh copy (int -> int32, float -> float64, as R's as.integer / as.double);
+    the copies come back as numpy arrays, like .C's returned list."""
+    fn = getattr(library(), name)
+    bufs, ptrs = [], []
+    for a in args:
+        arr = np.atleast_1d(np.asarray(a))
+        arr = np.ascontiguousarray(arr, dtype=np.int32 if arr.dtype.kind in "biu" else np.float64)
+        bufs.append(arr)
+        ptrs.append(arr.ctypes.data_as(ctypes.c_void_p))
+    fn.argtypes = [ctypes.c_void_p] * len(ptrs)
+    fn.restype = None
+    fn(*ptrs)
+    return bufs
 
 
 # ---------------------------------------------------------------------------

@@ -35,6 +35,9 @@ uint64_t g_stream = 0;
 int g_device = 0;
 int g_verbose = 1;
 int g_use_r_rng = 1;
+// bb_debug_fail_member: member `g_debug_fail_member` of the next RCCL group run throws
+// before its sweep `g_debug_fail_sweep` (test hook for the group's failure handling)
+std::atomic<int> g_debug_fail_member{-1}, g_debug_fail_sweep{-1};
 
 void set_error(const char *fmt, ...) {
     char buf[1024];
@@ -564,6 +567,12 @@ struct bb_engine {
     size_t red1_count() const { return (size_t)nbS + n_pad; }
     size_t red2_count() const { return tri_count(n_pad) + n_pad; }
 
+    // RCCL shard-group members (bb_group_run): the group's stop flag, raised when another
+    // member failed (its collectives will never be matched, so enqueueing more is pointless),
+    // and the sweep index at which this member fails on purpose (bb_debug_fail_member)
+    const std::atomic<bool> *stop = nullptr;
+    int fail_at = -1;
+
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
     void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
         if (fused) {
@@ -587,6 +596,8 @@ struct bb_engine {
             return;
         }
         for (int k = 0; k < count; ++k) {
+            if (stop && stop->load(std::memory_order_relaxed)) break;
+            if (k == fail_at) throw HipError("injected failure (bb_debug_fail_member)");
             const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
             sweep(t0 + (uint64_t)k, slot, mcmc_phase);
         }
@@ -1410,15 +1421,20 @@ struct bb_group {
     std::vector<hipEvent_t> mev;
     double *tmp = nullptr;
     size_t tmp_count = 0;
+    // an RCCL member failed mid-run: the communicators were aborted (the other members'
+    // pending all-reduces can never be matched), so nothing may wait on the streams again
+    bool poisoned = false;
     ~bb_group() {
         for (auto *m : members) {
             (void)hipSetDevice(m->cfg.device);
-            (void)hipStreamSynchronize(m->stream);
+            if (!poisoned) (void)hipStreamSynchronize(m->stream);
             if (rccl) m->comm = nullptr;  // lent by this group
+            m->stop = nullptr;
         }
-        for (auto c : comms) ncclCommDestroy(c);
+        for (auto c : comms)
+            if (c) ncclCommDestroy(c);
         if (!members.empty()) (void)hipSetDevice(members[0]->cfg.device);
-        if (stream) (void)hipStreamSynchronize(stream);
+        if (stream && !poisoned) (void)hipStreamSynchronize(stream);
         if (tmp) (void)hipFree(tmp);
         if (ev) (void)hipEventDestroy(ev);
         for (auto e : mev) (void)hipEventDestroy(e);
@@ -1524,6 +1540,11 @@ void bb_group_destroy(bb_group *g) { delete g; }
 
 int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_step,
                  int mcmc_phase) {
+    if (g->poisoned) {
+        set_error("shard group unusable: a member failed in an earlier run and its "
+                  "communicators were aborted");
+        return -1;
+    }
     if (g->rccl) {
         // one enqueue thread per device: member i runs its `count` sweeps exactly as rank i
         // of a one-process-per-GPU job would (phase a, all-reduce, phase b, all-reduce,
@@ -1532,22 +1553,39 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
         const size_t k = g->members.size();
         std::vector<std::string> errs(k);
         std::vector<std::thread> th;
+        std::atomic<bool> stop{false};
+        const int fail_member = g_debug_fail_member.exchange(-1), fail_sweep = g_debug_fail_sweep.load();
         th.reserve(k);
         for (size_t i = 0; i < k; ++i)
             th.emplace_back([&, i] {
                 bb_engine *m = g->members[i];
+                m->stop = &stop;
+                m->fail_at = (int)i == fail_member ? fail_sweep : -1;
                 try {
                     HIPCHECK(hipSetDevice(m->cfg.device));
                     m->run(t0, count, first_slot, slot_step, mcmc_phase);
                     HIPCHECK(hipGetLastError());
                 } catch (std::exception &ex) {
                     errs[i] = ex.what();
+                    stop.store(true);  // the others stop enqueueing sweeps
                 }
+                m->fail_at = -1;
             });
         for (auto &t : th) t.join();
         for (size_t i = 0; i < k; ++i)
             if (!errs[i].empty()) {
                 set_error("group member %zu: %s", i, errs[i].c_str());
+                // A member stopped part-way through its sweeps, so the all-reduces the others
+                // already enqueued can never be matched: abort every communicator (their
+                // pending collectives return) and poison the group, so that neither this call
+                // nor the destructor waits on those streams.
+                for (auto &c : g->comms)
+                    if (c) {
+                        (void)ncclCommAbort(c);
+                        c = nullptr;
+                    }
+                for (auto *m : g->members) m->comm = nullptr;
+                g->poisoned = true;
                 return -1;
             }
         return 0;
@@ -1596,6 +1634,10 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
 }
 
 int bb_group_sync(bb_group *g) {
+    if (g->poisoned) {
+        set_error("shard group unusable: a member failed and its communicators were aborted");
+        return -1;
+    }
     try {
         for (auto *m : g->members) {
             g->on(m);
@@ -2540,8 +2582,8 @@ int ring_capacity(int m, int p_local, int ntr) {
 // Devices for a column-sharded chain: 1 unless p > n (the Woodbury path, or the orthogonal
 // design; alpha known or unknown) and sharding was enabled (bb_set_device_count); at least
 // 4096 columns per device.
-int chain_devices(const bb_config &c) {
-    const int nvis = bb_device_count();
+int chain_devices(const bb_config &c, int nvis = -1) {
+    if (nvis < 0) nvis = bb_device_count();
     int k = g_max_devices > 0 ? std::min(g_max_devices, nvis) : nvis;
     if (c.p <= c.n || (c.method != 0 && c.method != 2 && c.method != 3)) return 1;
     k = std::min(k, std::max(1, c.p / 4096));
@@ -2783,6 +2825,44 @@ Outcome stable_dense(const bb_config &c, const double *yp, const double *Xp, int
 extern "C" {
 
 void bb_set_device_count(int count) { g_max_devices = count < 0 ? 0 : count; }
+
+// .C-callable forms of the controls (R's .C passes every argument as a pointer,
+// BridgeWrapper.h:164-245; the by-value forms above are for C / ctypes hosts)
+void bb_set_device_count_C(const int *count) { bb_set_device_count(*count); }
+void bb_get_device_count_C(int *count) { *count = g_max_devices; }
+void bb_plan_devices_C(const int *n, const int *p, const int *ortho, const int *nvisible,
+                       int *devices) {
+    bb_config c;
+    bb_config_default(&c);
+    c.n = *n;
+    c.p = *p;
+    c.ortho = *ortho != 0;
+    *devices = chain_devices(c, *nvisible >= 0 ? *nvisible : -1);
+}
+void bb_set_device_C(const int *device, int *status) {
+    const int rc = bb_set_device(*device);
+    if (status) *status = rc;
+}
+void bb_set_verbose_C(const int *verbose) { bb_set_verbose(*verbose); }
+void bb_use_r_rng_C(const int *enable) { bb_use_r_rng(*enable); }
+void bb_set_seed_C(const double *seed) { bb_set_seed((uint64_t)*seed); }
+void bb_set_rng_state_C(const double *seed, const double *stream) {
+    bb_set_rng_state((uint64_t)*seed, (uint64_t)*stream);
+}
+void bb_get_rng_state_C(double *seed, double *stream) {
+    uint64_t s = 0, t = 0;
+    bb_get_rng_state(&s, &t);
+    *seed = (double)s;
+    *stream = (double)t;
+}
+void bb_set_trace_budget_C(const double *bytes) { bb_set_trace_budget((long long)*bytes); }
+void bb_last_call_info_C(int *devices, int *trace_capacity, int *interrupted) {
+    (void)bb_last_call_info(devices, trace_capacity, interrupted);
+}
+void bb_debug_fail_member(int member, int sweep) {
+    g_debug_fail_sweep = sweep;
+    g_debug_fail_member = member;
+}
 
 int bb_set_chol_version(int version) {
     if (version == 0) return g_chol_version;  // query

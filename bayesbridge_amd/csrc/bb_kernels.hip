@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <stdexcept>
 #include <unordered_map>
 
 #include <algorithm>
@@ -1481,6 +1482,31 @@ __device__ __forceinline__ void st_sc1(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Bounded cross-workgroup waits.  A wait gives up (error bit 16) after kSpinTicks of the
+// 100 MHz s_memrealtime clock -- 2 s, three orders of magnitude beyond any hand-off of a
+// factorisation that takes milliseconds -- or as soon as any other wait of the launch gave
+// up (bit 16 already set), so a launch that cannot make progress (a workgroup of its grid
+// never became resident, a broken hand-off) ends within seconds with the error flag, which
+// the .C driver reports as "Aborting Gibbs sampler.", instead of timing out wait after wait.
+constexpr uint64_t kSpinTicks = 200000000ull;
+struct SpinGuard {
+    uint64_t t0;
+    unsigned n = 0;
+    __device__ SpinGuard() : t0(__builtin_amdgcn_s_memrealtime()) {}
+    // call once per unsuccessful poll, by every lane of the waiting wave (the answer is
+    // wave-uniform); true: stop waiting (bit 16 set in *err)
+    __device__ bool expired(uint32_t *err) {
+        if ((++n & 255u) != 0) return false;
+        if (err && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 16u))
+            return true;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
+            if (err && (threadIdx.x & 63) == 0) atomicOr(err, 16u);
+            return true;
+        }
+        return false;
+    }
+};
+
 __device__ __forceinline__ void flag_release(unsigned int *f, unsigned int ep) {
     // caller: every wave's sc1 stores issued; each wave drains them before the barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1491,14 +1517,11 @@ __device__ __forceinline__ void flag_release(unsigned int *f, unsigned int ep) {
 __device__ __forceinline__ void flag_acquire2(const unsigned int *f1, const unsigned int *f2,
                                               unsigned int ep, uint32_t *err) {
     if (threadIdx.x == 0) {
-        unsigned spins = 0;
+        SpinGuard sg;
         while (__hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep ||
                (f2 && __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep)) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 25)) {
-                atomicOr(err, 16u);
-                break;
-            }
+            if (sg.expired(err)) break;
         }
     }
     // the payload is read with sc1 loads only: no L1 invalidate, just keep the compiler
@@ -1723,15 +1746,12 @@ __device__ __forceinline__ void diag_eliminate(double (*T)[65], double (*ROWS)[1
     const bool fetch = pf && pf->f1 && wid < 4;
     double h1[16], h2[16];
     if (fetch) {
-        for (unsigned spins = 0;;) {
+        for (SpinGuard sg;;) {
             const unsigned int v1 = __hip_atomic_load(pf->f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned int v2 = __hip_atomic_load(pf->f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__builtin_amdgcn_readfirstlane((int)(v1 == pf->ep && v2 == pf->ep))) break;
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 25)) {
-                if (lane == 0) atomicOr(err, 16u);
-                break;
-            }
+            if (sg.expired(err)) break;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
@@ -1992,14 +2012,11 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
         // ---- the hand-off tile S = A_{k,k+1} (updated by its owner through step k-1) ----
         if (wid < 4) {
             const unsigned int *f1 = &F.R[2 * k + 1];
-            for (unsigned spins = 0;;) {
+            for (SpinGuard sg;;) {
                 const unsigned int v1 = __hip_atomic_load(f1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (__builtin_amdgcn_readfirstlane((int)(v1 == F.ep))) break;
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 25)) {
-                    if (lane == 0) atomicOr(err, 16u);
-                    break;
-                }
+                if (sg.expired(err)) break;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double *t1 = A + (size_t)k * kNB + (size_t)(k + 1) * kNB * lda;
@@ -2049,14 +2066,11 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
             }
             // the (k+1, k+1) hand-off: this wave's D blocks of A_{k+1,k+1}
             const unsigned int *f2 = &F.R[2 * (k + 1)];
-            for (unsigned spins = 0;;) {
+            for (SpinGuard sg;;) {
                 const unsigned int v2 = __hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (__builtin_amdgcn_readfirstlane((int)(v2 == F.ep))) break;
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 25)) {
-                    if (lane == 0) atomicOr(err, 16u);
-                    break;
-                }
+                if (sg.expired(err)) break;
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             const double *t2 = A + (size_t)(k + 1) * kNB + (size_t)(k + 1) * kNB * lda;
@@ -2516,6 +2530,25 @@ static int device_cus() {
 // slower -- DESIGN.md §5.2); bb_set_chol_version switches it for A/B measurements
 int g_chol_version = 1;
 
+// Workgroups of k_chol_persistent<V> the device can hold at once (occupancy query x CUs),
+// computed once per chain variant.
+static int chol_max_resident(int version) {
+    static int cache[4] = {-1, -1, -1, -1};
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    int &c = cache[version & 3];
+    if (c < 0) {
+        int nb = 0;
+        hipError_t e = version == 2
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<2>, 512, 0)
+            : version == 3
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<3>, 512, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<1>, 512, 0);
+        c = (e == hipSuccess ? nb : 0) * device_cus();
+    }
+    return c;
+}
+
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
                  double *Wd, unsigned int *flags, unsigned long long *trace) {
     const int nblk = m_pad / kNB;
@@ -2526,6 +2559,17 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
                 flags + bsolve_flag_offset(m_pad, nrhs_blocks) + nblk, ncb, ep};
     const int ntiles = nblk * (nblk + 1) / 2 + nblk * nrhs_blocks;
     const int grid = std::min(device_cus(), 1 + ntiles);
+    // every workgroup of the grid must be resident at once (the chain waits on tiles of every
+    // owner): refuse a launch the device cannot hold rather than let it stall into the
+    // bounded waits' error flag
+    const int resident = chol_max_resident(g_chol_version);
+    if (grid > resident) {
+        char b[200];
+        snprintf(b, sizeof(b),
+                 "persistent Cholesky: %d workgroups exceed the %d the device holds at once",
+                 grid, resident);
+        throw std::runtime_error(b);
+    }
     if (g_chol_version == 1)
         k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
     else if (g_chol_version == 2)

@@ -340,6 +340,34 @@ int bb_set_tuning(int key, int value);
 void bb_debug_interrupt_after(int polls);
 /* Last .C sampler call: devices used, trace ring slots, whether it was interrupted. */
 int bb_last_call_info(int *devices, int *trace_capacity, int *interrupted);
+/* Test hook: member `member` of the NEXT RCCL shard-group run throws before its sweep `sweep`
+ * (-1 clears).  The group then aborts every communicator, returns -1 and refuses further runs. */
+void bb_debug_fail_member(int member, int sweep);
+
+/*
+ * .C-callable forms of the controls.  R's .C passes every argument as a pointer (the
+ * reference's whole .C surface is pointer-only, BridgeWrapper.h:164-245), so a by-value
+ * `int` control called from R would receive the ADDRESS of the R integer.  From R:
+ *   .C("bb_set_device_count_C", 0L)       # shard p > n chains over every visible device
+ *   .C("bb_set_device_count_C", 1L)       # one device (the default)
+ *   .C("bb_last_call_info_C", devices = 0L, capacity = 0L, interrupted = 0L)$devices
+ * R integers are 32-bit and R doubles carry integers exactly up to 2^53, so the 64-bit seed,
+ * stream and byte counts are passed as doubles.
+ */
+void bb_set_device_count_C(const int *count);
+void bb_get_device_count_C(int *count);
+/* Devices a bridge_reg_stable call of this shape would use with `nvisible` devices
+ * visible (nvisible < 0: the devices actually visible). */
+void bb_plan_devices_C(const int *n, const int *p, const int *ortho, const int *nvisible,
+                       int *devices);
+void bb_set_device_C(const int *device, int *status); /* status: 0, or -1 (invalid device) */
+void bb_set_verbose_C(const int *verbose);
+void bb_use_r_rng_C(const int *enable);
+void bb_set_seed_C(const double *seed);
+void bb_set_rng_state_C(const double *seed, const double *stream);
+void bb_get_rng_state_C(double *seed, double *stream);
+void bb_set_trace_budget_C(const double *bytes);
+void bb_last_call_info_C(int *devices, int *trace_capacity, int *interrupted);
 
 /* Which beta-step path the engine uses: 1 chol (p <= n), 2 woodbury, 3 ortho, 4 triangle,
  * 5 sparse woodbury, 6 logistic. */

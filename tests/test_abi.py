@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 import bayesbridge_amd as bb
@@ -73,3 +74,48 @@ def test_no_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(RuntimeError):
         bb.retstable_ld(3, 0.5, 1.0, 1.0)
+
+
+def test_dot_c_controls_take_pointers():
+    """Every control R must call has a pointer-only `.C` form (R's .C passes pointers,
+    BridgeWrapper.h:164-245): .C("bb_set_device_count_C", k) stores k itself -- the by-value
+    bb_set_device_count(int) would receive the address of R's integer."""
+    try:
+        for k in (0, 1, 3):
+            bb.dot_c("bb_set_device_count_C", k)
+            (got,) = bb.dot_c("bb_get_device_count_C", 0)
+            assert int(got[0]) == k
+        # seed / stream / byte counts travel as R doubles (exact integers up to 2^53)
+        bb.dot_c("bb_set_rng_state_C", float(2 ** 52 + 7), 11.0)
+        assert bb.get_rng_state() == (2 ** 52 + 7, 11)
+        bb.dot_c("bb_set_seed_C", 4242.0)
+        s, t = bb.dot_c("bb_get_rng_state_C", 0.0, 0.0)
+        assert (s[0], t[0]) == (4242.0, 0.0)
+        bb.dot_c("bb_set_verbose_C", 0)
+        d, c, i = bb.dot_c("bb_last_call_info_C", 0, 0, 0)
+        assert d.dtype == np.int32 and c.dtype == np.int32 and i[0] in (0, 1)
+    finally:
+        bb.set_device_count(1)
+        bb.set_verbose(1)
+
+
+@pytest.mark.parametrize("setting,nvis,n,p,ortho,want", [
+    (1, 8, 2000, 50000, 0, 1),   # the default: one device
+    (0, 8, 2000, 50000, 0, 8),   # 0 = every visible device
+    (0, 1, 2000, 50000, 0, 1),
+    (4, 8, 2000, 50000, 0, 4),   # k
+    (16, 8, 2000, 50000, 0, 8),  # capped by the visible devices
+    (0, 8, 2000, 20000, 0, 4),   # >= 4096 columns per device
+    (0, 8, 1000, 900, 0, 1),     # p <= n: replicas only, never sharded
+    (2, 8, 200, 10000, 1, 2),    # the orthogonal design shards too
+])
+def test_dot_c_device_plan(setting, nvis, n, p, ortho, want):
+    """The device count a .C sampler call takes after .C("bb_set_device_count_C", k) for k =
+    0, 1 and k > 1 (bb_plan_devices_C evaluates the driver's own rule for a given number of
+    visible devices, so it runs without a GPU)."""
+    try:
+        bb.dot_c("bb_set_device_count_C", setting)
+        (dev,) = bb.dot_c("bb_plan_devices_C", n, p, ortho, nvis, 0)[-1:]
+        assert int(dev[0]) == want
+    finally:
+        bb.set_device_count(1)

@@ -131,3 +131,54 @@ def test_c_entry_device_count_control(gpu_lib):
         bb.set_device_count(1)
     if bb.device_count() == 1:
         _same(a, b)
+
+
+def test_c_entry_device_count_control_dot_c(gpu_lib):
+    """The same control through R's calling convention: .C("bb_set_device_count_C", k) with
+    k = 0, 1 and 2, each followed by a .C sampler call and .C("bb_last_call_info_C", ...)."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(50, 9000, seed=8)
+    nvis = bb.device_count()
+    try:
+        for k in (0, 1, 2):
+            bb.dot_c("bb_set_device_count_C", k)
+            bb.dot_c("bb_set_seed_C", float(SEED + 4))
+            out = bb.bridge_reg_stb(y, X, nsamp=4, burn=1)
+            d, cap, intr = bb.dot_c("bb_last_call_info_C", 0, 0, 0)
+            want = min(nvis if k == 0 else k, nvis, 9000 // 4096)
+            assert int(d[0]) == want, (k, int(d[0]))
+            assert int(cap[0]) == 4 and int(intr[0]) == 0
+            assert np.all(np.isfinite(out["beta"]))
+    finally:
+        bb.set_device_count(1)
+
+
+def test_rccl_group_member_failure_aborts_and_poisons(gpu_lib):
+    """A member that fails part-way through a run (bb_debug_fail_member) makes the RCCL group
+    abort its communicators, return an error instead of waiting on collectives that can never
+    be matched, and refuse further runs; closing it does not hang, and a fresh group on the
+    same device runs normally (one member: the only RCCL group a one-GPU box can hold)."""
+    bb = gpu_lib
+    n, p = 120, 1500
+    X, y, _ = synthetic_problem(n, p, seed=32)
+    e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=12, method=2, trace_capacity=4),
+                  X, y)
+    g = bb.ShardGroup([e], rccl=True)
+    g.init_state()
+    bb.debug_fail_member(0, 3)
+    with pytest.raises(RuntimeError, match="injected failure"):
+        g.run(1, 8, first_slot=-1)
+    with pytest.raises(RuntimeError, match="unusable"):
+        g.run(9, 1, first_slot=-1)
+    g.close()
+    e.close()
+    # the hook is one-shot, and the device is usable again
+    e2 = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=12, method=2, trace_capacity=4),
+                   X, y)
+    g2 = bb.ShardGroup([e2], rccl=True)
+    g2.init_state()
+    g2.run(1, 4, first_slot=0)
+    g2.sync()
+    assert np.all(np.isfinite(e2.trace(0, 4)["beta"]))
+    g2.close()
+    e2.close()

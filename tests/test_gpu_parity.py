@@ -395,16 +395,19 @@ def test_teacher_forced_bench_workload(gpu_lib):
 
 
 @pytest.mark.parametrize("world,kind", [(2, "known"), (3, "known"), (2, "alpha"), (3, "alpha"),
-                                        (2, "ortho")])
+                                        (2, "alpha_accept"), (2, "ortho")])
 def test_shard_group_matches_single_engine(gpu_lib, world, kind):
     """The column-sharded sweep (two exchanges per sweep; a third, of the two alpha MH sums,
     when alpha is unknown) on one GPU vs the unsharded engine, teacher-forced from identical
-    states for several sweeps.  "ortho": the orthogonal-design draw for p > n, sharded."""
+    states for several sweeps.  "ortho": the orthogonal-design draw for p > n, sharded.
+    "alpha_accept" starts alpha at 0.9, from where the MH step accepts (the oracle chain of
+    this state accepts at sweeps 5 and 8), so the split step's decide kernel is compared on
+    its accepting branch too; the test requires at least one acceptance."""
     bb = gpu_lib
     n, p = 200, 1100
     X, y, btrue = synthetic_problem(n, p, seed=21)
     seed, stream = SEED + 9, 0
-    ta = 0.0 if kind == "alpha" else 0.5
+    ta = 0.0 if kind.startswith("alpha") else 0.5
     ortho = kind == "ortho"
     single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=seed, stream=stream, true_alpha=ta,
                                        ortho=ortho), X, y)
@@ -421,7 +424,8 @@ def test_shard_group_matches_single_engine(gpu_lib, world, kind):
     grp.init_state()
     rng = np.random.default_rng(3)
     beta = btrue + 0.05 * rng.standard_normal(p)
-    tau, sig2, alpha = 0.9, 1.1, 0.5
+    tau, sig2, alpha = 0.9, 1.1, (0.9 if kind == "alpha_accept" else 0.5)
+    accepts = 0
     for t in range(1, 9):
         single.set_state(beta, tau, sig2, alpha)
         for r, e in enumerate(shards):
@@ -441,9 +445,12 @@ def test_shard_group_matches_single_engine(gpu_lib, world, kind):
         assert flips(lg, s1["lambda"]) == 0
         assert np.max(np.abs(lg - s1["lambda"]) / s1["lambda"]) < 1e-11
         assert rel_err(bg, s1["beta"]) < 1e-10, (t, rel_err(bg, s1["beta"]))
+        accepts += int(s1["alpha"] != alpha)
         beta, tau, sig2, alpha = s1["beta"], s1["tau"], s1["sig2"], s1["alpha"]
-    # (from this state the MH step mostly rejects; the accepting path of the split step is
-    # covered on the CPU by tests/test_sharded_cpu.py::test_sharded_alpha_mh_matches_unsharded)
+    # (from alpha = 0.5 the MH step mostly rejects; "alpha_accept" must see the accepting
+    # branch -- also covered on the CPU by tests/test_sharded_cpu.py)
+    if kind == "alpha_accept":
+        assert accepts >= 1, "the MH step never accepted: the accepting branch is untested"
     grp.close()
     single.close()
 
@@ -477,6 +484,56 @@ def test_shard_group_cu_filling_system(gpu_lib):
         grp.sync()
         s1 = single.state()
         bg = np.concatenate([e.state()["beta"] for e in shards])
+        assert rel_err(bg, s1["beta"]) < 1e-9, (t, rel_err(bg, s1["beta"]))
+        beta, tau, sig2 = s1["beta"], s1["tau"], s1["sig2"]
+    assert single.error_flags() == 0
+    assert all(e.error_flags() == 0 for e in shards)
+    grp.close()
+    single.close()
+    for e in shards:
+        e.close()
+
+
+def test_shard_group_c3_full_size(gpu_lib):
+    """The sharded decomposition at the size it exists for: the C3 workload itself (n = 2000,
+    p = 50000, bench.py's X, y and key, Ozaki-II Gram) as a 2-member on-device shard group,
+    25 000 columns per member -- the shard a 2-GPU .C call holds -- three sweeps
+    teacher-forced against the unsharded engine, no error flags.  The members' Grams are
+    rounded to fp64 separately and summed, so only the summation order differs."""
+    import bench
+    bb = gpu_lib
+    n, p, world = 2000, 50000, 2
+    X = bench.make_columns(n, 0, p)
+    y, btrue = bench.make_problem_y(n, p)
+    single = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, true_alpha=0.5,
+                                       gram_mode=bb.GRAM_OZAKI), X, y)
+    single.init_state()
+    per = p // world
+    shards = [bb.Engine(bb.EngineConfig(n=n, p=p, p_local=per, j0=r * per, rank=r, world=world,
+                                        seed=SEED, stream=0, true_alpha=0.5,
+                                        gram_mode=bb.GRAM_OZAKI),
+                        np.asfortranarray(X[:, r * per:(r + 1) * per]), y) for r in range(world)]
+    del X
+    grp = bb.ShardGroup(shards)
+    grp.init_state()
+    beta = btrue + 0.01 * np.random.default_rng(6).standard_normal(p)
+    tau, sig2 = 1.0, 1.0
+    for t in (201, 202, 203):
+        single.set_state(beta, tau, sig2, 0.5)
+        for r, e in enumerate(shards):
+            e.set_state(beta[r * per:(r + 1) * per], tau, sig2, 0.5)
+        single.run(t, 1)
+        grp.run(t, 1)
+        grp.sync()
+        s1 = single.state()
+        parts = [e.state() for e in shards]
+        bg = np.concatenate([q["beta"] for q in parts])
+        lg = np.concatenate([q["lambda"] for q in parts])
+        for q in parts:
+            assert abs(q["tau"] - s1["tau"]) <= 1e-12 * s1["tau"], t
+            assert abs(q["sig2"] - s1["sig2"]) <= 1e-11 * s1["sig2"], t
+        assert flips(lg, s1["lambda"]) == 0, t
+        assert np.max(np.abs(lg - s1["lambda"]) / s1["lambda"]) < 1e-10, t
         assert rel_err(bg, s1["beta"]) < 1e-9, (t, rel_err(bg, s1["beta"]))
         beta, tau, sig2 = s1["beta"], s1["tau"], s1["sig2"]
     assert single.error_flags() == 0

@@ -36,15 +36,16 @@ def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
 
 
 def test_lambda_lane_counts_same_chain(gpu_lib):
-    """p = 45000 runs k_lambda_spec<8> by default; forcing 16, 32 or 64 lanes per coefficient
-    (bb_set_tuning key 5) must give the same chain bit for bit."""
+    """p = 45000 runs k_lambda_spec<8> by default; forcing 4 (one outer attempt of 4 inner
+    attempts per round), 16, 32 or 64 lanes per coefficient (bb_set_tuning key 5) must give
+    the same chain bit for bit."""
     bb = gpu_lib
     n, p = 40, 45000
     X, y, _ = synthetic_problem(n, p, seed=12, s=8)
     traces = []
     old = bb.set_tuning(5, -1)
     try:
-        for lanes in (0, 16, 32, 64):
+        for lanes in (0, 4, 16, 32, 64):
             bb.set_tuning(5, lanes)
             e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=5,
                                           seed=78, stream=0), X, y)

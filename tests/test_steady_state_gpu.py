@@ -8,12 +8,16 @@ are teacher-forced against the oracle (the Woodbury restatement of BridgeRegress
 552-575 over numpy / scipy.sparse, the C tilted-stable sampler), each from the oracle's
 previous output.
 
-Two regimes (oracle chains at C2, /tmp-free measurement recorded in DESIGN.md s6): from
-beta0 = 0 the chain first sits near beta = 0 with tau tiny and sig2 ~ var(y), where
+Two regimes (oracle chains at C2, measurement recorded in DESIGN.md s6): from beta0 = 0
+the chain first sits near beta = 0 with tau tiny and sig2 ~ var(y), where
 M = I + X D X' / sig2 is the identity to 1e-8 (C3 after 120 sweeps: cond(M) - 1 = 2e-8);
 after ~700 sweeps (C2) it moves to the fitted regime (sig2 ~ 0.01, D over 9 decades,
-cond(M) ~ 1e5).  The free-run lengths below are chosen to end in the second regime where
-the chain gets there within a few seconds of GPU time; the regime reached is printed.
+cond(M) ~ 1e5).  test_steady_state_teacher_forced free-runs from beta0 = 0: C2 (2000
+sweeps) reaches the fitted regime, but C3 (2500) and C5 (1500) are still near beta = 0
+there, where M is the identity and the Cholesky, solves and beta map see a trivial system.
+test_fitted_regime_teacher_forced therefore STARTS C3 and C5 in the fitted regime (beta at
+the data-generating coefficients, tau = 1e-2, sig2 = 1), free-runs 300 sweeps so the state
+is the sampler's own, requires cond(M) > 1e3 and then teacher-forces three sweeps.
 
 Bars: beta 1e-9 relative L2, lambda / tau / sig2 1e-11 relative with no accept/reject
 decision flips.  The state reached is printed (tau, sig2, the span of D and the condition
@@ -47,28 +51,43 @@ def oracle_sweep(X, y, beta, tau, sig2, alpha, t, seed, stream):
     return b, lam, tau, sig2
 
 
-def workload(name):
+def workload(name, with_truth=False):
     import bench
     n, p, alpha, kind = bench.WORKLOADS[name]
     if kind == "sparse":
         X = bench.make_sparse_columns(n, 0, p)
-        y, _ = bench.make_sparse_problem_y(n, p)
+        y, b = bench.make_sparse_problem_y(n, p)
     else:
         X = bench.make_columns(n, 0, p)
-        y, _ = bench.make_problem_y(n, p)
-    return X, y, alpha
+        y, b = bench.make_problem_y(n, p)
+    return (X, y, alpha, b) if with_truth else (X, y, alpha)
+
 
 
 def m_condition(X, lam, tau, sig2):
-    """(cond(M) of the dense designs -- eigvalsh, n <= 2000 -- or NaN, log10 span of D)."""
+    """(cond_2(M) of M = I + X D X' / sig2, log10 span of D).  Dense designs (n <= 2000):
+    eigvalsh.  Sparse designs: M densified, its largest eigenvalue by Lanczos and its
+    smallest as 1 / the largest of M^-1 (Lanczos on Cholesky solves)."""
+    import scipy.linalg as sl
+    import scipy.sparse.linalg as sla
     D = tau * tau / lam
     span = float(np.log10(D.max() / D.min()))
-    if hasattr(X, "toarray") or X.shape[0] > 2000:
-        return float("nan"), span
-    M = (X * D) @ X.T / sig2
+    if hasattr(X, "toarray"):
+        import scipy.sparse as sps
+        M = (X @ sps.diags(D) @ X.T).toarray() / sig2
+    else:
+        M = (X * D) @ X.T / sig2
     M[np.diag_indices_from(M)] += 1.0
-    ev = np.linalg.eigvalsh(M)
-    return float(ev[-1] / ev[0]), span
+    if M.shape[0] <= 2000:
+        ev = np.linalg.eigvalsh(M)
+        return float(ev[-1] / ev[0]), span
+    n = M.shape[0]
+    lmax = float(sla.eigsh(M, k=1, which="LA", return_eigenvectors=False, tol=1e-6)[0])
+    cf = sl.cho_factor(M, lower=False, check_finite=False)
+    inv = sla.LinearOperator((n, n), matvec=lambda v: sl.cho_solve(cf, v, check_finite=False),
+                             dtype=np.float64)
+    lmin = 1.0 / float(sla.eigsh(inv, k=1, which="LA", return_eigenvectors=False, tol=1e-6)[0])
+    return lmax / lmin, span
 
 
 @pytest.mark.parametrize("name,free", [("c2", 2000), ("c3", 2500), ("c5", 1500)])
@@ -156,3 +175,53 @@ def test_free_running_posterior_moments_wide(gpu_lib):
     assert z_sd.max() < 5 and np.sum(z_sd > 2.5) <= 6, np.sort(z_sd)[-8:]
     # and the signal is found: the five true coefficients have the largest posterior |means|
     assert set(np.argsort(-np.abs(g.mean(axis=0)))[:5]) == set(range(5))
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_fitted_regime_teacher_forced(gpu_lib, name, capsys):
+    """C3 and C5 teacher-forced in the regime the sampler spends its run in:
+    the GPU chain starts at the data-generating coefficients with tau = 1e-2 and sig2 = 1 and
+    runs FREE for 300 sweeps, so lambda, tau, sig2 and D = tau^2 / lambda are the sampler's
+    own; then cond(M) of the next sweep's system must exceed 1e3 (printed, with tau, sig2 and
+    the span of D), and three sweeps are teacher-forced against the oracle (the Woodbury
+    restatement of BridgeRegression.cpp:552-575) at the steady-state bars: beta 1e-9
+    relative L2, lambda / tau / sig2 1e-11 relative, no decision flips."""
+    bb = gpu_lib
+    X, y, alpha, btrue = workload(name, with_truth=True)
+    n, p = X.shape
+    e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, true_alpha=alpha,
+                                  trace_capacity=1), X, y)
+    assert e.method() in (2, 5)
+    e.init_state()
+    e.set_state(btrue, 1e-2, 1.0, alpha)
+    e.run(2, 300, first_slot=-1)  # free-running from the fitted start
+    e.sync()
+    assert e.error_flags() == 0
+    s = e.state()
+    beta, tau, sig2 = s["beta"], s["tau"], s["sig2"]
+    assert np.all(np.isfinite(beta)) and tau > 0 and sig2 > 0
+    worst = dict(beta=0.0, lam=0.0, tau=0.0, sig2=0.0)
+    for t in (2001, 2002, 2003):
+        e.set_state(beta, tau, sig2, alpha)
+        e.run(t, 1, first_slot=-1)
+        g = e.state()
+        b, lam, tau, sig2 = oracle_sweep(X, y, beta, tau, sig2, alpha, t, SEED, 0)
+        if t == 2001:
+            cond, span = m_condition(X, lam, tau, sig2)
+            with capsys.disabled():
+                print(f"\n[{name} fitted start + 300 free sweeps] tau={tau:.4g} sig2={sig2:.4g} "
+                      f"|beta|>1e-3: {int(np.sum(np.abs(beta) > 1e-3))} D span 10^{span:.1f} "
+                      f"cond(M)={cond:.3g}")
+            assert cond > 1e3, f"not in the fitted regime: cond(M) = {cond:.3g}"
+        assert flips(g["lambda"], lam) == 0, t
+        worst["lam"] = max(worst["lam"], float(np.max(np.abs(g["lambda"] - lam) / lam)))
+        worst["tau"] = max(worst["tau"], abs(g["tau"] - tau) / tau)
+        worst["sig2"] = max(worst["sig2"], abs(g["sig2"] - sig2) / sig2)
+        worst["beta"] = max(worst["beta"], rel_err(g["beta"], b))
+        beta = b
+    with capsys.disabled():
+        print(f"[{name} fitted] worst over 3 teacher-forced sweeps: {worst}")
+    assert worst["tau"] < 1e-11 and worst["sig2"] < 1e-11 and worst["lam"] < 1e-11, worst
+    assert worst["beta"] < 1e-9, worst
+    assert e.error_flags() == 0
+    e.close()

@@ -1,0 +1,33 @@
+#!/bin/bash
+# MFMA-busy evidence (north_star): SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE, each in its
+# own rocprofv3 --pmc pass (no trace domain combined), over the bench command, for the Gram
+# kernels and the Cholesky:
+#   c3      default C3 bench (Ozaki-II: k_oz_gemm16u, k_oz_residues; k_chol_persistent)
+#   c3fp64  C3 with the fp64 MFMA Gram (k_gram)
+#   c2      C2 (k_chol_persistent at n = 1000, k_oz_gemm16u)
+# Summary: python tools/pmc_mfma_summary.py <round>  ->  profiles/<round>_pmc_mfma.json
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+ROUND=${ROUND:-r04}
+OUT=gpurun_out/pmc_mfma_$ROUND
+mkdir -p "$OUT"
+REGEX="k_oz_gemm16u|k_oz_residues|k_chol_persistent|k_gram"
+pass() {  # $1 = config name, $2 = counter, rest = bench args
+    local cfg=$1 ctr=$2; shift 2
+    timeout -s KILL 240 rocprofv3 --pmc "$ctr" --kernel-include-regex "$REGEX" \
+        -d "$OUT/$cfg/$ctr" -o run --output-format csv \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" \
+        > "$OUT/$cfg/$ctr.json" 2> "$OUT/$cfg/$ctr.err" || { echo "$cfg $ctr failed ($?)"; exit 1; }
+    echo "$cfg $ctr ok"
+}
+for cfg in c3 c3fp64 c2; do
+    mkdir -p "$OUT/$cfg"
+    case $cfg in
+        c3) args="" ;;
+        c3fp64) args="--gram fp64" ;;
+        c2) args="--workload c2" ;;
+    esac
+    pass $cfg SQ_VALU_MFMA_BUSY_CYCLES $args
+    pass $cfg GRBM_GUI_ACTIVE $args
+    pass $cfg SQ_BUSY_CU_CYCLES $args
+done

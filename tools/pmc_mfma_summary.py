@@ -1,0 +1,92 @@
+"""Summarise tools/pmc_mfma.sh into profiles/<round>_pmc_mfma.json.
+
+Per kernel and config: the average over dispatches of SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy
+cycles summed over every SIMD), GRBM_GUI_ACTIVE (GPU-busy cycles summed over the 8 XCDs,
+MI355X_MICROARCH.md "DVFS give-back") and SQ_BUSY_CU_CYCLES, and
+  kernel_cycles   = GRBM_GUI_ACTIVE / 8
+  mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel_cycles)
+i.e. the fraction of the SIMDs' cycles (at whatever clock the chip ran) in which an MFMA
+executed.  For k_oz_gemm16u the MFMA count is known exactly (16 n_oz-row residue Grams,
+v_mfma_i32_16x16x64_i8 = 16 cycles each), which checks the counter's normalisation.
+Usage: python tools/pmc_mfma_summary.py r04
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SIMDS = 1024
+XCDS = 8
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").strip()
+
+
+def avgs(d, counter):
+    tot, cnt = {}, {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            k = short(r["Kernel_Name"])
+            tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
+            cnt[k] = cnt.get(k, 0) + 1
+    return {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
+
+
+def bench_line(d):
+    for f in glob.glob(os.path.join(d, "*.json")):
+        for line in open(f):
+            if line.startswith("{"):
+                return json.loads(line)
+    return {}
+
+
+def main():
+    rnd = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", f"pmc_mfma_{rnd}")
+    out = {"round": rnd, "source": "tools/pmc_mfma.sh (one counter per rocprofv3 --pmc pass)",
+           "formula": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)",
+           "configs": {}}
+    for cfg in sorted(os.listdir(src)):
+        d = os.path.join(src, cfg)
+        if not os.path.isdir(d):
+            continue
+        mf = avgs(os.path.join(d, "SQ_VALU_MFMA_BUSY_CYCLES"), "SQ_VALU_MFMA_BUSY_CYCLES")
+        gr = avgs(os.path.join(d, "GRBM_GUI_ACTIVE"), "GRBM_GUI_ACTIVE")
+        cu = avgs(os.path.join(d, "SQ_BUSY_CU_CYCLES"), "SQ_BUSY_CU_CYCLES")
+        bl = bench_line(d)
+        c = bl.get("config", {})
+        ent = {"workload": c.get("workload"), "gram": c.get("gram"), "kernels": {}}
+        for k in sorted(set(mf) | set(gr)):
+            e = {"dispatches": (mf.get(k) or gr.get(k))[1]}
+            if k in mf:
+                e["SQ_VALU_MFMA_BUSY_CYCLES"] = mf[k][0]
+            if k in gr:
+                e["GRBM_GUI_ACTIVE"] = gr[k][0]
+                e["kernel_cycles"] = gr[k][0] / XCDS
+            if k in cu:
+                e["SQ_BUSY_CU_CYCLES"] = cu[k][0]
+            if k in mf and k in gr and gr[k][0] > 0:
+                e["mfma_busy_frac"] = mf[k][0] / (SIMDS * gr[k][0] / XCDS)
+            if k.startswith("bb::k_oz_gemm16u") and c.get("n"):
+                n, p = int(c["n"]), int(c["p"])
+                n_oz = -(-(-(-n // 128) * 128) // 256) * 256
+                p_pad = -(-p // 256) * 256
+                nt = n_oz // 256
+                # tiles computed: off-diagonal full + diagonal lower halves, 16 moduli
+                macs = 16 * (nt * (nt - 1) / 2 * 256 * 256 + nt * 256 * 128 + nt * 256 * 8) * p_pad
+                e["mfma_instructions_model"] = macs / (16 * 16 * 64)
+                e["busy_cycles_model_16_per_mfma"] = 16 * macs / (16 * 16 * 64)
+            ent["kernels"][k] = e
+        out["configs"][cfg] = ent
+    dst = os.path.join(ROOT, "profiles", f"{rnd}_pmc_mfma.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
