@@ -95,22 +95,21 @@ def make_logit_problem(n, p, seed=DATA_SEED):
     return X, y, b
 
 
-def cpu_baseline_logit(n, p, alpha, sweeps, log_every=True):
-    """Oracle logistic sweeps (numpy X'Omega X, LAPACK Cholesky, C PG and tilted-stable
-    samplers).  Returns (median s per sweep, threads)."""
-    from oracle import gibbs
+def cpu_baseline_logit(n, p, alpha, sweeps, threads=None):
+    """The compiled logistic CPU chain (oracle/bb_cpu_chain.c bbc_logit_chain: dsyrk for
+    X'Omega X + dpotrf + dtrsm on scipy's OpenBLAS, OpenMP Polya-Gamma and tilted-stable
+    draws; checked against oracle/gibbs.py by tests/test_cpu_chain.py) from beta = 0.
+    threads: BLAS / OpenMP threads (None: OMP_NUM_THREADS or every CPU).  Returns
+    (s per sweep, threads)."""
+    import oracle
 
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     X, y, _ = make_logit_problem(n, p)
-    beta, tau = np.zeros(p), 1.0
-    times = []
-    for t in range(1, sweeps + 1):
-        t0 = time.perf_counter()
-        beta, _, tau, _ = gibbs.logit_sweep(X, y, beta, tau, alpha, t, 1, 0)
-        times.append(time.perf_counter() - t0)
-        if log_every:
-            log(f"[cpu_baseline] logistic sweep {t}: {times[-1]:.3f} s")
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return float(np.median(times)), threads
+    r = oracle.cpu_logit_chain(y, X, sweeps + 1, burn=0, alpha=alpha, seed=0xB4E5B41D6E,
+                               threads=threads, record=False)
+    log(f"[cpu_baseline] logistic threads={threads}: {sweeps} sweeps in {r['runtime']:.3f} s")
+    return r["runtime"] / sweeps, threads
 
 
 def make_sparse_columns(n, j0, j1, density=SPARSE_DENSITY, seed=DATA_SEED, block=1000):
@@ -151,30 +150,21 @@ def make_sparse_problem_y(n, p, density=SPARSE_DENSITY, seed=DATA_SEED):
     return y - y.mean(), b
 
 
-def cpu_baseline_sparse(n, p, alpha, sweeps, log_every=True):
-    """Oracle Woodbury sweeps on the sparse design (scipy SpGEMM X diag(D) X', LAPACK
-    Cholesky, the C tilted-stable sampler).  Returns (median s per sweep, threads)."""
+def cpu_baseline_sparse(n, p, alpha, sweeps, threads=None):
+    """The compiled sparse Woodbury CPU chain (oracle/bb_cpu_chain.c bbc_sparse_chain: CSR /
+    CSC passes and the n x n sparse Gram by output column under OpenMP, LAPACK dpotrf on
+    scipy's OpenBLAS, OpenMP tilted-stable draws; checked against oracle/gibbs.py by
+    tests/test_cpu_chain.py) from beta = 0.  Returns (s per sweep, threads)."""
     import oracle
-    from oracle import gibbs
 
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     X = make_sparse_columns(n, 0, p)
     y, _ = make_sparse_problem_y(n, p)
-    beta = np.zeros(p)
-    times = []
-    for t in range(1, sweeps + 1):
-        t0 = time.perf_counter()
-        tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, 2.0, 2.0, 1, 0, t)
-        r = y - X @ beta
-        sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, 1, 0, t)
-        lam = oracle.sample_lambda(beta, alpha, tau, 1, 0, t)
-        z = oracle.normals(p, 1, 0, t, oracle.KIND_BETA_Z)
-        d = oracle.normals(n, 1, 0, t, oracle.KIND_DELTA)
-        beta = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
-        times.append(time.perf_counter() - t0)
-        if log_every:
-            log(f"[cpu_baseline] sparse sweep {t}: {times[-1]:.3f} s")
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return float(np.median(times)), threads
+    r = oracle.cpu_sparse_chain(y, X, sweeps + 1, burn=0, alpha=alpha, seed=0xB4E5B41D6E,
+                                threads=threads, record=False)
+    log(f"[cpu_baseline] sparse threads={threads}: {sweeps} sweeps in {r['runtime']:.3f} s")
+    return r["runtime"] / sweeps, threads
 
 
 def blas_threads(threads):
@@ -225,9 +215,38 @@ def pmc_traffic(n, p, world, kernel):
         if w.get("n") != n or w.get("p") != p or world != 1:
             continue
         for k, v in d.get("kernels", {}).items():
-            if (k == kernel or k.startswith(kernel + "<")) and v.get("hbm_bytes") == v.get(
+            # exact name, a template instance, or (for the latency-bound phases, named by
+            # their family: bb::k_lambda, bb::k_bsolve, bb::k_beta) any kernel of the family
+            if k.startswith(kernel) and v.get("hbm_bytes") == v.get(
                     "hbm_bytes"):  # skip NaN (kernel missing from one of the passes)
                 best = (v["hbm_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
+def pmc_mfma(n, p, world, kernel, gram):
+    """MFMA-busy evidence for `kernel` at this workload from the newest committed
+    profiles/rNN_pmc_mfma.json (tools/pmc_mfma.sh: SQ_VALU_MFMA_BUSY_CYCLES and
+    GRBM_GUI_ACTIVE in separate rocprofv3 --pmc passes; tools/pmc_mfma_summary.py), or None."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_mfma.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for cfg in d.get("configs", {}).values():
+            if cfg.get("n") != n or cfg.get("p") != p or world != 1 or cfg.get("gram") != gram:
+                continue
+            for k, v in cfg.get("kernels", {}).items():
+                if k.startswith(kernel) and "mfma_busy_frac" in v:
+                    best = {"mfma_busy_frac": v["mfma_busy_frac"],
+                            "mfma_busy_frac_nominal_clock": v.get("mfma_busy_frac_nominal_clock"),
+                            "effective_clock_GHz": v.get("effective_clock_GHz"),
+                            "source": os.path.relpath(f, ROOT),
+                            "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
+                                          "GRBM_GUI_ACTIVE / 8 XCDs); _nominal_clock: over "
+                                          "1024 x 2.4 GHz x the dispatch duration"}
     return best
 
 
@@ -297,7 +316,9 @@ def roofline_for(phase, ms, ctx, traffic_world):
         # m^3/3 algorithmic flops; its time is set by the chain of m_pad/64 dependent block
         # steps, reported as the latency model beside the flop rate
         m = p if logit else n
-        m_pad = -(-m // 256) * 256 if logit else -(-n // 128) * 128
+        # the p x p system is factored at round_up(p, 64) (bb_engine.cpp chol_m); the n x n
+        # Woodbury system at n_pad = round_up(n, 128)
+        m_pad = -(-m // CHOL_NB) * CHOL_NB if logit else -(-n // 128) * 128
         flops = m ** 3 / 3.0
         steps = m_pad // CHOL_NB
         kfull = "bb::k_chol_persistent"
@@ -316,6 +337,10 @@ def roofline_for(phase, ms, ctx, traffic_world):
         out.update(bound="latency", kernel=kfull, achieved=None, peak=None, unit=None)
     out["frac"] = (out["achieved"] / out["peak"]) if out.get("peak") else None
     tr = pmc_traffic(n, p, traffic_world, kfull)
+    if out.get("bound") == "mfma":
+        mf = pmc_mfma(n, p, traffic_world, kfull, ctx.get("gram_name"))
+        out["mfma_busy_frac"] = mf["mfma_busy_frac"] if mf else None
+        out["mfma_busy"] = mf
     out["traffic"] = tr[0] if tr else None
     out["traffic_unit"] = "HBM bytes per launch (rocprofv3 PMC)"
     out["traffic_source"] = tr[1] if tr else None
@@ -409,7 +434,7 @@ def run_chain(args, n, p, alpha, kind, mode):
 
     sparse, logit = kind == "sparse", kind == "logit"
     cpu_sweeps = args.cpu_sweeps if args.cpu_sweeps is not None else \
-        (2 if sparse else 20 if logit else 5)
+        (5 if sparse else 40 if logit else 5)
     world = args.gpus
     rank = int(os.environ.get("RANK", "0")) if mode == "ranks" else 0
     local_rank = int(os.environ.get("LOCAL_RANK", "0")) if mode == "ranks" else 0
@@ -520,7 +545,12 @@ def run_chain(args, n, p, alpha, kind, mode):
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
         log(f"[rank {rank}] WARNING: state tau={st['tau']} sig2={st['sig2']} flags={flags}")
 
-    ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode())
+    gram_name = ("pair-list sparse Gram (fp64)" if sparse else
+                 ("X'Omega X " if logit else "") +
+                 ("ozaki-II int8 (fp64-accurate)" if eng.gram_mode() == bb.GRAM_OZAKI
+                  else "fp64 mfma"))
+    ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
+               gram_name=gram_name)
     traffic_world = 1 if mode == "single" else world
     roof = roofline_for(dom, dom_ms, ctx, traffic_world)
     roof["timing"] = "HIP events on rank 0's engine stream around every timed launch"
@@ -547,14 +577,11 @@ def run_chain(args, n, p, alpha, kind, mode):
                   "alpha": alpha, "mode": mode, "parallelism": par,
                   "beta_step": ("p x p Cholesky of X'Omega X + diag(lambda/tau^2)" if logit
                                 else "woodbury (exact, p > n)")}
+        config["gram"] = gram_name
         if sparse:
             si = eng.sparse_info()
-            config.update(gram="pair-list sparse Gram (fp64)", density=SPARSE_DENSITY,
-                          nnz_local=si["nnz"], pairs_local=si["pairs"], max_row_nnz=si["max_row"])
-        else:
-            config["gram"] = (("X'Omega X " if logit else "") +
-                              ("ozaki-II int8 (fp64-accurate)"
-                               if eng.gram_mode() == bb.GRAM_OZAKI else "fp64 mfma"))
+            config.update(density=SPARSE_DENSITY, nnz_local=si["nnz"], pairs_local=si["pairs"],
+                          max_row_nnz=si["max_row"])
         rec = {
             "metric": f"Gibbs sweeps/sec at n={n},p={p},alpha={alpha}",
             "value": value,
@@ -661,11 +688,12 @@ def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
     log(f"[cpu_baseline] timing {cpu_sweeps} CPU sweeps at n={n}, p={p} ...")
     if sparse:
         per_sweep, threads = cpu_baseline_sparse(n, p, alpha, cpu_sweeps)
-        what = ("oracle Woodbury sweeps (scipy SpGEMM + LAPACK, numpy, + C tilted-stable "
-                "sampler)")
+        what = ("compiled C sparse Woodbury chain (oracle/bb_cpu_chain.c: OpenMP sparse Gram "
+                "by output column + dpotrf, scipy OpenBLAS, OpenMP lambda draws)")
     elif logit:
         per_sweep, threads = cpu_baseline_logit(n, p, alpha, cpu_sweeps)
-        what = "oracle logistic sweeps (numpy X'Omega X + LAPACK + C Polya-Gamma sampler)"
+        what = ("compiled C logistic chain (oracle/bb_cpu_chain.c: dsyrk X'Omega X + dpotrf, "
+                "scipy OpenBLAS, OpenMP Polya-Gamma and lambda draws)")
     else:
         per_sweep, threads = cpu_baseline(n, p, alpha, cpu_sweeps)
         what = ("compiled C Woodbury chain (oracle/bb_cpu_chain.c: dsyrk + dpotrf + dgemv, "
@@ -676,6 +704,15 @@ def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
     # the CPU baseline at 1 core and all cores, for the algorithm-matched
     # Woodbury chain and (p <= 8000) the reference-literal p x p path
     cpu_more = None
+    if sparse or logit:
+        # the same compiled chain on one core
+        ns = max(1, min(cpu_sweeps, 2 if sparse else 3))
+        per1, th1 = (cpu_baseline_sparse if sparse else cpu_baseline_logit)(n, p, alpha, ns,
+                                                                            threads=1)
+        cpu_more = [dict(cpu, path="all cores"),
+                    {"value": 1.0 / per1, "unit": "sweeps/s", "cores": th1, "kind": "port",
+                     "path": "1 core", "sample": f"{ns} sweeps of the same compiled C chain, "
+                                                 f"{per1:.3f} s per sweep"}]
     if kind == "dense":
         cpu_more = [dict(cpu, path="Woodbury (algorithm-matched to the GPU)")]
         variants = [(False, 1, max(1, min(cpu_sweeps, 3)))]

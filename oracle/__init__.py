@@ -298,3 +298,65 @@ def cpu_chain(y, X, nsamp, burn=500, alpha=0.5, method="auto", sig2_shape=0.0, s
     if rt < 0:
         raise RuntimeError(f"bbc_stable_chain failed ({rt})")
     return dict(beta=beta, tau=tau, sig2=sig2, runtime=rt, method=method)
+
+
+def _cpu_lib_ext():
+    L = cpu_lib()
+    if not getattr(L, "_ext", False):
+        d, i, u64 = ctypes.c_double, ctypes.c_int, ctypes.c_uint64
+        L.bbc_logit_chain.argtypes = [_dp, _dp, i, i, d, d, d, i, i, u64, u64, i, _dp, _dp]
+        L.bbc_logit_chain.restype = d
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.bbc_sparse_chain.argtypes = [ip, ip, _dp, _dp, i, i, d, d, d, d, d, i, i, u64, u64, i,
+                                       _dp, _dp, _dp]
+        L.bbc_sparse_chain.restype = d
+        L._ext = True
+    return L
+
+
+def cpu_logit_chain(y, X, nsamp, burn=500, alpha=0.5, nu_shape=2.0, nu_rate=2.0, seed=0,
+                    stream=0, threads=1, record=True):
+    """The logistic (Polya-Gamma) bridge chain in compiled C (bb_cpu_chain.c
+    bbc_logit_chain): gibbs.bridge_regression_logit with alpha known, on the same counters.
+    Returns dict(beta P x M, tau, runtime = post-burn seconds)."""
+    X = np.asfortranarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    n, p = X.shape
+    M = int(nsamp)
+    beta = np.zeros((p, M), order="F") if record else None
+    tau = np.zeros(M)
+    rt = _cpu_lib_ext().bbc_logit_chain(_ptr(X), _ptr(y), n, p, alpha, nu_shape, nu_rate,
+                                        int(burn), M, seed, stream, int(threads),
+                                        _ptr(beta) if record else None, _ptr(tau))
+    if rt < 0:
+        raise RuntimeError(f"bbc_logit_chain failed ({rt})")
+    return dict(beta=beta, tau=tau, runtime=rt)
+
+
+def cpu_sparse_chain(y, X, nsamp, burn=500, alpha=0.5, nu_shape=2.0, nu_rate=2.0,
+                     sig2_shape=0.0, sig2_scale=0.0, seed=0, stream=0, threads=1, record=True):
+    """The stable chain on a sparse CSC design (p > n, Woodbury form) in compiled C
+    (bb_cpu_chain.c bbc_sparse_chain: CSR/CSC passes, OpenMP sparse Gram, LAPACK dpotrf).
+    Same driver and counters as gibbs.bridge_regression_stable(method="woodbury").
+    Returns dict(beta P x M, tau, sig2, runtime = post-burn seconds)."""
+    import scipy.sparse as sps
+
+    Xc = sps.csc_matrix(X, dtype=np.float64)
+    Xc.sort_indices()
+    n, p = Xc.shape
+    colptr = np.ascontiguousarray(Xc.indptr, dtype=np.int32)
+    rowidx = np.ascontiguousarray(Xc.indices, dtype=np.int32)
+    val = np.ascontiguousarray(Xc.data, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    M = int(nsamp)
+    beta = np.zeros((p, M), order="F") if record else None
+    tau, sig2 = np.zeros(M), np.zeros(M)
+    ip = ctypes.POINTER(ctypes.c_int)
+    rt = _cpu_lib_ext().bbc_sparse_chain(colptr.ctypes.data_as(ip), rowidx.ctypes.data_as(ip),
+                                         _ptr(val), _ptr(y), n, p, alpha, nu_shape, nu_rate,
+                                         sig2_shape, sig2_scale, int(burn), M, seed, stream,
+                                         int(threads), _ptr(beta) if record else None,
+                                         _ptr(tau), _ptr(sig2))
+    if rt < 0:
+        raise RuntimeError(f"bbc_sparse_chain failed ({rt})")
+    return dict(beta=beta, tau=tau, sig2=sig2, runtime=rt)

@@ -326,3 +326,244 @@ done:
     free(ch.w);
     return rt;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* BASELINE config C4 (no reference counterpart): the logistic bridge by Polya-Gamma      */
+/* latents, oracle/gibbs.py logit_sweep / bridge_regression_logit compiled:               */
+/*   tau | beta (BridgeRegression.cpp:453-465), lambda | beta, tau (:506-510),            */
+/*   omega_i ~ PG(1, x_i'beta) (bbo_pg1), beta | omega, lambda, tau by the reference's    */
+/*   sample_beta_stable map (:552-575) with sig2 = 1, X'X -> X'Omega X (dsyrk of          */
+/*   diag(sqrt omega) X) and X'y -> X'(y - 1/2).                                          */
+/* beta0 = 0, the pre-burn tau draw at t = 0, burn + 1 sweeps in slot 0, MCMC sweep i at   */
+/* t = burn + 1 + i.  Returns the post-burn seconds, or < 0 on failure (-1 allocation,    */
+/* -2 a PG draw failed, -(1 + info) LAPACK).                                              */
+/* ------------------------------------------------------------------------------------ */
+long bbo_pg_batch(double *omega, const double *psi, long n, const uint64_t key[2], uint64_t t);
+double bbo_pg1(double psi, const uint64_t key[2], uint64_t t, uint64_t i, int *fail);
+
+double bbc_logit_chain(const double *X, const double *y, int n, int p, double alpha,
+                       double nu_shape, double nu_rate, int burn, int M, uint64_t seed,
+                       uint64_t stream, int threads, double *beta_out, double *tau_out)
+{
+    if (threads < 1) threads = 1;
+    scipy_openblas_set_num_threads(threads);
+    omp_set_num_threads(threads);
+    Chain ch = {0};
+    ch.n = n;
+    ch.p = p;
+    ch.method = 0;
+    ch.X = X;
+    ch.y = y;
+    ch.alpha = alpha;
+    ch.nu_shape = nu_shape;
+    ch.nu_rate = nu_rate;
+    ch.key[0] = seed;
+    ch.key[1] = stream;
+    const size_t pp = (size_t)p * p, np_ = (size_t)n * p;
+    double *beta = calloc(p, sizeof(double)), *lam = calloc(p, sizeof(double));
+    double *psi = calloc(n, sizeof(double)), *om = calloc(n, sizeof(double));
+    double *kap = calloc(n, sizeof(double)), *Yw = malloc(sizeof(double) * np_);
+    ch.c = calloc(p, sizeof(double));
+    ch.z = calloc(p, sizeof(double));
+    ch.G = malloc(sizeof(double) * pp);
+    ch.A = malloc(sizeof(double) * pp);
+    double rt = -1.0;
+    long fails = 0;
+    int info = 0;
+    if (!beta || !lam || !psi || !om || !kap || !Yw || !ch.c || !ch.z || !ch.G || !ch.A)
+        goto done;
+    for (int i = 0; i < n; ++i) kap[i] = y[i] - 0.5;
+    gemv('T', n, p, 1.0, X, kap, 0.0, ch.c); /* X'(y - 1/2) */
+    double tau = draw_tau(&ch, beta, 0);
+    double t0 = 0.0;
+    for (int s = -1 - burn; s < M && !info && !fails; ++s) {
+        /* s < 0: burn-in sweep (slot 0, t = burn + 2 + s); s = 0 starts the clock; s >= 1: MCMC */
+        if (s == 0) {
+            if (beta_out) memcpy(beta_out, beta, sizeof(double) * p);
+            if (tau_out) tau_out[0] = tau;
+            t0 = now_s();
+            continue;
+        }
+        const uint64_t t = s < 0 ? (uint64_t)(burn + 2 + s) : (uint64_t)burn + 1 + (uint64_t)s;
+        tau = draw_tau(&ch, beta, t);
+        draw_lambda(lam, beta, p, alpha, tau, ch.key, t);
+        gemv('N', n, p, 1.0, X, beta, 0.0, psi); /* x_i'beta */
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : fails)
+        for (long i = 0; i < n; ++i) {
+            int f = 0;
+            om[i] = bbo_pg1(psi[i], ch.key, t, (uint64_t)i, &f);
+            fails += f;
+        }
+#pragma omp parallel for schedule(static)
+        for (long j = 0; j < p; ++j) { /* Yw = diag(sqrt omega) X */
+            const double *xs = X + (size_t)j * n;
+            double *ys = Yw + (size_t)j * n;
+            for (int i = 0; i < n; ++i) ys[i] = xs[i] * sqrt(om[i]);
+        }
+        const double one = 1.0, zero = 0.0;
+        scipy_dsyrk_("U", "T", &p, &n, &one, Yw, &n, &zero, ch.G, &p, 1, 1); /* X'Omega X */
+        info = beta_chol(&ch, lam, 1.0, tau, t, beta);
+        if (s >= 1) {
+            if (beta_out) memcpy(beta_out + (size_t)s * p, beta, sizeof(double) * p);
+            if (tau_out) tau_out[s] = tau;
+        }
+    }
+    rt = fails ? -2.0 : info ? -(1.0 + info) : now_s() - t0;
+done:
+    free(beta);
+    free(lam);
+    free(psi);
+    free(om);
+    free(kap);
+    free(Yw);
+    free(ch.c);
+    free(ch.z);
+    free(ch.G);
+    free(ch.A);
+    return rt;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* BASELINE config C5 (no reference counterpart): the stable chain on a sparse CSC design */
+/* (p > n), the exact Woodbury form of BridgeRegression.cpp:552-575 as beta_woodbury above */
+/* with the three passes over X done sparse: X beta and X u by CSR rows, X'w by CSC       */
+/* columns, and the n x n Gram X diag(D) X' by output column (CSR row c x the CSC columns  */
+/* it touches, OpenMP over columns), then dpotrf.  Driver as bbc_stable_chain (beta0 = 0, */
+/* pre-burn tau, burn + 1 sweeps in slot 0).  Returns post-burn seconds or < 0.           */
+/* ------------------------------------------------------------------------------------ */
+double bbc_sparse_chain(const int *colptr, const int *rowidx, const double *val, const double *y,
+                        int n, int p, double alpha, double nu_shape, double nu_rate,
+                        double sig2_shape, double sig2_scale, int burn, int M, uint64_t seed,
+                        uint64_t stream, int threads, double *beta_out, double *tau_out,
+                        double *sig2_out)
+{
+    if (threads < 1) threads = 1;
+    scipy_openblas_set_num_threads(threads);
+    omp_set_num_threads(threads);
+    Chain ch = {0};
+    ch.n = n;
+    ch.p = p;
+    ch.alpha = alpha;
+    ch.nu_shape = nu_shape;
+    ch.nu_rate = nu_rate;
+    ch.sig2_shape = sig2_shape;
+    ch.sig2_scale = sig2_scale;
+    ch.key[0] = seed;
+    ch.key[1] = stream;
+    const long nnz = colptr[p];
+    const size_t nn = (size_t)n * n;
+    int *rowptr = calloc((size_t)n + 1, sizeof(int)), *colidx = malloc(sizeof(int) * (nnz + 1));
+    double *rval = malloc(sizeof(double) * (nnz + 1));
+    double *beta = calloc(p, sizeof(double)), *lam = calloc(p, sizeof(double));
+    double *D = calloc(p, sizeof(double)), *u = calloc(p, sizeof(double));
+    double *z = calloc(p, sizeof(double)), *xtw = calloc(p, sizeof(double));
+    double *r = calloc(n, sizeof(double)), *v = calloc(n, sizeof(double));
+    double *d = calloc(n, sizeof(double)), *w = calloc(n, sizeof(double));
+    double *Mm = malloc(sizeof(double) * nn);
+    double rt = -1.0;
+    int info = 0;
+    if (!rowptr || !colidx || !rval || !beta || !lam || !D || !u || !z || !xtw || !r || !v ||
+        !d || !w || !Mm)
+        goto done;
+    /* CSR copy (entries of a row in column order) */
+    for (long q = 0; q < nnz; ++q) ++rowptr[rowidx[q] + 1];
+    for (int i = 0; i < n; ++i) rowptr[i + 1] += rowptr[i];
+    {
+        int *next = malloc(sizeof(int) * (size_t)n);
+        if (!next) goto done;
+        memcpy(next, rowptr, sizeof(int) * (size_t)n);
+        for (int j = 0; j < p; ++j)
+            for (int q = colptr[j]; q < colptr[j + 1]; ++q) {
+                const int k = next[rowidx[q]]++;
+                colidx[k] = j;
+                rval[k] = val[q];
+            }
+        free(next);
+    }
+    double tau = draw_tau(&ch, beta, 0), sig2 = 0.0;
+    double t0 = 0.0;
+    for (int s = -1 - burn; s < M && !info; ++s) {
+        if (s == 0) {
+            if (beta_out) memcpy(beta_out, beta, sizeof(double) * p);
+            if (tau_out) tau_out[0] = tau;
+            if (sig2_out) sig2_out[0] = sig2;
+            t0 = now_s();
+            continue;
+        }
+        const uint64_t t = s < 0 ? (uint64_t)(burn + 2 + s) : (uint64_t)burn + 1 + (uint64_t)s;
+        tau = draw_tau(&ch, beta, t);
+        double rss = 0.0; /* r = y - X beta by CSR rows */
+#pragma omp parallel for schedule(static) reduction(+ : rss)
+        for (int i = 0; i < n; ++i) {
+            double a = 0.0;
+            for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) a += rval[k] * beta[colidx[k]];
+            const double ri = y[i] - a;
+            rss += ri * ri;
+        }
+        sig2 = bbo_sig2_from_rss(rss, n, sig2_shape, sig2_scale, ch.key, t);
+        draw_lambda(lam, beta, p, alpha, tau, ch.key, t);
+        /* beta | rest, Woodbury: u = sqrt(D) z, v = X u / sig + delta, M = I + X D X' / sig2 */
+        const double sig = sqrt(sig2);
+        bbo_normals(z, p, ch.key, t, KIND_BETA_Z, 0);
+        bbo_normals(d, n, ch.key, t, KIND_DELTA, 0);
+#pragma omp parallel for schedule(static)
+        for (long j = 0; j < p; ++j) {
+            D[j] = tau * tau / lam[j];
+            u[j] = sqrt(D[j]) * z[j];
+        }
+#pragma omp parallel for schedule(static)
+        for (int i = 0; i < n; ++i) {
+            double a = 0.0;
+            for (int k = rowptr[i]; k < rowptr[i + 1]; ++k) a += rval[k] * u[colidx[k]];
+            v[i] = a / sig + d[i];
+        }
+        /* upper triangle, column c: M[r][c] = sum_j X_rj X_cj D_j / sig2 over j in row c */
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int c = 0; c < n; ++c) {
+            double *mc = Mm + (size_t)c * n;
+            memset(mc, 0, sizeof(double) * (size_t)(c + 1));
+            for (int k = rowptr[c]; k < rowptr[c + 1]; ++k) {
+                const int j = colidx[k];
+                const double f = rval[k] * D[j];
+                for (int q = colptr[j]; q < colptr[j + 1] && rowidx[q] <= c; ++q)
+                    mc[rowidx[q]] += val[q] * f;
+            }
+            for (int rr = 0; rr <= c; ++rr) mc[rr] /= sig2;
+            mc[c] += 1.0;
+        }
+        scipy_dpotrf_("U", &n, Mm, &n, &info, 1);
+        if (info) break;
+        for (int i = 0; i < n; ++i) w[i] = y[i] / sig - v[i];
+        trsv_u('T', n, Mm, w);
+        trsv_u('N', n, Mm, w);
+#pragma omp parallel for schedule(static)
+        for (long j = 0; j < p; ++j) { /* X'w by CSC columns, beta = u + D X'w / sig */
+            double a = 0.0;
+            for (int q = colptr[j]; q < colptr[j + 1]; ++q) a += val[q] * w[rowidx[q]];
+            xtw[j] = a;
+            beta[j] = u[j] + D[j] * a / sig;
+        }
+        if (s >= 1) {
+            if (beta_out) memcpy(beta_out + (size_t)s * p, beta, sizeof(double) * p);
+            if (tau_out) tau_out[s] = tau;
+            if (sig2_out) sig2_out[s] = sig2;
+        }
+    }
+    rt = info ? -(1.0 + info) : now_s() - t0;
+done:
+    free(rowptr);
+    free(colidx);
+    free(rval);
+    free(beta);
+    free(lam);
+    free(D);
+    free(u);
+    free(z);
+    free(xtw);
+    free(r);
+    free(v);
+    free(d);
+    free(w);
+    free(Mm);
+    return rt;
+}

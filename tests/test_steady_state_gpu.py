@@ -36,11 +36,13 @@ SEED = 0xB4E5B41D6E
 HYPER = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
 
 
-def oracle_sweep(X, y, beta, tau, sig2, alpha, t, seed, stream):
-    """One oracle sweep (tau, sig2, lambda, beta) from a given state, Woodbury form."""
+def oracle_sweep(X, y, beta, tau, sig2, alpha, t, seed, stream, know_tau=False):
+    """One oracle sweep (tau, sig2, lambda, beta) from a given state, Woodbury form
+    (know_tau: tau stays as given, the reference's true_tau > 0)."""
     n, p = X.shape
-    tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, HYPER["nu_shape"],
-                              HYPER["nu_rate"], seed, stream, t)
+    if not know_tau:
+        tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, alpha), p, alpha, HYPER["nu_shape"],
+                                  HYPER["nu_rate"], seed, stream, t)
     r = y - X @ beta
     sig2 = oracle.sig2_from_rss(float(r @ r), n, HYPER["sig2_shape"], HYPER["sig2_scale"], seed,
                                 stream, t)
@@ -177,23 +179,33 @@ def test_free_running_posterior_moments_wide(gpu_lib):
     assert set(np.argsort(-np.abs(g.mean(axis=0)))[:5]) == set(range(5))
 
 
-@pytest.mark.parametrize("name", ["c3", "c5"])
-def test_fitted_regime_teacher_forced(gpu_lib, name, capsys):
-    """C3 and C5 teacher-forced in the regime the sampler spends its run in:
-    the GPU chain starts at the data-generating coefficients with tau = 1e-2 and sig2 = 1 and
-    runs FREE for 300 sweeps, so lambda, tau, sig2 and D = tau^2 / lambda are the sampler's
-    own; then cond(M) of the next sweep's system must exceed 1e3 (printed, with tau, sig2 and
-    the span of D), and three sweeps are teacher-forced against the oracle (the Woodbury
+@pytest.mark.parametrize("name,true_tau", [("c3", 0.0), ("c5", 1e-3)])
+def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, capsys):
+    """C3 and C5 teacher-forced in the fitted regime: the GPU chain starts at
+    the data-generating coefficients with tau = 1e-2 and sig2 = 1 and runs FREE for 300
+    sweeps, so lambda, sig2, D = tau^2 / lambda (and tau at C3) are the sampler's own; then
+    cond(M) of the next sweep's system must exceed 1e3 (printed, with tau, sig2 and the
+    span of D), and three sweeps are teacher-forced against the oracle (the Woodbury
     restatement of BridgeRegression.cpp:552-575) at the steady-state bars: beta 1e-9
-    relative L2, lambda / tau / sig2 1e-11 relative, no decision flips."""
+    relative L2, lambda / tau / sig2 1e-11 relative, no decision flips.
+
+    C5 (alpha = 0.3, p = 200 000, 99 % of the true coefficients exactly 0) has no fitted
+    regime with tau drawn: tau | beta ~ Ga(2 + p / alpha, 2 + sum |beta_j|^alpha)^(-1/alpha)
+    puts tau at 7.5e-9 already at the truth, and the oracle chain from there is back at
+    beta = 0 (sig2 = var(y) = 90, max_j D_j |x_j|^2 / sig2 = 2e-3) within four sweeps.  So
+    C5 runs with tau known (the reference's true_tau > 0, BridgeWrapper.cpp:248-250) at
+    1e-3, where the oracle chain stays fitted (sig2 ~ 0.77, D over 14 decades,
+    max_j D_j |x_j|^2 / sig2 ~ 5e3-1e4); tau's own conditional is checked at C5 by
+    test_steady_state_teacher_forced."""
     bb = gpu_lib
     X, y, alpha, btrue = workload(name, with_truth=True)
     n, p = X.shape
+    know_tau = true_tau > 0
     e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, true_alpha=alpha,
-                                  trace_capacity=1), X, y)
+                                  true_tau=true_tau, trace_capacity=1), X, y)
     assert e.method() in (2, 5)
     e.init_state()
-    e.set_state(btrue, 1e-2, 1.0, alpha)
+    e.set_state(btrue, true_tau if know_tau else 1e-2, 1.0, alpha)
     e.run(2, 300, first_slot=-1)  # free-running from the fitted start
     e.sync()
     assert e.error_flags() == 0
@@ -205,7 +217,8 @@ def test_fitted_regime_teacher_forced(gpu_lib, name, capsys):
         e.set_state(beta, tau, sig2, alpha)
         e.run(t, 1, first_slot=-1)
         g = e.state()
-        b, lam, tau, sig2 = oracle_sweep(X, y, beta, tau, sig2, alpha, t, SEED, 0)
+        b, lam, tau, sig2 = oracle_sweep(X, y, beta, tau, sig2, alpha, t, SEED, 0,
+                                         know_tau=know_tau)
         if t == 2001:
             cond, span = m_condition(X, lam, tau, sig2)
             with capsys.disabled():

@@ -6,7 +6,9 @@ MI355X_MICROARCH.md "DVFS give-back") and SQ_BUSY_CU_CYCLES, and
   kernel_cycles   = GRBM_GUI_ACTIVE / 8
   mfma_busy_frac  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel_cycles)
 i.e. the fraction of the SIMDs' cycles (at whatever clock the chip ran) in which an MFMA
-executed.  For k_oz_gemm16u the MFMA count is known exactly (16 n_oz-row residue Grams,
+executed, and mfma_busy_frac_nominal_clock, the same busy cycles over 1024 x 2.4 GHz x the
+dispatch's duration (the MFMA pass's timestamps) -- comparable with an ops fraction of the
+nominal peak.  For k_oz_gemm16u the MFMA count is known exactly (16 n_oz-row residue Grams,
 v_mfma_i32_16x16x64_i8 = 16 cycles each), which checks the counter's normalisation.
 Usage: python tools/pmc_mfma_summary.py r04
 """
@@ -26,7 +28,8 @@ def short(name):
 
 
 def avgs(d, counter):
-    tot, cnt = {}, {}
+    """{kernel: (average counter value, dispatches, average duration in s)}"""
+    tot, cnt, dur = {}, {}, {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
@@ -34,7 +37,8 @@ def avgs(d, counter):
             k = short(r["Kernel_Name"])
             tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
             cnt[k] = cnt.get(k, 0) + 1
-    return {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
+            dur[k] = dur.get(k, 0.0) + (float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9
+    return {k: (tot[k] / cnt[k], cnt[k], dur[k] / cnt[k]) for k in tot}
 
 
 def bench_line(d):
@@ -60,7 +64,8 @@ def main():
         cu = avgs(os.path.join(d, "SQ_BUSY_CU_CYCLES"), "SQ_BUSY_CU_CYCLES")
         bl = bench_line(d)
         c = bl.get("config", {})
-        ent = {"workload": c.get("workload"), "gram": c.get("gram"), "kernels": {}}
+        ent = {"workload": c.get("workload"), "n": c.get("n"), "p": c.get("p"),
+               "gram": c.get("gram"), "kernels": {}}
         for k in sorted(set(mf) | set(gr)):
             e = {"dispatches": (mf.get(k) or gr.get(k))[1]}
             if k in mf:
@@ -68,10 +73,18 @@ def main():
             if k in gr:
                 e["GRBM_GUI_ACTIVE"] = gr[k][0]
                 e["kernel_cycles"] = gr[k][0] / XCDS
+                # the dispatch's own duration in the profiled pass (counter-collection
+                # timestamps) and the clock it implies (MI355X_MICROARCH.md: reads high for
+                # dispatches shorter than ~0.3 ms)
+                e["duration_ms_profiled"] = gr[k][2] * 1e3
+                e["effective_clock_GHz"] = gr[k][0] / XCDS / gr[k][2] / 1e9
             if k in cu:
                 e["SQ_BUSY_CU_CYCLES"] = cu[k][0]
             if k in mf and k in gr and gr[k][0] > 0:
                 e["mfma_busy_frac"] = mf[k][0] / (SIMDS * gr[k][0] / XCDS)
+                # the same busy cycles against the nominal 2.4 GHz over the MFMA pass's own
+                # duration: comparable with the roofline's ops fraction at nominal peak
+                e["mfma_busy_frac_nominal_clock"] = mf[k][0] / (SIMDS * 2.4e9 * mf[k][2])
             if k.startswith("bb::k_oz_gemm16u") and c.get("n"):
                 n, p = int(c["n"]), int(c["p"])
                 n_oz = -(-(-(-n // 128) * 128) // 256) * 256
