@@ -132,6 +132,9 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_debug_interrupt_after.argtypes = [c.c_int]
     L.bb_last_call_info.argtypes = [_ip, _ip, _ip]
     L.bb_debug_fail_member.argtypes = [c.c_int, c.c_int]
+    u64p = c.POINTER(c.c_ulonglong)
+    L.bb_engine_nid_stats.argtypes = [c.c_void_p, u64p, u64p, u64p, _dp, _ip]
+    L.bb_engine_timed_brackets.argtypes = [c.c_void_p, _ip]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -1064,6 +1067,25 @@ class Engine:
         _check(L.bb_engine_phase_times(self._h, _p(ms), k, ctypes.byref(n)),
                "bb_engine_phase_times")
         return {L.bb_phase_name(i).decode(): float(ms[i]) for i in range(k) if ms[i] > 0}
+
+    def timed_brackets(self) -> int:
+        """Launches of the timed phase bracketed since the last reset_timing()."""
+        k = ctypes.c_int()
+        _check(library().bb_engine_timed_brackets(self._h, ctypes.byref(k)),
+               "bb_engine_timed_brackets")
+        return int(k.value)
+
+    def nid_stats(self):
+        """Near-identity (Chebyshev) solve counters: dict(cheb_sweeps,
+        products, chol_sweeps, eps, mode) -- mode/eps of the latest sweep, -1 when the engine
+        has no near-identity path."""
+        a, b, c = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        eps, mode = ctypes.c_double(), ctypes.c_int()
+        _check(library().bb_engine_nid_stats(self._h, ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(c), ctypes.byref(eps),
+                                             ctypes.byref(mode)), "bb_engine_nid_stats")
+        return dict(cheb_sweeps=a.value, products=b.value, chol_sweeps=c.value, eps=eps.value,
+                    mode=mode.value)
 
     def error_flags(self) -> int:
         f = ctypes.c_uint32()

@@ -244,13 +244,14 @@ struct SparseDesign {
     }
 
     // tri (packed upper triangle of X diag(D) X', n_pad wide) and xu = X u
-    void gram(hipStream_t s, const double *D, const double *u, double *tri, double *xu) const {
+    void gram(hipStream_t s, const double *D, const double *u, double *tri, double *xu,
+              const int *gate = nullptr) const {
         if (col_mode) {
             launch_sp_gram_col(s, rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad, max_row,
-                               tri, xu);
+                               tri, xu, gate);
         } else {
-            launch_sp_gram(s, estart, prod, pj, D, n_pad, tri);
-            launch_sp_rows(s, rowptr, colidx, rval, n_pad, u, D, xu, tri);
+            launch_sp_gram(s, estart, prod, pj, D, n_pad, tri, gate);
+            launch_sp_rows(s, rowptr, colidx, rval, n_pad, u, D, xu, tri, gate);
         }
     }
 };
@@ -262,13 +263,19 @@ struct SparseDesign {
 // ---------------------------------------------------------------------------
 enum Phase {
     PH_PRE, PH_SCALARS, PH_LAMBDA, PH_PG, PH_OZPREP, PH_GRAM, PH_XU, PH_REDUCE, PH_FORM, PH_CHOL,
-    PH_SOLVE, PH_BETA, PH_XB, PH_ALPHA, PH_END, PH_COUNT
+    PH_SOLVE, PH_BETA, PH_XB, PH_ALPHA, PH_NID, PH_EAPPLY, PH_END, PH_COUNT
 };
 // "gram" times the Gram GEMM kernel alone (k_gram, or k_oz_gemm after "ozprep" = row scales
-// + residues); "reduce" is the split/slab combine (k_slab_sum or the CRT k_oz_crt).
+// + residues); "reduce" is the split/slab combine (k_slab_sum or the CRT k_oz_crt); "nid" the
+// near-identity decision, X u and Chebyshev recurrences, "eapply" its passes over X
+// (bb_nid.hip).
+
+// Chebyshev iterations the near-identity solve may take per sweep (bb_set_tuning key 6; 0
+// turns the path off: every sweep forms the Gram and factors it)
+int g_nid_kmax = 16;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
-                                            "xb", "alpha", "end"};
+                                            "xb", "alpha", "nid", "eapply", "end"};
 
 struct bb_engine {
     bb_config cfg{};
@@ -319,6 +326,17 @@ struct bb_engine {
     double *tr_beta = nullptr, *tr_lam = nullptr, *tr_sig2 = nullptr, *tr_tau = nullptr,
            *tr_alpha = nullptr;
     int cap = 1;
+    // near-identity solve of the Woodbury system (bb_nid.hip): column norms,
+    // the device decision word, Chebyshev vectors (x is w), E-apply partials, the host-mapped
+    // eps of the latest decided sweep (the launch hint) and the enqueue throttle
+    double *cn = nullptr;
+    NidState *nid = nullptr;
+    double *ch_r = nullptr, *ch_d = nullptr, *ea_part = nullptr, *sp_s = nullptr,
+           *nid_xu = nullptr;
+    double *eps_host = nullptr;
+    int ea_parts = 1;
+    hipEvent_t thr_ev[3] = {nullptr, nullptr, nullptr};
+    long thr_n = 0;
     // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
     ncclComm_t comm = nullptr;
     bool own_comm = true;
@@ -348,6 +366,9 @@ struct bb_engine {
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm && own_comm) ncclCommDestroy(comm);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
+        for (auto e : thr_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (eps_host) (void)hipHostFree(eps_host);
         for (void *q : owned) (void)hipFree(q);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -373,6 +394,55 @@ struct bb_engine {
     }
 
     bool woodbury() const { return method == 2 || method == 5; }
+
+    // the near-identity path exists for an unsharded Woodbury engine (world == 1; a one-member
+    // RCCL group included: nothing is exchanged)
+    bool nid_enabled() const { return nid != nullptr && cfg.world == 1 && g_nid_kmax > 0; }
+
+    // Chebyshev iterations to launch for this sweep: from the eps of the latest sweep the
+    // device decided (host-mapped, at most ~8 sweeps old through the enqueue throttle) with an
+    // 8x growth margin; no observation yet: the maximum; beyond the maximum: 0 (only the Gram
+    // + Cholesky path is launched).  The device decides the sweep itself (k_nid_decide): too
+    // few iterations launched makes that sweep take the Gram + Cholesky path, never a wrong w.
+    int nid_launch_count() const {
+        if (!nid_enabled()) return 0;
+        const double h = *(volatile double *)eps_host;
+        if (!(h >= 0.0)) return g_nid_kmax;
+        return cheb_iterations(8.0 * h, g_nid_kmax, kNidTol);
+    }
+
+    // decision kernel of a Woodbury sweep (eps is tracked even when only the Gram + Cholesky
+    // path is launched, so the hint follows the chain back into the near-identity regime)
+    int nid_begin() {
+        if (!nid_enabled()) return 0;
+        const int kl = nid_launch_count();
+        mark(PH_NID);
+        launch_nid_decide(stream, D, cn, p_loc, sc, kl, kl > 0, nid, eps_dev);
+        return kl;
+    }
+    double *eps_dev = nullptr;  // device view of eps_host
+
+    // the Chebyshev solve (kl iterations launched, the device runs mode of them); x is w
+    void nid_solve(uint64_t t, int kl) {
+        mark(PH_NID);
+        if (method == 5)
+            launch_cheb_init(stream, nid_xu, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid, w,
+                             ch_r, ch_d);
+        else
+            launch_cheb_init(stream, nid_xu, nid_xu_parts(p_loc, n_pad), n, n_pad, y, sc,
+                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d);
+        for (int j = 1; j < kl; ++j) {
+            mark(PH_EAPPLY);
+            if (method == 5)
+                launch_sp_eapply(stream, spd.colptr, spd.rowidx, spd.cval, spd.rowptr, spd.colidx,
+                                 spd.rval, p_loc, n_pad, D, ch_d, nid, j, sp_s, ea_part);
+            else
+                launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part);
+            mark(PH_NID);
+            launch_cheb_step(stream, ea_part, method == 5 ? 1 : ea_parts, n_pad, sc, nid, j, w,
+                             ch_r, ch_d);
+        }
+    }
 
     // X beta of the current beta into the partials k_pre sums next
     void xbeta() {
@@ -418,34 +488,46 @@ struct bb_engine {
         if (method == 5) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            nid_kl = nid_begin();
+            const int *gate = nid_kl ? &nid->mode : nullptr;
             mark(PH_GRAM);
             // packed Gram (with its diagonal) and X u
-            spd.gram(stream, D, u, red2, red2 + tri_count(n_pad));
+            spd.gram(stream, D, u, red2, red2 + tri_count(n_pad), gate);
+            if (nid_kl) {
+                mark(PH_NID);
+                launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid, nid_xu);
+            }
         } else if (method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            nid_kl = nid_begin();
+            const int *gate = nid_kl ? &nid->mode : nullptr;
             if (cfg.gram_mode == 1) {
                 mark(PH_OZPREP);
                 launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowmax, oz_rscale,
-                                oz_escale);
+                                oz_escale, gate);
                 // the residue pass over X also forms the X u partials
                 launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R, u,
-                                   xu_part);
+                                   xu_part, gate);
                 mark(PH_GRAM);
-                launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P);
+                launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P, 0, kOzLeadDefault, -1, gate);
             } else {
                 mark(PH_GRAM);
-                launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride);
+                launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride, gate);
                 mark(PH_XU);
-                launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part);
+                launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part, gate);
             }
             mark(PH_REDUCE);
             if (cfg.gram_mode == 1)
                 launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
-                              oz_xu_parts(p_pad, n_oz), red2);
+                              oz_xu_parts(p_pad, n_oz), red2, gate);
             else
                 launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
-                                red2, 1);
+                                red2, 1, gate);
+            if (nid_kl) {
+                mark(PH_NID);
+                launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
+            }
         } else if (method == 6) {
             // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums): drawn by
             // trailing workgroups of the speculative lambda launch.  The logistic engine caps
@@ -487,22 +569,24 @@ struct bb_engine {
     void phase_c(uint64_t t, int slot, int mcmc_phase) {
         double *trb = slot_ptr(tr_beta, slot, p_loc);
         bool xb_fused = false;
-        if (method == 5) {
+        if (method == 5 || method == 2) {
+            // w = M^-1 (y / sig - v): the Gram + Cholesky path, or (nid_kl > 0 and the device
+            // decided so) the Chebyshev solve -- the kernels of the other path return at once
+            const int *gate = nid_kl ? &nid->mode : nullptr;
             mark(PH_FORM);
-            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
+            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad,
+                          gate);
             mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags);
+            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags, nullptr, gate);
             mark(PH_SOLVE);
-            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
+            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err,
+                        gate);
+            if (nid_kl) nid_solve(t, nid_kl);
+        }
+        if (method == 5) {
             mark(PH_BETA);
             launch_sp_beta(stream, spd.colptr, spd.rowidx, spd.cval, p_loc, w, u, D, sc, beta, trb);
         } else if (method == 2) {
-            mark(PH_FORM);
-            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad);
-            mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags);
-            mark(PH_SOLVE);
-            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err);
             mark(PH_BETA);
             if (beta_xb_supported(n_pad)) {
                 // beta and the X beta partials of the next sweep in one pass over X
@@ -572,6 +656,19 @@ struct bb_engine {
     // and the sweep index at which this member fails on purpose (bb_debug_fail_member)
     const std::atomic<bool> *stop = nullptr;
     int fail_at = -1;
+    int nid_kl = 0;  // Chebyshev iterations launched for the sweep being enqueued
+
+    // Near-identity engines keep the host at most ~8 sweeps ahead of the device, so the eps
+    // hint they launch from stays recent (the device is the bottleneck: no bubble)
+    void throttle_nid() {
+        if (!nid_enabled()) return;
+        if (++thr_n % 4 != 0) return;
+        const long m = thr_n / 4;
+        hipEvent_t &e = thr_ev[m % 3];
+        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(e, stream));
+        if (m >= 2) HIPCHECK(hipEventSynchronize(thr_ev[(m - 2) % 3]));
+    }
 
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
     void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
@@ -600,6 +697,7 @@ struct bb_engine {
             if (k == fail_at) throw HipError("injected failure (bb_debug_fail_member)");
             const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
             sweep(t0 + (uint64_t)k, slot, mcmc_phase);
+            throttle_nid();
         }
     }
 
@@ -861,6 +959,34 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         e->red2 = dalloc<double>(tri_count(n_pad) + n_pad, o);
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
         e->w = dalloc<double>(n_pad, o);
+        // near-identity solve (bb_nid.hip): unsharded engines; the dense E-apply keeps its
+        // rows in registers up to n_pad = 4096
+        if (c.world == 1 && (e->method == 5 || eapply_supported(n_pad))) {
+            e->cn = dalloc<double>(p_pad, o);
+            if (e->method == 5) {
+                std::vector<double> h(c.p_local, 0.0);
+                for (int j = 0; j < c.p_local; ++j)
+                    for (int q = spin->colptr[j]; q < spin->colptr[j + 1]; ++q)
+                        h[j] += spin->val[q] * spin->val[q];
+                HIPCHECK(hipMemcpy(e->cn, h.data(), h.size() * sizeof(double),
+                                   hipMemcpyHostToDevice));
+                e->sp_s = dalloc<double>(p_pad, o);
+                e->ea_parts = 1;
+                e->ea_part = dalloc<double>(n_pad, o);
+                e->nid_xu = dalloc<double>(n_pad, o);
+            } else {
+                launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->cn);
+                e->ea_parts = eapply_parts(c.p_local, n_pad);
+                e->ea_part = dalloc<double>((size_t)e->ea_parts * n_pad, o);
+                e->nid_xu = dalloc<double>((size_t)nid_xu_parts(c.p_local, n_pad) * n_pad, o);
+            }
+            e->nid = dalloc<NidState>(1, o);
+            e->ch_r = dalloc<double>(n_pad, o);
+            e->ch_d = dalloc<double>(n_pad, o);
+            HIPCHECK(hipHostMalloc((void **)&e->eps_host, sizeof(double), hipHostMallocMapped));
+            *e->eps_host = -1.0;  // no observation yet
+            HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
+        }
     }
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
     const bool small = c.p <= c.n && c.world == 1 && e->method != 5 && e->method != 6;
@@ -1384,6 +1510,36 @@ int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_a
         if (gram_ms_avg) *gram_ms_avg = ng ? g / ng : 0.0;
         if (sweep_ms_avg) *sweep_ms_avg = e->sweep_marks.empty() ? 0.0 : s / e->sweep_marks.size();
         if (samples) *samples = (int)e->sweep_marks.size();
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
+    return 0;
+}
+
+int bb_engine_timed_brackets(bb_engine *e, int *count) {
+    int ng = 0;
+    for (auto &marks : e->sweep_marks)
+        for (size_t i = 0; i + 1 < marks.size(); ++i)
+            if (marks[i].first == e->timed_phase) ++ng;
+    *count = ng;
+    return 0;
+}
+
+int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
+                        unsigned long long *products, unsigned long long *chol_sweeps,
+                        double *eps, int *mode) {
+    try {
+        NidState h{};
+        if (e->nid) {
+            HIPCHECK(hipMemcpyAsync(&h, e->nid, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+            HIPCHECK(hipStreamSynchronize(e->stream));
+        }
+        if (cheb_sweeps) *cheb_sweeps = h.n_cheb;
+        if (products) *products = h.n_products;
+        if (chol_sweeps) *chol_sweeps = h.n_chol;
+        if (eps) *eps = e->nid ? h.eps : -1.0;
+        if (mode) *mode = e->nid ? h.mode : -1;
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;
@@ -2896,6 +3052,11 @@ int bb_set_tuning(int key, int value) {
             const int old = g_lam_lanes;
             if (value == 0 || value == 4 || value == 8 || value == 16 || value == 32 || value == 64)
                 g_lam_lanes = value;
+            return old;
+        }
+        case 6: {
+            const int old = g_nid_kmax;
+            if (value >= 0) g_nid_kmax = value > 64 ? 64 : value;
             return old;
         }
         default: return -1;

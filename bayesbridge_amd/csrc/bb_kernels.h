@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <cmath>
+
 namespace bb {
 
 struct Key;
@@ -37,6 +39,72 @@ __host__ __device__ inline size_t tri_count(int n) { return (size_t)n * (n + 1) 
 
 enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
 
+// Per-sweep choice between the two exact solves of the Woodbury system (bb_nid.hip, DESIGN.md
+// s6.5): mode 0 = Gram + Cholesky, mode K > 0 = Chebyshev iteration with K iterates on the
+// certified spectrum interval [1, 1 + eps].  Written on the device by k_nid_decide every
+// sweep; the kernels of the path not taken return at once.
+struct NidState {
+    double eps, theta, delta, sigma1;
+    int mode, pad;
+    unsigned long long n_cheb, n_products, n_chol;  // sweeps per path, E-apply passes run
+};
+constexpr double kNidTol = 1.3877787807814457e-17;  // 2^-56: bound on the relative error
+constexpr int kNidXuCols = 128;                      // columns per X u partial (k_nid_xu)
+
+// Chebyshev scalars of the interval [1, 1 + eps]
+struct ChebConst {
+    double theta, delta, sigma1;
+};
+__host__ __device__ inline ChebConst cheb_const(double eps) {
+    ChebConst c;
+    c.theta = 1.0 + 0.5 * eps;
+    c.delta = 0.5 * eps;
+    c.sigma1 = c.delta > 0.0 ? c.theta / c.delta : 0.0;
+    return c;
+}
+// smallest K (1 <= K <= kmax) with sqrt(1 + eps) / T_K(sigma1) <= tol, else 0 (the bound on
+// |w - x_K| / |w| of K Chebyshev iterates from x_0 = 0 on the spectrum interval [1, 1 + eps])
+__host__ __device__ inline int cheb_iterations(double eps, int kmax, double tol) {
+    if (!(eps >= 0.0) || !(eps < 1e300)) return 0;
+    if (eps == 0.0) return kmax >= 1 ? 1 : 0;  // E = 0: x_1 = r / theta = r exactly
+    const ChebConst c = cheb_const(eps);
+    const double lim = sqrt(1.0 + eps) / tol;
+    double tm1 = 1.0, tk = c.sigma1;  // T_0, T_1
+    for (int k = 1; k <= kmax; ++k) {
+        if (tk >= lim) return k;
+        const double tn = 2.0 * c.sigma1 * tk - tm1;
+        tm1 = tk;
+        tk = tn;
+    }
+    return 0;
+}
+
+// a kernel of the Gram + Cholesky path: skip it when the sweep took the Chebyshev path
+__device__ __forceinline__ bool gated(const int *gate) { return gate && *gate != 0; }
+
+int eapply_parts(int p_loc, int n_pad);  // E-apply partial n-vectors (one per workgroup)
+bool eapply_supported(int n_pad);        // dense E-apply register tiling covers n_pad
+int nid_xu_parts(int p_loc, int n_pad);
+void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
+                       const DevScalars *sc, int k_launched, int allow, NidState *nid,
+                       double *eps_host);
+void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
+                   int n_pad, const NidState *nid, double *part);
+void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
+                      const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
+                      uint64_t t, const NidState *nid, double *x, double *r, double *d);
+void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
+                      const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
+                      double *d);
+void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
+                   const double *D, const double *v, const NidState *nid, int j, double *part);
+void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,
+                      const int *rowptr, const int *colidx, const double *rval, int p_loc,
+                      int n_pad, const double *D, const double *v, const NidState *nid, int j,
+                      double *scratch_p, double *out);
+void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
+                      int n_pad, const double *u, const NidState *nid, double *out);
+
 // Number of lanes cooperating on one tilted-stable draw for a problem of `count` draws.
 int stable_group_for(long count);
 bool stable_noinline_for(long count);
@@ -64,13 +132,13 @@ void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevSc
 // K-range s; Y is n_pad x K column-major with ld = ldy (n_pad multiple of 128).
 int gram_splits_for(int n_pad, int K);
 void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n_pad, int K,
-                 int S, double *slabs, int ldo, size_t slab_stride);
+                 int S, double *slabs, int ldo, size_t slab_stride, const int *gate = nullptr);
 
 // part[cb * n_pad + r] = sum over columns j of chunk cb of X[r, j] * v[j].
 int xv_chunks(int ncols, int n_pad);  // X.v partials launch_xv writes (= k_pre's nparts)
 int xv_chunks_max(int ncols);         // upper bound over n_pad, for allocation
 void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
-               double *part);
+               double *part, const int *gate = nullptr);
 
 // red1 = [S_alpha partials (nbS) | sum_q part[q] (n_pad)].
 int pre_blocks_s(int p_loc);
@@ -86,12 +154,12 @@ void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y,
 // red2 = [sum_s slabs, upper triangle | sum_q xu_part (n_pad)]; packed = 1: the triangle is
 // packed (tri_index, the Woodbury red2), 0: full column-major n_pad^2 (lower part zero).
 void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
-                     const double *xu_part, int nxu, double *red2, int packed);
+                     const double *xu_part, int nxu, double *red2, int packed, const int *gate = nullptr);
 
 // M (upper, ld = ldm) = I + red2 / sig2; column rhs_col = y/sig - (xu/sig + delta).
 void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,
                    const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *M,
-                   int ldm, int rhs_col);
+                   int ldm, int rhs_col, const int *gate = nullptr);
 
 // A (upper) = G + diag(lambda sig2 / tau^2) (or G alone if lam == nullptr); column
 // rhs_col = c.  Padding: identity.
@@ -135,7 +203,7 @@ extern int g_lam_lanes;  // lanes per coefficient of k_lambda_spec, 0 = default 
 // k_chol_persistent chain variant: 1 (default) or the pipelined 2 / 3, for A/B
 extern int g_chol_version;
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *Wd, unsigned int *flags, unsigned long long *trace = nullptr);
+                 double *Wd, unsigned int *flags, unsigned long long *trace = nullptr, const int *gate = nullptr);
 
 
 // Backward solve U W = Y (Y, W: m_pad x nrhs <= 2, ld = m_pad); Y may be overwritten.
@@ -144,7 +212,7 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
 // launch per kBsNB blocks.
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
                  double *Y, double *W, int nrhs, unsigned int *flags = nullptr,
-                 uint32_t *err = nullptr);
+                 uint32_t *err = nullptr, const int *gate = nullptr);
 
 // beta_j = u_j + D_j (X_j . w) / sig (Woodbury update); writes beta and trace.
 void launch_beta_woodbury(hipStream_t s, const double *X, int ldx, int n_pad, const double *w,

@@ -499,7 +499,8 @@ constexpr int kGLD = 144;
 __global__ __launch_bounds__(256, 2) void k_gram(const double *__restrict__ Y, int ldy,
                                                  const double *__restrict__ w, int K, int S,
                                                  double *__restrict__ out, int ldo,
-                                                 size_t slab_stride) {
+                                                 size_t slab_stride, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double As[kGramBK * kGLD];
     __shared__ double Bs[kGramBK * kGLD];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -599,10 +600,10 @@ int gram_splits_for(int n_pad, int K) {
 }
 
 void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n_pad, int K,
-                 int S, double *slabs, int ldo, size_t slab_stride) {
+                 int S, double *slabs, int ldo, size_t slab_stride, const int *gate) {
     const int nt = n_pad / kGramTile;
     const int tiles = nt * (nt + 1) / 2;
-    k_gram<<<tiles * S, 256, 0, s>>>(Y, ldy, w, K, S, slabs, ldo, slab_stride);
+    k_gram<<<tiles * S, 256, 0, s>>>(Y, ldy, w, K, S, slabs, ldo, slab_stride, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -610,7 +611,8 @@ void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_xv(const double *__restrict__ X, int ldx,
                                             const double *__restrict__ v, int ncols, int n_pad,
-                                            int cols, double *__restrict__ part) {
+                                            int cols, double *__restrict__ part, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double vs[kXvCols];
     const int cb = blockIdx.x, rb = blockIdx.y;
     const int c0 = cb * cols;
@@ -661,10 +663,10 @@ int xv_chunks(int ncols, int n_pad) {
 int xv_chunks_max(int ncols) { return (ncols + kXvMinCols - 1) / kXvMinCols; }
 
 void launch_xv(hipStream_t s, const double *X, int ldx, const double *v, int ncols, int n_pad,
-               double *part) {
+               double *part, const int *gate) {
     const int cols = xv_cols(ncols, n_pad);
     dim3 grid((ncols + cols - 1) / cols, (n_pad + kXvRows - 1) / kXvRows);
-    k_xv<<<grid, 256, 0, s>>>(X, ldx, v, ncols, n_pad, cols, part);
+    k_xv<<<grid, 256, 0, s>>>(X, ldx, v, ncols, n_pad, cols, part, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -783,7 +785,8 @@ void launch_scalars(hipStream_t s, const double *red1, int nbS, const double *y,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_slab_sum(const double *slabs, int S, size_t stride,
                                                   int n_pad, const double *xu_part, int nxu,
-                                                  double *red2, int packed) {
+                                                  double *red2, int packed, const int *gate) {
+    if (gated(gate)) return;
     const size_t nn = (size_t)n_pad * n_pad;
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx < nn) {
@@ -804,10 +807,10 @@ __global__ __launch_bounds__(256) void k_slab_sum(const double *slabs, int S, si
 }
 
 void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stride, int n_pad,
-                     const double *xu_part, int nxu, double *red2, int packed) {
+                     const double *xu_part, int nxu, double *red2, int packed, const int *gate) {
     const size_t tot = (size_t)n_pad * n_pad + n_pad;
     k_slab_sum<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(slabs, S, slab_stride, n_pad,
-                                                             xu_part, nxu, red2, packed);
+                                                             xu_part, nxu, red2, packed, gate);
 }
 
 // One thread per upper-triangle entry (packed index e -> (r, c): consecutive threads walk a
@@ -816,7 +819,8 @@ void launch_slab_sum(hipStream_t s, const double *slabs, int S, size_t slab_stri
 // n_pad x (n_pad + 64) matrix, half of them idle: C3 13.3 -> 11.6 us, C5 57 -> 45 us.)
 __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n_pad,
                                                 const double *y, const DevScalars *sc, Key key,
-                                                uint64_t t, double *M, int ldm, int rhs_col) {
+                                                uint64_t t, double *M, int ldm, int rhs_col, const int *gate) {
+    if (gated(gate)) return;
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t ntri = tri_count(n_pad);
     const double sig2 = sc->sig2;
@@ -849,10 +853,10 @@ __global__ __launch_bounds__(256) void k_form_m(const double *red2, int n, int n
 
 void launch_form_m(hipStream_t s, const double *red2, int n, int n_pad, const double *y,
                    const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *M,
-                   int ldm, int rhs_col) {
+                   int ldm, int rhs_col, const int *gate) {
     const size_t tot = tri_count(n_pad) + (size_t)n_pad * kNB;
     k_form_m<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(red2, n, n_pad, y, sc, Key{k0, k1}, t,
-                                                           M, ldm, rhs_col);
+                                                           M, ldm, rhs_col, gate);
 }
 
 __global__ __launch_bounds__(256) void k_form_a(const double *G, int ldg, const double *lam,
@@ -2142,7 +2146,8 @@ template <int V>
 __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int nblk, int ncb,
                                                          double *Wd, CholFlags F,
                                                          uint32_t *err,
-                                                         unsigned long long *trace) {
+                                                         unsigned long long *trace, const int *gate) {
+    if (gated(gate)) return;
     // T: tile being updated / the chain's diagonal block -> W; S: staging U_ki / the chain's
     // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
     // During the v1 chain's elimination S and Q together hold the published pivot rows; the
@@ -2550,7 +2555,7 @@ static int chol_max_resident(int version) {
 }
 
 void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, uint32_t *err,
-                 double *Wd, unsigned int *flags, unsigned long long *trace) {
+                 double *Wd, unsigned int *flags, unsigned long long *trace, const int *gate) {
     const int nblk = m_pad / kNB;
     const int ncb = nblk + nrhs_blocks;
     const size_t words = chol_flag_words(m_pad, nrhs_blocks);
@@ -2571,11 +2576,11 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
         throw std::runtime_error(b);
     }
     if (g_chol_version == 1)
-        k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+        k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
     else if (g_chol_version == 2)
-        k_chol_persistent<2><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+        k_chol_persistent<2><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
     else
-        k_chol_persistent<3><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace);
+        k_chol_persistent<3><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
 }
 
 
@@ -2587,7 +2592,8 @@ constexpr int kBsNB = 4;
 
 __global__ __launch_bounds__(256) void k_bsolve_multi(const double *A, int lda, int kb, int nb,
                                                       int m_pad, const double *__restrict__ Wd,
-                                                      double *Y, double *Wout, int nrhs) {
+                                                      double *Y, double *Wout, int nrhs, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double yv[2][kBsNB][64];
     __shared__ double wv[2][kBsNB][64];
     __shared__ double part[4][2][64];
@@ -2676,7 +2682,8 @@ __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda
                                                         int m_pad, const double *__restrict__ Wd,
                                                         const double *Y, double *Wout, int nrhs,
                                                         unsigned int *fl, unsigned int ep,
-                                                        uint32_t *err) {
+                                                        uint32_t *err, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double yv[2][64];
     __shared__ double wv[2][64];
     __shared__ double part[4][2][64];
@@ -2729,7 +2736,7 @@ __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda
 }
 
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
-                 double *Y, double *W, int nrhs, unsigned int *flags, uint32_t *err) {
+                 double *Y, double *W, int nrhs, unsigned int *flags, uint32_t *err, const int *gate) {
     const int nblk = m_pad / kNB;
     // one persistent launch (a workgroup per 64-row block, resident together) after the
     // factorisation that filled `flags`; otherwise one launch per kBsNB blocks
@@ -2737,13 +2744,13 @@ void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const doubl
         // the solve's flags have their own epoch sequence (one per solve)
         unsigned int *bf = flags + bsolve_flag_offset(m_pad, 1);
         const unsigned int ep = flag_epoch(bf, (size_t)nblk, s, true);
-        k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err);
+        k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err, gate);
         return;
     }
     for (int kb = nblk - 1; kb >= 0; kb -= kBsNB) {
         const int nb = std::min(kBsNB, kb + 1);
         const int nrow = kb - nb + 1;
-        k_bsolve_multi<<<nrow > 0 ? nrow : 1, 256, 0, s>>>(A, lda, kb, nb, m_pad, Wd, Y, W, nrhs);
+        k_bsolve_multi<<<nrow > 0 ? nrow : 1, 256, 0, s>>>(A, lda, kb, nb, m_pad, Wd, Y, W, nrhs, gate);
     }
 }
 

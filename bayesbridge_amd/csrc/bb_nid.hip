@@ -1,0 +1,357 @@
+// bb_nid.hip -- the near-identity solve of the Woodbury system.
+//
+// The beta | rest draw for p > n (the reference's BridgeRegression.cpp:552-575 in its
+// Woodbury form) needs w = M^-1 r with M = I + E, E = X diag(D) X' / sig2,
+// r = y / sig - (X u / sig + delta).  E is symmetric positive semi-definite and
+//   ||E||_2 <= tr(E) = eps = sum_j D_j |x_j|^2 / sig2,
+// with the column norms |x_j|^2 computed once at setup.  So the spectrum of M lies in the
+// certified interval [1, 1 + eps], and Chebyshev iteration on that interval converges with
+// the guaranteed bound (Saad, Iterative Methods, Alg. 12.1 / Prop. 12.2; x_0 = 0)
+//   |w - x_K| / |w| <= sqrt(1 + eps) / T_K(sigma1),  sigma1 = (1 + eps / 2) / (eps / 2),
+// T_K the Chebyshev polynomial.  The engine takes this path for a sweep when K <= the
+// iterations it launched and the bound is below 2^-56 (the solve is then more accurate
+// than the dense Cholesky it replaces); otherwise the same sweep runs the Gram + Cholesky
+// path.  The decision is made on the device (k_nid_decide) every sweep; the kernels of the
+// path not taken return at once (the gate word NidState::mode).
+//
+// x_K needs K - 1 products E d, each ONE pass over X: k_eapply forms X diag(D) (X' d)
+// column chunk by column chunk with the chunk in registers (the dot products X_J' d and
+// the update X_J (D_J s_J) read X_J once), writing one n-vector partial per workgroup;
+// k_cheb_step sums the partials in a fixed order and advances the recurrence.  In the
+// near-null regime a p > n chain starts in (beta0 = 0, BridgeRegression.cpp:85-89: tau and
+// D tiny, eps ~ 1e-12 .. 1e-4 over the first hundreds of C3 sweeps) K is 2-4, so a sweep
+// reads X 3-5 times instead of forming the n x n Gram and factoring it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "bb_kernels.h"
+#include "bb_sampler.h"
+
+namespace bb {
+
+namespace {
+
+// rho_0 = 1 / sigma1, rho_{j} = 1 / (2 sigma1 - rho_{j-1})
+__device__ inline double cheb_rho(double sigma1, int j) {
+    double rho = 1.0 / sigma1;
+    for (int i = 1; i <= j; ++i) rho = 1.0 / (2.0 * sigma1 - rho);
+    return rho;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Decision: eps = sum_j D_j cn_j / sig2 (fixed-order tree), the iteration count K, mode.
+// One workgroup of 1024 threads.  mode = K if this sweep takes the Chebyshev path (allow,
+// K <= k_launched), else 0 (the Gram + Cholesky path).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_nid_decide(const double *__restrict__ D,
+                                                     const double *__restrict__ cn, int p_loc,
+                                                     const DevScalars *sc, int k_launched,
+                                                     int allow, NidState *nid,
+                                                     double *eps_host) {
+    __shared__ double part[16];
+    double a = 0.0;
+    for (int j = threadIdx.x; j < p_loc; j += 1024) a += D[j] * cn[j];
+    a = wave_sum(a);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < 16; ++w) s += part[w];
+        // rounding of the sum: a relative margin far above its worst case (p u)
+        const double eps = s / sc->sig2 * (1.0 + 1e-6);
+        const int K = cheb_iterations(eps, k_launched, kNidTol);
+        const int mode = (allow && K > 0) ? K : 0;
+        nid->eps = eps;
+        nid->mode = mode;
+        const ChebConst c = cheb_const(eps);
+        nid->theta = c.theta;
+        nid->delta = c.delta;
+        nid->sigma1 = c.sigma1;
+        if (mode) {
+            nid->n_cheb += 1;
+            nid->n_products += (unsigned long long)(mode - 1);
+        } else {
+            nid->n_chol += 1;
+        }
+        if (eps_host) *eps_host = eps;  // host-mapped: the engine's launch hint
+    }
+}
+
+// r_0 = y / sig - (X u / sig + delta), x_1 = d_0 = r_0 / theta (x_0 = 0).  X u arrives as
+// nparts column-chunk partials (k_xv, or the sparse row pass with nparts = 1).
+__global__ __launch_bounds__(256) void k_cheb_init(const double *__restrict__ xu_part,
+                                                   int nparts, int n, int n_pad,
+                                                   const double *__restrict__ y,
+                                                   const DevScalars *sc, Key key, uint64_t t,
+                                                   const NidState *nid, double *x, double *r,
+                                                   double *d) {
+    if (nid->mode == 0) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_pad) return;
+    double rhs = 0.0;
+    if (i < n) {
+        double xu = 0.0;
+        for (int q = 0; q < nparts; ++q) xu += xu_part[(size_t)q * n_pad + i];
+        const double sig = sqrt(sc->sig2);
+        const double delta = normal_at(key, t, KIND_DELTA, (uint64_t)i);
+        rhs = y[i] / sig - (xu / sig + delta);  // k_form_m's right-hand side
+    }
+    const double d0 = rhs / nid->theta;
+    r[i] = rhs;
+    d[i] = d0;
+    x[i] = d0;
+}
+
+// Chebyshev step j (1 <= j <= K - 1): q = d + (sum of the E-apply partials) / sig2,
+// r_j = r_{j-1} - q, d_j = rho_j rho_{j-1} d_{j-1} + (2 rho_j / delta) r_j, x_{j+1} = x_j + d_j.
+__global__ __launch_bounds__(256) void k_cheb_step(const double *__restrict__ part, int nparts,
+                                                   int n_pad, const DevScalars *sc,
+                                                   const NidState *nid, int j, double *x,
+                                                   double *r, double *d) {
+    if (nid->mode <= j) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_pad) return;
+    double e = 0.0;
+    for (int q = 0; q < nparts; ++q) e += part[(size_t)q * n_pad + i];
+    const double dv = d[i];
+    const double qv = dv + e / sc->sig2;
+    const double rv = r[i] - qv;
+    const double s1 = nid->sigma1;
+    const double rho0 = cheb_rho(s1, j - 1), rho1 = 1.0 / (2.0 * s1 - rho0);
+    const double dn = rho1 * rho0 * dv + (2.0 * rho1 / nid->delta) * rv;
+    r[i] = rv;
+    d[i] = dn;
+    x[i] += dn;
+}
+
+// ---------------------------------------------------------------------------------------
+// One pass over dense X: part[wg][row] = sum over the workgroup's columns c of
+//   X[row, c] D_c (X[:, c]' v).
+// Workgroup g takes column chunks of kEaCols = 8 columns g, g + G, ...; thread t holds rows
+// t + 256 m (m < NR = n_pad / 256) of the chunk in registers, so each column is read from
+// HBM once for both its dot product and its update.  Dot products: per-thread partial sums,
+// a fixed xor tree per wave, the four waves' sums added in order.
+// ---------------------------------------------------------------------------------------
+constexpr int kEaCols = 8;
+constexpr int kEaThreads = 256;
+
+template <int NR>
+__global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict__ X, int ldx,
+                                                       int n_pad, int p_loc,
+                                                       const double *__restrict__ D,
+                                                       const double *__restrict__ v,
+                                                       const NidState *nid, int j,
+                                                       double *__restrict__ part) {
+    if (nid->mode <= j) return;
+    __shared__ double ws[4][kEaCols];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double vr[NR], acc[NR];
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+        const int row = tid + kEaThreads * m;
+        vr[m] = row < n_pad ? v[row] : 0.0;
+        acc[m] = 0.0;
+    }
+    const int nchunk = (p_loc + kEaCols - 1) / kEaCols;
+    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int c0 = ch * kEaCols;
+        double xv[kEaCols][NR];
+#pragma unroll
+        for (int c = 0; c < kEaCols; ++c) {
+            const bool ok = c0 + c < p_loc;
+            const double *col = X + (size_t)(c0 + c) * ldx;
+#pragma unroll
+            for (int m = 0; m < NR; ++m) {
+                const int row = tid + kEaThreads * m;
+                xv[c][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(col + row) : 0.0;
+            }
+        }
+        double s[kEaCols];
+#pragma unroll
+        for (int c = 0; c < kEaCols; ++c) {
+            double a = 0.0;
+#pragma unroll
+            for (int m = 0; m < NR; ++m) a = __builtin_fma(xv[c][m], vr[m], a);
+            s[c] = wave_sum(a);
+        }
+        __syncthreads();  // the previous chunk's ws reads are done
+        if (lane == 0)
+#pragma unroll
+            for (int c = 0; c < kEaCols; ++c) ws[wid][c] = s[c];
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kEaCols; ++c) {
+            const double dc = (c0 + c < p_loc) ? D[c0 + c] : 0.0;
+            const double f = dc * (((ws[0][c] + ws[1][c]) + ws[2][c]) + ws[3][c]);
+#pragma unroll
+            for (int m = 0; m < NR; ++m) acc[m] = __builtin_fma(xv[c][m], f, acc[m]);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+        const int row = tid + kEaThreads * m;
+        if (row < n_pad) part[(size_t)blockIdx.x * n_pad + row] = acc[m];
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Sparse X (CSC + CSR): s_j = D_j (X_j' v) by columns (16 lanes per column), then
+// part[row] = X_row . s by rows (a wave per row) -- two passes over the non-zeros.
+// ---------------------------------------------------------------------------------------
+constexpr int kSpEaLanes = 16;
+
+__global__ __launch_bounds__(256) void k_sp_eapply_cols(const int *__restrict__ colptr,
+                                                        const int *__restrict__ rowidx,
+                                                        const double *__restrict__ cval,
+                                                        int p_loc, const double *__restrict__ D,
+                                                        const double *__restrict__ v,
+                                                        const NidState *nid, int j,
+                                                        double *__restrict__ s) {
+    if (nid->mode <= j) return;
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const int c = (int)(gid / kSpEaLanes);
+    const int q = (int)(gid % kSpEaLanes);
+    double a = 0.0;
+    if (c < p_loc)
+        for (int k = colptr[c] + q; k < colptr[c + 1]; k += kSpEaLanes) a += cval[k] * v[rowidx[k]];
+#pragma unroll
+    for (int o = kSpEaLanes / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (q == 0 && c < p_loc) s[c] = D[c] * a;
+}
+
+__global__ __launch_bounds__(256) void k_sp_eapply_rows(const int *__restrict__ rowptr,
+                                                        const int *__restrict__ colidx,
+                                                        const double *__restrict__ rval,
+                                                        int n_pad, const double *__restrict__ s,
+                                                        const NidState *nid, int j, int pol,
+                                                        double *__restrict__ out) {
+    // pol 0: gated as an E-apply (step j); pol 1: X u for the right-hand side (mode != 0)
+    if (pol == 0 ? nid->mode <= j : nid->mode == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n_pad) return;
+    double a = 0.0;
+    for (int k = rowptr[row] + lane; k < rowptr[row + 1]; k += 64) a += rval[k] * s[colidx[k]];
+    a = wave_sum(a);
+    if (lane == 0) out[row] = a;
+}
+
+// X u partials for the right-hand side (dense): k_xv's column-chunk layout, gated on mode.
+__global__ __launch_bounds__(256) void k_nid_xu(const double *__restrict__ X, int ldx,
+                                                const double *__restrict__ u, int ncols,
+                                                int n_pad, int cols, const NidState *nid,
+                                                double *__restrict__ part) {
+    if (nid->mode == 0) return;
+    const int cb = blockIdx.x;
+    const int c0 = cb * cols;
+    const int nc = min(cols, ncols - c0);
+    const int r = blockIdx.y * 512 + 2 * threadIdx.x;
+    if (r >= n_pad) return;
+    const double *xp = X + (size_t)c0 * ldx + r;
+    double ax = 0.0, ay = 0.0;
+    for (int jj = 0; jj < nc; ++jj) {
+        const double2 xx = *(const double2 *)(xp + (size_t)jj * ldx);
+        const double uj = u[c0 + jj];
+        ax += xx.x * uj;
+        ay += xx.y * uj;
+    }
+    *(double2 *)(part + (size_t)cb * n_pad + r) = make_double2(ax, ay);
+}
+
+// ---------------------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------------------
+static int nid_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
+
+int eapply_parts(int p_loc, int n_pad) {
+    (void)n_pad;
+    const int nchunk = (p_loc + kEaCols - 1) / kEaCols;
+    return std::max(1, std::min(nchunk, 2 * nid_cus()));
+}
+
+bool eapply_supported(int n_pad) { return n_pad <= 16 * kEaThreads; }
+
+int nid_xu_parts(int p_loc, int n_pad) {
+    (void)n_pad;
+    return (p_loc + kNidXuCols - 1) / kNidXuCols;
+}
+
+void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
+                       const DevScalars *sc, int k_launched, int allow, NidState *nid,
+                       double *eps_host) {
+    k_nid_decide<<<1, 1024, 0, s>>>(D, cn, p_loc, sc, k_launched, allow, nid, eps_host);
+}
+
+void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
+                   int n_pad, const NidState *nid, double *part) {
+    dim3 grid((ncols + kNidXuCols - 1) / kNidXuCols, (n_pad + 511) / 512);
+    k_nid_xu<<<grid, 256, 0, s>>>(X, ldx, u, ncols, n_pad, kNidXuCols, nid, part);
+}
+
+void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
+                      const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
+                      uint64_t t, const NidState *nid, double *x, double *r, double *d) {
+    k_cheb_init<<<(n_pad + 255) / 256, 256, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
+                                                    Key{k0, k1}, t, nid, x, r, d);
+}
+
+void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
+                      const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
+                      double *d) {
+    k_cheb_step<<<(n_pad + 255) / 256, 256, 0, s>>>(part, nparts, n_pad, sc, nid, j, x, r, d);
+}
+
+void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
+                   const double *D, const double *v, const NidState *nid, int j, double *part) {
+    const int g = eapply_parts(p_loc, n_pad);
+    switch ((n_pad + kEaThreads - 1) / kEaThreads) {
+        case 1: k_eapply<1><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 2: k_eapply<2><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 3: case 4:
+            k_eapply<4><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 5: case 6: case 7: case 8:
+            k_eapply<8><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        default:
+            k_eapply<16><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+    }
+}
+
+void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,
+                      const int *rowptr, const int *colidx, const double *rval, int p_loc,
+                      int n_pad, const double *D, const double *v, const NidState *nid, int j,
+                      double *scratch_p, double *out) {
+    const long threads = (long)p_loc * kSpEaLanes;
+    k_sp_eapply_cols<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(colptr, rowidx, cval,
+                                                                       p_loc, D, v, nid, j,
+                                                                       scratch_p);
+    k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, scratch_p,
+                                                     nid, j, 0, out);
+}
+
+void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
+                      int n_pad, const double *u, const NidState *nid, double *out) {
+    k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, u, nid, 0, 1,
+                                                     out);
+}
+
+}  // namespace bb

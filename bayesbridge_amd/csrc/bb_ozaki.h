@@ -48,7 +48,7 @@ void launch_oz_xmax(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz
 // oz_bound_groups(p_pad) * n_oz doubles (per chunk-group row maxima).
 int oz_bound_groups(int p_pad);
 void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
-                     int b, double *part, double *rscale, int *escale);
+                     int b, double *part, double *rscale, int *escale, const int *gate = nullptr);
 // Residues r = round(X_ij sqrt(D_j) rscale_i) mod m_k (int8), plane k, 64-column chunk c,
 // stored as [16-row block][16-byte unit 0..3][row in block][16 B].  When u is
 // given, the same pass writes the X.u partials xu_part[g * n_pad + i] (g = 256-column group,
@@ -56,7 +56,7 @@ void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xm
 int oz_xu_parts(int p_pad, int n_oz);  // X.u partials of launch_oz_residues (<= p_pad / 64)
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R,
-                        const double *u = nullptr, double *xu_part = nullptr);
+                        const double *u = nullptr, double *xu_part = nullptr, const int *gate = nullptr);
 // P[split][k][tile] = (R_k R_k')_tile mod m_k over the split's K chunks (int8, balanced).
 extern int g_oz_res_nt;  // residue-plane stores non-temporal (bb_set_tuning key 1)
 // lead_pm: the diagonal pairs' K lead in 1/1000 of the pass (kOzLeadDefault: the tuned
@@ -65,10 +65,10 @@ extern int g_oz_res_nt;  // residue-plane stores non-temporal (bb_set_tuning key
 // either.
 constexpr int kOzLeadDefault = -1000000;
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
-                    int dbg = 0, int lead_pm = kOzLeadDefault, int late_pm = -1);
+                    int dbg = 0, int lead_pm = kOzLeadDefault, int late_pm = -1, const int *gate = nullptr);
 // red2[tri_index(r, c)] (r <= c < n_pad) = G(r, c); red2[tri_count(n_pad) + r] = sum_q
 // xu_part[q][r].
 void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
-                   const int *escale, const double *xu_part, int nxu, double *red2);
+                   const int *escale, const double *xu_part, int nxu, double *red2, const int *gate = nullptr);
 
 }  // namespace bb

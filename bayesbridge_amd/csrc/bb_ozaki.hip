@@ -172,7 +172,8 @@ int oz_bound_groups(int p_pad) { return (p_pad / kOzKC + kOzBoundChunks - 1) / k
 
 __global__ __launch_bounds__(256) void k_oz_bound(const double *__restrict__ D, int nkc,
                                                   const double *__restrict__ xmax, int n_oz,
-                                                  double *__restrict__ part) {
+                                                  double *__restrict__ part, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double sdm[kOzBoundChunks];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cg = blockIdx.y * kOzBoundChunks;
@@ -199,7 +200,8 @@ __global__ __launch_bounds__(256) void k_oz_bound(const double *__restrict__ D, 
 // 16 lanes per row, each over every 16th group, then a max across the 16 lanes
 __global__ __launch_bounds__(256) void k_oz_finalize(const double *__restrict__ part, int ng,
                                                      int n_oz, int b, double *__restrict__ rscale,
-                                                     int *__restrict__ escale) {
+                                                     int *__restrict__ escale, const int *gate) {
+    if (gated(gate)) return;
     const int i = blockIdx.x * 16 + (threadIdx.x >> 4), l = threadIdx.x & 15;
     double m = 0.0;
     if (i < n_oz)
@@ -215,11 +217,11 @@ __global__ __launch_bounds__(256) void k_oz_finalize(const double *__restrict__ 
 }
 
 void launch_oz_scale(hipStream_t s, const double *D, int p_pad, const double *xmax, int n_oz,
-                     int b, double *part, double *rscale, int *escale) {
+                     int b, double *part, double *rscale, int *escale, const int *gate) {
     const int nkc = p_pad / kOzKC;
     const int ng = oz_bound_groups(p_pad);
-    k_oz_bound<<<dim3(n_oz / 256, ng), 256, 0, s>>>(D, nkc, xmax, n_oz, part);
-    k_oz_finalize<<<(n_oz + 15) / 16, 256, 0, s>>>(part, ng, n_oz, b, rscale, escale);
+    k_oz_bound<<<dim3(n_oz / 256, ng), 256, 0, s>>>(D, nkc, xmax, n_oz, part, gate);
+    k_oz_finalize<<<(n_oz + 15) / 16, 256, 0, s>>>(part, ng, n_oz, b, rscale, escale, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -252,7 +254,8 @@ __global__ __launch_bounds__(512) void k_oz_residues(const double *__restrict__ 
                                                      const double *__restrict__ rscale,
                                                      int8_t *__restrict__ R, OzConsts C,
                                                      const double *__restrict__ u,
-                                                     double *__restrict__ xu_part, int cpw) {
+                                                     double *__restrict__ xu_part, int cpw, const int *gate) {
+    if (gated(gate)) return;
     __shared__ double xu_half[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int half = w & 1;
@@ -350,18 +353,18 @@ int g_oz_res_nt = 2;
 
 void launch_oz_residues(hipStream_t s, const double *X, int ldx, int n_pad, int n_oz, int p_pad,
                         const double *D, const double *rscale, int8_t *R, const double *u,
-                        double *xu_part) {
+                        double *xu_part, const int *gate) {
     const int nkc = p_pad / kOzKC, cpw = oz_res_cpw(nkc, n_oz);
     dim3 grid((nkc + cpw - 1) / cpw, n_oz / 256);
     if (g_oz_res_nt == 2)
         k_oz_residues<true, true><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R,
-                                                       oz_consts(), u, xu_part, cpw);
+                                                       oz_consts(), u, xu_part, cpw, gate);
     else if (g_oz_res_nt)
         k_oz_residues<true, false><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale, R,
-                                                        oz_consts(), u, xu_part, cpw);
+                                                        oz_consts(), u, xu_part, cpw, gate);
     else
         k_oz_residues<false, false><<<grid, 512, 0, s>>>(X, ldx, n_pad, n_oz, nkc, D, rscale,
-                                                         R, oz_consts(), u, xu_part, cpw);
+                                                         R, oz_consts(), u, xu_part, cpw, gate);
 }
 
 // ---------------------------------------------------------------------------
@@ -677,7 +680,8 @@ template <int dbg>
 __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict__ R, int n_oz,
                                                        int nkc, int nsplit,
                                                        int8_t *__restrict__ P, int lead_pm,
-                                                       int late_pm, OzConsts C) {
+                                                       int late_pm, OzConsts C, const int *gate) {
+    if (gated(gate)) return;
     __shared__ __attribute__((aligned(1024))) int8_t smem[kOzStages * kOzStageBytes];
     const int nt = n_oz / kOzT;
     const int ntiles = nt * (nt + 1) / 2;
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(256, 1) void k_oz_gemm16u(const int8_t *__restrict_
 }
 
 void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsplit, int8_t *P,
-                    int dbg, int lead_pm, int late_pm) {
+                    int dbg, int lead_pm, int late_pm, const int *gate) {
     const int nt = n_oz / kOzT;
     const int nkc = p_pad / kOzKC;
     const OzConsts &C = oz_consts();
@@ -770,13 +774,13 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
     }();
     const unsigned gu = gu0 < cus8 ? gu0 : cus8;
     switch (dbg) {  // dbg != 0: timing ablations of bb_bench_ozaki only (results meaningless)
-        case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C); break;
-        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C);
+        case 1: k_oz_gemm16u<1><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        case 2: k_oz_gemm16u<2><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        case 3: k_oz_gemm16u<3><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
+        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate);
     }
 }
 
@@ -797,7 +801,8 @@ template <int NS>
 __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, int nsplit, int nt,
                                                 int n_pad, const int *__restrict__ escale,
                                                 const double *__restrict__ xu_part, int nxu,
-                                                double *__restrict__ red2, OzConsts C) {
+                                                double *__restrict__ red2, OzConsts C, const int *gate) {
+    if (gated(gate)) return;
     const int ntiles = nt * (nt + 1) / 2;
     // the first blocks sum the X.u partials (a long dependent-load chain per row: started
     // first, it overlaps the residue reconstruction instead of trailing it), 8 lanes per row
@@ -931,17 +936,17 @@ __global__ __launch_bounds__(256) void k_oz_crt(const int8_t *__restrict__ P, in
 }
 
 void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_pad,
-                   const int *escale, const double *xu_part, int nxu, double *red2) {
+                   const int *escale, const double *xu_part, int nxu, double *red2, const int *gate) {
     const int nt = n_oz / kOzT;
     const long nquad = (long)(nt * (nt + 1) / 2) * kOzT * kOzT / 4;
     const unsigned g = (unsigned)((nquad + 255) / 256 + (n_pad * 8 + 255) / 256);
     const OzConsts &C = oz_consts();
     switch (nsplit) {
-        case 1: k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C); break;
-        case 2: k_oz_crt<2><<<g, 256, 0, s>>>(P, 2, nt, n_pad, escale, xu_part, nxu, red2, C); break;
-        case 4: k_oz_crt<4><<<g, 256, 0, s>>>(P, 4, nt, n_pad, escale, xu_part, nxu, red2, C); break;
+        case 1: k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
+        case 2: k_oz_crt<2><<<g, 256, 0, s>>>(P, 2, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
+        case 4: k_oz_crt<4><<<g, 256, 0, s>>>(P, 4, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
         default:
-            k_oz_crt<0><<<g, 256, 0, s>>>(P, nsplit, nt, n_pad, escale, xu_part, nxu, red2, C);
+            k_oz_crt<0><<<g, 256, 0, s>>>(P, nsplit, nt, n_pad, escale, xu_part, nxu, red2, C, gate);
     }
 }
 

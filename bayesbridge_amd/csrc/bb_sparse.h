@@ -44,17 +44,17 @@ void launch_sp_build(hipStream_t s, const int *rowptr, const int *colidx, const 
 void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                         const unsigned *estart, const double *prod, const unsigned short *pidx,
                         const double *D, const double *u, int n_pad, int max_row, double *tri,
-                        double *xu);
+                        double *xu, const int *gate = nullptr);
 
 // out[e] = sum_k prod[k] D[pj[k]] over every packed entry e < tri_count(n_pad)
 // (diagonal entries come out 0; k_sp_rows fills them).
 void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, const int *pj,
-                    const double *D, int n_pad, double *out);
+                    const double *D, int n_pad, double *out, const int *gate = nullptr);
 
 // Row pass over the CSR: xv[c] = sum_j X_cj v_j; with D != nullptr also
 // tri[tri_index(c, c)] = sum_j X_cj^2 D_j (the Gram diagonal).
 void launch_sp_rows(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
-                    int n_pad, const double *v, const double *D, double *xv, double *tri);
+                    int n_pad, const double *v, const double *D, double *xv, double *tri, const int *gate = nullptr);
 
 // Woodbury beta update from the CSC: beta_j = u_j + D_j (X_j . w) / sig.
 void launch_sp_beta(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,

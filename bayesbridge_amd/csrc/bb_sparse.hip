@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void k_sp_gram(const unsigned *__restrict__ es
                                                  const double *__restrict__ prod,
                                                  const int *__restrict__ pj,
                                                  const double *__restrict__ D, size_t nent,
-                                                 double *__restrict__ out) {
+                                                 double *__restrict__ out, const int *gate) {
+    if (gated(gate)) return;
     const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
     const size_t e = gid / kSpLpe;
     const unsigned q = (unsigned)(gid % kSpLpe);
@@ -180,10 +181,10 @@ __global__ __launch_bounds__(256) void k_sp_gram(const unsigned *__restrict__ es
 }
 
 void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, const int *pj,
-                    const double *D, int n_pad, double *out) {
+                    const double *D, int n_pad, double *out, const int *gate) {
     const size_t nent = tri_count(n_pad);
     const size_t threads = nent * kSpLpe;
-    k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out);
+    k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out, gate);
 }
 
 // Gram by output column (used when every row of X has at most kSpColMaxRow non-zeros;
@@ -205,7 +206,8 @@ __global__ __launch_bounds__(256) void k_sp_gram_col(
     const double *__restrict__ rval, const unsigned *__restrict__ estart,
     const double *__restrict__ prod, const unsigned short *__restrict__ pidx,
     const double *__restrict__ D, const double *__restrict__ u, int n_pad,
-    double *__restrict__ tri, double *__restrict__ xu) {
+    double *__restrict__ tri, double *__restrict__ xu, const int *gate) {
+    if (gated(gate)) return;
     extern __shared__ double Dl[];  // D over row c's support
     __shared__ double red[2][4];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -277,7 +279,8 @@ __global__ __launch_bounds__(256) void k_sp_gram_flat(
     const double *__restrict__ rval, const unsigned *__restrict__ estart,
     const double *__restrict__ prod, const unsigned short *__restrict__ pidx,
     const double *__restrict__ D, const double *__restrict__ u, int n_pad,
-    double *__restrict__ tri, double *__restrict__ xu) {
+    double *__restrict__ tri, double *__restrict__ xu, const int *gate) {
+    if (gated(gate)) return;
     extern __shared__ double Dl[];  // D over row c's support
     constexpr int kSpFlatCap = 256 * kSpFlatV;
     __shared__ double vals[kSpFlatCap];
@@ -391,18 +394,18 @@ int g_sp_nt = 3;
 void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                         const unsigned *estart, const double *prod, const unsigned short *pidx,
                         const double *D, const double *u, int n_pad, int max_row, double *tri,
-                        double *xu) {
+                        double *xu, const int *gate) {
     const size_t lds = (size_t)(max_row > 0 ? max_row : 1) * sizeof(double);
     if (g_sp_nt >= 2) {
         auto kern = g_sp_nt == 2 ? k_sp_gram_flat<8> : k_sp_gram_flat<16>;
         kern<<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad, tri,
-                                     xu);
+                                     xu, gate);
     } else if (g_sp_nt)
         k_sp_gram_col<true><<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D,
-                                                    u, n_pad, tri, xu);
+                                                    u, n_pad, tri, xu, gate);
     else
         k_sp_gram_col<false><<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D,
-                                                     u, n_pad, tri, xu);
+                                                     u, n_pad, tri, xu, gate);
 }
 
 // One wave per row c of X (CSR), lanes strided over the row's entries, fixed tree.
@@ -413,7 +416,8 @@ __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
                                                  const double *__restrict__ v,
                                                  const double *__restrict__ D,
                                                  double *__restrict__ xv,
-                                                 double *__restrict__ tri) {
+                                                 double *__restrict__ tri, const int *gate) {
+    if (gated(gate)) return;
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= n_pad) return;
@@ -433,12 +437,12 @@ __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
 }
 
 void launch_sp_rows(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
-                    int n_pad, const double *v, const double *D, double *xv, double *tri) {
+                    int n_pad, const double *v, const double *D, double *xv, double *tri, const int *gate) {
     const int blocks = (n_pad + 3) / 4;
     if (D)
-        k_sp_rows<true><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri);
+        k_sp_rows<true><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
     else
-        k_sp_rows<false><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri);
+        k_sp_rows<false><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
 }
 
 // 16 lanes per column of the CSC: s = X_j . w, beta_j = u_j + D_j s / sig.

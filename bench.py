@@ -259,7 +259,7 @@ def rel_l2(a, b):
 # engine's per-sweep order (bb_engine.cpp phase_b / phase_c): the candidates for the
 # `roofline` kernel.  "ozprep" (k_oz_bound + k_oz_finalize + k_oz_residues) is not a single
 # kernel and is reported through phases_ms only.
-SINGLE_KERNEL_PHASES = ("lambda", "gram", "reduce", "chol", "solve", "beta")
+SINGLE_KERNEL_PHASES = ("lambda", "gram", "reduce", "chol", "solve", "beta", "eapply")
 CHOL_NB = 64  # k_chol_persistent block size (bb_kernels.hip kNB)
 
 
@@ -331,6 +331,22 @@ def roofline_for(phase, ms, ctx, traffic_world):
                                   "model": "time = steps x (in-LDS elimination of the 64-block "
                                            "+ W = U_kk^-T + U_k,k+1 + next diagonal update) "
                                            "(DESIGN.md s5.2)"})
+    elif phase == "eapply":
+        # the near-identity solve's pass over X: X diag(D) X' d in one read
+        # of X (dense: 8 n_pad p_loc bytes, plus the d vector and the per-workgroup partial
+        # n-vectors it writes; sparse: the CSC and CSR non-zeros, 12 B each, plus D, s, d).
+        # ms: the time per pass that actually ran (ctx["eapply_passes"] of the bracketed
+        # launches did; the others returned at once and their time is charged to the passes)
+        n_pad = -(-n // 128) * 128
+        if sparse:
+            si = eng.sparse_info()
+            byts = 24.0 * si["nnz"] + 24.0 * p_loc + 16.0 * n_pad
+            kname, kfull = "k_sp_eapply_cols + k_sp_eapply_rows (X D X' d)", "bb::k_sp_eapply"
+        else:
+            byts = 8.0 * n_pad * p_loc + 8.0 * p_loc + 8.0 * n_pad * (1 + ctx.get("ea_parts", 512))
+            kname, kfull = "k_eapply (X D X' d, one pass over X)", "bb::k_eapply"
+        out.update(bound="hbm", kernel=kname, achieved=byts / sec / 1e9, peak=8000.0,
+                   unit="GB/s", algorithmic_bytes_per_launch=byts)
     else:
         kfull = {"lambda": "bb::k_lambda", "reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve",
                  "beta": "bb::k_beta"}[phase]
@@ -372,6 +388,8 @@ def main():
                     help="drive --gpus N devices from ONE process through an RCCL shard group "
                          "(ncclCommInitAll) -- the path the .C entry points use under R; the "
                          "default for --gpus N > 1 without a torch.distributed launcher")
+    ap.add_argument("--no-fitted", action="store_true",
+                    help="skip the fitted-regime measurement that follows the timed run")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
                     help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: the "
                          "library default, Ozaki)")
@@ -517,15 +535,20 @@ def run_chain(args, n, p, alpha, kind, mode):
     nph = max(1, min(args.steps, 20))
     eng.enable_timing(True, phases=True)
     eng.reset_timing()
+    ph0 = eng.nid_stats()
     runner.run(t, nph, first_slot=-1)
     t += nph
     sync_all()
     phases = eng.phase_times()
+    ph1 = eng.nid_stats()
+    # the phase-split sweeps took the near-identity path (their Gram phases are no-ops)
+    nid_phase_cheb = ph1["mode"] >= 0 and (ph1["cheb_sweeps"] - ph0["cheb_sweeps"]) * 2 > nph
     _, sweep_ms_phases, _ = eng.kernel_times()
     dom = max((ph for ph in SINGLE_KERNEL_PHASES if ph in phases), key=lambda k: phases[k])
     barrier()
     eng.enable_timing(True, phases=False, timed_phase=dom)
     eng.reset_timing()
+    nid0 = eng.nid_stats()
     t0 = time.perf_counter()
     # the timed loop records every sweep's beta / lambda / sig2 / tau into the device trace
     # ring, as the reference's MCMC loop writes its output slots (BridgeWrapper.cpp:287-298)
@@ -539,7 +562,23 @@ def run_chain(args, n, p, alpha, kind, mode):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     dom_ms, _, _ = eng.kernel_times()
+    brackets = eng.timed_brackets()
+    nid1 = eng.nid_stats()
     eng.enable_timing(False)
+    nid = None
+    if nid1["mode"] >= 0:
+        dc = nid1["cheb_sweeps"] - nid0["cheb_sweeps"]
+        dp = nid1["products"] - nid0["products"]
+        nid = {"timed_sweeps": args.steps, "chebyshev_sweeps": dc,
+               "cholesky_sweeps": nid1["chol_sweeps"] - nid0["chol_sweeps"],
+               "eapply_passes_per_chebyshev_sweep": (dp / dc) if dc else None,
+               "eps_last": nid1["eps"],
+               "rule": "per sweep on the device: Chebyshev iteration on the certified spectrum "
+                       "interval [1, 1 + eps], eps = tr(X D X') / sig2, when K <= 16 iterates "
+                       "bound the relative error of w by 2^-56; else Gram + Cholesky "
+                       "(DESIGN.md s6.5)"}
+        if dom == "eapply" and dp > 0:
+            dom_ms = dom_ms * brackets / dp  # per pass that ran (see roofline_for)
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
@@ -551,13 +590,22 @@ def run_chain(args, n, p, alpha, kind, mode):
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
                gram_name=gram_name)
+    fitted = None
+    if mode == "single" and not logit and not args.no_fitted:
+        fitted = fitted_regime(bb, eng, kind, n, p, alpha, t)
+        t += 10000
     traffic_world = 1 if mode == "single" else world
     roof = roofline_for(dom, dom_ms, ctx, traffic_world)
     roof["timing"] = "HIP events on rank 0's engine stream around every timed launch"
     secondary = None
-    if dom != "gram" and "gram" in phases:
-        secondary = roofline_for("gram", phases["gram"], ctx, traffic_world)
-        secondary["timing"] = f"HIP events at phase starts, {nph} untimed sweeps"
+    # the Gram's roofline beside the dominant kernel's: from this run's phase split when its
+    # sweeps formed the Gram, else from the fitted-regime run (near-identity sweeps skip it)
+    gram_src = (phases, f"HIP events at phase starts, {nph} untimed sweeps")
+    if nid_phase_cheb and fitted:
+        gram_src = (fitted["phases_ms"], "HIP events at phase starts, fitted-regime run")
+    if dom != "gram" and "gram" in gram_src[0] and not (nid_phase_cheb and not fitted):
+        secondary = roofline_for("gram", gram_src[0]["gram"], ctx, traffic_world)
+        secondary["timing"] = gram_src[1]
     gram_total_ms = sum(phases.get(k, 0.0) for k in ("ozprep", "gram", "reduce"))
 
     cpu = cpu_more = None
@@ -605,6 +653,8 @@ def run_chain(args, n, p, alpha, kind, mode):
             "cpu_baseline": cpu,
             "parity_check": parity,
             "setup_s": setup_s,
+            "near_identity": nid,
+            "fitted_regime": fitted,
         }
         if cpu_more:
             rec["cpu_baselines"] = cpu_more
@@ -615,6 +665,39 @@ def run_chain(args, n, p, alpha, kind, mode):
         e.close()
     if dist:
         dist.destroy_process_group()
+
+
+def fitted_regime(bb, eng, kind, n, p, alpha, t, warm=20, steps=50):
+    """The same engine timed in the fitted regime: the chain restarted at
+    the data-generating coefficients with tau = 1e-2, sig2 = 1, `warm` untimed sweeps, then
+    `steps` sweeps between stream synchronisations, with the per-phase split and the path the
+    Woodbury solve took.  (From the reference start a C3 chain stays in the near-null regime
+    for thousands of sweeps; the C5 posterior collapses back to it within a few sweeps,
+    whatever the start.)"""
+    _, btrue = (make_sparse_problem_y(n, p) if kind == "sparse" else make_problem_y(n, p))
+    eng.set_state(btrue[:eng.p_local], 1e-2, 1.0, alpha)
+    eng.run(t, warm, first_slot=-1)
+    eng.sync()
+    eng.enable_timing(True, phases=True)
+    eng.reset_timing()
+    s0 = eng.nid_stats()
+    t0 = time.perf_counter()
+    eng.run(t + warm, steps, first_slot=-1)
+    eng.sync()
+    el = time.perf_counter() - t0
+    phases = eng.phase_times()
+    s1 = eng.nid_stats()
+    eng.enable_timing(False)
+    st = eng.state()
+    return {"value": steps / el, "unit": "sweeps/s", "ms_per_step": 1e3 * el / steps,
+            "steps": steps, "warmup": warm,
+            "start": "beta = data-generating coefficients, tau = 1e-2, sig2 = 1",
+            "state_after": {"tau": st["tau"], "sig2": st["sig2"],
+                            "coefficients_above_1e-3": int(np.sum(np.abs(st["beta"]) > 1e-3))},
+            "chebyshev_sweeps": (s1["cheb_sweeps"] - s0["cheb_sweeps"]) if s1["mode"] >= 0 else 0,
+            "eps_last": s1["eps"],
+            "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+            "timing": "wall clock around the sweeps with phase events on (adds ~1 us per phase)"}
 
 
 def shard_parity_check(bb, dist, rank, engines, my_ranks, runner, make_engine, dev0, p, world,

@@ -333,7 +333,10 @@ void bb_set_trace_budget(long long bytes);
  * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane;
  * key 4: occupancy of the lambda launches, bit 0 = k_lambda_spec and bit 1 = k_lambda_cb
  * capped at 128 VGPRs for 4 waves per SIMD instead of their register-minimal 3 (default 2:
- * k_lambda_cb only, 4 % faster at C5; no change at C3); the draws are the same.
+ * k_lambda_cb only, 4 % faster at C5; no change at C3); the draws are the same;
+ * key 5: lanes per coefficient of the speculative lambda launch (0 = the size-based default);
+ * key 6: the most Chebyshev iterations a Woodbury sweep may take on the near-identity path
+ * (default 16; 0 = every sweep forms the Gram and factors it).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
@@ -392,6 +395,16 @@ int bb_engine_reset_timing(bb_engine *e);
 int bb_engine_phase_times(bb_engine *e, double *ms, int cap, int *samples);
 int bb_phase_count(void);
 const char *bb_phase_name(int i);
+
+/* Number of timed-phase brackets (launches of the timed phase) recorded since the last reset. */
+int bb_engine_timed_brackets(bb_engine *e, int *count);
+/* Near-identity solve of the Woodbury system: sweeps that took the Chebyshev
+ * path, E-apply passes they ran, sweeps that formed the Gram and factored it (counts since the
+ * engine was created), and the eps = tr(X D X') / sig2 bound and mode of the latest sweep (-1
+ * when the engine has no near-identity path: sharded, p <= n or n > 4096 dense). */
+int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
+                        unsigned long long *products, unsigned long long *chol_sweeps,
+                        double *eps, int *mode);
 
 /* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags);

@@ -76,6 +76,68 @@ def beta_step_woodbury(X, y, lam, sig2, tau, z, delta):
     return u + D * (X.T @ w) / sig
 
 
+NID_TOL = 2.0 ** -56  # bb_kernels.h kNidTol
+
+
+def cheb_iterations(eps, kmax, tol=NID_TOL):
+    """Restates bb_kernels.h cheb_iterations: the smallest K <= kmax with
+    sqrt(1 + eps) / T_K(sigma1) <= tol on the spectrum interval [1, 1 + eps], else 0."""
+    if not (eps >= 0.0) or not (eps < 1e300):
+        return 0
+    if eps == 0.0:
+        return 1 if kmax >= 1 else 0
+    theta, delta = 1.0 + 0.5 * eps, 0.5 * eps
+    sigma1 = theta / delta
+    lim = np.sqrt(1.0 + eps) / tol
+    tm1, tk = 1.0, sigma1
+    for k in range(1, kmax + 1):
+        if tk >= lim:
+            return k
+        tm1, tk = tk, 2.0 * sigma1 * tk - tm1
+    return 0
+
+
+def woodbury_solve_cheb(apply_E, rhs, eps, K):
+    """Chebyshev iteration (Saad, Iterative Methods, Alg. 12.1; x_0 = 0) for (I + E) w = rhs
+    with the spectrum of I + E in [1, 1 + eps] -- the device's near-identity solve
+    (bb_nid.hip: k_cheb_init, then K - 1 steps of k_eapply + k_cheb_step)."""
+    theta, delta = 1.0 + 0.5 * eps, 0.5 * eps
+    sigma1 = theta / delta if delta > 0 else 0.0
+    r = rhs.copy()
+    d = r / theta
+    x = d.copy()
+    rho = 1.0 / sigma1 if sigma1 else 0.0
+    for _ in range(1, K):
+        q = d + apply_E(d)
+        r = r - q
+        rho1 = 1.0 / (2.0 * sigma1 - rho)
+        d = rho1 * rho * d + (2.0 * rho1 / delta) * r
+        x = x + d
+        rho = rho1
+    return x
+
+
+def beta_step_woodbury_nid(X, y, lam, sig2, tau, z, delta, kmax=16):
+    """The same conditional draw as beta_step_woodbury, with w = M^-1 (y/sig - v) solved by
+    the certified Chebyshev iteration when eps = tr(X D X') / sig2 admits K <= kmax
+    iterates, else by the Cholesky factor.  Returns (beta, K) (K = 0: the
+    Cholesky path)."""
+    sig = np.sqrt(sig2)
+    D = (tau * tau) / lam
+    u = np.sqrt(D) * z
+    v = (X @ u) / sig + delta
+    if sps.issparse(X):
+        cn = np.asarray(X.multiply(X).sum(axis=0)).ravel()
+    else:
+        cn = (X * X).sum(axis=0)
+    eps = float(np.sum(D * cn)) / sig2 * (1.0 + 1e-6)
+    K = cheb_iterations(eps, kmax)
+    if K == 0:
+        return beta_step_woodbury(X, y, lam, sig2, tau, z, delta), 0
+    w = woodbury_solve_cheb(lambda t: (X @ (D * (X.T @ t))) / sig2, y / sig - v, eps, K)
+    return u + D * (X.T @ w) / sig, K
+
+
 def beta_step_ortho(Gdiag, c, lam, sig2, tau, z):
     """BridgeRegression.cpp:514-521."""
     u = Gdiag + lam * sig2 / (tau * tau)

@@ -1,0 +1,66 @@
+"""The near-identity (Chebyshev) solve of the Woodbury system, restated on
+the CPU (oracle/gibbs.py woodbury_solve_cheb / beta_step_woodbury_nid): its certified bound
+holds and its draw equals the Cholesky draw of beta_step_woodbury (BridgeRegression.cpp:
+552-575 in Woodbury form) to rounding across the regimes where it is taken."""
+import numpy as np
+import pytest
+
+from oracle import gibbs
+from tests.conftest import synthetic_problem
+
+
+def test_iteration_rule():
+    # tiny eps: two iterates (one product); the count grows with eps; beyond kmax: 0
+    assert gibbs.cheb_iterations(0.0, 16) == 1
+    assert gibbs.cheb_iterations(1e-12, 16) == 2
+    assert gibbs.cheb_iterations(1e-6, 16) == 3
+    ks = [gibbs.cheb_iterations(e, 64) for e in (1e-9, 1e-6, 1e-3, 1e-2, 0.1, 1.0)]
+    assert ks == sorted(ks) and ks[-1] > ks[0]
+    assert gibbs.cheb_iterations(10.0, 16) == 0
+    assert gibbs.cheb_iterations(float("nan"), 16) == 0
+
+
+@pytest.mark.parametrize("eps_target", [1e-12, 1e-8, 1e-5, 1e-3, 1e-1, 1.0])
+def test_certified_bound_holds(eps_target):
+    """Random PSD E scaled so tr(E) = eps: the K-iterate solve is within the bound of the
+    exact solve (and within 2^-56 relative, the decision tolerance)."""
+    rng = np.random.default_rng(int(-np.log10(eps_target)) + 3)
+    n = 120
+    B = rng.standard_normal((n, 300)) * rng.uniform(0, 1, 300)
+    E = B @ B.T
+    E *= eps_target / np.trace(E)
+    rhs = rng.standard_normal(n)
+    K = gibbs.cheb_iterations(eps_target, 64)
+    assert K > 0
+    x = gibbs.woodbury_solve_cheb(lambda t: E @ t, rhs, eps_target, K)
+    w = np.linalg.solve(np.eye(n) + E, rhs)
+    err = np.linalg.norm(x - w) / np.linalg.norm(w)
+    assert err < 1e-15 + 4e-16 * np.sqrt(n), (K, err)
+
+
+@pytest.mark.parametrize("tau", [1e-7, 1e-4, 1e-3, 3e-3])
+def test_nid_draw_matches_cholesky_draw(tau):
+    """Woodbury beta draws (n = 80, p = 400) at prior scales from the near-null regime up to
+    where the path hands over to the Cholesky factor: same draw to rounding."""
+    X, y, b = synthetic_problem(80, 400, seed=9)
+    rng = np.random.default_rng(1)
+    lam = rng.exponential(1.0, 400) * 2.0
+    z, d = rng.standard_normal(400), rng.standard_normal(80)
+    sig2 = float(np.var(y))
+    bn, K = gibbs.beta_step_woodbury_nid(X, y, lam, sig2, tau, z, d)
+    bc = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
+    assert np.linalg.norm(bn - bc) / np.linalg.norm(bc) < 1e-13, K
+    if tau <= 1e-4:
+        assert 1 <= K <= 4
+
+
+def test_nid_draw_sparse():
+    import bench
+    X = bench.make_sparse_columns(300, 0, 3000, density=0.02, seed=4)
+    y = np.asarray(X[:, :5] @ np.ones(5)).ravel() + np.random.default_rng(2).standard_normal(300)
+    rng = np.random.default_rng(3)
+    lam = rng.exponential(1.0, 3000) * 2.0
+    z, d = rng.standard_normal(3000), rng.standard_normal(300)
+    bn, K = gibbs.beta_step_woodbury_nid(X, y, lam, 50.0, 1e-4, z, d)
+    bc = gibbs.beta_step_woodbury(X, y, lam, 50.0, 1e-4, z, d)
+    assert K > 0 and np.linalg.norm(bn - bc) / np.linalg.norm(bc) < 1e-13

@@ -1,0 +1,151 @@
+"""The near-identity (Chebyshev) solve of the Woodbury system on the GPU (bb_nid.hip,
+DESIGN.md s6.5).  Both paths of a Woodbury sweep -- Gram + Cholesky and the certified
+Chebyshev iteration -- solve the same system exactly, so a sweep drawn through either gives
+the same beta to rounding; the device decides per sweep from eps = tr(X D X') / sig2.
+Checks: the decision (near-null states take the Chebyshev path, fitted states the factor),
+per-sweep equality with the path disabled (bb_set_tuning key 6 = 0) for dense (Ozaki and
+fp64 Gram) and sparse engines at iteration counts from 2 to ~12, and teacher-forced parity
+with the oracle's Cholesky-based Woodbury draw (BridgeRegression.cpp:552-575)."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import gibbs
+from tests.conftest import synthetic_problem
+from tests.test_gpu_parity import flips, rel_err
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xB4E5B41D6E
+
+
+def _design(kind, n, p, seed):
+    if kind == "sparse":
+        import bench
+        X = bench.make_sparse_columns(n, 0, p, density=0.03, seed=seed)
+        rng = np.random.default_rng(seed)
+        y = np.asarray(X[:, :8] @ rng.uniform(1, 2, 8)).ravel() + rng.standard_normal(n)
+        return X, y - y.mean(), None
+    return synthetic_problem(n, p, seed=seed)
+
+
+def _engine(bb, X, y, n, p, gram_mode=1, stream=0):
+    return bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=stream, true_alpha=0.5,
+                                     trace_capacity=1, gram_mode=gram_mode), X, y)
+
+
+@pytest.mark.parametrize("kind,gram_mode", [("dense", 1), ("dense", 0), ("sparse", 1)])
+@pytest.mark.parametrize("scale", [1e-6, 1e-3, 3e-2])
+def test_nid_sweep_equals_cholesky_sweep(gpu_lib, kind, gram_mode, scale):
+    """One sweep from the same state through the engine with the near-identity path (auto)
+    and with it disabled: same beta to 1e-12 relative.  `scale` sets tau (and beta), so the
+    sweeps span eps from ~1e-10 (2 iterates) to ~1e-1 (about 12) -- or the hand-over to the
+    factor, reported by mode 0."""
+    bb = gpu_lib
+    n, p = 200, 2400
+    X, y, btrue = _design(kind, n, p, 31)
+    rng = np.random.default_rng(7)
+    beta = (btrue if btrue is not None else np.zeros(p)) * scale + scale * rng.standard_normal(p)
+    auto = _engine(bb, X, y, n, p, gram_mode)
+    old = bb.set_tuning(6, 0)
+    try:
+        off = _engine(bb, X, y, n, p, gram_mode)
+        off.init_state()
+    finally:
+        bb.set_tuning(6, old)
+    auto.init_state()
+    modes = []
+    for t in (3, 4, 5):
+        auto.set_state(beta, scale, 1.0, 0.5)
+        off.set_state(beta, scale, 1.0, 0.5)
+        auto.run(t, 1)
+        old = bb.set_tuning(6, 0)
+        try:
+            off.run(t, 1)
+            off.sync()
+        finally:
+            bb.set_tuning(6, old)
+        a, o = auto.state(), off.state()
+        st = auto.nid_stats()
+        modes.append(st["mode"])
+        assert a["tau"] == o["tau"] and a["sig2"] == o["sig2"]
+        assert np.array_equal(a["lambda"], o["lambda"])
+        assert rel_err(a["beta"], o["beta"]) < 1e-12, (t, st, rel_err(a["beta"], o["beta"]))
+        beta = o["beta"]
+    assert off.nid_stats()["cheb_sweeps"] == 0
+    if scale <= 1e-6:
+        assert all(m >= 2 for m in modes), modes  # the near-identity path was taken
+    print(f"\n[{kind} gram_mode={gram_mode} scale={scale}] iterates per sweep {modes}")
+    assert auto.error_flags() == 0 and off.error_flags() == 0
+    auto.close()
+    off.close()
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_nid_teacher_forced_from_reference_start(gpu_lib, kind, capsys):
+    """A chain from the reference start (beta0 = 0, BridgeRegression.cpp:85-89) sits in the
+    near-null regime: 40 free sweeps, then 3 sweeps teacher-forced against the oracle's
+    Cholesky-based Woodbury draw at the steady-state bars (beta 1e-10 relative L2; lambda,
+    tau, sig2 1e-11; no flips), each taking the Chebyshev path."""
+    bb = gpu_lib
+    n, p = 400, 6000
+    X, y, _ = _design(kind, n, p, 41)
+    e = _engine(bb, X, y, n, p)
+    e.init_state()
+    e.run(1, 40)
+    e.sync()
+    s = e.state()
+    beta, tau, sig2 = s["beta"], s["tau"], s["sig2"]
+    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
+    for t in (101, 102, 103):
+        e.set_state(beta, tau, sig2, 0.5)
+        e.run(t, 1)
+        g = e.state()
+        st = e.nid_stats()
+        tau = oracle.tau_from_sum(oracle.sum_abs_pow(beta, 0.5), p, 0.5, 2.0, 2.0, SEED, 0, t)
+        r = y - X @ beta
+        sig2 = oracle.sig2_from_rss(float(r @ r), n, 0.0, 0.0, SEED, 0, t)
+        lam = oracle.sample_lambda(beta, 0.5, tau, SEED, 0, t)
+        z = oracle.normals(p, SEED, 0, t, oracle.KIND_BETA_Z)
+        d = oracle.normals(n, SEED, 0, t, oracle.KIND_DELTA)
+        b = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
+        with capsys.disabled():
+            print(f"\n[{kind} t={t}] eps={st['eps']:.3g} iterates={st['mode']} "
+                  f"beta rel {rel_err(g['beta'], b):.2e}")
+        assert st["mode"] >= 2, st
+        assert abs(g["tau"] - tau) / tau < 1e-11 and abs(g["sig2"] - sig2) / sig2 < 1e-11
+        assert flips(g["lambda"], lam) == 0
+        assert np.max(np.abs(g["lambda"] - lam) / lam) < 1e-11
+        assert rel_err(g["beta"], b) < 1e-10
+        beta = b
+    assert e.error_flags() == 0
+    e.close()
+
+
+def test_nid_fitted_state_takes_the_factor(gpu_lib):
+    """A fitted state (beta at the truth, tau = 1): eps is far above the Chebyshev range, the
+    device decides mode 0 and the sweep forms the Gram and factors it."""
+    bb = gpu_lib
+    n, p = 300, 3000
+    X, y, btrue = synthetic_problem(n, p, seed=12)
+    e = _engine(bb, X, y, n, p)
+    e.init_state()
+    before = e.nid_stats()
+    e.set_state(btrue, 1.0, 1.0, 0.5)
+    e.run(5, 3)
+    e.sync()
+    st = e.nid_stats()
+    assert st["mode"] == 0 and st["eps"] > 1.0, st
+    assert st["chol_sweeps"] - before["chol_sweeps"] == 3
+    e.close()
+
+
+def test_nid_disabled_for_shards(gpu_lib):
+    """Column shards (world > 1) exchange the Gram: no near-identity path (mode -1)."""
+    bb = gpu_lib
+    n, p = 100, 900
+    X, y, _ = synthetic_problem(n, p, seed=13)
+    e = bb.Engine(bb.EngineConfig(n=n, p=p, p_local=450, j0=0, rank=0, world=2, seed=SEED,
+                                  stream=0), np.asfortranarray(X[:, :450]), y)
+    assert e.nid_stats()["mode"] == -1
+    e.close()
