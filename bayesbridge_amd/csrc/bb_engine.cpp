@@ -663,7 +663,7 @@ struct bb_engine {
     void throttle_nid() {
         if (!nid_enabled()) return;
         if (++thr_n % 4 != 0) return;
-        const long m = thr_n / 4;
+        const long m = thr_n / 4 - 1;  // marks 0, 1, 2, ...
         hipEvent_t &e = thr_ev[m % 3];
         if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHECK(hipEventRecord(e, stream));
