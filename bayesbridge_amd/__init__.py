@@ -135,6 +135,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     u64p = c.POINTER(c.c_ulonglong)
     L.bb_engine_nid_stats.argtypes = [c.c_void_p, u64p, u64p, u64p, _dp, _ip]
     L.bb_engine_timed_brackets.argtypes = [c.c_void_p, _ip]
+    L.bb_engine_nid_bound.argtypes = [c.c_void_p, _dp, _ip]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -1084,8 +1085,10 @@ class Engine:
         _check(library().bb_engine_nid_stats(self._h, ctypes.byref(a), ctypes.byref(b),
                                              ctypes.byref(c), ctypes.byref(eps),
                                              ctypes.byref(mode)), "bb_engine_nid_stats")
+        lam, kmax = ctypes.c_double(), ctypes.c_int()
+        library().bb_engine_nid_bound(self._h, ctypes.byref(lam), ctypes.byref(kmax))
         return dict(cheb_sweeps=a.value, products=b.value, chol_sweeps=c.value, eps=eps.value,
-                    mode=mode.value)
+                    mode=mode.value, lambda_x=lam.value, kmax=kmax.value)
 
     def error_flags(self) -> int:
         f = ctypes.c_uint32()

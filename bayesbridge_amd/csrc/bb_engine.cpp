@@ -335,6 +335,8 @@ struct bb_engine {
            *nid_xu = nullptr;
     double *eps_host = nullptr;
     int ea_parts = 1;
+    int nid_kmax = 0;  // iterations beyond which the Gram + Cholesky path is cheaper (model)
+    double lambda_x = 0.0;  // certified lambda_max(X X') bound (0: none)
     hipEvent_t thr_ev[3] = {nullptr, nullptr, nullptr};
     long thr_n = 0;
     // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
@@ -397,7 +399,32 @@ struct bb_engine {
 
     // the near-identity path exists for an unsharded Woodbury engine (world == 1; a one-member
     // RCCL group included: nothing is exchanged)
-    bool nid_enabled() const { return nid != nullptr && cfg.world == 1 && g_nid_kmax > 0; }
+    bool nid_enabled() const {
+        return nid != nullptr && cfg.world == 1 && std::min(g_nid_kmax, nid_kmax) > 0;
+    }
+
+    // Cost model of the two exact solves, from the round-3/4 measured rates:
+    // a Chebyshev solve of K iterates reads X K times (the X u pass and K - 1 products, ~6 TB/s
+    // dense, ~3 TB/s for the sparse gathers, plus ~10 us of launches and the recurrence per
+    // pass); the Gram + Cholesky path costs the Gram (Ozaki int8 GEMM at ~2.6 POP/s and its
+    // 24 B per X element of residue traffic at ~5 TB/s; the fp64 MFMA Gram at ~33 TF/s; the
+    // sparse pair stream at ~4 TB/s) plus ~19 us per 64-column block step of the factor and
+    // solve.  Returns the largest K for which the Chebyshev solve is the cheaper one.
+    int nid_kmax_model() const {
+        double t_pass, t_chol;
+        const double steps = n_pad / 64.0;
+        if (method == 5) {
+            t_pass = 24.0 * (double)spd.nnz / 3.0e12 + 10e-6;
+            t_chol = 10.0 * (double)spd.pairs / 4.0e12 + steps * 21e-6 + 60e-6;
+        } else {
+            t_pass = 8.0 * n_pad * (double)p_loc / 6.0e12 + 10e-6;
+            const double gram = cfg.gram_mode == 1
+                ? 16.0 * (double)n_pad * n_pad * p_pad / 2.6e15 + 24.0 * (double)n_pad * p_pad / 5.0e12
+                : 2.0 * (double)n_pad * n_pad * p_pad / 33e12;
+            t_chol = gram + steps * 19e-6 + 40e-6;
+        }
+        return (int)std::min(64.0, std::floor(t_chol / t_pass));
+    }
 
     // Chebyshev iterations to launch for this sweep: from the eps of the latest sweep the
     // device decided (host-mapped, at most ~8 sweeps old through the enqueue throttle) with an
@@ -406,9 +433,10 @@ struct bb_engine {
     // few iterations launched makes that sweep take the Gram + Cholesky path, never a wrong w.
     int nid_launch_count() const {
         if (!nid_enabled()) return 0;
+        const int kmax = std::min(g_nid_kmax, nid_kmax);
         const double h = *(volatile double *)eps_host;
-        if (!(h >= 0.0)) return g_nid_kmax;
-        return cheb_iterations(8.0 * h, g_nid_kmax, kNidTol);
+        if (!(h >= 0.0)) return kmax;
+        return cheb_iterations(8.0 * h, kmax, kNidTol);
     }
 
     // decision kernel of a Woodbury sweep (eps is tracked even when only the Gram + Cholesky
@@ -429,8 +457,8 @@ struct bb_engine {
             launch_cheb_init(stream, nid_xu, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid, w,
                              ch_r, ch_d);
         else
-            launch_cheb_init(stream, nid_xu, nid_xu_parts(p_loc, n_pad), n, n_pad, y, sc,
-                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d);
+            launch_cheb_init(stream, nid_xu, ea_parts, n, n_pad, y, sc, cfg.seed, cfg.stream,
+                             t, nid, w, ch_r, ch_d);
         for (int j = 1; j < kl; ++j) {
             mark(PH_EAPPLY);
             if (method == 5)
@@ -862,6 +890,85 @@ struct SparseIn {
     const double *val;
 };
 
+// Certified upper bound Lambda >= lambda_max(X X') for the near-identity bound (bb_nid.hip
+// k_nid_decide): 40 power iterations on X X' (the E-apply pass with D = 1) give the Rayleigh
+// quotient rho; U = 1.02 rho is certified by factoring U I - X X' (the Gram with D = 1, the
+// device Cholesky): a non-positive pivot (error bit 8) raises U by 25 %, at most six times,
+// after which the bound is left out (Lambda = 0: the trace bound alone).  The factor's
+// backward error (~n u |A|) is far below the 2 % margin.  Setup only, ~10 ms at C3.
+void nid_certify_lambda(bb_engine *e) {
+    const int n_pad = e->n_pad, p_pad = e->p_pad;
+    hipStream_t s = e->stream;
+    double *ones = nullptr;
+    NidState *gate = nullptr;
+    HIPCHECK(hipMalloc(&ones, (size_t)p_pad * sizeof(double)));
+    HIPCHECK(hipMalloc(&gate, sizeof(NidState)));
+    std::vector<double> h1(p_pad, 0.0);
+    for (int j = 0; j < e->p_loc; ++j) h1[j] = 1.0;
+    HIPCHECK(hipMemcpyAsync(ones, h1.data(), h1.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    NidState g{};
+    g.mode = 64;  // every pass of the power iteration runs
+    HIPCHECK(hipMemcpyAsync(gate, &g, sizeof(g), hipMemcpyHostToDevice, s));
+    std::vector<double> v(n_pad, 0.0), w(n_pad);
+    double nv = 0.0;
+    for (int i = 0; i < e->n; ++i) {
+        v[i] = std::cos(0.7 * i + 0.3) + 0.5 * std::sin(1.3 * i * i + 0.1);
+        nv += v[i] * v[i];
+    }
+    for (auto &x : v) x /= std::sqrt(nv);
+    double rho = 0.0;
+    for (int it = 0; it < 40; ++it) {
+        HIPCHECK(hipMemcpyAsync(e->ch_d, v.data(), n_pad * sizeof(double), hipMemcpyHostToDevice, s));
+        if (e->method == 5)
+            launch_sp_eapply(s, e->spd.colptr, e->spd.rowidx, e->spd.cval, e->spd.rowptr,
+                             e->spd.colidx, e->spd.rval, e->p_loc, n_pad, ones, e->ch_d, gate, 0,
+                             e->sp_s, e->ea_part);
+        else
+            launch_eapply(s, e->X, n_pad, n_pad, e->p_loc, ones, e->ch_d, gate, 0, e->ea_part);
+        launch_part_sum(s, e->ea_part, e->method == 5 ? 1 : e->ea_parts, n_pad, e->ch_r);
+        HIPCHECK(hipMemcpyAsync(w.data(), e->ch_r, n_pad * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        double vw = 0.0, ww = 0.0;
+        for (int i = 0; i < n_pad; ++i) {
+            vw += v[i] * w[i];
+            ww += w[i] * w[i];
+        }
+        rho = vw;
+        if (!(ww > 0.0)) break;
+        for (int i = 0; i < n_pad; ++i) v[i] = w[i] / std::sqrt(ww);
+    }
+    double lam = 0.0;
+    if (rho > 0.0 && std::isfinite(rho)) {
+        // the Gram X X' into red2 (packed upper triangle)
+        if (e->method == 5) {
+            e->spd.gram(s, ones, ones, e->red2, e->red2 + tri_count(n_pad));
+        } else if (e->cfg.gram_mode == 1) {
+            launch_oz_scale(s, ones, p_pad, e->oz_xmax, e->n_oz, e->oz_b, e->oz_rowmax,
+                            e->oz_rscale, e->oz_escale);
+            launch_oz_residues(s, e->X, n_pad, n_pad, e->n_oz, p_pad, ones, e->oz_rscale, e->oz_R);
+            launch_oz_gemm(s, e->oz_R, e->n_oz, p_pad, e->oz_S, e->oz_P);
+            launch_oz_crt(s, e->oz_P, e->oz_S, e->n_oz, n_pad, e->oz_escale, nullptr, 0, e->red2);
+        } else {
+            launch_gram(s, e->X, n_pad, ones, n_pad, p_pad, e->S, e->slabs, n_pad, e->slab_stride);
+            launch_slab_sum(s, e->slabs, e->S, e->slab_stride, n_pad, nullptr, 0, e->red2, 1);
+        }
+        double U = 1.02 * rho;
+        for (int attempt = 0; attempt < 7 && lam == 0.0; ++attempt, U *= 1.25) {
+            e->clear_err();
+            launch_shift_gram(s, e->red2, n_pad, U, e->M, n_pad);
+            chol_factor(s, e->M, n_pad, n_pad, 1, e->err, e->Wd, e->flags);
+            if ((e->read_err() & (8u | 16u)) == 0) lam = U * (1.0 + 1e-9);
+        }
+        e->clear_err();
+    }
+    HIPCHECK(hipMemsetAsync(e->nid, 0, sizeof(NidState), s));
+    HIPCHECK(hipMemcpyAsync(&e->nid->lambda_x, &lam, sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    e->lambda_x = lam;
+    (void)hipFree(ones);
+    (void)hipFree(gate);
+}
+
 void engine_setup(bb_engine *e, const double *Xh, const double *yh, const SparseIn *spin) {
     const bb_config &c = e->cfg;
     e->n = c.n;
@@ -978,7 +1085,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
                 launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->cn);
                 e->ea_parts = eapply_parts(c.p_local, n_pad);
                 e->ea_part = dalloc<double>((size_t)e->ea_parts * n_pad, o);
-                e->nid_xu = dalloc<double>((size_t)nid_xu_parts(c.p_local, n_pad) * n_pad, o);
+                e->nid_xu = dalloc<double>((size_t)e->ea_parts * n_pad, o);
             }
             e->nid = dalloc<NidState>(1, o);
             e->ch_r = dalloc<double>(n_pad, o);
@@ -986,6 +1093,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             HIPCHECK(hipHostMalloc((void **)&e->eps_host, sizeof(double), hipHostMallocMapped));
             *e->eps_host = -1.0;  // no observation yet
             HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
+            e->nid_kmax = e->nid_kmax_model();
         }
     }
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
@@ -1070,6 +1178,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
     if (e->method == 4)  // bb_tri.hip k_tri_chain (general and orthogonal designs)
         e->fused = c.p <= kTriChainMaxP && c.world == 1 && e->hy.know_alpha &&
                    (!c.ortho || (e->tri_G && e->cvec));
+    if (e->nid) nid_certify_lambda(e);
     HIPCHECK(hipStreamSynchronize(e->stream));
 }
 
@@ -1523,6 +1632,12 @@ int bb_engine_timed_brackets(bb_engine *e, int *count) {
         for (size_t i = 0; i + 1 < marks.size(); ++i)
             if (marks[i].first == e->timed_phase) ++ng;
     *count = ng;
+    return 0;
+}
+
+int bb_engine_nid_bound(bb_engine *e, double *lambda_x, int *kmax) {
+    if (lambda_x) *lambda_x = e->lambda_x;
+    if (kmax) *kmax = e->nid ? std::min(g_nid_kmax, e->nid_kmax) : -1;
     return 0;
 }
 

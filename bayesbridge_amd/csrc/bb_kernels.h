@@ -47,9 +47,9 @@ struct NidState {
     double eps, theta, delta, sigma1;
     int mode, pad;
     unsigned long long n_cheb, n_products, n_chol;  // sweeps per path, E-apply passes run
+    double lambda_x;  // certified upper bound on lambda_max(X X') (0: none; setup)
 };
 constexpr double kNidTol = 1.3877787807814457e-17;  // 2^-56: bound on the relative error
-constexpr int kNidXuCols = 128;                      // columns per X u partial (k_nid_xu)
 
 // Chebyshev scalars of the interval [1, 1 + eps]
 struct ChebConst {
@@ -84,7 +84,6 @@ __device__ __forceinline__ bool gated(const int *gate) { return gate && *gate !=
 
 int eapply_parts(int p_loc, int n_pad);  // E-apply partial n-vectors (one per workgroup)
 bool eapply_supported(int n_pad);        // dense E-apply register tiling covers n_pad
-int nid_xu_parts(int p_loc, int n_pad);
 void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                        const DevScalars *sc, int k_launched, int allow, NidState *nid,
                        double *eps_host);
@@ -102,6 +101,9 @@ void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const
                       const int *rowptr, const int *colidx, const double *rval, int p_loc,
                       int n_pad, const double *D, const double *v, const NidState *nid, int j,
                       double *scratch_p, double *out);
+void launch_part_sum(hipStream_t s, const double *part, int nparts, int n_pad, double *out);
+void launch_shift_gram(hipStream_t s, const double *red2, int n_pad, double U, double *M,
+                       int ldm);
 void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                       int n_pad, const double *u, const NidState *nid, double *out);
 

@@ -53,22 +53,74 @@ __device__ __forceinline__ double wave_sum(double v) {
 // One workgroup of 1024 threads.  mode = K if this sweep takes the Chebyshev path (allow,
 // K <= k_launched), else 0 (the Gram + Cholesky path).
 // ---------------------------------------------------------------------------------------
+// The bound: for any threshold T, E = sum_{D_j > T} D_j x_j x_j' / sig2 + (the rest) and the
+// rest is <= (T / sig2) X X' in the semidefinite order, so
+//   lambda_max(E) <= [ sum_{D_j > T} D_j |x_j|^2 + T Lambda ] / sig2
+// with Lambda >= lambda_max(X X') certified at setup (nid_certify_lambda).  T = 0 gives the
+// trace; the kernel takes the least of T = 0 and T = Dmax 4^-k, k = 0 .. kNidT - 1.
+constexpr int kNidT = 16;
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
 __global__ __launch_bounds__(1024) void k_nid_decide(const double *__restrict__ D,
                                                      const double *__restrict__ cn, int p_loc,
                                                      const DevScalars *sc, int k_launched,
                                                      int allow, NidState *nid,
                                                      double *eps_host) {
-    __shared__ double part[16];
-    double a = 0.0;
-    for (int j = threadIdx.x; j < p_loc; j += 1024) a += D[j] * cn[j];
-    a = wave_sum(a);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __shared__ double part[16][kNidT + 1];
+    __shared__ double dmax_s;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double m = 0.0;
+    for (int j = threadIdx.x; j < p_loc; j += 1024) m = fmax(m, D[j]);
+    m = wave_max(m);
+    if (lane == 0) part[wid][0] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double mm = 0.0;
+        for (int w = 0; w < 16; ++w) mm = fmax(mm, part[w][0]);
+        dmax_s = mm;
+    }
+    __syncthreads();
+    const double dmax = dmax_s;
+    const double lam_x = nid->lambda_x;  // 0: not certified (the trace bound only)
+    double acc[kNidT + 1];
+#pragma unroll
+    for (int k = 0; k <= kNidT; ++k) acc[k] = 0.0;
+    for (int j = threadIdx.x; j < p_loc; j += 1024) {
+        const double dj = D[j], v = dj * cn[j];
+        acc[kNidT] += v;  // T = 0: the trace
+        double tk = dmax;
+#pragma unroll
+        for (int k = 0; k < kNidT; ++k) {
+            tk *= 0.25;
+            if (dj > tk) acc[k] += v;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k <= kNidT; ++k) acc[k] = wave_sum(acc[k]);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k <= kNidT; ++k) part[wid][k] = acc[k];
     __syncthreads();
     if (threadIdx.x == 0) {
         double s = 0.0;
-        for (int w = 0; w < 16; ++w) s += part[w];
-        // rounding of the sum: a relative margin far above its worst case (p u)
-        const double eps = s / sc->sig2 * (1.0 + 1e-6);
+        for (int w = 0; w < 16; ++w) s += part[w][kNidT];
+        double best = s;
+        if (lam_x > 0.0) {
+            double tk = dmax;
+            for (int k = 0; k < kNidT; ++k) {
+                tk *= 0.25;
+                double sk = 0.0;
+                for (int w = 0; w < 16; ++w) sk += part[w][k];
+                best = fmin(best, sk + tk * lam_x);
+            }
+        }
+        // rounding of the sums: a relative margin far above its worst case (p u)
+        const double eps = best / sc->sig2 * (1.0 + 1e-6);
         const int K = cheb_iterations(eps, k_launched, kNidTol);
         const int mode = (allow && K > 0) ? K : 0;
         nid->eps = eps;
@@ -87,21 +139,38 @@ __global__ __launch_bounds__(1024) void k_nid_decide(const double *__restrict__ 
     }
 }
 
+// Row sums of the nparts partial n-vectors for rows [64 b, 64 b + 64): wave w adds partials
+// w, w + 8, ... for its lane's row, then the eight wave sums are added in order (fixed order:
+// bitwise reproducible).  Returns the sum on wave 0 (lane = row offset).
+constexpr int kRedWaves = 8;
+__device__ __forceinline__ double part_rowsum(const double *__restrict__ part, int nparts,
+                                              int n_pad, int row, double (*red)[64]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double a = 0.0;
+    if (row < n_pad)
+        for (int q = wid; q < nparts; q += kRedWaves) a += part[(size_t)q * n_pad + row];
+    red[wid][lane] = a;
+    __syncthreads();
+    double s = 0.0;
+    if (wid == 0)
+#pragma unroll
+        for (int w = 0; w < kRedWaves; ++w) s += red[w][lane];
+    return s;
+}
+
 // r_0 = y / sig - (X u / sig + delta), x_1 = d_0 = r_0 / theta (x_0 = 0).  X u arrives as
-// nparts column-chunk partials (k_xv, or the sparse row pass with nparts = 1).
-__global__ __launch_bounds__(256) void k_cheb_init(const double *__restrict__ xu_part,
-                                                   int nparts, int n, int n_pad,
-                                                   const double *__restrict__ y,
-                                                   const DevScalars *sc, Key key, uint64_t t,
-                                                   const NidState *nid, double *x, double *r,
-                                                   double *d) {
+// nparts partial n-vectors (k_xu_pass, or the sparse row pass with nparts = 1).
+__global__ __launch_bounds__(64 * kRedWaves) void k_cheb_init(
+    const double *__restrict__ xu_part, int nparts, int n, int n_pad,
+    const double *__restrict__ y, const DevScalars *sc, Key key, uint64_t t, const NidState *nid,
+    double *x, double *r, double *d) {
     if (nid->mode == 0) return;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_pad) return;
+    __shared__ double red[kRedWaves][64];
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double xu = part_rowsum(xu_part, nparts, n_pad, i, red);
+    if (threadIdx.x >= 64 || i >= n_pad) return;
     double rhs = 0.0;
     if (i < n) {
-        double xu = 0.0;
-        for (int q = 0; q < nparts; ++q) xu += xu_part[(size_t)q * n_pad + i];
         const double sig = sqrt(sc->sig2);
         const double delta = normal_at(key, t, KIND_DELTA, (uint64_t)i);
         rhs = y[i] / sig - (xu / sig + delta);  // k_form_m's right-hand side
@@ -114,15 +183,14 @@ __global__ __launch_bounds__(256) void k_cheb_init(const double *__restrict__ xu
 
 // Chebyshev step j (1 <= j <= K - 1): q = d + (sum of the E-apply partials) / sig2,
 // r_j = r_{j-1} - q, d_j = rho_j rho_{j-1} d_{j-1} + (2 rho_j / delta) r_j, x_{j+1} = x_j + d_j.
-__global__ __launch_bounds__(256) void k_cheb_step(const double *__restrict__ part, int nparts,
-                                                   int n_pad, const DevScalars *sc,
-                                                   const NidState *nid, int j, double *x,
-                                                   double *r, double *d) {
+__global__ __launch_bounds__(64 * kRedWaves) void k_cheb_step(
+    const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
+    const NidState *nid, int j, double *x, double *r, double *d) {
     if (nid->mode <= j) return;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n_pad) return;
-    double e = 0.0;
-    for (int q = 0; q < nparts; ++q) e += part[(size_t)q * n_pad + i];
+    __shared__ double red[kRedWaves][64];
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double e = part_rowsum(part, nparts, n_pad, i, red);
+    if (threadIdx.x >= 64 || i >= n_pad) return;
     const double dv = d[i];
     const double qv = dv + e / sc->sig2;
     const double rv = r[i] - qv;
@@ -132,6 +200,28 @@ __global__ __launch_bounds__(256) void k_cheb_step(const double *__restrict__ pa
     r[i] = rv;
     d[i] = dn;
     x[i] += dn;
+}
+
+// out[i] = sum of the nparts partials of row i (setup: power iteration on X X')
+__global__ __launch_bounds__(64 * kRedWaves) void k_part_sum(const double *__restrict__ part,
+                                                             int nparts, int n_pad,
+                                                             double *__restrict__ out) {
+    __shared__ double red[kRedWaves][64];
+    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double v = part_rowsum(part, nparts, n_pad, i, red);
+    if (threadIdx.x < 64 && i < n_pad) out[i] = v;
+}
+
+// M = U I - G (upper triangle, column-major ldm) from the packed Gram G (red2 layout)
+__global__ __launch_bounds__(256) void k_shift_gram(const double *__restrict__ red2, int n_pad,
+                                                    double U, double *__restrict__ M, int ldm) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= tri_count(n_pad)) return;
+    int c = (int)((sqrt(8.0 * (double)idx + 1.0) - 1.0) * 0.5);
+    while ((size_t)c * (c + 1) / 2 > idx) --c;
+    while ((size_t)(c + 1) * (c + 2) / 2 <= idx) ++c;
+    const int r = (int)(idx - (size_t)c * (c + 1) / 2);
+    M[(size_t)r + (size_t)c * ldm] = (r == c ? U : 0.0) - red2[idx];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -145,14 +235,16 @@ __global__ __launch_bounds__(256) void k_cheb_step(const double *__restrict__ pa
 constexpr int kEaCols = 8;
 constexpr int kEaThreads = 256;
 
-template <int NR>
+// XU: the same pass forming X u (part[wg][row] = sum_c X[row, c] D_c, with D = u), for the
+// right-hand side: no dot products, gated on mode != 0.
+template <int NR, bool XU>
 __global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict__ X, int ldx,
                                                        int n_pad, int p_loc,
                                                        const double *__restrict__ D,
                                                        const double *__restrict__ v,
                                                        const NidState *nid, int j,
                                                        double *__restrict__ part) {
-    if (nid->mode <= j) return;
+    if (XU ? nid->mode == 0 : nid->mode <= j) return;
     __shared__ double ws[4][kEaCols];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     double vr[NR], acc[NR];
@@ -175,6 +267,15 @@ __global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict_
                 const int row = tid + kEaThreads * m;
                 xv[c][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(col + row) : 0.0;
             }
+        }
+        if constexpr (XU) {
+#pragma unroll
+            for (int c = 0; c < kEaCols; ++c) {
+                const double f = (c0 + c < p_loc) ? D[c0 + c] : 0.0;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) acc[m] = __builtin_fma(xv[c][m], f, acc[m]);
+            }
+            continue;
         }
         double s[kEaCols];
 #pragma unroll
@@ -246,28 +347,6 @@ __global__ __launch_bounds__(256) void k_sp_eapply_rows(const int *__restrict__ 
     if (lane == 0) out[row] = a;
 }
 
-// X u partials for the right-hand side (dense): k_xv's column-chunk layout, gated on mode.
-__global__ __launch_bounds__(256) void k_nid_xu(const double *__restrict__ X, int ldx,
-                                                const double *__restrict__ u, int ncols,
-                                                int n_pad, int cols, const NidState *nid,
-                                                double *__restrict__ part) {
-    if (nid->mode == 0) return;
-    const int cb = blockIdx.x;
-    const int c0 = cb * cols;
-    const int nc = min(cols, ncols - c0);
-    const int r = blockIdx.y * 512 + 2 * threadIdx.x;
-    if (r >= n_pad) return;
-    const double *xp = X + (size_t)c0 * ldx + r;
-    double ax = 0.0, ay = 0.0;
-    for (int jj = 0; jj < nc; ++jj) {
-        const double2 xx = *(const double2 *)(xp + (size_t)jj * ldx);
-        const double uj = u[c0 + jj];
-        ax += xx.x * uj;
-        ay += xx.y * uj;
-    }
-    *(double2 *)(part + (size_t)cb * n_pad + r) = make_double2(ax, ay);
-}
-
 // ---------------------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------------------
@@ -291,10 +370,6 @@ int eapply_parts(int p_loc, int n_pad) {
 
 bool eapply_supported(int n_pad) { return n_pad <= 16 * kEaThreads; }
 
-int nid_xu_parts(int p_loc, int n_pad) {
-    (void)n_pad;
-    return (p_loc + kNidXuCols - 1) / kNidXuCols;
-}
 
 void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                        const DevScalars *sc, int k_launched, int allow, NidState *nid,
@@ -302,38 +377,45 @@ void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_l
     k_nid_decide<<<1, 1024, 0, s>>>(D, cn, p_loc, sc, k_launched, allow, nid, eps_host);
 }
 
+template <bool XU>
+static void launch_pass(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
+                        const double *D, const double *v, const NidState *nid, int j,
+                        double *part) {
+    const int g = eapply_parts(p_loc, n_pad);
+    switch ((n_pad + kEaThreads - 1) / kEaThreads) {
+        case 1: k_eapply<1, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 2: k_eapply<2, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 3: case 4:
+            k_eapply<4, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 5: case 6: case 7: case 8:
+            k_eapply<8, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        default:
+            k_eapply<16, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+    }
+}
+
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
                    int n_pad, const NidState *nid, double *part) {
-    dim3 grid((ncols + kNidXuCols - 1) / kNidXuCols, (n_pad + 511) / 512);
-    k_nid_xu<<<grid, 256, 0, s>>>(X, ldx, u, ncols, n_pad, kNidXuCols, nid, part);
+    launch_pass<true>(s, X, ldx, n_pad, ncols, u, nullptr, nid, 0, part);
 }
 
 void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
                       const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
                       uint64_t t, const NidState *nid, double *x, double *r, double *d) {
-    k_cheb_init<<<(n_pad + 255) / 256, 256, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
-                                                    Key{k0, k1}, t, nid, x, r, d);
+    k_cheb_init<<<(n_pad + 63) / 64, 64 * kRedWaves, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
+                                                             Key{k0, k1}, t, nid, x, r, d);
 }
 
 void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
                       const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
                       double *d) {
-    k_cheb_step<<<(n_pad + 255) / 256, 256, 0, s>>>(part, nparts, n_pad, sc, nid, j, x, r, d);
+    k_cheb_step<<<(n_pad + 63) / 64, 64 * kRedWaves, 0, s>>>(part, nparts, n_pad, sc, nid, j, x,
+                                                             r, d);
 }
 
 void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
                    const double *D, const double *v, const NidState *nid, int j, double *part) {
-    const int g = eapply_parts(p_loc, n_pad);
-    switch ((n_pad + kEaThreads - 1) / kEaThreads) {
-        case 1: k_eapply<1><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 2: k_eapply<2><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 3: case 4:
-            k_eapply<4><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 5: case 6: case 7: case 8:
-            k_eapply<8><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        default:
-            k_eapply<16><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-    }
+    launch_pass<false>(s, X, ldx, n_pad, p_loc, D, v, nid, j, part);
 }
 
 void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,
@@ -346,6 +428,16 @@ void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const
                                                                        scratch_p);
     k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, scratch_p,
                                                      nid, j, 0, out);
+}
+
+void launch_part_sum(hipStream_t s, const double *part, int nparts, int n_pad, double *out) {
+    k_part_sum<<<(n_pad + 63) / 64, 64 * kRedWaves, 0, s>>>(part, nparts, n_pad, out);
+}
+
+void launch_shift_gram(hipStream_t s, const double *red2, int n_pad, double U, double *M,
+                       int ldm) {
+    const size_t tot = tri_count(n_pad);
+    k_shift_gram<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(red2, n_pad, U, M, ldm);
 }
 
 void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,

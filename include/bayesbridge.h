@@ -396,6 +396,10 @@ int bb_engine_phase_times(bb_engine *e, double *ms, int cap, int *samples);
 int bb_phase_count(void);
 const char *bb_phase_name(int i);
 
+/* The near-identity path's setup: the certified bound lambda_x >= lambda_max(X X') (0: none)
+ * and the most Chebyshev iterations a sweep may take (cost model and bb_set_tuning key 6; -1:
+ * no near-identity path). */
+int bb_engine_nid_bound(bb_engine *e, double *lambda_x, int *kmax);
 /* Number of timed-phase brackets (launches of the timed phase) recorded since the last reset. */
 int bb_engine_timed_brackets(bb_engine *e, int *count);
 /* Near-identity solve of the Woodbury system: sweeps that took the Chebyshev
