@@ -333,12 +333,14 @@ struct bb_engine {
     NidState *nid = nullptr;
     double *ch_r = nullptr, *ch_d = nullptr, *ea_part = nullptr, *sp_s = nullptr,
            *nid_xu = nullptr;
-    double *eps_host = nullptr;
+    double *eps_host = nullptr;  // ring of kNidRing: eps of sweep q in slot q % kNidRing
     int ea_parts = 1;
     int nid_kmax = 0;  // iterations beyond which the Gram + Cholesky path is cheaper (model)
     double lambda_x = 0.0;  // certified lambda_max(X X') bound (0: none)
-    hipEvent_t thr_ev[3] = {nullptr, nullptr, nullptr};
-    long thr_n = 0;
+    // decided-sweep events (after k_nid_decide of sweep q, slot q % kNidRing) and the number of
+    // Woodbury sweeps enqueued since init_state (q)
+    hipEvent_t nid_ev[8] = {};
+    long nid_seq = 0;
     // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
     ncclComm_t comm = nullptr;
     bool own_comm = true;
@@ -368,7 +370,7 @@ struct bb_engine {
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm && own_comm) ncclCommDestroy(comm);
         for (auto e : ev_pool) (void)hipEventDestroy(e);
-        for (auto e : thr_ev)
+        for (auto e : nid_ev)
             if (e) (void)hipEventDestroy(e);
         if (eps_host) (void)hipHostFree(eps_host);
         for (void *q : owned) (void)hipFree(q);
@@ -426,15 +428,21 @@ struct bb_engine {
         return (int)std::min(64.0, std::floor(t_chol / t_pass));
     }
 
-    // Chebyshev iterations to launch for this sweep: from the eps of the latest sweep the
-    // device decided (host-mapped, at most ~8 sweeps old through the enqueue throttle) with an
-    // 8x growth margin; no observation yet: the maximum; beyond the maximum: 0 (only the Gram
-    // + Cholesky path is launched).  The device decides the sweep itself (k_nid_decide): too
-    // few iterations launched makes that sweep take the Gram + Cholesky path, never a wrong w.
-    int nid_launch_count() const {
-        if (!nid_enabled()) return 0;
+    // Chebyshev iterations to launch for Woodbury sweep q: from eps of sweep q - kNidLag
+    // (host-mapped ring; the host waits for that sweep's decision, so it stays at most
+    // kNidLag sweeps ahead of the device -- no bubble, the device has that many queued) with
+    // an 8x growth margin; the first kNidLag sweeps after init_state: the maximum; beyond the
+    // maximum: 0 (only the Gram + Cholesky path is launched).  The device decides sweep q
+    // itself (k_nid_decide): K iterates needed > launched makes it take the Gram + Cholesky
+    // path, never a wrong w.  The hint is eps of a fixed earlier sweep, so the path a sweep
+    // takes -- and its bits -- depend only on the chain, not on host / device timing.
+    static constexpr int kNidRing = 8, kNidLag = 3;
+    int nid_launch_count() {
         const int kmax = std::min(g_nid_kmax, nid_kmax);
-        const double h = *(volatile double *)eps_host;
+        if (nid_seq < kNidLag) return kmax;
+        const long q = nid_seq - kNidLag;
+        HIPCHECK(hipEventSynchronize(nid_ev[q % kNidRing]));
+        const double h = ((volatile double *)eps_host)[q % kNidRing];
         if (!(h >= 0.0)) return kmax;
         return cheb_iterations(8.0 * h, kmax, kNidTol);
     }
@@ -445,7 +453,11 @@ struct bb_engine {
         if (!nid_enabled()) return 0;
         const int kl = nid_launch_count();
         mark(PH_NID);
-        launch_nid_decide(stream, D, cn, p_loc, sc, kl, kl > 0, nid, eps_dev);
+        const long q = nid_seq++;
+        launch_nid_decide(stream, D, cn, p_loc, sc, kl, kl > 0, nid, eps_dev + q % kNidRing);
+        hipEvent_t &ev = nid_ev[q % kNidRing];
+        if (!ev) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(ev, stream));
         return kl;
     }
     double *eps_dev = nullptr;  // device view of eps_host
@@ -686,18 +698,6 @@ struct bb_engine {
     int fail_at = -1;
     int nid_kl = 0;  // Chebyshev iterations launched for the sweep being enqueued
 
-    // Near-identity engines keep the host at most ~8 sweeps ahead of the device, so the eps
-    // hint they launch from stays recent (the device is the bottleneck: no bubble)
-    void throttle_nid() {
-        if (!nid_enabled()) return;
-        if (++thr_n % 4 != 0) return;
-        const long m = thr_n / 4 - 1;  // marks 0, 1, 2, ...
-        hipEvent_t &e = thr_ev[m % 3];
-        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIPCHECK(hipEventRecord(e, stream));
-        if (m >= 2) HIPCHECK(hipEventSynchronize(thr_ev[(m - 2) % 3]));
-    }
-
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
     void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
         if (fused) {
@@ -725,7 +725,6 @@ struct bb_engine {
             if (k == fail_at) throw HipError("injected failure (bb_debug_fail_member)");
             const int slot = first_slot < 0 ? -1 : first_slot + k * slot_step;
             sweep(t0 + (uint64_t)k, slot, mcmc_phase);
-            throttle_nid();
         }
     }
 
@@ -1090,8 +1089,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->nid = dalloc<NidState>(1, o);
             e->ch_r = dalloc<double>(n_pad, o);
             e->ch_d = dalloc<double>(n_pad, o);
-            HIPCHECK(hipHostMalloc((void **)&e->eps_host, sizeof(double), hipHostMallocMapped));
-            *e->eps_host = -1.0;  // no observation yet
+            HIPCHECK(hipHostMalloc((void **)&e->eps_host, 8 * sizeof(double), hipHostMallocMapped));
+            for (int q = 0; q < 8; ++q) e->eps_host[q] = -1.0;  // no observation yet
             HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
             e->nid_kmax = e->nid_kmax_model();
         }
@@ -1236,6 +1235,7 @@ void engine_init_state_local(bb_engine *e) {
 }
 
 void engine_init_state(bb_engine *e) {
+    e->nid_seq = 0;  // the near-identity launch hint restarts with the chain
     engine_init_state_local(e);
     if (e->method == 4 && e->cfg.ortho) {
         // triangle ortho driver draws sig2 then tau before burn-in (BridgeWrapper.cpp:374-375)
