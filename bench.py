@@ -334,9 +334,9 @@ def roofline_for(phase, ms, ctx, traffic_world):
     elif phase == "eapply":
         # the near-identity solve's pass over X: X diag(D) X' d in one read
         # of X (dense: 8 n_pad p_loc bytes, plus the d vector and the per-workgroup partial
-        # n-vectors it writes; sparse: the CSC and CSR non-zeros, 12 B each, plus D, s, d).
-        # ms: the time per pass that actually ran (ctx["eapply_passes"] of the bracketed
-        # launches did; the others returned at once and their time is charged to the passes)
+        # n-vectors it writes; sparse: the CSC and CSR non-zeros, 12 B each, plus D, s, d),
+        # times the fraction of the launches that ran a pass (the others, past the sweep's
+        # iteration count, return at once)
         n_pad = -(-n // 128) * 128
         if sparse:
             si = eng.sparse_info()
@@ -345,8 +345,10 @@ def roofline_for(phase, ms, ctx, traffic_world):
         else:
             byts = 8.0 * n_pad * p_loc + 8.0 * p_loc + 8.0 * n_pad * (1 + ctx.get("ea_parts", 512))
             kname, kfull = "k_eapply (X D X' d, one pass over X)", "bb::k_eapply"
-        out.update(bound="hbm", kernel=kname, achieved=byts / sec / 1e9, peak=8000.0,
-                   unit="GB/s", algorithmic_bytes_per_launch=byts)
+        pf = ctx.get("pass_frac", 1.0)
+        out.update(bound="hbm", kernel=kname, achieved=byts * pf / sec / 1e9, peak=8000.0,
+                   unit="GB/s", algorithmic_bytes_per_launch=byts * pf,
+                   bytes_per_pass=byts, passes_per_launch=pf)
     else:
         kfull = {"lambda": "bb::k_lambda", "reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve",
                  "beta": "bb::k_beta"}[phase]
@@ -566,6 +568,7 @@ def run_chain(args, n, p, alpha, kind, mode):
     nid1 = eng.nid_stats()
     eng.enable_timing(False)
     nid = None
+    ctx_pass_frac = 1.0
     if nid1["mode"] >= 0:
         dc = nid1["cheb_sweeps"] - nid0["cheb_sweeps"]
         dp = nid1["products"] - nid0["products"]
@@ -577,8 +580,10 @@ def run_chain(args, n, p, alpha, kind, mode):
                        "interval [1, 1 + eps], eps = tr(X D X') / sig2, when K <= 16 iterates "
                        "bound the relative error of w by 2^-56; else Gram + Cholesky "
                        "(DESIGN.md s6.5)"}
-        if dom == "eapply" and dp > 0:
-            dom_ms = dom_ms * brackets / dp  # per pass that ran (see roofline_for)
+        # E-apply launches past a sweep's iteration count return at once: the roofline's
+        # bytes per launch are a pass's bytes x (passes run / launches), its time the average
+        # over all launches (what a rocprofv3 kernel trace averages)
+        ctx_pass_frac = (dp / brackets) if (dom == "eapply" and brackets) else 1.0
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
@@ -589,7 +594,7 @@ def run_chain(args, n, p, alpha, kind, mode):
                  ("ozaki-II int8 (fp64-accurate)" if eng.gram_mode() == bb.GRAM_OZAKI
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
-               gram_name=gram_name)
+               gram_name=gram_name, pass_frac=ctx_pass_frac)
     fitted = None
     if mode == "single" and not logit and not args.no_fitted:
         fitted = fitted_regime(bb, eng, kind, n, p, alpha, t)
@@ -678,17 +683,19 @@ def fitted_regime(bb, eng, kind, n, p, alpha, t, warm=20, steps=50):
     eng.set_state(btrue[:eng.p_local], 1e-2, 1.0, alpha)
     eng.run(t, warm, first_slot=-1)
     eng.sync()
-    eng.enable_timing(True, phases=True)
-    eng.reset_timing()
     s0 = eng.nid_stats()
     t0 = time.perf_counter()
-    eng.run(t + warm, steps, first_slot=-1)
+    eng.run(t + warm, steps, first_slot=-1)  # timed without events
     eng.sync()
     el = time.perf_counter() - t0
-    phases = eng.phase_times()
     s1 = eng.nid_stats()
-    eng.enable_timing(False)
     st = eng.state()
+    eng.enable_timing(True, phases=True)  # then 10 sweeps with the per-phase split
+    eng.reset_timing()
+    eng.run(t + warm + steps, 10, first_slot=-1)
+    eng.sync()
+    phases = eng.phase_times()
+    eng.enable_timing(False)
     return {"value": steps / el, "unit": "sweeps/s", "ms_per_step": 1e3 * el / steps,
             "steps": steps, "warmup": warm,
             "start": "beta = data-generating coefficients, tau = 1e-2, sig2 = 1",
@@ -697,7 +704,8 @@ def fitted_regime(bb, eng, kind, n, p, alpha, t, warm=20, steps=50):
             "chebyshev_sweeps": (s1["cheb_sweeps"] - s0["cheb_sweeps"]) if s1["mode"] >= 0 else 0,
             "eps_last": s1["eps"],
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},
-            "timing": "wall clock around the sweeps with phase events on (adds ~1 us per phase)"}
+            "timing": "wall clock around the timed sweeps (no events); phases_ms from 10 more "
+                      "sweeps with an event at every phase start"}
 
 
 def shard_parity_check(bb, dist, rank, engines, my_ranks, runner, make_engine, dev0, p, world,

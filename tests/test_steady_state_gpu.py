@@ -179,8 +179,8 @@ def test_free_running_posterior_moments_wide(gpu_lib):
     assert set(np.argsort(-np.abs(g.mean(axis=0)))[:5]) == set(range(5))
 
 
-@pytest.mark.parametrize("name,true_tau", [("c3", 0.0), ("c5", 1e-2)])
-def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, capsys):
+@pytest.mark.parametrize("name,true_tau,free", [("c3", 0.0, 300), ("c5", 1e-2, 20)])
+def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, free, capsys):
     """C3 and C5 teacher-forced in the fitted regime: the GPU chain starts at
     the data-generating coefficients with tau = 1e-2 and sig2 = 1 and runs FREE for 300
     sweeps, so lambda, sig2, D = tau^2 / lambda (and tau at C3) are the sampler's own; then
@@ -194,9 +194,11 @@ def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, capsys):
     puts tau at 7.5e-9 already at the truth, and the oracle chain from there is back at
     beta = 0 (sig2 = var(y) = 90, max_j D_j |x_j|^2 / sig2 = 2e-3) within four sweeps.  So
     C5 runs with tau known (the reference's true_tau > 0, BridgeWrapper.cpp:248-250) at
-    1e-2, where the oracle chain stays fitted (sig2 ~ 0.9, D over 13-17 decades,
-    max_j D_j |x_j|^2 / sig2 ~ 2e5-6e5; at tau = 1e-3 the GPU chain after 300 sweeps had
-    cond(M) = 69 only); tau's own conditional is checked at C5 by
+    1e-2 and 20 free sweeps, where the oracle chain is fitted (sig2 ~ 0.9, D over 13-17
+    decades, max_j D_j |x_j|^2 / sig2 ~ 2e5-6e5).  Run longer, even the tau-known chain
+    spreads its mass over all 200 000 coefficients (after 300 sweeps at tau = 1e-2: sig2 =
+    0.6, 198 500 |beta_j| > 1e-3, cond(M) = 62; at tau = 1e-3: cond(M) = 69), so C5 has no
+    long-run regime with a badly conditioned M.  tau's own conditional is checked at C5 by
     test_steady_state_teacher_forced."""
     bb = gpu_lib
     X, y, alpha, btrue = workload(name, with_truth=True)
@@ -207,7 +209,7 @@ def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, capsys):
     assert e.method() in (2, 5)
     e.init_state()
     e.set_state(btrue, true_tau if know_tau else 1e-2, 1.0, alpha)
-    e.run(2, 300, first_slot=-1)  # free-running from the fitted start
+    e.run(2, free, first_slot=-1)  # free-running from the fitted start
     e.sync()
     assert e.error_flags() == 0
     s = e.state()
@@ -223,7 +225,7 @@ def test_fitted_regime_teacher_forced(gpu_lib, name, true_tau, capsys):
         if t == 2001:
             cond, span = m_condition(X, lam, tau, sig2)
             with capsys.disabled():
-                print(f"\n[{name} fitted start + 300 free sweeps] tau={tau:.4g} sig2={sig2:.4g} "
+                print(f"\n[{name} fitted start + {free} free sweeps] tau={tau:.4g} sig2={sig2:.4g} "
                       f"|beta|>1e-3: {int(np.sum(np.abs(beta) > 1e-3))} D span 10^{span:.1f} "
                       f"cond(M)={cond:.3g}")
             assert cond > 1e3, f"not in the fitted regime: cond(M) = {cond:.3g}"

@@ -1,0 +1,29 @@
+#!/bin/bash
+# VALU evidence for the tilted-stable lambda launch ("lambda-step: VALU /
+# transcendental ... report draws/s and VALU-busy"): one counter per rocprofv3 --pmc pass
+# (no trace domain combined), bench C3 (k_lambda_spec) and C5 (k_lambda_cb), plus the
+# near-identity pass k_eapply for reference.  Summary: python tools/pmc_valu_summary.py <round>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+ROUND=${ROUND:-r04}
+OUT=gpurun_out/pmc_valu_$ROUND
+mkdir -p "$OUT"
+REGEX="k_lambda|k_eapply"
+pass() {  # $1 = config name, $2 = counter, rest = bench args
+    local cfg=$1 ctr=$2; shift 2
+    timeout -s KILL 240 rocprofv3 --pmc "$ctr" --kernel-include-regex "$REGEX" \
+        -d "$OUT/$cfg/$ctr" -o run --output-format csv \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fitted "$@" \
+        > "$OUT/$cfg/$ctr.json" 2> "$OUT/$cfg/$ctr.err" || { echo "$cfg $ctr failed ($?)"; exit 1; }
+    echo "$cfg $ctr ok"
+}
+for cfg in c3 c5; do
+    mkdir -p "$OUT/$cfg"
+    case $cfg in
+        c3) args="" ;;
+        c5) args="--workload c5" ;;
+    esac
+    for ctr in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES; do
+        pass $cfg $ctr $args
+    done
+done
