@@ -337,10 +337,18 @@ struct bb_engine {
     int ea_parts = 1;
     int nid_kmax = 0;  // iterations beyond which the Gram + Cholesky path is cheaper (model)
     double lambda_x = 0.0;  // certified lambda_max(X X') bound (0: none)
-    // decided-sweep events (after k_nid_decide of sweep q, slot q % kNidRing) and the number of
+    // decided-sweep events (after the decision of sweep q, slot q % kNidRing) and the number of
     // Woodbury sweeps enqueued since init_state (q)
     hipEvent_t nid_ev[8] = {};
     long nid_seq = 0;
+    // column shards (world > 1): the bound sums exchanged before the decision, the reduced
+    // X u / E d vector, the decision event the host waits on, whether this sweep took the
+    // Chebyshev path, and membership of an on-device shard group (its exchanges are the
+    // group's reduce; RCCL ranks and RCCL group members exchange through their communicator)
+    double *nid_red = nullptr, *nid_sum = nullptr, *nid_wg = nullptr;
+    hipEvent_t nid_sev = nullptr;
+    bool nid_only = false;
+    bool group_member = false;
     // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
     ncclComm_t comm = nullptr;
     bool own_comm = true;
@@ -372,6 +380,7 @@ struct bb_engine {
         for (auto e : ev_pool) (void)hipEventDestroy(e);
         for (auto e : nid_ev)
             if (e) (void)hipEventDestroy(e);
+        if (nid_sev) (void)hipEventDestroy(nid_sev);
         if (eps_host) (void)hipHostFree(eps_host);
         for (void *q : owned) (void)hipFree(q);
         if (stream) (void)hipStreamDestroy(stream);
@@ -399,11 +408,15 @@ struct bb_engine {
 
     bool woodbury() const { return method == 2 || method == 5; }
 
-    // the near-identity path exists for an unsharded Woodbury engine (world == 1; a one-member
-    // RCCL group included: nothing is exchanged)
+    // the near-identity path: an unsharded Woodbury engine (a one-member RCCL group included:
+    // nothing is exchanged) decides on the device against a launch hint; column shards
+    // (world > 1, exchanging through a communicator or an on-device group) decide from the
+    // reduced bound sums and the host waits for that decision (nid_sync)
     bool nid_enabled() const {
-        return nid != nullptr && cfg.world == 1 && std::min(g_nid_kmax, nid_kmax) > 0;
+        return nid != nullptr && (cfg.world == 1 || comm != nullptr || group_member) &&
+               std::min(g_nid_kmax, nid_kmax) > 0;
     }
+    bool nid_sync() const { return cfg.world > 1 && nid_enabled(); }
 
     // Cost model of the two exact solves, from the round-3/4 measured rates:
     // a Chebyshev solve of K iterates reads X K times (the X u pass and K - 1 products, ~6 TB/s
@@ -425,6 +438,12 @@ struct bb_engine {
                 : 2.0 * (double)n_pad * n_pad * p_pad / 33e12;
             t_chol = gram + steps * 19e-6 + 40e-6;
         }
+        if (cfg.world > 1) {
+            // shards: an n-vector all-reduce per pass; the packed Gram's all-reduce (~100 GB/s
+            // effective over xGMI rings) and the replicated factor on the other side
+            t_pass += 25e-6;
+            t_chol += 8.0 * (double)red2_count() / 100e9 + 25e-6;
+        }
         return (int)std::min(64.0, std::floor(t_chol / t_pass));
     }
 
@@ -433,7 +452,7 @@ struct bb_engine {
     // kNidLag sweeps ahead of the device -- no bubble, the device has that many queued) with
     // an 8x growth margin; the first kNidLag sweeps after init_state: the maximum; beyond the
     // maximum: 0 (only the Gram + Cholesky path is launched).  The device decides sweep q
-    // itself (k_nid_decide): K iterates needed > launched makes it take the Gram + Cholesky
+    // itself (k_nid_reduce): K iterates needed > launched makes it take the Gram + Cholesky
     // path, never a wrong w.  The hint is eps of a fixed earlier sweep, so the path a sweep
     // takes -- and its bits -- depend only on the chain, not on host / device timing.
     static constexpr int kNidRing = 8, kNidLag = 3;
@@ -454,7 +473,8 @@ struct bb_engine {
         const int kl = nid_launch_count();
         mark(PH_NID);
         const long q = nid_seq++;
-        launch_nid_decide(stream, D, cn, p_loc, sc, kl, kl > 0, nid, eps_dev + q % kNidRing);
+        launch_nid_sums(stream, D, cn, p_loc, sc, nid, kl, kl > 0, 1, nid_wg, nid_red,
+                        eps_dev + q % kNidRing);
         hipEvent_t &ev = nid_ev[q % kNidRing];
         if (!ev) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         HIPCHECK(hipEventRecord(ev, stream));
@@ -481,6 +501,79 @@ struct bb_engine {
             mark(PH_NID);
             launch_cheb_step(stream, ea_part, method == 5 ? 1 : ea_parts, n_pad, sc, nid, j, w,
                              ch_r, ch_d);
+        }
+    }
+
+    // ---- column shards (nid_sync): the stages between the exchanges of a Woodbury sweep ----
+    static constexpr int kNidRed = kNidTS + 2;
+    // this shard's bound sums into nid_red (exchanged: kNidRed doubles)
+    void nidx_partials() {
+        mark(PH_NID);
+        launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
+    }
+    // the decision from the reduced sums (identical on every rank), then wait for it
+    void nidx_decide_launch() {
+        launch_nid_decide_from(stream, nid_red, sc, std::min(g_nid_kmax, nid_kmax), nid,
+                               eps_dev + kNidRing);
+        if (!nid_sev) HIPCHECK(hipEventCreateWithFlags(&nid_sev, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(nid_sev, stream));
+    }
+    int nidx_decide_read() {
+        HIPCHECK(hipEventSynchronize(nid_sev));
+        return (int)((volatile double *)eps_host)[kNidRing + 1];
+    }
+    // this shard's X u into nid_sum (exchanged: n_pad)
+    void nidx_xu() {
+        mark(PH_NID);
+        if (method == 5) {
+            launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid, nid_sum);
+        } else {
+            launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
+            launch_part_sum(stream, nid_xu, ea_parts, n_pad, nid_sum);
+        }
+    }
+    void nidx_init(uint64_t t) {
+        launch_cheb_init(stream, nid_sum, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid, w,
+                         ch_r, ch_d);
+    }
+    // this shard's E d of step j into nid_sum (exchanged: n_pad)
+    void nidx_eapply(int j) {
+        mark(PH_EAPPLY);
+        if (method == 5) {
+            launch_sp_eapply(stream, spd.colptr, spd.rowidx, spd.cval, spd.rowptr, spd.colidx,
+                             spd.rval, p_loc, n_pad, D, ch_d, nid, j, sp_s, nid_sum);
+        } else {
+            launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part);
+            launch_part_sum(stream, ea_part, ea_parts, n_pad, nid_sum);
+        }
+    }
+    void nidx_step(int j) {
+        mark(PH_NID);
+        launch_cheb_step(stream, nid_sum, 1, n_pad, sc, nid, j, w, ch_r, ch_d);
+    }
+    // a shard's Woodbury sweep between phase b and phase c, through exchange(buf, count)
+    template <class Exchange>
+    void shard_solve(uint64_t t, Exchange exchange) {
+        if (!nid_sync()) {
+            exchange(red2, red2_count());
+            return;
+        }
+        exchange(nid_red, (size_t)kNidRed);
+        nidx_decide_launch();
+        const int K = nidx_decide_read();
+        nid_only = K > 0;
+        if (K > 0) {
+            nidx_xu();
+            exchange(nid_sum, (size_t)n_pad);
+            nidx_init(t);
+            for (int j = 1; j < K; ++j) {
+                nidx_eapply(j);
+                exchange(nid_sum, (size_t)n_pad);
+                nidx_step(j);
+            }
+        } else {
+            wb_gram(nullptr);
+            exchange(red2, red2_count());
         }
     }
 
@@ -518,6 +611,38 @@ struct bb_engine {
         launch_pre(stream, xb_part, nparts, n_pad, beta, p_loc, sc, red1, nbS);
     }
 
+    // this shard's (or the whole) Gram X D X' with X u into red2 (packed upper triangle, then
+    // the n-vector); gate: the near-identity decision word (its kernels skip on mode != 0)
+    void wb_gram(const int *gate) {
+        if (method == 5) {
+            mark(PH_GRAM);
+            spd.gram(stream, D, u, red2, red2 + tri_count(n_pad), gate);
+            return;
+        }
+        if (cfg.gram_mode == 1) {
+            mark(PH_OZPREP);
+            launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowmax, oz_rscale,
+                            oz_escale, gate);
+            // the residue pass over X also forms the X u partials
+            launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R, u,
+                               xu_part, gate);
+            mark(PH_GRAM);
+            launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P, 0, kOzLeadDefault, -1, gate);
+        } else {
+            mark(PH_GRAM);
+            launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride, gate);
+            mark(PH_XU);
+            launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part, gate);
+        }
+        mark(PH_REDUCE);
+        if (cfg.gram_mode == 1)
+            launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
+                          oz_xu_parts(p_pad, n_oz), red2, gate);
+        else
+            launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
+                            red2, 1, gate);
+    }
+
     void phase_b(uint64_t t, int slot) {
         mark(PH_SCALARS);
         launch_scalars(stream, red1, nbS, y, n, p, sc, hy, cfg.seed, cfg.stream, t,
@@ -525,48 +650,25 @@ struct bb_engine {
                        slot_ptr(tr_alpha, slot, 1), 0, err);
         double *trl = slot_ptr(tr_lam, slot, p_loc);
         mark(PH_LAMBDA);
-        if (method == 5) {
+        if (method == 5 || method == 2) {
             launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
                           t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            nid_only = false;
+            if (nid_sync()) {
+                // a shard: the bound sums now, the path after their exchange (shard_solve)
+                nid_kl = 0;
+                nidx_partials();
+                return;
+            }
             nid_kl = nid_begin();
-            const int *gate = nid_kl ? &nid->mode : nullptr;
-            mark(PH_GRAM);
-            // packed Gram (with its diagonal) and X u
-            spd.gram(stream, D, u, red2, red2 + tri_count(n_pad), gate);
+            wb_gram(nid_kl ? &nid->mode : nullptr);
             if (nid_kl) {
                 mark(PH_NID);
-                launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid, nid_xu);
-            }
-        } else if (method == 2) {
-            launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
-                          t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
-            nid_kl = nid_begin();
-            const int *gate = nid_kl ? &nid->mode : nullptr;
-            if (cfg.gram_mode == 1) {
-                mark(PH_OZPREP);
-                launch_oz_scale(stream, D, p_pad, oz_xmax, n_oz, oz_b, oz_rowmax, oz_rscale,
-                                oz_escale, gate);
-                // the residue pass over X also forms the X u partials
-                launch_oz_residues(stream, X, n_pad, n_pad, n_oz, p_pad, D, oz_rscale, oz_R, u,
-                                   xu_part, gate);
-                mark(PH_GRAM);
-                launch_oz_gemm(stream, oz_R, n_oz, p_pad, oz_S, oz_P, 0, kOzLeadDefault, -1, gate);
-            } else {
-                mark(PH_GRAM);
-                launch_gram(stream, X, n_pad, D, n_pad, p_pad, S, slabs, n_pad, slab_stride, gate);
-                mark(PH_XU);
-                launch_xv(stream, X, n_pad, u, p_pad, n_pad, xu_part, gate);
-            }
-            mark(PH_REDUCE);
-            if (cfg.gram_mode == 1)
-                launch_oz_crt(stream, oz_P, oz_S, n_oz, n_pad, oz_escale, xu_part,
-                              oz_xu_parts(p_pad, n_oz), red2, gate);
-            else
-                launch_slab_sum(stream, slabs, S, slab_stride, n_pad, xu_part, xv_chunks(p_pad, n_pad),
-                                red2, 1, gate);
-            if (nid_kl) {
-                mark(PH_NID);
-                launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
+                if (method == 5)
+                    launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid,
+                                     nid_xu);
+                else
+                    launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
             }
         } else if (method == 6) {
             // omega_i ~ PG(1, x_i' beta), x_i' beta from red1 (k_pre's row sums): drawn by
@@ -612,15 +714,18 @@ struct bb_engine {
         if (method == 5 || method == 2) {
             // w = M^-1 (y / sig - v): the Gram + Cholesky path, or (nid_kl > 0 and the device
             // decided so) the Chebyshev solve -- the kernels of the other path return at once
+            // (a shard that took the Chebyshev path solved it in shard_solve: nid_only)
             const int *gate = nid_kl ? &nid->mode : nullptr;
-            mark(PH_FORM);
-            launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad, n_pad,
-                          gate);
-            mark(PH_CHOL);
-            chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags, nullptr, gate);
-            mark(PH_SOLVE);
-            chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags, err,
-                        gate);
+            if (!nid_only) {
+                mark(PH_FORM);
+                launch_form_m(stream, red2, n, n_pad, y, sc, cfg.seed, cfg.stream, t, M, n_pad,
+                              n_pad, gate);
+                mark(PH_CHOL);
+                chol_factor(stream, M, n_pad, n_pad, 1, err, Wd, flags, nullptr, gate);
+                mark(PH_SOLVE);
+                chol_bsolve(stream, M, n_pad, n_pad, Wd, M + (size_t)n_pad * n_pad, w, 1, flags,
+                            err, gate);
+            }
             if (nid_kl) nid_solve(t, nid_kl);
         }
         if (method == 5) {
@@ -732,7 +837,8 @@ struct bb_engine {
         phase_a(t);
         allreduce(red1, red1_count());
         phase_b(t, slot);
-        if (woodbury()) allreduce(red2, red2_count());
+        if (woodbury())
+            shard_solve(t, [this](double *buf, size_t count) { allreduce(buf, count); });
         phase_c(t, slot, mcmc_phase);
         if (alpha_exchange()) {
             allreduce(red3, 2);
@@ -890,7 +996,7 @@ struct SparseIn {
 };
 
 // Certified upper bound Lambda >= lambda_max(X X') for the near-identity bound (bb_nid.hip
-// k_nid_decide): 40 power iterations on X X' (the E-apply pass with D = 1) give the Rayleigh
+// k_nid_reduce): 40 power iterations on X X' (the E-apply pass with D = 1) give the Rayleigh
 // quotient rho; U = 1.02 rho is certified by factoring U I - X X' (the Gram with D = 1, the
 // device Cholesky): a non-positive pivot (error bit 8) raises U by 25 %, at most six times,
 // after which the bound is left out (Lambda = 0: the trace bound alone).  The factor's
@@ -1065,9 +1171,9 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
         e->red2 = dalloc<double>(tri_count(n_pad) + n_pad, o);
         e->M = dalloc<double>((size_t)n_pad * (n_pad + kNB), o);
         e->w = dalloc<double>(n_pad, o);
-        // near-identity solve (bb_nid.hip): unsharded engines; the dense E-apply keeps its
-        // rows in registers up to n_pad = 4096
-        if (c.world == 1 && (e->method == 5 || eapply_supported(n_pad))) {
+        // near-identity solve (bb_nid.hip); the dense E-apply keeps its rows in registers up
+        // to n_pad = 4096
+        if (e->method == 5 || eapply_supported(n_pad)) {
             e->cn = dalloc<double>(p_pad, o);
             if (e->method == 5) {
                 std::vector<double> h(c.p_local, 0.0);
@@ -1089,8 +1195,13 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->nid = dalloc<NidState>(1, o);
             e->ch_r = dalloc<double>(n_pad, o);
             e->ch_d = dalloc<double>(n_pad, o);
-            HIPCHECK(hipHostMalloc((void **)&e->eps_host, 8 * sizeof(double), hipHostMallocMapped));
-            for (int q = 0; q < 8; ++q) e->eps_host[q] = -1.0;  // no observation yet
+            e->nid_red = dalloc<double>(bb_engine::kNidRed, o);
+            e->nid_wg = dalloc<double>((size_t)nid_sum_groups(c.p_local) * (kNidTS + 1), o);
+            if (c.world > 1) e->nid_sum = dalloc<double>(n_pad, o);
+            // the hint ring, then a shard's [eps, mode] of the sweep being decided
+            const int nh = bb_engine::kNidRing + 2;
+            HIPCHECK(hipHostMalloc((void **)&e->eps_host, nh * sizeof(double), hipHostMallocMapped));
+            for (int q = 0; q < nh; ++q) e->eps_host[q] = -1.0;  // no observation yet
             HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
             e->nid_kmax = e->nid_kmax_model();
         }
@@ -1701,6 +1812,7 @@ struct bb_group {
             if (!poisoned) (void)hipStreamSynchronize(m->stream);
             if (rccl) m->comm = nullptr;  // lent by this group
             m->stop = nullptr;
+            m->group_member = false;
         }
         for (auto c : comms)
             if (c) ncclCommDestroy(c);
@@ -1784,6 +1896,7 @@ bb_group *group_create(bb_engine **engines, int count, bool rccl) {
                 g->mev.push_back(e);
             }
             HIPCHECK(hipMalloc(&g->tmp, c * sizeof(double)));
+            for (int i = 0; i < count; ++i) engines[i]->group_member = true;
         }
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
@@ -1874,8 +1987,49 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
                 g->on(m);
                 m->phase_b(t, slot);
             }
-            if (g->members[0]->woodbury())
-                g->reduce(&bb_engine::red2, g->members[0]->red2_count());
+            bb_engine *m0 = g->members[0];
+            if (m0->woodbury() && m0->nid_sync()) {
+                // the stages of bb_engine::shard_solve, each over all members, with the
+                // group's reduce as the exchange; every member decides from the same reduced
+                // sums, so member 0's decision is every member's
+                g->reduce(&bb_engine::nid_red, (size_t)bb_engine::kNidRed);
+                for (auto *m : g->members) {
+                    g->on(m);
+                    m->nidx_decide_launch();
+                }
+                const int K = m0->nidx_decide_read();
+                for (auto *m : g->members) m->nid_only = K > 0;
+                if (K > 0) {
+                    for (auto *m : g->members) {
+                        g->on(m);
+                        m->nidx_xu();
+                    }
+                    g->reduce(&bb_engine::nid_sum, (size_t)m0->n_pad);
+                    for (auto *m : g->members) {
+                        g->on(m);
+                        m->nidx_init(t);
+                    }
+                    for (int j = 1; j < K; ++j) {
+                        for (auto *m : g->members) {
+                            g->on(m);
+                            m->nidx_eapply(j);
+                        }
+                        g->reduce(&bb_engine::nid_sum, (size_t)m0->n_pad);
+                        for (auto *m : g->members) {
+                            g->on(m);
+                            m->nidx_step(j);
+                        }
+                    }
+                } else {
+                    for (auto *m : g->members) {
+                        g->on(m);
+                        m->wb_gram(nullptr);
+                    }
+                    g->reduce(&bb_engine::red2, m0->red2_count());
+                }
+            } else if (m0->woodbury()) {
+                g->reduce(&bb_engine::red2, m0->red2_count());
+            }
             // phase c holds the persistent Cholesky / backward-solve kernels, which need every
             // workgroup of their grid resident at once: two members' launches on the shared
             // device must not overlap (two C3-sized factorisations side by side each hold part

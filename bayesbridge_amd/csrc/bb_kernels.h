@@ -41,8 +41,9 @@ enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
 
 // Per-sweep choice between the two exact solves of the Woodbury system (bb_nid.hip, DESIGN.md
 // s6.5): mode 0 = Gram + Cholesky, mode K > 0 = Chebyshev iteration with K iterates on the
-// certified spectrum interval [1, 1 + eps].  Written on the device by k_nid_decide every
-// sweep; the kernels of the path not taken return at once.
+// certified spectrum interval [1, 1 + eps].  Written on the device every sweep by
+// k_nid_reduce (k_nid_decide_from for shards); the kernels of the path not taken return at
+// once.
 struct NidState {
     double eps, theta, delta, sigma1;
     int mode, pad;
@@ -84,9 +85,17 @@ __device__ __forceinline__ bool gated(const int *gate) { return gate && *gate !=
 
 int eapply_parts(int p_loc, int n_pad);  // E-apply partial n-vectors (one per workgroup)
 bool eapply_supported(int n_pad);        // dense E-apply register tiling covers n_pad
-void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
-                       const DevScalars *sc, int k_launched, int allow, NidState *nid,
-                       double *eps_host);
+// the decision's bound sums (bb_nid.hip): G = nid_sum_groups(p_loc) workgroup partials
+// (wg_part, G x (kNidTS + 1)) reduced in order into red (kNidTS + 2: [S_k | trace | Lambda]);
+// decide != 0: the unsharded decision at once (eps into the host-mapped eps_host); a shard
+// exchanges red, then launch_nid_decide_from (host2 = host-mapped [eps, mode])
+constexpr int kNidTS = 32;
+int nid_sum_groups(int p_loc);
+void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc,
+                     const DevScalars *sc, NidState *nid, int k_launched, int allow, int decide,
+                     double *wg_part, double *red, double *eps_host);
+void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
+                            int k_launched, NidState *nid, double *host2);
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
                    int n_pad, const NidState *nid, double *part);
 void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,

@@ -11,7 +11,7 @@
 // T_K the Chebyshev polynomial.  The engine takes this path for a sweep when K <= the
 // iterations it launched and the bound is below 2^-56 (the solve is then more accurate
 // than the dense Cholesky it replaces); otherwise the same sweep runs the Gram + Cholesky
-// path.  The decision is made on the device (k_nid_decide) every sweep; the kernels of the
+// path.  The decision is made on the device (k_nid_sums, k_nid_reduce) every sweep; the kernels of the
 // path not taken return at once (the gate word NidState::mode).
 //
 // x_K needs K - 1 products E d, each ONE pass over X: k_eapply forms X diag(D) (X' d)
@@ -49,94 +49,121 @@ __device__ __forceinline__ double wave_sum(double v) {
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-// Decision: eps = sum_j D_j cn_j / sig2 (fixed-order tree), the iteration count K, mode.
-// One workgroup of 1024 threads.  mode = K if this sweep takes the Chebyshev path (allow,
-// K <= k_launched), else 0 (the Gram + Cholesky path).
-// ---------------------------------------------------------------------------------------
-// The bound: for any threshold T, E = sum_{D_j > T} D_j x_j x_j' / sig2 + (the rest) and the
+// Decision.  For any threshold T, E = sum_{D_j > T} D_j x_j x_j' / sig2 + (the rest) and the
 // rest is <= (T / sig2) X X' in the semidefinite order, so
 //   lambda_max(E) <= [ sum_{D_j > T} D_j |x_j|^2 + T Lambda ] / sig2
-// with Lambda >= lambda_max(X X') certified at setup (nid_certify_lambda).  T = 0 gives the
-// trace; the kernel takes the least of T = 0 and T = Dmax 4^-k, k = 0 .. kNidT - 1.
-constexpr int kNidT = 16;
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+// with Lambda >= lambda_max(X X') certified at setup (nid_certify_lambda); T = 0 gives the
+// trace.  The thresholds are fixed multiples of tau^2, T_k = tau^2 2^(40 - 2k), k < kNidTS
+// (D_j = tau^2 / lambda_j: they span 1 / lambda_j from 2^40 down to 2^-22), so one pass over
+// D gives every candidate, and column shards (world > 1), which hold disjoint columns, can
+// add their sums:
+//   red = [ S_0 .. S_{kNidTS-1}, trace, Lambda ],  S_k = sum_{D_j > T_k} D_j |x_j|^2,
+// red[kNidTS + 1] = this engine's certified Lambda; after a shard exchange (sum) it is the sum
+// of the shards' certificates, >= lambda_max(X X') (Weyl).  An engine without a certificate
+// contributes +inf: the bound is the trace alone.  eps = least candidate / sig2 (x 1 + 1e-6).
+//
+// k_nid_sums: G workgroups, each writes its kNidTS + 1 partial sums; k_nid_reduce adds them
+// in workgroup order (bitwise reproducible) and -- unsharded -- decides at once; a shard
+// exchanges red first and decides in k_nid_decide_from (the same bits on every rank, so every
+// rank takes the same path).  mode = K if the sweep takes the Chebyshev path (allow,
+// K <= k_launched), else 0 (the Gram + Cholesky path).
+// ---------------------------------------------------------------------------------------
+constexpr int kNidSumWG = 256;
+
+__device__ __forceinline__ double shard_threshold(double tau2, int k) {
+    return ldexp(tau2, 40 - 2 * k);
 }
 
-__global__ __launch_bounds__(1024) void k_nid_decide(const double *__restrict__ D,
-                                                     const double *__restrict__ cn, int p_loc,
-                                                     const DevScalars *sc, int k_launched,
-                                                     int allow, NidState *nid,
-                                                     double *eps_host) {
-    __shared__ double part[16][kNidT + 1];
-    __shared__ double dmax_s;
+// eps from the least bound, the iteration count K and the sweep's mode (thread 0)
+__device__ void nid_finish(const double *red, const DevScalars *sc, int k_launched, int allow,
+                           NidState *nid, double *eps_host, double *mode_host) {
+    const double tau2 = sc->tau * sc->tau;
+    const double lam = red[kNidTS + 1];
+    double best = red[kNidTS];
+    if (lam > 0.0 && lam < HUGE_VAL)
+        for (int k = 0; k < kNidTS; ++k)
+            best = fmin(best, red[k] + shard_threshold(tau2, k) * lam);
+    // rounding of the sums: a relative margin far above its worst case (p u)
+    const double eps = best / sc->sig2 * (1.0 + 1e-6);
+    const int K = cheb_iterations(eps, k_launched, kNidTol);
+    const int mode = (allow && K > 0) ? K : 0;
+    nid->eps = eps;
+    nid->mode = mode;
+    const ChebConst c = cheb_const(eps);
+    nid->theta = c.theta;
+    nid->delta = c.delta;
+    nid->sigma1 = c.sigma1;
+    if (mode) {
+        nid->n_cheb += 1;
+        nid->n_products += (unsigned long long)(mode - 1);
+    } else {
+        nid->n_chol += 1;
+    }
+    if (eps_host) *eps_host = eps;  // host-mapped: the launch hint / the shard's decision
+    if (mode_host) *mode_host = (double)mode;
+}
+
+__global__ __launch_bounds__(kNidSumWG) void k_nid_sums(const double *__restrict__ D,
+                                                        const double *__restrict__ cn, int p_loc,
+                                                        const DevScalars *sc,
+                                                        double *__restrict__ wg_part) {
+    __shared__ double part[kNidSumWG / 64][kNidTS + 1];
+    __shared__ double thr[kNidTS];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double m = 0.0;
-    for (int j = threadIdx.x; j < p_loc; j += 1024) m = fmax(m, D[j]);
-    m = wave_max(m);
-    if (lane == 0) part[wid][0] = m;
+    const double tau2 = sc->tau * sc->tau;
+    if (threadIdx.x < kNidTS) thr[threadIdx.x] = shard_threshold(tau2, threadIdx.x);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double mm = 0.0;
-        for (int w = 0; w < 16; ++w) mm = fmax(mm, part[w][0]);
-        dmax_s = mm;
-    }
-    __syncthreads();
-    const double dmax = dmax_s;
-    const double lam_x = nid->lambda_x;  // 0: not certified (the trace bound only)
-    double acc[kNidT + 1];
+    double acc[kNidTS + 1];
 #pragma unroll
-    for (int k = 0; k <= kNidT; ++k) acc[k] = 0.0;
-    for (int j = threadIdx.x; j < p_loc; j += 1024) {
+    for (int k = 0; k <= kNidTS; ++k) acc[k] = 0.0;
+    for (int j = blockIdx.x * kNidSumWG + threadIdx.x; j < p_loc; j += gridDim.x * kNidSumWG) {
         const double dj = D[j], v = dj * cn[j];
-        acc[kNidT] += v;  // T = 0: the trace
-        double tk = dmax;
+        acc[kNidTS] += v;
 #pragma unroll
-        for (int k = 0; k < kNidT; ++k) {
-            tk *= 0.25;
-            if (dj > tk) acc[k] += v;
-        }
+        for (int k = 0; k < kNidTS; ++k)
+            if (dj > thr[k]) acc[k] += v;
     }
 #pragma unroll
-    for (int k = 0; k <= kNidT; ++k) acc[k] = wave_sum(acc[k]);
-    __syncthreads();
+    for (int k = 0; k <= kNidTS; ++k) acc[k] = wave_sum(acc[k]);
     if (lane == 0)
 #pragma unroll
-        for (int k = 0; k <= kNidT; ++k) part[wid][k] = acc[k];
+        for (int k = 0; k <= kNidTS; ++k) part[wid][k] = acc[k];
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x <= kNidTS) {
         double s = 0.0;
-        for (int w = 0; w < 16; ++w) s += part[w][kNidT];
-        double best = s;
-        if (lam_x > 0.0) {
-            double tk = dmax;
-            for (int k = 0; k < kNidT; ++k) {
-                tk *= 0.25;
-                double sk = 0.0;
-                for (int w = 0; w < 16; ++w) sk += part[w][k];
-                best = fmin(best, sk + tk * lam_x);
-            }
-        }
-        // rounding of the sums: a relative margin far above its worst case (p u)
-        const double eps = best / sc->sig2 * (1.0 + 1e-6);
-        const int K = cheb_iterations(eps, k_launched, kNidTol);
-        const int mode = (allow && K > 0) ? K : 0;
-        nid->eps = eps;
-        nid->mode = mode;
-        const ChebConst c = cheb_const(eps);
-        nid->theta = c.theta;
-        nid->delta = c.delta;
-        nid->sigma1 = c.sigma1;
-        if (mode) {
-            nid->n_cheb += 1;
-            nid->n_products += (unsigned long long)(mode - 1);
-        } else {
-            nid->n_chol += 1;
-        }
-        if (eps_host) *eps_host = eps;  // host-mapped: the engine's launch hint
+        for (int w = 0; w < kNidSumWG / 64; ++w) s += part[w][threadIdx.x];
+        wg_part[(size_t)blockIdx.x * (kNidTS + 1) + threadIdx.x] = s;
     }
+}
+
+// red = the G workgroups' sums (in workgroup order) and Lambda; decide: the unsharded
+// decision at once
+__global__ __launch_bounds__(64) void k_nid_reduce(const double *__restrict__ wg_part, int G,
+                                                   const DevScalars *sc, int k_launched,
+                                                   int allow, int decide, NidState *nid,
+                                                   double *__restrict__ red, double *eps_host) {
+    __shared__ double r[kNidTS + 2];
+    if (threadIdx.x <= kNidTS) {
+        double s = 0.0;
+        for (int b = 0; b < G; ++b) s += wg_part[(size_t)b * (kNidTS + 1) + threadIdx.x];
+        r[threadIdx.x] = s;
+        red[threadIdx.x] = s;
+    }
+    if (threadIdx.x == kNidTS + 1) {
+        const double lam = nid->lambda_x;
+        const double v = lam > 0.0 ? lam : HUGE_VAL;
+        r[threadIdx.x] = v;
+        red[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (decide && threadIdx.x == 0) nid_finish(r, sc, k_launched, allow, nid, eps_host, nullptr);
+}
+
+__global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
+                                                        const DevScalars *sc, int k_launched,
+                                                        NidState *nid, double *host2) {
+    if (threadIdx.x != 0) return;
+    nid_finish(red, sc, k_launched, 1, nid, host2, host2 + 1);
 }
 
 // Row sums of the nparts partial n-vectors for rows [64 b, 64 b + 64): wave w adds partials
@@ -371,10 +398,20 @@ int eapply_parts(int p_loc, int n_pad) {
 bool eapply_supported(int n_pad) { return n_pad <= 16 * kEaThreads; }
 
 
-void launch_nid_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
-                       const DevScalars *sc, int k_launched, int allow, NidState *nid,
-                       double *eps_host) {
-    k_nid_decide<<<1, 1024, 0, s>>>(D, cn, p_loc, sc, k_launched, allow, nid, eps_host);
+int nid_sum_groups(int p_loc) { return std::max(1, std::min(256, (p_loc + 1023) / 1024)); }
+
+void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc,
+                     const DevScalars *sc, NidState *nid, int k_launched, int allow, int decide,
+                     double *wg_part, double *red, double *eps_host) {
+    const int G = nid_sum_groups(p_loc);
+    k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
+    k_nid_reduce<<<1, 64, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
+                                  eps_host);
+}
+
+void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
+                            int k_launched, NidState *nid, double *host2) {
+    k_nid_decide_from<<<1, 64, 0, s>>>(red, sc, k_launched, nid, host2);
 }
 
 template <bool XU>

@@ -577,9 +577,13 @@ def run_chain(args, n, p, alpha, kind, mode):
                "eapply_passes_per_chebyshev_sweep": (dp / dc) if dc else None,
                "eps_last": nid1["eps"],
                "rule": "per sweep on the device: Chebyshev iteration on the certified spectrum "
-                       "interval [1, 1 + eps], eps = tr(X D X') / sig2, when K <= 16 iterates "
+                       "interval [1, 1 + eps], eps >= lambda_max(X D X') / sig2 (the least of "
+                       "the trace and thresholded sums + T Lambda, Lambda >= lambda_max(X X') "
+                       "certified at setup), when K iterates (at most the cost model's cap) "
                        "bound the relative error of w by 2^-56; else Gram + Cholesky "
-                       "(DESIGN.md s6.5)"}
+                       "(DESIGN.md s6.5)" + (
+                           "; column shards decide from the all-reduced shard sums (every rank "
+                           "alike) and exchange X u and each product E d" if world > 1 else "")}
         # E-apply launches past a sweep's iteration count return at once: the roofline's
         # bytes per launch are a pass's bytes x (passes run / launches), its time the average
         # over all launches (what a rocprofv3 kernel trace averages)

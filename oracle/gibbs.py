@@ -117,11 +117,12 @@ def woodbury_solve_cheb(apply_E, rhs, eps, K):
     return x
 
 
-def beta_step_woodbury_nid(X, y, lam, sig2, tau, z, delta, kmax=16):
+def beta_step_woodbury_nid(X, y, lam, sig2, tau, z, delta, kmax=16, lam_x=0.0):
     """The same conditional draw as beta_step_woodbury, with w = M^-1 (y/sig - v) solved by
-    the certified Chebyshev iteration when eps = tr(X D X') / sig2 admits K <= kmax
-    iterates, else by the Cholesky factor.  Returns (beta, K) (K = 0: the
-    Cholesky path)."""
+    the certified Chebyshev iteration when the bound eps >= lambda_max(X D X') / sig2 admits
+    K <= kmax iterates, else by the Cholesky factor.  eps: the trace, or
+    with lam_x >= lambda_max(X X') the least thresholded bound (nid_decide_from).  Returns
+    (beta, K) (K = 0: the Cholesky path)."""
     sig = np.sqrt(sig2)
     D = (tau * tau) / lam
     u = np.sqrt(D) * z
@@ -130,12 +131,43 @@ def beta_step_woodbury_nid(X, y, lam, sig2, tau, z, delta, kmax=16):
         cn = np.asarray(X.multiply(X).sum(axis=0)).ravel()
     else:
         cn = (X * X).sum(axis=0)
-    eps = float(np.sum(D * cn)) / sig2 * (1.0 + 1e-6)
-    K = cheb_iterations(eps, kmax)
+    eps, K = nid_decide_from(nid_shard_partials(D, cn, tau, lam_x), tau, sig2, kmax)
     if K == 0:
         return beta_step_woodbury(X, y, lam, sig2, tau, z, delta), 0
     w = woodbury_solve_cheb(lambda t: (X @ (D * (X.T @ t))) / sig2, y / sig - v, eps, K)
     return u + D * (X.T @ w) / sig, K
+
+
+NID_TS = 32  # bb_kernels.h kNidTS
+
+
+def nid_shard_partials(D, cn, tau, lam_shard):
+    """Restates bb_nid.hip k_nid_partials: a column shard's bound sums
+    [S_0 .. S_31, trace, Lambda_shard], S_k = sum_{D_j > T_k} D_j |x_j|^2 with the thresholds
+    T_k = tau^2 2^(40 - 2k) every rank knows; Lambda_shard >= lambda_max(X_r X_r') (+inf when
+    the shard has no certificate).  Summed over ranks by the exchange."""
+    t2 = tau * tau
+    v = D * cn
+    out = np.empty(NID_TS + 2)
+    for k in range(NID_TS):
+        out[k] = v[D > np.ldexp(t2, 40 - 2 * k)].sum()
+    out[NID_TS] = v.sum()
+    out[NID_TS + 1] = lam_shard if lam_shard > 0 else np.inf
+    return out
+
+
+def nid_decide_from(red, tau, sig2, kmax=16):
+    """Restates k_nid_decide_from: eps = min(trace, min_k S_k + T_k sum_r Lambda_r) / sig2
+    (times 1 + 1e-6), valid because sum_r lambda_max(X_r X_r') >= lambda_max(X X') (Weyl) and
+    E <= [sum_{D_j > T} D_j x_j x_j' + T X X'] / sig2; returns (eps, K)."""
+    t2 = tau * tau
+    lam = red[NID_TS + 1]
+    best = red[NID_TS]
+    if 0 < lam < np.inf:
+        for k in range(NID_TS):
+            best = min(best, red[k] + np.ldexp(t2, 40 - 2 * k) * lam)
+    eps = best / sig2 * (1.0 + 1e-6)
+    return eps, cheb_iterations(eps, kmax)
 
 
 def beta_step_ortho(Gdiag, c, lam, sig2, tau, z):
@@ -254,7 +286,8 @@ def bridge_regression_stable(y, X, nsamp, burn=500, alpha=0.5, sig2_shape=0.0, s
 
 
 def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stream,
-                           allreduce, hyper, know_tau=False, know_sig2=False):
+                           allreduce, hyper, know_tau=False, know_sig2=False, nid_lam=None,
+                           kmax=16, info=None):
     """One Gibbs sweep (tau, sig2, lambda, beta) on a column shard of X.
 
     The multi-GPU decomposition of SURVEY.md 8(e) restated on the CPU:
@@ -279,13 +312,28 @@ def woodbury_sweep_sharded(Xk, y, beta_k, j0, p, alpha, tau, sig2, t, seed, stre
     z = normals(beta_k.shape[0], seed, stream, t, KIND_BETA_Z, j0=j0)
     D = (tau * tau) / lam
     u = np.sqrt(D) * z
+    sig = np.sqrt(sig2)
+    delta = normals(n, seed, stream, t, KIND_DELTA)
+    if nid_lam is not None:
+        # the near-identity decision from the exchanged bound sums (bb_engine.cpp
+        # shard_solve), then either the Chebyshev solve with one exchange of X_k u_k and one
+        # per product, or the Gram exchange below
+        cn = (Xk * Xk).sum(axis=0)
+        eps, K = nid_decide_from(allreduce(nid_shard_partials(D, cn, tau, nid_lam)), tau, sig2,
+                                 kmax)
+        if info is not None:
+            info.append((eps, K))
+        if K > 0:
+            Xu = allreduce(Xk @ u)
+            rhs = y / sig - (Xu / sig + delta)
+            w = woodbury_solve_cheb(lambda d: allreduce(Xk @ (D * (Xk.T @ d))) / sig2, rhs, eps,
+                                    K)
+            return u + D * (Xk.T @ w) / sig, lam, tau, sig2
     Gk = (Xk * D) @ Xk.T
     buf = allreduce(np.concatenate([Gk.ravel(), Xk @ u]))
     G = buf[: n * n].reshape(n, n)
     Xu = buf[n * n:]
     # 3. replicated n x n solve, then the local beta update
-    sig = np.sqrt(sig2)
-    delta = normals(n, seed, stream, t, KIND_DELTA)
     v = Xu / sig + delta
     Mm = G / sig2
     Mm[np.diag_indices_from(Mm)] += 1.0

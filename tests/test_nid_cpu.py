@@ -38,16 +38,19 @@ def test_certified_bound_holds(eps_target):
     assert err < 1e-15 + 4e-16 * np.sqrt(n), (K, err)
 
 
+@pytest.mark.parametrize("certified", [False, True])
 @pytest.mark.parametrize("tau", [1e-7, 1e-4, 1e-3, 3e-3])
-def test_nid_draw_matches_cholesky_draw(tau):
+def test_nid_draw_matches_cholesky_draw(tau, certified):
     """Woodbury beta draws (n = 80, p = 400) at prior scales from the near-null regime up to
-    where the path hands over to the Cholesky factor: same draw to rounding."""
+    where the path hands over to the Cholesky factor: same draw to rounding, with the trace
+    bound alone or the thresholded bound (Lambda = 1.02 lambda_max(X X'))."""
     X, y, b = synthetic_problem(80, 400, seed=9)
     rng = np.random.default_rng(1)
     lam = rng.exponential(1.0, 400) * 2.0
     z, d = rng.standard_normal(400), rng.standard_normal(80)
     sig2 = float(np.var(y))
-    bn, K = gibbs.beta_step_woodbury_nid(X, y, lam, sig2, tau, z, d)
+    lam_x = 1.02 * np.linalg.eigvalsh(X @ X.T)[-1] if certified else 0.0
+    bn, K = gibbs.beta_step_woodbury_nid(X, y, lam, sig2, tau, z, d, lam_x=lam_x)
     bc = gibbs.beta_step_woodbury(X, y, lam, sig2, tau, z, d)
     assert np.linalg.norm(bn - bc) / np.linalg.norm(bc) < 1e-13, K
     if tau <= 1e-4:
@@ -64,3 +67,33 @@ def test_nid_draw_sparse():
     bn, K = gibbs.beta_step_woodbury_nid(X, y, lam, 50.0, 1e-4, z, d)
     bc = gibbs.beta_step_woodbury(X, y, lam, 50.0, 1e-4, z, d)
     assert K > 0 and np.linalg.norm(bn - bc) / np.linalg.norm(bc) < 1e-13
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("log_tau", [-6.0, -3.0, -1.0])
+def test_shard_bound_is_certified(world, log_tau):
+    """The column-sharded decision (bb_nid.hip k_nid_sums / k_nid_decide_from): the bound
+    from the summed shard sums and the summed shard certificates Lambda_r is an upper bound of
+    lambda_max(E), E = X D X' / sig2, and never above the trace bound."""
+    rng = np.random.default_rng(world * 10 + int(-log_tau))
+    n, p = 60, 400
+    X = rng.standard_normal((n, p)) * rng.uniform(0.2, 2.0, p)
+    tau, sig2 = 10.0 ** log_tau, 0.7
+    lam = rng.exponential(1.0, p) ** 3 + 1e-12  # heavy-tailed 1 / lambda
+    D = tau * tau / lam
+    E = (X * D) @ X.T / sig2
+    lmax = np.linalg.eigvalsh(E)[-1]
+    per = (p + world - 1) // world
+    red = np.zeros(gibbs.NID_TS + 2)
+    for r in range(world):
+        Xr = X[:, r * per:(r + 1) * per]
+        lam_r = 1.02 * np.linalg.eigvalsh(Xr @ Xr.T)[-1]
+        red += gibbs.nid_shard_partials(D[r * per:(r + 1) * per], (Xr * Xr).sum(axis=0), tau,
+                                        lam_r)
+    eps, K = gibbs.nid_decide_from(red, tau, sig2)
+    trace = float(np.sum(D * (X * X).sum(axis=0))) / sig2
+    assert lmax <= eps <= trace * (1 + 2e-6)
+    # an uncertified shard leaves the trace bound
+    red[gibbs.NID_TS + 1] = np.inf
+    eps_t, _ = gibbs.nid_decide_from(red, tau, sig2)
+    assert abs(eps_t - trace * (1 + 1e-6)) <= 1e-12 * trace

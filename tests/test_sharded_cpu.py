@@ -97,6 +97,61 @@ def test_sharded_sweep_equals_dense_woodbury_step():
     np.testing.assert_allclose(b1, b2, rtol=1e-11, atol=1e-13)
 
 
+def _nid_worker(rank, world, port, n, p, sweeps, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, y, _ = synthetic_problem(n, p, seed=6)
+    per = (p + world - 1) // world
+    j0, j1 = rank * per, min(p, (rank + 1) * per)
+    Xk = np.asfortranarray(X[:, j0:j1])
+    lam_k = 1.02 * np.linalg.eigvalsh(Xk @ Xk.T)[-1]
+
+    def allreduce(v):
+        t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64))
+        dist.all_reduce(t)
+        return t.numpy()
+
+    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
+    beta_k = np.full(j1 - j0, 1e-4)
+    tau, sig2 = 1e-3, 1.0
+    hist, info = [], []
+    for t in range(1, sweeps + 1):
+        beta_k, _, tau, sig2 = gibbs.woodbury_sweep_sharded(
+            Xk, y, beta_k, j0, p, 0.5, tau, sig2, t, 11, 0, allreduce, hyper, know_tau=True,
+            nid_lam=lam_k, info=info)
+        full = [torch.zeros(per, dtype=torch.float64) for _ in range(world)]
+        pad = np.zeros(per)
+        pad[:j1 - j0] = beta_k
+        dist.all_gather(full, torch.from_numpy(pad))
+        hist.append(np.concatenate([f.numpy() for f in full])[:p])
+    if rank == 0:
+        np.savez(out_path, beta=np.array(hist), K=np.array([k for _, k in info]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_near_identity_matches_unsharded(tmp_path, world):
+    """The shards' near-identity solve (the exchanged bound sums decide the path; one exchange
+    of X_k u_k and one per product E d) against the unsharded Cholesky draw, from a
+    near-null state (tau = 1e-3 known): every sweep takes the Chebyshev path."""
+    n, p, sweeps = 40, 150, 4
+    out = str(tmp_path / "nid.npz")
+    mp.spawn(_nid_worker, args=(world, _free_port(), n, p, sweeps, out), nprocs=world, join=True)
+    got = np.load(out)
+    assert np.all(got["K"] > 0), got["K"]
+    X, y, _ = synthetic_problem(n, p, seed=6)
+    hyper = dict(nu_shape=2.0, nu_rate=2.0, sig2_shape=0.0, sig2_scale=0.0)
+    beta, tau, sig2 = np.full(p, 1e-4), 1e-3, 1.0
+    for t in range(1, sweeps + 1):
+        beta, _, tau, sig2 = gibbs.woodbury_sweep_sharded(
+            np.asfortranarray(X), y, beta, 0, p, 0.5, tau, sig2, t, 11, 0, lambda v: v, hyper,
+            know_tau=True)
+        d = np.linalg.norm(got["beta"][t - 1] - beta) / np.linalg.norm(beta)
+        assert d < 1e-11, (t, d)
+
+
 def _alpha_worker(rank, world, port, p, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
