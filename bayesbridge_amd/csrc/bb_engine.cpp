@@ -468,9 +468,8 @@ struct bb_engine {
 
     // decision kernel of a Woodbury sweep (eps is tracked even when only the Gram + Cholesky
     // path is launched, so the hint follows the chain back into the near-identity regime)
-    int nid_begin() {
+    int nid_begin(int kl) {
         if (!nid_enabled()) return 0;
-        const int kl = nid_launch_count();
         mark(PH_NID);
         const long q = nid_seq++;
         launch_nid_sums(stream, D, cn, p_loc, sc, nid, kl, kl > 0, 1, nid_wg, nid_red,
@@ -489,8 +488,8 @@ struct bb_engine {
             launch_cheb_init(stream, nid_xu, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid, w,
                              ch_r, ch_d);
         else
-            launch_cheb_init(stream, nid_xu, ea_parts, n, n_pad, y, sc, cfg.seed, cfg.stream,
-                             t, nid, w, ch_r, ch_d);
+            launch_cheb_init(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n, n_pad, y, sc,
+                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d);
         for (int j = 1; j < kl; ++j) {
             mark(PH_EAPPLY);
             if (method == 5)
@@ -528,8 +527,8 @@ struct bb_engine {
         if (method == 5) {
             launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid, nid_sum);
         } else {
-            launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
-            launch_part_sum(stream, nid_xu, ea_parts, n_pad, nid_sum);
+            if (!xu_fused) launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
+            launch_part_sum(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n_pad, nid_sum);
         }
     }
     void nidx_init(uint64_t t) {
@@ -651,18 +650,28 @@ struct bb_engine {
         double *trl = slot_ptr(tr_lam, slot, p_loc);
         mark(PH_LAMBDA);
         if (method == 5 || method == 2) {
-            launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed, cfg.stream,
-                          t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            const bool sync = nid_sync();
+            const int kl = (!sync && nid_enabled()) ? nid_launch_count() : 0;
+            // a sweep that may take the Chebyshev path draws lambda and forms the X u partials
+            // in one launch (k_lambda_xu, dense)
+            xu_fused = 0;
+            if (method == 2 && (sync || kl > 0))
+                xu_fused = launch_lambda_xu(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc,
+                                            cfg.seed, cfg.stream, t, lam, D, u, trl, err, X,
+                                            n_pad, n_pad, nid_xu);
+            if (!xu_fused)
+                launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed,
+                              cfg.stream, t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
             nid_only = false;
-            if (nid_sync()) {
+            if (sync) {
                 // a shard: the bound sums now, the path after their exchange (shard_solve)
                 nid_kl = 0;
                 nidx_partials();
                 return;
             }
-            nid_kl = nid_begin();
+            nid_kl = nid_begin(kl);
             wb_gram(nid_kl ? &nid->mode : nullptr);
-            if (nid_kl) {
+            if (nid_kl && !xu_fused) {
                 mark(PH_NID);
                 if (method == 5)
                     launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid,
@@ -802,6 +811,7 @@ struct bb_engine {
     const std::atomic<bool> *stop = nullptr;
     int fail_at = -1;
     int nid_kl = 0;  // Chebyshev iterations launched for the sweep being enqueued
+    int xu_fused = 0;  // X u partials formed by this sweep's lambda launch (k_lambda_xu), or 0
 
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
     void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
@@ -1190,7 +1200,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
                 launch_colnorm2(e->stream, e->X, n_pad, n_pad, c.p_local, e->cn);
                 e->ea_parts = eapply_parts(c.p_local, n_pad);
                 e->ea_part = dalloc<double>((size_t)e->ea_parts * n_pad, o);
-                e->nid_xu = dalloc<double>((size_t)e->ea_parts * n_pad, o);
+                const int xp = std::max(e->ea_parts, lambda_xu_parts(c.p_local, p_pad, n_pad));
+                e->nid_xu = dalloc<double>((size_t)xp * n_pad, o);
             }
             e->nid = dalloc<NidState>(1, o);
             e->ch_r = dalloc<double>(n_pad, o);
@@ -3326,6 +3337,11 @@ int bb_set_tuning(int key, int value) {
         case 6: {
             const int old = g_nid_kmax;
             if (value >= 0) g_nid_kmax = value > 64 ? 64 : value;
+            return old;
+        }
+        case 7: {
+            const int old = g_lam_xu;
+            if (value >= 0) g_lam_xu = value ? 1 : 0;
             return old;
         }
         default: return -1;

@@ -135,6 +135,16 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
                    int group, double *lam, double *D, double *u, double *lam_trace,
                    uint32_t *err);
 
+// lambda (LAMBDA_WOODBURY) fused with the X u pass (dense, bb_kernels.hip k_lambda_xu):
+// returns the partial n-vectors written to xu_part (xu_part holds lambda_xu_parts of them),
+// 0 when the shape does not take the fused launch (nothing launched)
+int lambda_xu_parts(int p_loc, int p_pad, int n_pad);
+int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                     const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
+                     double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
+                     int ldx, int n_pad, double *xu_part);
+extern int g_lam_xu;
+
 void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
                            uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,
                            double *lam, uint32_t *err);

@@ -407,6 +407,121 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
     }
 }
 
+// lambda fused with the X u pass of the near-identity solve (dense Woodbury, DESIGN.md
+// s6.5): the draws are VALU-bound and X u is HBM-bound, and u_j is known as soon as the
+// draw of column j is, so a workgroup draws the C = 256 / L coefficients of a column chunk,
+// then streams those C columns of X into its X u partial (rows t + 256 m of the chunk held
+// by thread t, accumulated in LDS across chunks), while the other workgroups on the CU are
+// drawing.  Chunks g, g + G, ... per workgroup (G <= 3 per CU, the sampler's occupancy);
+// each workgroup writes one partial n-vector, summed in workgroup order by k_cheb_init, so
+// the result is bitwise reproducible.  The draws are those of k_lambda_spec<L>.
+int g_lam_xu = 1;  // bb_set_tuning key 7: 0 = separate lambda and X u launches (A/B)
+template <int L, int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
+                                                   uint64_t j0, const DevScalars *sc, Key key,
+                                                   uint64_t t, double *lam, double *D,
+                                                   double *u, double *lam_trace, uint32_t *err,
+                                                   const double *__restrict__ X, int ldx,
+                                                   int n_pad, int nchunk,
+                                                   double *__restrict__ xu_part) {
+    constexpr int C = 256 / L;
+    constexpr int CQ = NR >= 16 ? 1 : 16 / NR;  // columns in flight: 16 loads per thread
+    __shared__ double us[C];
+    __shared__ double accs[NR * 256];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int m = 0; m < NR; ++m) accs[m * 256 + tid] = 0.0;
+    const double tau = sc->tau;
+    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int i = ch * C + tid / L;  // group-uniform
+        const bool active = i < p_loc;
+        const double b = active ? beta[i] : 0.0;
+        const double x = stable_spec_draw<L, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
+                                                key, t, j0 + (uint64_t)i, err);
+        if ((tid % L) == 0) {
+            double uv = 0.0;
+            if (active) {
+                const double l = 2 * x;
+                lam[i] = l;
+                if (lam_trace) lam_trace[i] = l;
+                const double d = (tau * tau) / l;
+                D[i] = d;
+                uv = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
+                u[i] = uv;
+            } else if (i < p_pad) {
+                lam[i] = 1.0;
+                D[i] = 0.0;
+                u[i] = 0.0;
+            }
+            us[tid / L] = uv;
+        }
+        __syncthreads();  // the chunk's u
+        double a[NR];
+#pragma unroll
+        for (int m = 0; m < NR; ++m) a[m] = accs[m * 256 + tid];
+#pragma unroll 1
+        for (int c = 0; c < C; c += CQ) {
+            double xv[CQ][NR];
+#pragma unroll
+            for (int q = 0; q < CQ; ++q) {
+                const int col = ch * C + c + q;
+                const bool ok = col < p_loc;
+                const double *xc = X + (size_t)col * ldx;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {
+                    const int row = tid + 256 * m;
+                    xv[q][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(xc + row) : 0.0;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CQ; ++q) {
+                const double f = us[c + q];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] = __builtin_fma(xv[q][m], f, a[m]);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < NR; ++m) accs[m * 256 + tid] = a[m];
+        __syncthreads();  // us is rewritten by the next chunk
+    }
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+        const int row = tid + 256 * m;
+        if (row < n_pad) xu_part[(size_t)blockIdx.x * n_pad + row] = accs[m * 256 + tid];
+    }
+}
+
+// partial n-vectors of the fused launch for this shape, 0 if the shape does not take it
+int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
+    if (p_loc > kLamSpecMax || n_pad > 4096) return 0;
+    const int L = spec_lanes(p_loc);
+    if (L != 8 && L != 16) return 0;
+    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
+    return std::min(nchunk, 3 * device_cus_lam());
+}
+
+int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                     const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
+                     double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
+                     int ldx, int n_pad, double *xu_part) {
+    const int G = (g_lam_xu && !g_lam_lanes) ? lambda_xu_parts(p_loc, p_pad, n_pad) : 0;
+    if (!G) return 0;
+    const Key key{k0, k1};
+    const int L = spec_lanes(p_loc);
+    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
+    const int nr = (n_pad + 255) / 256;
+#define BB_LXU(LL, NN)                                                                        \
+    k_lambda_xu<LL, NN><<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u,      \
+                                          lam_trace, err, X, ldx, n_pad, nchunk, xu_part)
+    if (L == 8) {
+        if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
+    } else {
+        if (nr <= 4) BB_LXU(16, 4); else if (nr <= 8) BB_LXU(16, 8); else BB_LXU(16, 16);
+    }
+#undef BB_LXU
+    return G;
+}
+
 bool launch_lambda_pg(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                       const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, int group,
                       double *lam, double *lam_trace, const double *psi, int n, int n_pad,

@@ -363,7 +363,7 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
 // draw is the same as stable_group_draw's.  About 1 in 8 draws needs a second round at
 // I = 8, O = 4 (inner acceptance ~0.3, outer ~0.7 at alpha = 0.25).
 template <int L, int I>
-__device__ inline double stable_spec_draw(bool active, double h, double alpha, double V0, Key key,
+__device__ __forceinline__ double stable_spec_draw(bool active, double h, double alpha, double V0, Key key,
                                           uint64_t t, uint64_t j, uint32_t *err) {
     static_assert(L <= 64 && (L & (L - 1)) == 0 && L % I == 0 && I < 64, "group shape");
     constexpr int O = L / I;

@@ -166,3 +166,39 @@ def test_nid_disabled_for_shards(gpu_lib):
                                   stream=0), np.asfortranarray(X[:, :450]), y)
     assert e.nid_stats()["mode"] == -1
     e.close()
+
+
+@pytest.mark.parametrize("n,p", [(200, 2400), (700, 6000), (2000, 50000)])
+def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
+    """The fused lambda + X u launch (k_lambda_xu, bb_set_tuning key 7 = 1, the default)
+    against separate lambda and X u launches (key 7 = 0) on near-null states: the same
+    lambda bits (the same draws), beta to rounding (X u summed in another order), both on
+    the Chebyshev path.  (2000, 50000) is C3's shape."""
+    import bench
+    bb = gpu_lib
+    if n == 2000:
+        X = bench.make_columns(n, 0, p)
+        y, _ = bench.make_problem_y(n, p)
+    else:
+        X, y, _ = synthetic_problem(n, p, seed=n)
+    rng = np.random.default_rng(11)
+    beta = 1e-6 * rng.standard_normal(p)
+    out = []
+    for fused in (1, 0):
+        old = bb.set_tuning(7, fused)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            e.set_state(beta, 1e-6, 1.0, 0.5)
+            e.run(7, 2)
+            e.sync()
+            out.append((e.state(), e.nid_stats()))
+            assert e.error_flags() == 0
+            e.close()
+        finally:
+            bb.set_tuning(7, old)
+    (a, sa), (b, sb) = out
+    assert sa["cheb_sweeps"] == 2 and sb["cheb_sweeps"] == 2, (sa, sb)
+    assert rel_err(a["beta"], b["beta"]) < 1e-12
+    assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
+    assert abs(a["tau"] - b["tau"]) <= 1e-12 * b["tau"]
