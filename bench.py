@@ -250,6 +250,30 @@ def pmc_mfma(n, p, world, kernel, gram):
     return best
 
 
+VALU_PEAK_GINST = 1024 * 2.4e9 / 4 / 1e9  # wave64 VALU instructions per second (1024 SIMDs)
+
+
+def pmc_valu(n, p, world, kernel):
+    """VALU evidence for `kernel` at this workload from the newest committed
+    profiles/rNN_pmc_valu.json (tools/pmc_valu.sh: SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU,
+    GRBM_GUI_ACTIVE in separate rocprofv3 --pmc passes; tools/pmc_valu_summary.py), or None."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for cfg in d.get("configs", {}).values():
+            if cfg.get("n") != n or cfg.get("p") != p or world != 1:
+                continue
+            for k, v in cfg.get("kernels", {}).items():
+                if k.startswith(kernel) and "SQ_INSTS_VALU" in v:
+                    best = dict(v, kernel=k, source=os.path.relpath(f, ROOT))
+    return best
+
+
 def rel_l2(a, b):
     a, b = np.asarray(a), np.asarray(b)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
@@ -270,7 +294,8 @@ def roofline_for(phase, ms, ctx, traffic_world):
     n, p, p_loc = ctx["n"], ctx["p"], ctx["p_loc"]
     gram_mode = ctx["gram_mode"]
     logit, sparse = kind == "logit", kind == "sparse"
-    sec = ms * 1e-3
+    # (a phase whose launches all returned at once can time as 0: no rate then)
+    sec = max(ms, 1e-9) * 1e-3
     out = {"phase": phase, "kernel_ms_avg": ms}
     if phase == "gram":
         n_pad = -(-n // 128) * 128
@@ -349,9 +374,50 @@ def roofline_for(phase, ms, ctx, traffic_world):
         out.update(bound="hbm", kernel=kname, achieved=byts * pf / sec / 1e9, peak=8000.0,
                    unit="GB/s", algorithmic_bytes_per_launch=byts * pf,
                    bytes_per_pass=byts, passes_per_launch=pf)
+    elif phase == "lambda":
+        # the tilted-stable draws: VALU-bound arithmetic with a rejection tail.
+        # achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, committed
+        # profile of this workload) / the live average launch time, against one wave64 VALU
+        # instruction per 4 cycles on each of the 1024 SIMDs at 2.4 GHz.  The fused launch
+        # (k_lambda_xu, dense near-identity sweeps) also streams X for X u: its HBM rate too.
+        fused = (not sparse and not logit and ctx.get("nid_cheb") and bb.set_tuning(7, -1) == 1
+                 and n <= 4096)
+        if fused:
+            kfull = "bb::k_lambda_xu"
+        elif p_loc > 50000:
+            kfull = "bb::k_lambda_cb"
+        else:
+            kfull = "bb::k_lambda_spec"
+        v = pmc_valu(n, p, traffic_world, kfull)
+        ginst = (v["SQ_INSTS_VALU"] / sec / 1e9) if v else None
+        out.update(bound="valu", kernel=kfull, achieved=ginst, peak=VALU_PEAK_GINST,
+                   unit="G VALU wave-instructions/s", draws_per_launch=p_loc,
+                   draws_per_s=p_loc / sec,
+                   valu_insts_per_launch=v["SQ_INSTS_VALU"] if v else None,
+                   valu_busy_frac=v.get("valu_busy_frac") if v else None,
+                   valu_source=v["source"] if v else None)
+        if fused:
+            n_pad = -(-n // 128) * 128
+            byts = 8.0 * n * p_loc + 32.0 * p_loc
+            out["hbm"] = {"algorithmic_bytes_per_launch": byts, "achieved_GBps": byts / sec / 1e9,
+                          "peak_GBps": 8000.0, "frac": byts / sec / 1e9 / 8000.0,
+                          "note": "X read once for X u (8 B per element) + beta read and "
+                                  "lambda, D, u written (8 B each per coefficient)"}
+    elif phase == "beta" and not logit:
+        # the Woodbury beta update: one read of X for X' w (dense: fused with the
+        # next sweep's X beta partials, k_beta_wb_xb; sparse: the CSC non-zeros), D, u read and
+        # beta written (8 B each per coefficient)
+        if sparse:
+            si = eng.sparse_info()
+            byts = 12.0 * si["nnz"] + 32.0 * p_loc
+            kfull = "bb::k_sp_beta"
+        else:
+            byts = 8.0 * n * p_loc + 32.0 * p_loc
+            kfull = "bb::k_beta_wb"
+        out.update(bound="hbm", kernel=kfull, achieved=byts / sec / 1e9, peak=8000.0,
+                   unit="GB/s", algorithmic_bytes_per_launch=byts)
     else:
-        kfull = {"lambda": "bb::k_lambda", "reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve",
-                 "beta": "bb::k_beta"}[phase]
+        kfull = {"reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve", "beta": "bb::k_beta"}[phase]
         out.update(bound="latency", kernel=kfull, achieved=None, peak=None, unit=None)
     out["frac"] = (out["achieved"] / out["peak"]) if out.get("peak") else None
     tr = pmc_traffic(n, p, traffic_world, kfull)
@@ -395,6 +461,9 @@ def main():
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
                     help="dense Woodbury Gram: fp64 MFMA or Ozaki-II int8 MFMA (default: the "
                          "library default, Ozaki)")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
+                    help="bb_set_tuning(KEY, VALUE) before the engines are built (A/B runs; "
+                         "include/bayesbridge.h lists the keys)")
     args = ap.parse_args()
     wn, wp, walpha, kind = WORKLOADS[args.workload]
     n = args.rows or wn
@@ -472,6 +541,9 @@ def run_chain(args, n, p, alpha, kind, mode):
     devices = list(range(world)) if mode == "group" else [local_rank]
     torch.cuda.set_device(devices[0])
     bb.set_verbose(0)
+    for kv in args.tuning:
+        k, v = kv.split("=")
+        bb.set_tuning(int(k), int(v))
     gram_mode = None if args.gram is None else (bb.GRAM_OZAKI if args.gram == "ozaki"
                                                 else bb.GRAM_FP64)
     shard_world = 1 if mode == "single" else world
@@ -598,7 +670,7 @@ def run_chain(args, n, p, alpha, kind, mode):
                  ("ozaki-II int8 (fp64-accurate)" if eng.gram_mode() == bb.GRAM_OZAKI
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
-               gram_name=gram_name, pass_frac=ctx_pass_frac)
+               gram_name=gram_name, pass_frac=ctx_pass_frac, nid_cheb=nid_phase_cheb)
     fitted = None
     if mode == "single" and not logit and not args.no_fitted:
         fitted = fitted_regime(bb, eng, kind, n, p, alpha, t)

@@ -157,14 +157,20 @@ def test_nid_lambda_bound_certified(gpu_lib, kind):
     e.close()
 
 
-def test_nid_disabled_for_shards(gpu_lib):
-    """Column shards (world > 1) exchange the Gram: no near-identity path (mode -1)."""
+def test_nid_shard_certifies_its_columns(gpu_lib):
+    """A column shard (world > 1) holds the near-identity path (round 4; the sweeps are in
+    tests/test_shard_nid_gpu.py): its Lambda certifies lambda_max(X_k X_k') of ITS columns
+    from above (the decision sums the shards' certificates)."""
     bb = gpu_lib
     n, p = 100, 900
     X, y, _ = synthetic_problem(n, p, seed=13)
+    Xk = np.asfortranarray(X[:, :450])
     e = bb.Engine(bb.EngineConfig(n=n, p=p, p_local=450, j0=0, rank=0, world=2, seed=SEED,
-                                  stream=0), np.asfortranarray(X[:, :450]), y)
-    assert e.nid_stats()["mode"] == -1
+                                  stream=0), Xk, y)
+    st = e.nid_stats()
+    lmax = np.linalg.eigvalsh(Xk @ Xk.T)[-1]
+    assert st["mode"] >= 0
+    assert lmax <= st["lambda_x"] <= 2.0 * lmax, (st, lmax)
     e.close()
 
 
