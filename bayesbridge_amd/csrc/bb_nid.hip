@@ -136,27 +136,43 @@ __global__ __launch_bounds__(kNidSumWG) void k_nid_sums(const double *__restrict
     }
 }
 
-// red = the G workgroups' sums (in workgroup order) and Lambda; decide: the unsharded
-// decision at once
-__global__ __launch_bounds__(64) void k_nid_reduce(const double *__restrict__ wg_part, int G,
-                                                   const DevScalars *sc, int k_launched,
-                                                   int allow, int decide, NidState *nid,
-                                                   double *__restrict__ red, double *eps_host) {
+// red = the G workgroups' sums and Lambda (thread (k, q) adds workgroups q, q + 8, ... of
+// sum k, then the eight in order: a fixed order); decide: the unsharded decision at once
+constexpr int kNidRedQ = 8;
+__global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict__ wg_part, int G,
+                                                       const DevScalars *sc, int k_launched,
+                                                       int allow, int decide, NidState *nid,
+                                                       double *__restrict__ red,
+                                                       double *eps_host) {
+    __shared__ double pq[kNidRedQ][kNidTS + 1];
     __shared__ double r[kNidTS + 2];
-    if (threadIdx.x <= kNidTS) {
-        double s = 0.0;
-        for (int b = 0; b < G; ++b) s += wg_part[(size_t)b * (kNidTS + 1) + threadIdx.x];
-        r[threadIdx.x] = s;
-        red[threadIdx.x] = s;
-    }
-    if (threadIdx.x == kNidTS + 1) {
-        const double lam = nid->lambda_x;
-        const double v = lam > 0.0 ? lam : HUGE_VAL;
-        r[threadIdx.x] = v;
-        red[threadIdx.x] = v;
+    const int t = threadIdx.x;
+    if (t < kNidRedQ * (kNidTS + 1)) {
+        const int k = t % (kNidTS + 1), q = t / (kNidTS + 1);
+        double a[4] = {0.0, 0.0, 0.0, 0.0};
+        int b = q;
+        for (; b + 3 * kNidRedQ < G; b += 4 * kNidRedQ)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] += wg_part[(size_t)(b + u * kNidRedQ) * (kNidTS + 1) + k];
+        for (; b < G; b += kNidRedQ) a[0] += wg_part[(size_t)b * (kNidTS + 1) + k];
+        pq[q][k] = (a[0] + a[1]) + (a[2] + a[3]);
     }
     __syncthreads();
-    if (decide && threadIdx.x == 0) nid_finish(r, sc, k_launched, allow, nid, eps_host, nullptr);
+    if (t <= kNidTS) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < kNidRedQ; ++q) s += pq[q][t];
+        r[t] = s;
+        red[t] = s;
+    }
+    if (t == kNidTS + 1) {
+        const double lam = nid->lambda_x;
+        const double v = lam > 0.0 ? lam : HUGE_VAL;
+        r[t] = v;
+        red[t] = v;
+    }
+    __syncthreads();
+    if (decide && t == 0) nid_finish(r, sc, k_launched, allow, nid, eps_host, nullptr);
 }
 
 __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
@@ -167,16 +183,25 @@ __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict
 }
 
 // Row sums of the nparts partial n-vectors for rows [64 b, 64 b + 64): wave w adds partials
-// w, w + 8, ... for its lane's row, then the eight wave sums are added in order (fixed order:
+// w, w + 16, ... for its lane's row into eight independent accumulators (eight loads in
+// flight per lane: the partials were written by every XCD, so each load is an L2 miss), the
+// accumulators are added pairwise, then the sixteen wave sums in order (a fixed order:
 // bitwise reproducible).  Returns the sum on wave 0 (lane = row offset).
-constexpr int kRedWaves = 8;
+constexpr int kRedWaves = 16;
 __device__ __forceinline__ double part_rowsum(const double *__restrict__ part, int nparts,
                                               int n_pad, int row, double (*red)[64]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double a = 0.0;
-    if (row < n_pad)
-        for (int q = wid; q < nparts; q += kRedWaves) a += part[(size_t)q * n_pad + row];
-    red[wid][lane] = a;
+    double a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = 0.0;
+    if (row < n_pad) {
+        int q = wid;
+        for (; q + 7 * kRedWaves < nparts; q += 8 * kRedWaves)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] += part[(size_t)(q + u * kRedWaves) * n_pad + row];
+        for (; q < nparts; q += kRedWaves) a[0] += part[(size_t)q * n_pad + row];
+    }
+    red[wid][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
     double s = 0.0;
     if (wid == 0)
@@ -405,7 +430,7 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
                      double *wg_part, double *red, double *eps_host) {
     const int G = nid_sum_groups(p_loc);
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
-    k_nid_reduce<<<1, 64, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
+    k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
                                   eps_host);
 }
 
