@@ -273,6 +273,9 @@ enum Phase {
 // Chebyshev iterations the near-identity solve may take per sweep (bb_set_tuning key 6; 0
 // turns the path off: every sweep forms the Gram and factors it)
 int g_nid_kmax = 16;
+// bb_set_tuning key 8: an unsharded engine decides like a shard (the host waits for each
+// sweep's decision, then launches only that path) instead of launching both paths gated
+int g_nid_sync = 0;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -416,7 +419,10 @@ struct bb_engine {
         return nid != nullptr && (cfg.world == 1 || comm != nullptr || group_member) &&
                std::min(g_nid_kmax, nid_kmax) > 0;
     }
-    bool nid_sync() const { return cfg.world > 1 && nid_enabled(); }
+    bool nid_sync() const { return (cfg.world > 1 || g_nid_sync) && nid_enabled(); }
+    // the exchanged vectors are single n-vectors on a shard; an unsharded engine in the
+    // synchronous mode reads the partials directly
+    bool nid_vec() const { return cfg.world > 1 || method == 5; }
 
     // Cost model of the two exact solves, from the round-3/4 measured rates:
     // a Chebyshev solve of K iterates reads X K times (the X u pass and K - 1 products, ~6 TB/s
@@ -528,12 +534,17 @@ struct bb_engine {
             launch_sp_nid_xu(stream, spd.rowptr, spd.colidx, spd.rval, n_pad, u, nid, nid_sum);
         } else {
             if (!xu_fused) launch_nid_xu(stream, X, n_pad, u, p_loc, n_pad, nid, nid_xu);
-            launch_part_sum(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n_pad, nid_sum);
+            if (nid_vec())
+                launch_part_sum(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n_pad, nid_sum);
         }
     }
     void nidx_init(uint64_t t) {
-        launch_cheb_init(stream, nid_sum, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid, w,
-                         ch_r, ch_d);
+        if (nid_vec())
+            launch_cheb_init(stream, nid_sum, 1, n, n_pad, y, sc, cfg.seed, cfg.stream, t, nid,
+                             w, ch_r, ch_d);
+        else
+            launch_cheb_init(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n, n_pad, y, sc,
+                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d);
     }
     // this shard's E d of step j into nid_sum (exchanged: n_pad)
     void nidx_eapply(int j) {
@@ -543,12 +554,15 @@ struct bb_engine {
                              spd.rval, p_loc, n_pad, D, ch_d, nid, j, sp_s, nid_sum);
         } else {
             launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part);
-            launch_part_sum(stream, ea_part, ea_parts, n_pad, nid_sum);
+            if (nid_vec()) launch_part_sum(stream, ea_part, ea_parts, n_pad, nid_sum);
         }
     }
     void nidx_step(int j) {
         mark(PH_NID);
-        launch_cheb_step(stream, nid_sum, 1, n_pad, sc, nid, j, w, ch_r, ch_d);
+        if (nid_vec())
+            launch_cheb_step(stream, nid_sum, 1, n_pad, sc, nid, j, w, ch_r, ch_d);
+        else
+            launch_cheb_step(stream, ea_part, ea_parts, n_pad, sc, nid, j, w, ch_r, ch_d);
     }
     // a shard's Woodbury sweep between phase b and phase c, through exchange(buf, count)
     template <class Exchange>
@@ -1208,7 +1222,7 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->ch_d = dalloc<double>(n_pad, o);
             e->nid_red = dalloc<double>(bb_engine::kNidRed, o);
             e->nid_wg = dalloc<double>((size_t)nid_sum_groups(c.p_local) * (kNidTS + 1), o);
-            if (c.world > 1) e->nid_sum = dalloc<double>(n_pad, o);
+            e->nid_sum = dalloc<double>(n_pad, o);
             // the hint ring, then a shard's [eps, mode] of the sweep being decided
             const int nh = bb_engine::kNidRing + 2;
             HIPCHECK(hipHostMalloc((void **)&e->eps_host, nh * sizeof(double), hipHostMallocMapped));
@@ -3342,6 +3356,11 @@ int bb_set_tuning(int key, int value) {
         case 7: {
             const int old = g_lam_xu;
             if (value >= 0) g_lam_xu = value ? 1 : 0;
+            return old;
+        }
+        case 8: {
+            const int old = g_nid_sync;
+            if (value >= 0) g_nid_sync = value ? 1 : 0;
             return old;
         }
         default: return -1;

@@ -419,7 +419,8 @@ def roofline_for(phase, ms, ctx, traffic_world):
     else:
         kfull = {"reduce": "bb::k_oz_crt", "solve": "bb::k_bsolve", "beta": "bb::k_beta"}[phase]
         out.update(bound="latency", kernel=kfull, achieved=None, peak=None, unit=None)
-    out["frac"] = (out["achieved"] / out["peak"]) if out.get("peak") else None
+    out["frac"] = (out["achieved"] / out["peak"]) if (out.get("peak") and
+                                                       out.get("achieved") is not None) else None
     tr = pmc_traffic(n, p, traffic_world, kfull)
     if out.get("bound") == "mfma":
         mf = pmc_mfma(n, p, traffic_world, kfull, ctx.get("gram_name"))

@@ -74,3 +74,43 @@ def test_dominant_phase_roofline_formulas():
     r = bench.roofline_for("chol", 0.25, lg, 1)
     assert r["latency_model"]["system"] == 1000
     assert r["latency_model"]["system_padded"] == 1024
+
+
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("kind,n,p", [("dense", 2000, 50000), ("dense", 1000, 5000),
+                                      ("sparse", 5000, 200000)])
+def test_lambda_and_beta_roofline_entries(world, kind, n, p):
+    """The lambda entry (bound "valu": VALU wave-instructions from a committed PMC profile
+    over the live time; no profile -- another shape, or a shard -- gives achieved = frac =
+    None, never an error) and the dense beta entry (one read of X)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class FakeBB:
+        GRAM_OZAKI, GRAM_FP64 = 1, 0
+
+        @staticmethod
+        def set_tuning(key, value):
+            return 1
+
+    class FakeEng:
+        @staticmethod
+        def sparse_info():
+            return dict(nnz=n * p // 100, pairs=0, col_mode=1, max_row=0)
+
+    p_loc = p // world
+    ctx = dict(bb=FakeBB, eng=FakeEng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=1,
+               nid_cheb=True)
+    r = bench.roofline_for("lambda", 0.24, ctx, world)
+    assert r["bound"] == "valu" and r["peak"] == bench.VALU_PEAK_GINST
+    assert abs(r["draws_per_s"] - p_loc / 0.24e-3) < 1e-6 * p_loc / 0.24e-3
+    if r["achieved"] is None:
+        assert r["frac"] is None
+    else:
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    if kind == "dense" and world == 1 and n == 2000:
+        assert r["kernel"] == "bb::k_lambda_xu"
+        assert r["valu_insts_per_launch"] > 0 and 0 < r["frac"] < 1  # profiles/r04_pmc_valu.json
+        assert abs(r["hbm"]["achieved_GBps"] - (8.0 * n * p + 32.0 * p) / 0.24e-3 / 1e9) < 1e-6
+    b = bench.roofline_for("beta", 0.135, ctx, world)
+    assert b["bound"] == "hbm" and b["frac"] is not None

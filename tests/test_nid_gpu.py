@@ -208,3 +208,31 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
     assert rel_err(a["beta"], b["beta"]) < 1e-12
     assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
     assert abs(a["tau"] - b["tau"]) <= 1e-12 * b["tau"]
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
+    """bb_set_tuning key 8 = 1: the unsharded engine waits for each sweep's decision and
+    launches that path only (the shards' protocol) instead of launching both paths gated.
+    The decision is the same least K, so from the reference start the two modes draw the
+    same chain bit for bit (the same kernels on the same partials)."""
+    bb = gpu_lib
+    n, p = 300, 4000
+    X, y, _ = _design(kind, n, p, 51)
+    out = []
+    for mode in (0, 1):
+        old = bb.set_tuning(8, mode)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            e.run(1, 12)
+            e.sync()
+            out.append((e.state(), e.nid_stats()))
+            assert e.error_flags() == 0
+            e.close()
+        finally:
+            bb.set_tuning(8, old)
+    (a, sa), (b, sb) = out
+    assert sa["cheb_sweeps"] == sb["cheb_sweeps"] >= 10, (sa, sb)
+    assert np.array_equal(a["beta"], b["beta"]) and np.array_equal(a["lambda"], b["lambda"])
+    assert a["tau"] == b["tau"] and a["sig2"] == b["sig2"]
