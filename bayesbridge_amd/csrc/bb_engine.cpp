@@ -274,8 +274,11 @@ enum Phase {
 // turns the path off: every sweep forms the Gram and factors it)
 int g_nid_kmax = 16;
 // bb_set_tuning key 8: an unsharded engine decides like a shard (the host waits for each
-// sweep's decision, then launches only that path) instead of launching both paths gated
-int g_nid_sync = 0;
+// sweep's decision, then launches only that path: 1, the default) or launches both paths
+// gated with the hint of nid_launch_count (0).  Measured at the driver's settings (round 4,
+// gpurun_out/r04f_*): C3 1781 against 1746-1749 sweeps/s, C2 5840 against 5519, C5 1672
+// against 1636 -- the host's wake-up and first launch cost less than the gated no-ops.
+int g_nid_sync = 1;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -3355,7 +3358,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 7: {
             const int old = g_lam_xu;
-            if (value >= 0) g_lam_xu = value ? 1 : 0;
+            if (value >= 0) g_lam_xu = value > 2 ? 2 : value;
             return old;
         }
         case 8: {

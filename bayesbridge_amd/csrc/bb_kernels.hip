@@ -317,13 +317,15 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
     if (have) start();
     for (long iter = 0; iter < (1l << 26); ++iter) {
         bool acc = false;
-        double U = 0.0, z = 0.0, Z = 0.0;
-        if (have && draw) acc = stable_inner<true>(sp, key, t, j0 + (uint64_t)j, o, ib + (uint64_t)g, U, z, Z);
+        double U = 0.0, z = 0.0, Z = 0.0, B = 1.0;
+        if (have && draw)
+            acc = stable_inner<true>(sp, key, t, j0 + (uint64_t)j, o, ib + (uint64_t)g, U, z, Z, B);
         const uint64_t m = (__ballot(acc) >> gbase) & gmask;
         const int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
         const double Uw = __shfl(U, gbase + win, 64);
         const double zw = __shfl(z, gbase + win, 64);
         const double Zw = __shfl(Z, gbase + win, 64);
+        const double Bw = __shfl(B, gbase + win, 64);
         bool fin = false;
         if (have) {
             if (!draw) {
@@ -333,7 +335,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
                 ib += G;
             } else {
                 double X;
-                if (stable_outer<true>(sp, key, t, j0 + (uint64_t)j, o, Uw, zw, Zw, X)) {
+                if (stable_outer<true>(sp, key, t, j0 + (uint64_t)j, o, Uw, zw, Zw, Bw, X)) {
                     finish(stable_finish(sp, X));
                     fin = true;
                 } else {
@@ -415,7 +417,7 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // drawing.  Chunks g, g + G, ... per workgroup (G <= 3 per CU, the sampler's occupancy);
 // each workgroup writes one partial n-vector, summed in workgroup order by k_cheb_init, so
 // the result is bitwise reproducible.  The draws are those of k_lambda_spec<L>.
-int g_lam_xu = 1;  // bb_set_tuning key 7: 0 = separate lambda and X u launches (A/B)
+int g_lam_xu = 1;  // bb_set_tuning key 7: 0 = separate lambda and X u launches; 1, 2: below
 template <int L, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
@@ -492,19 +494,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
 }
 
 // partial n-vectors of the fused launch for this shape, 0 if the shape does not take it
-int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
-    if (p_loc > kLamSpecMax || n_pad > 4096) return 0;
+// (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
+// chunk per workgroup, the hardware scheduling them -- more partials, no static tail, and the
+// workgroups' draw and stream phases drift apart; bb_set_tuning key 7 picks the mode)
+static int lambda_xu_groups(int p_loc, int p_pad, int n_pad, int mode) {
+    if (!mode || p_loc > kLamSpecMax || n_pad > 4096) return 0;
     const int L = spec_lanes(p_loc);
     if (L != 8 && L != 16) return 0;
     const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
-    return std::min(nchunk, 3 * device_cus_lam());
+    return mode == 2 ? nchunk : std::min(nchunk, 3 * device_cus_lam());
+}
+int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
+    return lambda_xu_groups(p_loc, p_pad, n_pad, 2);  // the most either mode writes
 }
 
 int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
                      int ldx, int n_pad, double *xu_part) {
-    const int G = (g_lam_xu && !g_lam_lanes) ? lambda_xu_parts(p_loc, p_pad, n_pad) : 0;
+    const int G = g_lam_lanes ? 0 : lambda_xu_groups(p_loc, p_pad, n_pad, g_lam_xu);
     if (!G) return 0;
     const Key key{k0, k1};
     const int L = spec_lanes(p_loc);

@@ -171,6 +171,7 @@ __device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia)
 // the inner loop hoisted (same expressions, so the same bits).
 struct StableParams {
     double h, alpha, ia, V0, b, lambda_alpha, gamma, sgamma, xi, psi, c1;
+    double c_alpha;  // ia^ia alpha^alpha = A(x) * B(x) / B(0) (the outer test's A from B / B0)
     double thr_w1, thr_w3;  // w1/(w1+w2), w3/(w2+w3)
     double neg_inv_alpha, inv_ia, inv_alpha;
 };
@@ -198,6 +199,7 @@ __device__ __forceinline__ StableParams stable_params(double h, double alpha, do
     s.neg_inv_alpha = -1 / alpha;
     s.inv_ia = 1. / (1. - alpha);
     s.inv_alpha = 1 / alpha;
+    s.c_alpha = powp(s.ia, s.ia) * powp(alpha, alpha);
     return s;
 }
 
@@ -205,7 +207,7 @@ __device__ __forceinline__ StableParams stable_params(double h, double alpha, do
 // Returns whether (U, z, Z) is accepted by the inner test.
 __device__ __forceinline__ bool stable_inner_body(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, uint64_t i, double &U,
-                                             double &z, double &Z) {
+                                             double &z, double &Z, double &B) {
     const double alpha = s.alpha, gamma = s.gamma, sgamma = s.sgamma;
     U4 r = uniforms(key, t, KIND_LAMBDA_INNER, j, o, i);
     double V = r.r[0];
@@ -221,7 +223,8 @@ __device__ __forceinline__ bool stable_inner_body(const StableParams &s, Key key
         else U = kPi * (1. - W_ * W_);
     }
     double W = r.r[1];
-    double zeta = sqrt(b_over_b0_p(U, alpha, s.ia));
+    B = b_over_b0_p(U, alpha, s.ia);
+    double zeta = sqrt(B);
     z = 1 / (1 - powp(1 + alpha * zeta / sgamma, s.neg_inv_alpha));
     double rho = kPi * exp(-s.lambda_alpha * (1. - 1. / (zeta * zeta))) /
                  ((1. + s.c1) * sgamma / zeta + z);
@@ -234,12 +237,17 @@ __device__ __forceinline__ bool stable_inner_body(const StableParams &s, Key key
     return (U < kPi && Z <= 1.);
 }
 
-// Outer test of outer attempt o (retstable.cpp:212-256) given the accepted inner triple.
+// Outer test of outer attempt o (retstable.cpp:212-256) given the accepted inner triple and
+// its B = B(U) / B(0).  The reference evaluates Zolotarev's A(U) afresh (retstable.cpp:213:
+// three more sines and two more powers); A(U) B(U) / B(0) = (1 - alpha)^(1 - alpha) alpha^alpha
+// identically (both are products of the same sinc powers), so A = c_alpha / B: the same value
+// to rounding, and about a fifth of a sampler round's VALU instructions fewer.
 __device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, double U, double z,
-                                             double Z, double &X) {
+                                             double Z, double B, double &X) {
     const double alpha = s.alpha;
-    double a = powp(zolotarev_A_p(U, alpha, s.ia), s.inv_ia);
+    (void)U;
+    double a = powp(s.c_alpha / B, s.inv_ia);
     double m = powp(s.b / a, alpha) * s.lambda_alpha;
     double delta = sqrt(m * alpha / a);
     double a1 = delta * s.c1;
@@ -270,27 +278,27 @@ __device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key
 
 __device__ __noinline__ bool stable_inner_ni(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, uint64_t i, double &U,
-                                             double &z, double &Z) {
-    return stable_inner_body(s, key, t, j, o, i, U, z, Z);
+                                             double &z, double &Z, double &B) {
+    return stable_inner_body(s, key, t, j, o, i, U, z, Z, B);
 }
 __device__ __noinline__ bool stable_outer_ni(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, double U, double z,
-                                             double Z, double &X) {
-    return stable_outer_body(s, key, t, j, o, U, z, Z, X);
+                                             double Z, double B, double &X) {
+    return stable_outer_body(s, key, t, j, o, U, z, Z, B, X);
 }
 template <bool NI>
 __device__ __forceinline__ bool stable_inner(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, uint64_t i, double &U,
-                                             double &z, double &Z) {
-    if constexpr (NI) return stable_inner_ni(s, key, t, j, o, i, U, z, Z);
-    else return stable_inner_body(s, key, t, j, o, i, U, z, Z);
+                                             double &z, double &Z, double &B) {
+    if constexpr (NI) return stable_inner_ni(s, key, t, j, o, i, U, z, Z, B);
+    else return stable_inner_body(s, key, t, j, o, i, U, z, Z, B);
 }
 template <bool NI>
 __device__ __forceinline__ bool stable_outer(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, double U, double z,
-                                             double Z, double &X) {
-    if constexpr (NI) return stable_outer_ni(s, key, t, j, o, U, z, Z, X);
-    else return stable_outer_body(s, key, t, j, o, U, z, Z, X);
+                                             double Z, double B, double &X) {
+    if constexpr (NI) return stable_outer_ni(s, key, t, j, o, U, z, Z, B, X);
+    else return stable_outer_body(s, key, t, j, o, U, z, Z, B, X);
 }
 
 #ifndef BB_STABLE_NOINLINE
@@ -324,19 +332,20 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
     uint64_t o = 0, ib = 0;
     for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
         bool acc = false;
-        double U = 0.0, z = 0.0, Z = 0.0;
-        if (!done) acc = stable_inner<NI>(s, key, t, j, o, ib + (uint64_t)g, U, z, Z);
+        double U = 0.0, z = 0.0, Z = 0.0, B = 1.0;
+        if (!done) acc = stable_inner<NI>(s, key, t, j, o, ib + (uint64_t)g, U, z, Z, B);
         const uint64_t m = (__ballot(acc) >> gbase) & gmask;
         const int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
         const double Uw = __shfl(U, gbase + win, 64);
         const double zw = __shfl(z, gbase + win, 64);
         const double Zw = __shfl(Z, gbase + win, 64);
+        const double Bw = __shfl(B, gbase + win, 64);
         if (!done) {
             if (!m) {
                 ib += G;
             } else {
                 double X;
-                if (stable_outer<NI>(s, key, t, j, o, Uw, zw, Zw, X)) {
+                if (stable_outer<NI>(s, key, t, j, o, Uw, zw, Zw, Bw, X)) {
                     result = stable_finish(s, X);
                     done = true;
                 } else {
@@ -382,16 +391,18 @@ __device__ __forceinline__ double stable_spec_draw(bool active, double h, double
     uint64_t o0 = 0, ib = 0;  // window's first outer attempt, its next inner attempt
     for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
         const uint64_t o = o0 + (uint64_t)seg;
-        double U = 0.0, z = 0.0, Z = 0.0;
+        double U = 0.0, z = 0.0, Z = 0.0, B = 1.0;
         bool acc = false;
         if (!done)
-            acc = stable_inner<false>(s, key, t, j, o, (seg == 0 ? ib : 0) + (uint64_t)ii, U, z, Z);
+            acc = stable_inner<false>(s, key, t, j, o, (seg == 0 ? ib : 0) + (uint64_t)ii, U, z, Z,
+                                      B);
         const uint64_t sb = ((__ballot(acc) >> gbase) >> (seg * I)) & imask;
         const int src = gbase + seg * I + (sb ? (__ffsll((unsigned long long)sb) - 1) : 0);
         const double Uw = __shfl(U, src, 64), zw = __shfl(z, src, 64), Zw = __shfl(Z, src, 64);
+        const double Bw = __shfl(B, src, 64);
         double X = 0.0;
         bool oacc = false;
-        if (!done && sb) oacc = stable_outer<false>(s, key, t, j, o, Uw, zw, Zw, X);
+        if (!done && sb) oacc = stable_outer<false>(s, key, t, j, o, Uw, zw, Zw, Bw, X);
         const uint64_t hb = __ballot(ii == 0 && sb != 0) >> gbase;
         const uint64_t ab = __ballot(ii == 0 && oacc) >> gbase;
         unsigned H = 0, A = 0;

@@ -380,7 +380,7 @@ def roofline_for(phase, ms, ctx, traffic_world):
         # profile of this workload) / the live average launch time, against one wave64 VALU
         # instruction per 4 cycles on each of the 1024 SIMDs at 2.4 GHz.  The fused launch
         # (k_lambda_xu, dense near-identity sweeps) also streams X for X u: its HBM rate too.
-        fused = (not sparse and not logit and ctx.get("nid_cheb") and bb.set_tuning(7, -1) == 1
+        fused = (not sparse and not logit and ctx.get("nid_cheb") and bb.set_tuning(7, -1) >= 1
                  and n <= 4096)
         if fused:
             kfull = "bb::k_lambda_xu"

@@ -338,10 +338,12 @@ void bb_set_trace_budget(long long bytes);
  * key 6: the most Chebyshev iterations a Woodbury sweep may take on the near-identity path
  * (default 16; 0 = every sweep forms the Gram and factors it);
  * key 7: a dense Woodbury sweep that may take the near-identity path draws lambda and forms
- * the X u partials in one launch (1, the default) or in two (0); the draws are the same;
+ * the X u partials in one launch (1: up to 3 workgroups per CU looping over column chunks,
+ * the default; 2: one workgroup per chunk) or in two (0); the draws are the same;
  * key 8: an unsharded Woodbury engine decides each sweep's path as a column shard does (the
- * host waits for the decision, then launches that path only: 1) or launches both paths with
- * the kernels of the one not taken returning at once (0, the default); the draws are the same.
+ * host waits for the decision, then launches that path only: 1, the default) or launches both
+ * paths with the kernels of the one not taken returning at once (0); the draws are the same
+ * except on sweeps where mode 0's launch hint fell short (it then takes the factor).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

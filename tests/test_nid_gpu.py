@@ -176,8 +176,9 @@ def test_nid_shard_certifies_its_columns(gpu_lib):
 
 @pytest.mark.parametrize("n,p", [(200, 2400), (700, 6000), (2000, 50000)])
 def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
-    """The fused lambda + X u launch (k_lambda_xu, bb_set_tuning key 7 = 1, the default)
-    against separate lambda and X u launches (key 7 = 0) on near-null states: the same
+    """The fused lambda + X u launch (k_lambda_xu, bb_set_tuning key 7 = 1, the default, and
+    7 = 2, one workgroup per chunk) against separate lambda and X u launches (key 7 = 0) on
+    near-null states: the same
     lambda bits (the same draws), beta to rounding (X u summed in another order), both on
     the Chebyshev path.  (2000, 50000) is C3's shape."""
     import bench
@@ -190,7 +191,7 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
     rng = np.random.default_rng(11)
     beta = 1e-6 * rng.standard_normal(p)
     out = []
-    for fused in (1, 0):
+    for fused in (1, 2, 0):
         old = bb.set_tuning(7, fused)
         try:
             e = _engine(bb, X, y, n, p)
@@ -203,19 +204,24 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
             e.close()
         finally:
             bb.set_tuning(7, old)
-    (a, sa), (b, sb) = out
-    assert sa["cheb_sweeps"] == 2 and sb["cheb_sweeps"] == 2, (sa, sb)
-    assert rel_err(a["beta"], b["beta"]) < 1e-12
-    assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
-    assert abs(a["tau"] - b["tau"]) <= 1e-12 * b["tau"]
+    b, sb = out[-1]
+    assert sb["cheb_sweeps"] == 2, sb
+    for a, sa in out[:-1]:  # modes 1 (workgroups loop over chunks) and 2 (one chunk each)
+        assert sa["cheb_sweeps"] == 2, (sa, sb)
+        assert rel_err(a["beta"], b["beta"]) < 1e-12
+        assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
+        assert abs(a["tau"] - b["tau"]) <= 1e-12 * b["tau"]
 
 
 @pytest.mark.parametrize("kind", ["dense", "sparse"])
 def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
-    """bb_set_tuning key 8 = 1: the unsharded engine waits for each sweep's decision and
-    launches that path only (the shards' protocol) instead of launching both paths gated.
-    The decision is the same least K, so from the reference start the two modes draw the
-    same chain bit for bit (the same kernels on the same partials)."""
+    """bb_set_tuning key 8 = 1 (the default): the unsharded engine waits for each sweep's
+    decision and launches that path only (the shards' protocol); key 8 = 0 launches both
+    paths gated, with at most the iterations its lagged hint allows.  Both decide the same
+    least K where the hint allows it; where it does not (eps grew more than 8x in three
+    sweeps -- seen once in the first sweeps from the reference start) mode 0 takes the
+    factor, the same draw to rounding.  From the reference start: the synchronous mode takes
+    the Chebyshev path on every sweep mode 0 does, and the chains agree."""
     bb = gpu_lib
     n, p = 300, 4000
     X, y, _ = _design(kind, n, p, 51)
@@ -233,6 +239,7 @@ def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
         finally:
             bb.set_tuning(8, old)
     (a, sa), (b, sb) = out
-    assert sa["cheb_sweeps"] == sb["cheb_sweeps"] >= 10, (sa, sb)
-    assert np.array_equal(a["beta"], b["beta"]) and np.array_equal(a["lambda"], b["lambda"])
-    assert a["tau"] == b["tau"] and a["sig2"] == b["sig2"]
+    assert sb["cheb_sweeps"] == 12 and sa["cheb_sweeps"] >= 10, (sa, sb)
+    assert rel_err(a["beta"], b["beta"]) < 1e-9, rel_err(a["beta"], b["beta"])
+    assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-9
+    assert abs(a["tau"] - b["tau"]) <= 1e-9 * b["tau"]
