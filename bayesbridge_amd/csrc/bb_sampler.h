@@ -172,7 +172,6 @@ __device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia)
 struct StableParams {
     double h, alpha, ia, V0, b, lambda_alpha, gamma, sgamma, xi, psi, c1;
     double c_alpha;  // ia^ia alpha^alpha = A(x) * B(x) / B(0) (the outer test's A from B / B0)
-    double lm0;  // log lambda_alpha + alpha log b: the outer test's log m = lm0 - alpha log a
     double thr_w1, thr_w3;  // w1/(w1+w2), w3/(w2+w3)
     double neg_inv_alpha, inv_ia, inv_alpha;
 };
@@ -201,7 +200,6 @@ __device__ __forceinline__ StableParams stable_params(double h, double alpha, do
     s.inv_ia = 1. / (1. - alpha);
     s.inv_alpha = 1 / alpha;
     s.c_alpha = powp(s.ia, s.ia) * powp(alpha, alpha);
-    s.lm0 = log(s.lambda_alpha) + alpha * log(s.b);  // -inf at h = 0 (then m = 0, as below)
     return s;
 }
 
@@ -243,18 +241,14 @@ __device__ __forceinline__ bool stable_inner_body(const StableParams &s, Key key
 // its B = B(U) / B(0).  The reference evaluates Zolotarev's A(U) afresh (retstable.cpp:213:
 // three more sines and two more powers); A(U) B(U) / B(0) = (1 - alpha)^(1 - alpha) alpha^alpha
 // identically (both are products of the same sinc powers), so A = c_alpha / B: the same value
-// to rounding, and about a fifth of a sampler round's VALU instructions fewer.  With
-// log a = log(A) / (1 - alpha) in hand, m = (b / a)^alpha lambda_alpha and m^-b come from
-// logs already formed: log m = log lambda_alpha + alpha log b - alpha log a.
+// to rounding, and about a fifth of a sampler round's VALU instructions fewer.
 __device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key, uint64_t t,
                                              uint64_t j, uint64_t o, double U, double z,
                                              double Z, double B, double &X) {
     const double alpha = s.alpha;
     (void)U;
-    const double la = s.inv_ia * log(s.c_alpha / B);
-    double a = exp(la);
-    const double lm = s.lm0 - alpha * la;
-    double m = exp(lm);
+    double a = powp(s.c_alpha / B, s.inv_ia);
+    double m = powp(s.b / a, alpha) * s.lambda_alpha;
     double delta = sqrt(m * alpha / a);
     double a1 = delta * s.c1;
     double a2 = delta;
@@ -275,7 +269,7 @@ __device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key
     }
     double E = -log(Z);
     double c = a * (Xc - m);
-    c += (m != 0) ? s.h * (powp(Xc, -1. * s.b) - exp(-1. * s.b * lm)) : 0.0;
+    c += (m != 0) ? s.h * (powp(Xc, -1. * s.b) - powp(m, -1. * s.b)) : 0.0;
     if (Xc < m) c -= N_ * N_ / 2.;
     else if (Xc > m + delta) c -= E_;
     X = Xc;
