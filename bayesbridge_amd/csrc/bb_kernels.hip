@@ -417,7 +417,10 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // drawing.  Chunks g, g + G, ... per workgroup (G <= 3 per CU, the sampler's occupancy);
 // each workgroup writes one partial n-vector, summed in workgroup order by k_cheb_init, so
 // the result is bitwise reproducible.  The draws are those of k_lambda_spec<L>.
-int g_lam_xu = 1;  // bb_set_tuning key 7: 0 = separate lambda and X u launches; 1, 2: below
+// bb_set_tuning key 7: 0 = separate lambda and X u launches; 1, 2: below.  Measured at the
+// driver's settings (round 4, gpurun_out/r04i_*): C3 mode 2 1899 / 1902 sweeps/s against mode 1
+// 1871 / 1871 (the lambda phase 0.202 against 0.220 ms); C2 6109 / 5931 against 6088 / 6023.
+int g_lam_xu = 2;
 template <int L, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
