@@ -162,9 +162,11 @@ __device__ __forceinline__ double zolotarev_A_p(double x, double alpha, double i
     return powp(ia * sinc_mm(ia * x), ia) * powp(alpha * sinc_mm(alpha * x), alpha) / sinc_mm(x);
 }
 
+// B(x) / B(0) = sinc(x) / (sinc(alpha x)^alpha sinc(ia x)^ia), the two powers as one exp:
+// sinc(x) exp(-(alpha log sinc(alpha x) + ia log sinc(ia x))) (the same value to rounding)
 __device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia) {
-    double den = powp(sinc_mm(alpha * x), alpha) * powp(sinc_mm(ia * x), ia);
-    return sinc_mm(x) / den;
+    const double l = alpha * log(sinc_mm(alpha * x)) + ia * log(sinc_mm(ia * x));
+    return sinc_mm(x) * exp(-l);
 }
 
 // Per-coefficient constants (retstable.cpp:121-147), with the loop-invariant ratios of
