@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-4 session j: B/B0 with one exp in the sampler's inner attempt, fused-launch mode 2 by
+# default: the sampler-facing GPU tests, then bench lines at the driver's settings (C3 twice,
+# C5, C2).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+stop() { echo "[session] $1 exit $2"; if [ "$2" -ge 124 ] || [ "$2" -eq 134 ] || [ "$2" -eq 139 ]; then exit "$2"; fi; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_steady_state_gpu.py \
+    tests/test_lambda_occ_gpu.py tests/test_nid_gpu.py \
+    -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+    > gpurun_out/r04j_tests.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED" gpurun_out/r04j_tests.log | tail -15
+stop tests $rc
+B="python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fitted"
+for w in c3 c5 c2 c3; do
+    timeout -k 10 300 $B --workload $w > gpurun_out/r04j_$w.json 2>> gpurun_out/r04j_bench.err
+    stop $w $?
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/r04j_$w.json').read().strip().splitlines()[-1])
+print('$w', round(d['value'],1), d['phases_ms'].get('lambda'), d['roofline'].get('kernel'), d['roofline'].get('frac'))"
+done
+echo "[session] done"
