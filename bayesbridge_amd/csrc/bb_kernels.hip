@@ -262,16 +262,19 @@ static int device_cus_lam() {
     return n;
 }
 
-template <int G>
+// chunk: the workgroup's range is [chunk per_wg, chunk per_wg + per_wg); us (LDS, or null):
+// u_j of the range, for the fused X u pass (k_lambda_xu); NI: the sampler bodies out of line
+template <int G, bool NI = true>
 __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, int p_pad,
                                                int per_wg, uint64_t j0, const DevScalars *sc,
                                                Key key, uint64_t t, int mode, double *lam,
                                                double *D, double *u, double *lam_trace,
-                                               uint32_t *err, int &s_next) {
+                                               uint32_t *err, int &s_next, int chunk,
+                                               double *us = nullptr) {
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1), gbase = lane & ~(G - 1);
     const uint64_t gmask = (G == 64) ? ~0ull : ((1ull << (G & 63)) - 1ull);
-    const int jbeg = blockIdx.x * per_wg;
+    const int jbeg = chunk * per_wg;
     const int jend = min(p_pad, jbeg + per_wg);
     if (threadIdx.x == 0) s_next = jbeg + kLamCbWG / G;
     __syncthreads();
@@ -296,6 +299,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
     };
     auto finish = [&](double x) {  // x: the tilted-stable draw of coefficient j
         if (g == 0) {
+            double uv = 0.0;
             if (j < p_loc) {
                 const double l = 2 * x;
                 lam[j] = l;
@@ -303,7 +307,8 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
                 if (mode == LAMBDA_WOODBURY) {
                     const double d = (tau * tau) / l;
                     D[j] = d;
-                    u[j] = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)j);
+                    uv = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)j);
+                    u[j] = uv;
                 }
             } else {
                 lam[j] = 1.0;
@@ -312,6 +317,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
                     u[j] = 0.0;
                 }
             }
+            if (us) us[j - jbeg] = uv;
         }
     };
     if (have) start();
@@ -319,7 +325,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
         bool acc = false;
         double U = 0.0, z = 0.0, Z = 0.0, B = 1.0;
         if (have && draw)
-            acc = stable_inner<true>(sp, key, t, j0 + (uint64_t)j, o, ib + (uint64_t)g, U, z, Z, B);
+            acc = stable_inner<NI>(sp, key, t, j0 + (uint64_t)j, o, ib + (uint64_t)g, U, z, Z, B);
         const uint64_t m = (__ballot(acc) >> gbase) & gmask;
         const int win = m ? (__ffsll((unsigned long long)m) - 1) : 0;
         const double Uw = __shfl(U, gbase + win, 64);
@@ -335,7 +341,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
                 ib += G;
             } else {
                 double X;
-                if (stable_outer<true>(sp, key, t, j0 + (uint64_t)j, o, Uw, zw, Zw, Bw, X)) {
+                if (stable_outer<NI>(sp, key, t, j0 + (uint64_t)j, o, Uw, zw, Zw, Bw, X)) {
                     finish(stable_finish(sp, X));
                     fin = true;
                 } else {
@@ -365,14 +371,14 @@ template <int G>
 __global__ __launch_bounds__(kLamCbWG) void k_lambda_cb(BB_LAMBDA_CB_ARGS) {
     __shared__ int s_next;
     lambda_cb_body<G>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u, lam_trace,
-                      err, s_next);
+                      err, s_next, blockIdx.x);
 }
 template <int G>
 __global__ __launch_bounds__(kLamCbWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 k_lambda_cb_o4(BB_LAMBDA_CB_ARGS) {
     __shared__ int s_next;
     lambda_cb_body<G>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u, lam_trace,
-                      err, s_next);
+                      err, s_next, blockIdx.x);
 }
 #undef BB_LAMBDA_CB_ARGS
 
@@ -421,7 +427,7 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // driver's settings (round 4, gpurun_out/r04i_*): C3 mode 2 1899 / 1902 sweeps/s against mode 1
 // 1871 / 1871 (the lambda phase 0.202 against 0.220 ms); C2 6109 / 5931 against 6088 / 6023.
 int g_lam_xu = 2;
-template <int L, int NR>
+template <int L, int NR, bool BATCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
                                                    uint64_t t, double *lam, double *D,
@@ -429,15 +435,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
                                                    const double *__restrict__ X, int ldx,
                                                    int n_pad, int nchunk,
                                                    double *__restrict__ xu_part) {
-    constexpr int C = 256 / L;
+    // BATCH: a chunk holds two coefficients per lane group, drawn with continuous batching
+    // (lambda_cb_body: a group that finishes takes the chunk's next coefficient)
+    constexpr int C = (BATCH ? 2 : 1) * (256 / L);
     constexpr int CQ = NR >= 16 ? 1 : 16 / NR;  // columns in flight: 16 loads per thread
     __shared__ double us[C];
+    __shared__ int s_next;
     __shared__ double accs[NR * 256];
     const int tid = threadIdx.x;
 #pragma unroll
     for (int m = 0; m < NR; ++m) accs[m * 256 + tid] = 0.0;
     const double tau = sc->tau;
     for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+      if constexpr (BATCH) {
+        lambda_cb_body<L, false>(beta, p_loc, p_pad, C, j0, sc, key, t, LAMBDA_WOODBURY, lam, D, u,
+                                 lam_trace, err, s_next, ch, us);
+      } else {
         const int i = ch * C + tid / L;  // group-uniform
         const bool active = i < p_loc;
         const double b = active ? beta[i] : 0.0;
@@ -460,6 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
             }
             us[tid / L] = uv;
         }
+      }
         __syncthreads();  // the chunk's u
         double a[NR];
 #pragma unroll
@@ -500,15 +514,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
 // (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
 // chunk per workgroup, the hardware scheduling them -- more partials, no static tail, and the
 // workgroups' draw and stream phases drift apart; bb_set_tuning key 7 picks the mode)
+static int lambda_xu_chunk(int L, int mode) { return (mode == 3 ? 2 : 1) * (256 / L); }
 static int lambda_xu_groups(int p_loc, int p_pad, int n_pad, int mode) {
     if (!mode || p_loc > kLamSpecMax || n_pad > 4096) return 0;
     const int L = spec_lanes(p_loc);
     if (L != 8 && L != 16) return 0;
-    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
-    return mode == 2 ? nchunk : std::min(nchunk, 3 * device_cus_lam());
+    const int cw = lambda_xu_chunk(L, mode);
+    const int nchunk = (p_pad + cw - 1) / cw;
+    return mode == 1 ? std::min(nchunk, 3 * device_cus_lam()) : nchunk;
 }
 int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
-    return lambda_xu_groups(p_loc, p_pad, n_pad, 2);  // the most either mode writes
+    return lambda_xu_groups(p_loc, p_pad, n_pad, 2);  // the most any mode writes
 }
 
 int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
@@ -519,11 +535,14 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     if (!G) return 0;
     const Key key{k0, k1};
     const int L = spec_lanes(p_loc);
-    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
+    const int cw = lambda_xu_chunk(L, g_lam_xu);
+    const int nchunk = (p_pad + cw - 1) / cw;
     const int nr = (n_pad + 255) / 256;
+    const bool batch = g_lam_xu == 3;
 #define BB_LXU(LL, NN)                                                                        \
-    k_lambda_xu<LL, NN><<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u,      \
-                                          lam_trace, err, X, ldx, n_pad, nchunk, xu_part)
+    (batch ? k_lambda_xu<LL, NN, true> : k_lambda_xu<LL, NN, false>)<<<G, 256, 0, s>>>(       \
+        beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad, nchunk,  \
+        xu_part)
     if (L == 8) {
         if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
     } else {
