@@ -380,6 +380,13 @@ k_lambda_cb_o4(BB_LAMBDA_CB_ARGS) {
     lambda_cb_body<G>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u, lam_trace,
                       err, s_next, blockIdx.x);
 }
+// the sampler bodies inlined (bb_set_tuning key 4 bit 2; 3 waves per SIMD)
+template <int G>
+__global__ __launch_bounds__(kLamCbWG) void k_lambda_cb_in(BB_LAMBDA_CB_ARGS) {
+    __shared__ int s_next;
+    lambda_cb_body<G, false>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u,
+                             lam_trace, err, s_next, blockIdx.x);
+}
 #undef BB_LAMBDA_CB_ARGS
 
 // One speculative lambda launch with L lanes per coefficient (the draws do not depend on L);
@@ -580,12 +587,13 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
         return;
     }
     if (ni && group == 8) {
-        // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy)
-        const int nwg = std::max(1, std::min(4 * device_cus_lam(), (p_pad + 31) / 32));
+        // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy; 3 inlined)
+        const bool inl = (g_lam_occ & 4) != 0;
+        const int nwg = std::max(1, std::min((inl ? 3 : 4) * device_cus_lam(), (p_pad + 31) / 32));
         const int per = (p_pad + nwg - 1) / nwg;
-        ((g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>)<<<(p_pad + per - 1) / per, kLamCbWG, 0,
-                                                            s>>>(
-            beta, p_loc, p_pad, per, j0, sc, key, t, mode, lam, D, u, lam_trace, err);
+        auto *kern = inl ? k_lambda_cb_in<8> : (g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>;
+        kern<<<(p_pad + per - 1) / per, kLamCbWG, 0, s>>>(beta, p_loc, p_pad, per, j0, sc, key,
+                                                          t, mode, lam, D, u, lam_trace, err);
         return;
     }
     switch (group) {

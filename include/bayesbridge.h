@@ -333,7 +333,8 @@ void bb_set_trace_budget(long long bytes);
  * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane;
  * key 4: occupancy of the lambda launches, bit 0 = k_lambda_spec and bit 1 = k_lambda_cb
  * capped at 128 VGPRs for 4 waves per SIMD instead of their register-minimal 3 (default 2:
- * k_lambda_cb only, 4 % faster at C5; no change at C3); the draws are the same;
+ * k_lambda_cb only, 4 % faster at C5; no change at C3); bit 2: k_lambda_cb with the sampler
+ * bodies inlined (3 waves per SIMD) instead; the draws are the same;
  * key 5: lanes per coefficient of the speculative lambda launch (0 = the size-based default);
  * key 6: the most Chebyshev iterations a Woodbury sweep may take on the near-identity path
  * (default 16; 0 = every sweep forms the Gram and factors it);

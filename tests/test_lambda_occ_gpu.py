@@ -1,7 +1,8 @@
 """The lambda launches' two occupancy instances (bb_set_tuning key 4) draw the same chain.
 
 k_lambda_spec<16> (1024 < p <= 50000) and k_lambda_cb<8> (p > 50000) each exist at their
-register-minimal 3 waves per SIMD and capped at 128 VGPRs for 4 waves per SIMD; both run
+register-minimal 3 waves per SIMD and capped at 128 VGPRs for 4 waves per SIMD (and
+k_lambda_cb with its sampler bodies inlined, key 4 bit 2); all run
 the sequential retstable_LD loop of every coefficient on its own counters
 (retstable.cpp:94-271, BridgeRegression.cpp:506-510), so the traces must be bit-identical."""
 import numpy as np
@@ -18,8 +19,9 @@ def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
     X, y, _ = synthetic_problem(n, p, seed=11, s=10)
     traces = []
     old = bb.set_tuning(4, -1)
+    old6 = bb.set_tuning(6, 0)  # the separate lambda launch on every sweep (no fused X u)
     try:
-        for occ in (0, 3):
+        for occ in (0, 3, 4):
             bb.set_tuning(4, occ)
             e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=6,
                                           seed=77, stream=0), X, y)
@@ -31,8 +33,10 @@ def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
             e.close()
     finally:
         bb.set_tuning(4, old)
+        bb.set_tuning(6, old6)
     for k in ("beta", "lambda", "tau", "sig2"):
-        assert np.array_equal(traces[0][k], traces[1][k]), k
+        for tr in traces[1:]:
+            assert np.array_equal(traces[0][k], tr[k]), k
 
 
 def test_lambda_lane_counts_same_chain(gpu_lib):
@@ -44,6 +48,7 @@ def test_lambda_lane_counts_same_chain(gpu_lib):
     X, y, _ = synthetic_problem(n, p, seed=12, s=8)
     traces = []
     old = bb.set_tuning(5, -1)
+    old6 = bb.set_tuning(6, 0)  # the separate lambda launch on every sweep (no fused X u)
     try:
         for lanes in (0, 4, 16, 32, 64):
             bb.set_tuning(5, lanes)
@@ -57,6 +62,7 @@ def test_lambda_lane_counts_same_chain(gpu_lib):
             e.close()
     finally:
         bb.set_tuning(5, old)
+        bb.set_tuning(6, old6)
     for tr in traces[1:]:
         for k in ("beta", "lambda", "tau", "sig2"):
             assert np.array_equal(traces[0][k], tr[k]), k
