@@ -514,15 +514,21 @@ struct bb_engine {
 
     // ---- column shards (nid_sync): the stages between the exchanges of a Woodbury sweep ----
     static constexpr int kNidRed = kNidTS + 2;
-    // this shard's bound sums into nid_red (exchanged: kNidRed doubles)
+    // this shard's bound sums into nid_red (exchanged: kNidRed doubles); an unsharded engine
+    // decides in the same launch (its sums need no exchange)
     void nidx_partials() {
         mark(PH_NID);
-        launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
+        if (cfg.world > 1)
+            launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
+        else
+            launch_nid_sums_decide(stream, D, cn, p_loc, sc, nid, std::min(g_nid_kmax, nid_kmax),
+                                   nid_wg, nid_red, eps_dev + kNidRing);
     }
     // the decision from the reduced sums (identical on every rank), then wait for it
     void nidx_decide_launch() {
-        launch_nid_decide_from(stream, nid_red, sc, std::min(g_nid_kmax, nid_kmax), nid,
-                               eps_dev + kNidRing);
+        if (cfg.world > 1)
+            launch_nid_decide_from(stream, nid_red, sc, std::min(g_nid_kmax, nid_kmax), nid,
+                                   eps_dev + kNidRing);
         if (!nid_sev) HIPCHECK(hipEventCreateWithFlags(&nid_sev, hipEventDisableTiming));
         HIPCHECK(hipEventRecord(nid_sev, stream));
     }
@@ -576,13 +582,26 @@ struct bb_engine {
         }
         exchange(nid_red, (size_t)kNidRed);
         nidx_decide_launch();
+        // An unsharded engine enqueues the start of the Chebyshev solve before it waits for
+        // the decision -- X u, the initial iterate and one product, each returning at once
+        // unless the device decided so -- so the device runs them while the host wakes up
+        // (no bubble on the common near-identity sweep); the rest follows the decision.
+        const int spec = (cfg.world == 1 && g_nid_sync != 2) ? 2 : 0;
+        if (spec) {
+            nidx_xu();
+            nidx_init(t);
+            nidx_eapply(1);
+            nidx_step(1);
+        }
         const int K = nidx_decide_read();
         nid_only = K > 0;
         if (K > 0) {
-            nidx_xu();
-            exchange(nid_sum, (size_t)n_pad);
-            nidx_init(t);
-            for (int j = 1; j < K; ++j) {
+            if (!spec) {
+                nidx_xu();
+                exchange(nid_sum, (size_t)n_pad);
+                nidx_init(t);
+            }
+            for (int j = spec ? spec : 1; j < K; ++j) {
                 nidx_eapply(j);
                 exchange(nid_sum, (size_t)n_pad);
                 nidx_step(j);
@@ -3363,7 +3382,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 8: {
             const int old = g_nid_sync;
-            if (value >= 0) g_nid_sync = value ? 1 : 0;
+            if (value >= 0) g_nid_sync = value > 2 ? 2 : value;
             return old;
         }
         default: return -1;

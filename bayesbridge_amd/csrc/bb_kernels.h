@@ -94,6 +94,10 @@ int nid_sum_groups(int p_loc);
 void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc,
                      const DevScalars *sc, NidState *nid, int k_launched, int allow, int decide,
                      double *wg_part, double *red, double *eps_host);
+// unsharded, synchronous protocol: the sums and the decision, [eps, mode] into host2
+void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
+                            const DevScalars *sc, NidState *nid, int k_launched,
+                            double *wg_part, double *red, double *host2);
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
                             int k_launched, NidState *nid, double *host2);
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,

@@ -172,7 +172,9 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
         red[t] = v;
     }
     __syncthreads();
-    if (decide && t == 0) nid_finish(r, sc, k_launched, allow, nid, eps_host, nullptr);
+    // decide 1: eps into eps_host (the launch hint); 2: [eps, mode] into eps_host[0..1]
+    if (decide && t == 0)
+        nid_finish(r, sc, k_launched, allow, nid, eps_host, decide == 2 ? eps_host + 1 : nullptr);
 }
 
 __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
@@ -432,6 +434,14 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
     k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
                                   eps_host);
+}
+
+void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
+                            const DevScalars *sc, NidState *nid, int k_launched,
+                            double *wg_part, double *red, double *host2) {
+    const int G = nid_sum_groups(p_loc);
+    k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
+    k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, 1, 2, nid, red, host2);
 }
 
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,

@@ -343,7 +343,9 @@ void bb_set_trace_budget(long long bytes);
  * 2: one workgroup per chunk, the default; 3: one workgroup per chunk of two coefficients
  * per lane group, drawn with continuous batching) or in two (0); the draws are the same;
  * key 8: an unsharded Woodbury engine decides each sweep's path as a column shard does (the
- * host waits for the decision, then launches that path only: 1, the default) or launches both
+ * host waits for the decision, then launches that path only: 1, the default, with the
+ * Chebyshev solve's first kernels enqueued before the wait and returning at once unless the
+ * device decided so; 2: without them) or launches both
  * paths with the kernels of the one not taken returning at once (0); the draws are the same
  * except on sweeps where mode 0's launch hint fell short (it then takes the factor).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
