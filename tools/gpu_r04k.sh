@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop() { echo "[session] $1 exit $2"; if [ "$2" -ge 124 ] || [ "$2" -eq 134 ] || [ "$2" -eq 139 ]; then exit "$2"; fi; }
-timeout -k 10 600 python -u -m pytest tests/test_lambda_occ_gpu.py tests/test_nid_gpu.py \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_steady_state_gpu.py tests/test_lambda_occ_gpu.py tests/test_nid_gpu.py tests/test_shard_nid_gpu.py tests/test_sparse_gpu.py \
     -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread \
     > gpurun_out/r04k_tests.log 2>&1
 rc=$?
