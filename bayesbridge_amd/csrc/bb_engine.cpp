@@ -3377,7 +3377,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 7: {
             const int old = g_lam_xu;
-            if (value >= 0) g_lam_xu = value > 3 ? 3 : value;
+            if (value >= 0) g_lam_xu = value > 2 ? 2 : value;
             return old;
         }
         case 8: {

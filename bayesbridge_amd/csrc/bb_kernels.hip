@@ -234,10 +234,14 @@ k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
                         lam_blocks, pgt);
 }
 #undef BB_LAMBDA_SPEC_ARGS
-// bb_set_tuning key 4: bit 0 = k_lambda_spec at 4 waves per SIMD, bit 1 = k_lambda_cb at 4.
-// Measured (tools/lambda_occ_ab.py, three alternations): C3 k_lambda_spec<16> 0.200-0.208 ms at
-// either occupancy; C5 k_lambda_cb<8> 0.418-0.428 -> 0.402-0.407 ms at 4 waves.  Default 2.
-int g_lam_occ = 2;
+// bb_set_tuning key 4: bit 0 = k_lambda_spec at 4 waves per SIMD, bit 1 = k_lambda_cb at 4,
+// bit 2 = k_lambda_cb with the sampler bodies inlined (3 waves; overrides bit 1).  Measured
+// (round 3, tools/lambda_occ_ab.py, three alternations): C3 k_lambda_spec<16> 0.200-0.208 ms
+// at either occupancy; C5 k_lambda_cb<8> 0.418-0.428 -> 0.402-0.407 ms at 4 waves; round 4
+// (gpurun_out/r04k_*, two alternations at the driver's settings): C5 inlined 1933-1939
+// sweeps/s against 1824-1831 out of line at 4 waves (lambda 0.334-0.341 against 0.351-0.356
+// ms).  Default 4.
+int g_lam_occ = 4;
 
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
 // as long as its slowest wave, and a wave is as long as the slowest of its G-lane groups'
@@ -433,8 +437,11 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // bb_set_tuning key 7: 0 = separate lambda and X u launches; 1, 2: below.  Measured at the
 // driver's settings (round 4, gpurun_out/r04i_*): C3 mode 2 1899 / 1902 sweeps/s against mode 1
 // 1871 / 1871 (the lambda phase 0.202 against 0.220 ms); C2 6109 / 5931 against 6088 / 6023.
+// (A batched mode -- chunks of two coefficients per lane group drawn by lambda_cb_body with
+// continuous batching -- measured slower, C3 1895 against 1937-1948, C2 5532-5557 against
+// 6322-6372, gpurun_out/r04k_*, and was removed.)
 int g_lam_xu = 2;
-template <int L, int NR, bool BATCH>
+template <int L, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
                                                    uint64_t t, double *lam, double *D,
@@ -442,22 +449,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
                                                    const double *__restrict__ X, int ldx,
                                                    int n_pad, int nchunk,
                                                    double *__restrict__ xu_part) {
-    // BATCH: a chunk holds two coefficients per lane group, drawn with continuous batching
-    // (lambda_cb_body: a group that finishes takes the chunk's next coefficient)
-    constexpr int C = (BATCH ? 2 : 1) * (256 / L);
+    constexpr int C = 256 / L;
     constexpr int CQ = NR >= 16 ? 1 : 16 / NR;  // columns in flight: 16 loads per thread
     __shared__ double us[C];
-    __shared__ int s_next;
     __shared__ double accs[NR * 256];
     const int tid = threadIdx.x;
 #pragma unroll
     for (int m = 0; m < NR; ++m) accs[m * 256 + tid] = 0.0;
     const double tau = sc->tau;
     for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-      if constexpr (BATCH) {
-        lambda_cb_body<L, false>(beta, p_loc, p_pad, C, j0, sc, key, t, LAMBDA_WOODBURY, lam, D, u,
-                                 lam_trace, err, s_next, ch, us);
-      } else {
         const int i = ch * C + tid / L;  // group-uniform
         const bool active = i < p_loc;
         const double b = active ? beta[i] : 0.0;
@@ -480,7 +480,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
             }
             us[tid / L] = uv;
         }
-      }
         __syncthreads();  // the chunk's u
         double a[NR];
 #pragma unroll
@@ -521,13 +520,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
 // (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
 // chunk per workgroup, the hardware scheduling them -- more partials, no static tail, and the
 // workgroups' draw and stream phases drift apart; bb_set_tuning key 7 picks the mode)
-static int lambda_xu_chunk(int L, int mode) { return (mode == 3 ? 2 : 1) * (256 / L); }
 static int lambda_xu_groups(int p_loc, int p_pad, int n_pad, int mode) {
     if (!mode || p_loc > kLamSpecMax || n_pad > 4096) return 0;
     const int L = spec_lanes(p_loc);
     if (L != 8 && L != 16) return 0;
-    const int cw = lambda_xu_chunk(L, mode);
-    const int nchunk = (p_pad + cw - 1) / cw;
+    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
     return mode == 1 ? std::min(nchunk, 3 * device_cus_lam()) : nchunk;
 }
 int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
@@ -542,14 +539,11 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     if (!G) return 0;
     const Key key{k0, k1};
     const int L = spec_lanes(p_loc);
-    const int cw = lambda_xu_chunk(L, g_lam_xu);
-    const int nchunk = (p_pad + cw - 1) / cw;
+    const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
     const int nr = (n_pad + 255) / 256;
-    const bool batch = g_lam_xu == 3;
 #define BB_LXU(LL, NN)                                                                        \
-    (batch ? k_lambda_xu<LL, NN, true> : k_lambda_xu<LL, NN, false>)<<<G, 256, 0, s>>>(       \
-        beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad, nchunk,  \
-        xu_part)
+    k_lambda_xu<LL, NN><<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u,      \
+                                          lam_trace, err, X, ldx, n_pad, nchunk, xu_part)
     if (L == 8) {
         if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
     } else {

@@ -333,15 +333,15 @@ void bb_set_trace_budget(long long bytes);
  * loads (1), or the flat chunked pair stream with 8 (2) or 16 (3, the default) pairs per lane;
  * key 4: occupancy of the lambda launches, bit 0 = k_lambda_spec and bit 1 = k_lambda_cb
  * capped at 128 VGPRs for 4 waves per SIMD instead of their register-minimal 3 (default 2:
- * k_lambda_cb only, 4 % faster at C5; no change at C3); bit 2: k_lambda_cb with the sampler
- * bodies inlined (3 waves per SIMD) instead; the draws are the same;
+ * k_lambda_cb only: 4 % faster at C5 than 3 waves); bit 2: k_lambda_cb with the sampler
+ * bodies inlined (3 waves per SIMD) instead -- the default (value 4), 6 % faster at C5 than
+ * the out-of-line instance at 4 waves; the draws are the same;
  * key 5: lanes per coefficient of the speculative lambda launch (0 = the size-based default);
  * key 6: the most Chebyshev iterations a Woodbury sweep may take on the near-identity path
  * (default 16; 0 = every sweep forms the Gram and factors it);
  * key 7: a dense Woodbury sweep that may take the near-identity path draws lambda and forms
  * the X u partials in one launch (1: up to 3 workgroups per CU looping over column chunks;
- * 2: one workgroup per chunk, the default; 3: one workgroup per chunk of two coefficients
- * per lane group, drawn with continuous batching) or in two (0); the draws are the same;
+ * 2: one workgroup per chunk, the default) or in two (0); the draws are the same;
  * key 8: an unsharded Woodbury engine decides each sweep's path as a column shard does (the
  * host waits for the decision, then launches that path only: 1, the default, with the
  * Chebyshev solve's first kernels enqueued before the wait and returning at once unless the

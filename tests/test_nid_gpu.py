@@ -191,7 +191,7 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
     rng = np.random.default_rng(11)
     beta = 1e-6 * rng.standard_normal(p)
     out = []
-    for fused in (1, 2, 3, 0):
+    for fused in (1, 2, 0):
         old = bb.set_tuning(7, fused)
         try:
             e = _engine(bb, X, y, n, p)
@@ -206,7 +206,7 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
             bb.set_tuning(7, old)
     b, sb = out[-1]
     assert sb["cheb_sweeps"] == 2, sb
-    for a, sa in out[:-1]:  # modes 1 (loop over chunks), 2 (one chunk each), 3 (batched)
+    for a, sa in out[:-1]:  # modes 1 (loop over chunks) and 2 (one chunk each)
         assert sa["cheb_sweeps"] == 2, (sa, sb)
         assert rel_err(a["beta"], b["beta"]) < 1e-12
         assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
