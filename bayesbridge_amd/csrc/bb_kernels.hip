@@ -893,11 +893,16 @@ __global__ __launch_bounds__(256) void k_scalars(const double *red1, int nbS, co
     if (threadIdx.x == 0) sh[4] = rss0;
     __syncthreads();
     const double rss = sh[4];
+    // S_alpha: the nbS workgroup partials summed by all threads (strided, then the fixed
+    // tree of block_sum) -- one thread adding them in turn paid a load latency per partial
+    // (nbS = 782 at p = 200 000)
+    double sv = 0.0;
+    for (int q = threadIdx.x; q < nbS; q += 256) sv += red1[q];
+    const double S0 = block_sum<256>(sv, sh);
     // tau (wave 0) and sig2 (wave 1) are independent draws on their own counters: one lane
     // of each wave, concurrently
     if (threadIdx.x == 0) {
-        double S = 0.0;
-        for (int q = 0; q < nbS; ++q) S += red1[q];
+        const double S = S0;
         const double alpha = sc->alpha;
         if (!hy.know_tau) {
             const double shape = hy.nu_shape + ((double)p) / alpha;
