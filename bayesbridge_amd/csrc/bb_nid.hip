@@ -391,23 +391,20 @@ __global__ __launch_bounds__(256) void k_sp_eapply_rows(const int *__restrict__ 
                                                         const NidState *nid, int j, int pol,
                                                         double *__restrict__ out) {
     // pol 0: gated as an E-apply (step j); pol 1: X u for the right-hand side (mode != 0).
-    // One workgroup per row, four gathers in flight per thread (as bb_sparse.hip k_sp_rows).
+    // A wave per row, four gathers in flight per lane (as bb_sparse.hip k_sp_rows).
     if (pol == 0 ? nid->mode <= j : nid->mode == 0) return;
-    const int row = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_pad) return;
-    __shared__ double sh[4];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     const int e = rowptr[row + 1];
-    int k = rowptr[row] + (int)threadIdx.x;
-    for (; k + 768 < e; k += 1024)
+    int k = rowptr[row] + lane;
+    for (; k + 192 < e; k += 256)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] += rval[k + 256 * q] * s[colidx[k + 256 * q]];
-    for (; k < e; k += 256) a[0] += rval[k] * s[colidx[k]];
+        for (int q = 0; q < 4; ++q) a[q] += rval[k + 64 * q] * s[colidx[k + 64 * q]];
+    for (; k < e; k += 64) a[0] += rval[k] * s[colidx[k]];
     const double t = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
-    if (lane == 0) sh[w] = t;
-    __syncthreads();
-    if (threadIdx.x == 0) out[row] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    if (lane == 0) out[row] = t;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -507,8 +504,8 @@ void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const
     k_sp_eapply_cols<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(colptr, rowidx, cval,
                                                                        p_loc, D, v, nid, j,
                                                                        scratch_p);
-    k_sp_eapply_rows<<<n_pad, 256, 0, s>>>(rowptr, colidx, rval, n_pad, scratch_p, nid, j, 0,
-                                           out);
+    k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, scratch_p,
+                                                     nid, j, 0, out);
 }
 
 void launch_part_sum(hipStream_t s, const double *part, int nparts, int n_pad, double *out) {
@@ -523,7 +520,8 @@ void launch_shift_gram(hipStream_t s, const double *red2, int n_pad, double U, d
 
 void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                       int n_pad, const double *u, const NidState *nid, double *out) {
-    k_sp_eapply_rows<<<n_pad, 256, 0, s>>>(rowptr, colidx, rval, n_pad, u, nid, 0, 1, out);
+    k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, u, nid, 0, 1,
+                                                     out);
 }
 
 }  // namespace bb

@@ -408,10 +408,11 @@ void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, con
                                                      u, n_pad, tri, xu, gate);
 }
 
-// One workgroup per row c of X (CSR): its 256 threads strided over the row's entries with
-// four independent accumulators (four gathers in flight per thread), then a fixed tree (the
-// accumulators pairwise, wave xor trees, the four waves in order).  A wave per row with one
-// accumulator paid a gather latency per 64 entries: 45 us for C5's 5000 rows of ~2000.
+// One wave per row c of X (CSR), four rows per workgroup: lanes strided over the row's
+// entries with four independent accumulators (four gathers in flight per lane), then a fixed
+// tree (the accumulators pairwise, the wave's xor tree).  (One accumulator paid a gather
+// latency per 64 entries; a workgroup per row measured slower at C5's ~2000 entries per row:
+// 53 against 45 us, its barrier and launch per row.)
 template <bool DIAG>
 __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
                                                  const int *__restrict__ colidx,
@@ -421,48 +422,43 @@ __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
                                                  double *__restrict__ xv,
                                                  double *__restrict__ tri, const int *gate) {
     if (gated(gate)) return;
-    const int c = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= n_pad) return;
-    __shared__ double sh[2][4];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, d[4] = {0.0, 0.0, 0.0, 0.0};
     const int e = rowptr[c + 1];
-    int k = rowptr[c] + (int)threadIdx.x;
-    for (; k + 768 < e; k += 1024) {
+    int k = rowptr[c] + lane;
+    for (; k + 192 < e; k += 256) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int kk = k + 256 * q;
+            const int kk = k + 64 * q;
             const int j = colidx[kk];
             const double x = rval[kk];
             s[q] += x * v[j];
             if (DIAG) d[q] += x * x * D[j];
         }
     }
-    for (; k < e; k += 256) {
+    for (; k < e; k += 64) {
         const int j = colidx[k];
         const double x = rval[k];
         s[0] += x * v[j];
         if (DIAG) d[0] += x * x * D[j];
     }
-    double ss = group_sum<64>((s[0] + s[1]) + (s[2] + s[3]));
-    double dd = DIAG ? group_sum<64>((d[0] + d[1]) + (d[2] + d[3])) : 0.0;
+    const double ss = group_sum<64>((s[0] + s[1]) + (s[2] + s[3]));
+    const double dd = DIAG ? group_sum<64>((d[0] + d[1]) + (d[2] + d[3])) : 0.0;
     if (lane == 0) {
-        sh[0][w] = ss;
-        sh[1][w] = dd;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        xv[c] = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
-        if (DIAG) tri[tri_index(c, c)] = ((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3];
+        xv[c] = ss;
+        if (DIAG) tri[tri_index(c, c)] = dd;
     }
 }
 
 void launch_sp_rows(hipStream_t s, const int *rowptr, const int *colidx, const double *rval,
                     int n_pad, const double *v, const double *D, double *xv, double *tri, const int *gate) {
+    const int blocks = (n_pad + 3) / 4;
     if (D)
-        k_sp_rows<true><<<n_pad, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
+        k_sp_rows<true><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
     else
-        k_sp_rows<false><<<n_pad, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
+        k_sp_rows<false><<<blocks, 256, 0, s>>>(rowptr, colidx, rval, n_pad, v, D, xv, tri, gate);
 }
 
 // 16 lanes per column of the CSC: s = X_j . w, beta_j = u_j + D_j s / sig.
