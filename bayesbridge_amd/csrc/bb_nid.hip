@@ -390,21 +390,15 @@ __global__ __launch_bounds__(256) void k_sp_eapply_rows(const int *__restrict__ 
                                                         int n_pad, const double *__restrict__ s,
                                                         const NidState *nid, int j, int pol,
                                                         double *__restrict__ out) {
-    // pol 0: gated as an E-apply (step j); pol 1: X u for the right-hand side (mode != 0).
-    // A wave per row, four gathers in flight per lane (as bb_sparse.hip k_sp_rows).
+    // pol 0: gated as an E-apply (step j); pol 1: X u for the right-hand side (mode != 0)
     if (pol == 0 ? nid->mode <= j : nid->mode == 0) return;
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= n_pad) return;
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    const int e = rowptr[row + 1];
-    int k = rowptr[row] + lane;
-    for (; k + 192 < e; k += 256)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] += rval[k + 64 * q] * s[colidx[k + 64 * q]];
-    for (; k < e; k += 64) a[0] += rval[k] * s[colidx[k]];
-    const double t = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
-    if (lane == 0) out[row] = t;
+    double a = 0.0;
+    for (int k = rowptr[row] + lane; k < rowptr[row + 1]; k += 64) a += rval[k] * s[colidx[k]];
+    a = wave_sum(a);
+    if (lane == 0) out[row] = a;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -408,11 +408,8 @@ void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, con
                                                      u, n_pad, tri, xu, gate);
 }
 
-// One wave per row c of X (CSR), four rows per workgroup: lanes strided over the row's
-// entries with four independent accumulators (four gathers in flight per lane), then a fixed
-// tree (the accumulators pairwise, the wave's xor tree).  (One accumulator paid a gather
-// latency per 64 entries; a workgroup per row measured slower at C5's ~2000 entries per row:
-// 53 against 45 us, its barrier and launch per row.)
+// One wave per row c of X (CSR), lanes strided over the row's entries, fixed tree.  (Four
+// independent accumulators, or a workgroup per row, measured slower at C5: 53 against 45 us.)
 template <bool DIAG>
 __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
                                                  const int *__restrict__ colidx,
@@ -425,30 +422,18 @@ __global__ __launch_bounds__(256) void k_sp_rows(const int *__restrict__ rowptr,
     const int lane = threadIdx.x & 63;
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= n_pad) return;
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, d[4] = {0.0, 0.0, 0.0, 0.0};
-    const int e = rowptr[c + 1];
-    int k = rowptr[c] + lane;
-    for (; k + 192 < e; k += 256) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int kk = k + 64 * q;
-            const int j = colidx[kk];
-            const double x = rval[kk];
-            s[q] += x * v[j];
-            if (DIAG) d[q] += x * x * D[j];
-        }
-    }
-    for (; k < e; k += 64) {
+    double s = 0.0, d = 0.0;
+    for (int k = rowptr[c] + lane; k < rowptr[c + 1]; k += 64) {
         const int j = colidx[k];
         const double x = rval[k];
-        s[0] += x * v[j];
-        if (DIAG) d[0] += x * x * D[j];
+        s += x * v[j];
+        if (DIAG) d += x * x * D[j];
     }
-    const double ss = group_sum<64>((s[0] + s[1]) + (s[2] + s[3]));
-    const double dd = DIAG ? group_sum<64>((d[0] + d[1]) + (d[2] + d[3])) : 0.0;
+    s = group_sum<64>(s);
+    if (DIAG) d = group_sum<64>(d);
     if (lane == 0) {
-        xv[c] = ss;
-        if (DIAG) tri[tri_index(c, c)] = dd;
+        xv[c] = s;
+        if (DIAG) tri[tri_index(c, c)] = d;
     }
 }
 
