@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_lambda(const double *beta, int p_loc, i
     const double alpha = sc->alpha;
     const double b = active ? beta[i] : 0.0;
     const double h = b * b / (tau * tau);
-    double x = stable_group_draw<G, NI>(active, h, 0.5 * alpha, 1.0, key, t, j0 + (uint64_t)i,
+    double x = stable_group_draw<G, NI, true>(active, h, 0.5 * alpha, 1.0, key, t, j0 + (uint64_t)i,
                                         err);
     if ((threadIdx.x & (G - 1)) == 0 && i < p_pad) {
         if (active) {
@@ -298,7 +298,7 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
             const double b = beta[j];
             const double h = b * b / (tau * tau);
             if (h < 0 || a2 < 0 || a2 > 1) atomicOr(err, 4u);  // :112-115
-            sp = stable_params(h, a2, 1.0);
+            sp = stable_params<true>(h, a2, 1.0);
         }
     };
     auto finish = [&](double x) {  // x: the tilted-stable draw of coefficient j
@@ -442,7 +442,7 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // 6322-6372, gpurun_out/r04k_*, and was removed.)
 int g_lam_xu = 2;
 template <int L, int NR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_lambda_xu(const double *beta, int p_loc, int p_pad,
+__device__ __forceinline__ void lambda_xu_body(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
                                                    uint64_t t, double *lam, double *D,
                                                    double *u, double *lam_trace, uint32_t *err,
@@ -517,6 +517,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
 }
 
 // partial n-vectors of the fused launch for this shape, 0 if the shape does not take it
+#define BB_LXU_ARGS                                                                          \
+    const double *beta, int p_loc, int p_pad, uint64_t j0, const DevScalars *sc, Key key,    \
+        uint64_t t, double *lam, double *D, double *u, double *lam_trace, uint32_t *err,     \
+        const double *__restrict__ X, int ldx, int n_pad, int nchunk, double *__restrict__ xu_part
+template <int L, int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void
+k_lambda_xu(BB_LXU_ARGS) {
+    lambda_xu_body<L, NR>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx,
+                          n_pad, nchunk, xu_part);
+}
+// capped at 128 VGPRs for 4 waves per SIMD (bb_set_tuning key 4 bit 0, as k_lambda_spec_o4)
+template <int L, int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_lambda_xu_o4(BB_LXU_ARGS) {
+    lambda_xu_body<L, NR>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx,
+                          n_pad, nchunk, xu_part);
+}
+#undef BB_LXU_ARGS
+
 // (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
 // chunk per workgroup, the hardware scheduling them -- more partials, no static tail, and the
 // workgroups' draw and stream phases drift apart; bb_set_tuning key 7 picks the mode)
@@ -541,9 +560,11 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     const int L = spec_lanes(p_loc);
     const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
     const int nr = (n_pad + 255) / 256;
+    const bool o4 = (g_lam_occ & 1) != 0;
 #define BB_LXU(LL, NN)                                                                        \
-    k_lambda_xu<LL, NN><<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u,      \
-                                          lam_trace, err, X, ldx, n_pad, nchunk, xu_part)
+    (o4 ? k_lambda_xu_o4<LL, NN> : k_lambda_xu<LL, NN>)<<<G, 256, 0, s>>>(                   \
+        beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad, nchunk,  \
+        xu_part)
     if (L == 8) {
         if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
     } else {

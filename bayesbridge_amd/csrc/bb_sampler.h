@@ -178,15 +178,32 @@ struct StableParams {
     double neg_inv_alpha, inv_ia, inv_alpha;
 };
 
+// a wave-uniform double held in scalar registers (readfirstlane of both halves)
+__device__ __forceinline__ double uniform_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// UA: alpha and V0 are the same on every lane of the wave (the lambda launches and the small
+// chain; not retstable_LD's batch, whose arguments are per draw), so the alpha-only
+// constants are kept in scalar registers -- 16 VGPRs fewer across the sampler loop.
+template <bool UA = false>
 __device__ __forceinline__ StableParams stable_params(double h, double alpha, double V0) {
     StableParams s;
+    if constexpr (UA) {
+        alpha = uniform_d(alpha);
+        V0 = uniform_d(V0);
+    }
+    auto un = [](double v) { return UA ? uniform_d(v) : v; };
     s.h = h;
     s.alpha = alpha;
-    s.ia = 1. - alpha;
+    s.ia = un(1. - alpha);
     s.V0 = V0;
     s.c1 = sqrt(kPi2);
     const double c2 = 2. + s.c1;
-    s.b = (1. - alpha) / alpha;
+    s.b = un((1. - alpha) / alpha);
     s.lambda_alpha = powp(h, alpha) * V0;
     s.gamma = s.lambda_alpha * alpha * (1. - alpha);
     s.sgamma = sqrt(s.gamma);
@@ -198,10 +215,10 @@ __device__ __forceinline__ StableParams stable_params(double h, double alpha, do
     const double w3 = s.xi * kPi;
     s.thr_w1 = w1 / (w1 + w2);
     s.thr_w3 = w3 / (w2 + w3);
-    s.neg_inv_alpha = -1 / alpha;
-    s.inv_ia = 1. / (1. - alpha);
-    s.inv_alpha = 1 / alpha;
-    s.c_alpha = powp(s.ia, s.ia) * powp(alpha, alpha);
+    s.neg_inv_alpha = un(-1 / alpha);
+    s.inv_ia = un(1. / (1. - alpha));
+    s.inv_alpha = un(1 / alpha);
+    s.c_alpha = un(powp(s.ia, s.ia) * powp(alpha, alpha));
     return s;
 }
 
@@ -316,7 +333,7 @@ __device__ __forceinline__ double stable_finish(const StableParams &s, double X)
 // lowest accepted inner attempt (counter order) feeds the outer test, which every lane of
 // the group evaluates on identical inputs.  This reproduces the sequential double
 // rejection loop exactly.  Every lane of the wave must call this (ballot/shuffle inside).
-template <int G, bool NI = (BB_STABLE_NOINLINE != 0)>
+template <int G, bool NI = (BB_STABLE_NOINLINE != 0), bool UA = false>
 __device__ inline double stable_group_draw(bool active, double h, double alpha, double V0,
                                            Key key, uint64_t t, uint64_t j, uint32_t *err) {
     const int lane = threadIdx.x & 63;
@@ -329,7 +346,7 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
     StableParams s;
     if (active) {
         if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) atomicOr(err, 4u);  // :112-115
-        s = stable_params(h, alpha, V0);
+        s = stable_params<UA>(h, alpha, V0);
     }
     uint64_t o = 0, ib = 0;
     for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
@@ -373,7 +390,7 @@ __device__ inline double stable_group_draw(bool active, double h, double alpha, 
 // outer attempts before it were rejected exactly as the sequential loop rejects them, so the
 // draw is the same as stable_group_draw's.  About 1 in 8 draws needs a second round at
 // I = 8, O = 4 (inner acceptance ~0.3, outer ~0.7 at alpha = 0.25).
-template <int L, int I>
+template <int L, int I, bool UA = true>
 __device__ __forceinline__ double stable_spec_draw(bool active, double h, double alpha, double V0, Key key,
                                           uint64_t t, uint64_t j, uint32_t *err) {
     static_assert(L <= 64 && (L & (L - 1)) == 0 && L % I == 0 && I < 64, "group shape");
@@ -388,7 +405,7 @@ __device__ __forceinline__ double stable_spec_draw(bool active, double h, double
     StableParams s;
     if (active) {
         if (h < 0 || alpha < 0 || alpha > 1 || V0 < 0) atomicOr(err, 4u);  // :112-115
-        s = stable_params(h, alpha, V0);
+        s = stable_params<UA>(h, alpha, V0);
     }
     uint64_t o0 = 0, ib = 0;  // window's first outer attempt, its next inner attempt
     for (int iter = 0; iter < BB_MAX_STABLE_ROUNDS; ++iter) {
