@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round profile of the bench workload (run on the GPU box):
-#   1. rocprofv3 --kernel-trace --stats       -> per-kernel average durations
+#   1. rocprofv3 --kernel-trace --stats       -> per-kernel average durations (the driver's
+#      --steps 20 --warmup 5)
 #   2. rocprofv3 --pmc FETCH_SIZE  (own pass) -> HBM read KB per dispatch
 #   3. rocprofv3 --pmc WRITE_SIZE  (own pass) -> HBM write KB per dispatch
 # No --pmc pass is combined with any trace domain.  Each step has its own time limit and
@@ -13,7 +14,7 @@ mkdir -p "$OUT"
 ARGS="--no-cpu-baseline $*"
 set -o pipefail
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
-    -- python3 bench.py --steps 10 --warmup 2 $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
+    -- python3 bench.py --steps 20 --warmup 5 $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
     || { echo "kernel-trace pass failed ($?)"; exit 1; }
 echo "kernel-trace pass ok"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \

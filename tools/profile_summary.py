@@ -54,8 +54,9 @@ def main():
     try:  # the bench line the kernel-trace pass printed
         line = [l for l in open(os.path.join(src, "kt_bench.json")) if l.startswith("{")][-1]
         bench = json.loads(line)
-        cfg = bench.get("config", {})
+        cfg = dict(bench.get("config", {}))
         n, p = int(cfg.get("n", n)), int(cfg.get("p", p))
+        cfg["_steps"] = f"--steps {bench.get('steps')} --warmup {bench.get('warmup')} "
     except (OSError, IndexError, ValueError):
         pass
     wl = cfg.get("workload", "")
@@ -66,7 +67,8 @@ def main():
     shutil.copy(ks, os.path.join(dst, f"{rnd}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(ks)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    lines = [f"# rocprofv3 --kernel-trace --stats of: python3 bench.py --steps 10 --warmup 2 "
+    steps = cfg.get("_steps", "")
+    lines = [f"# rocprofv3 --kernel-trace --stats of: python3 bench.py {steps}"
              f"--no-cpu-baseline ({wl or f'n={n}, p={p}'}, 1 GPU)",
              f"{'kernel':48s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'tot_ms':>9s}  share"]
     avg_us = {}
