@@ -240,7 +240,9 @@ k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
 // at either occupancy; C5 k_lambda_cb<8> 0.418-0.428 -> 0.402-0.407 ms at 4 waves; round 4
 // (gpurun_out/r04k_*, two alternations at the driver's settings): C5 inlined 1933-1939
 // sweeps/s against 1824-1831 out of line at 4 waves (lambda 0.334-0.341 against 0.351-0.356
-// ms).  Default 4.
+// ms); the fused k_lambda_xu and k_lambda_spec at 4 waves (bit 0, 128 VGPRs with 92-124 B of
+// spills) are slower: C3 1791-1794 against 1944-1948 sweeps/s, C2 6097-6114 against 6312-6423
+// (gpurun_out/r04n_*).  Default 4.
 int g_lam_occ = 4;
 
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
