@@ -582,15 +582,19 @@ struct bb_engine {
         }
         exchange(nid_red, (size_t)kNidRed);
         nidx_decide_launch();
-        // An unsharded engine enqueues the start of the Chebyshev solve before it waits for
-        // the decision -- X u, the initial iterate and one product, each returning at once
-        // unless the device decided so -- so the device runs them while the host wakes up
-        // (no bubble on the common near-identity sweep); the rest follows the decision.
-        const int spec = (cfg.world == 1 && g_nid_sync != 2) ? 2 : 0;
+        // The start of the Chebyshev solve is enqueued before the host waits for the
+        // decision -- X u, the initial iterate and one product, each returning at once unless
+        // the device decided so -- so the device runs them while the host wakes up (no bubble
+        // on the common near-identity sweep); the rest follows the decision.  A shard's two
+        // exchanges among them run on every rank whatever the decision (the same sequence of
+        // collectives everywhere; on a factor sweep they carry unused vectors).
+        const int spec = g_nid_sync != 2 ? 2 : 0;
         if (spec) {
             nidx_xu();
+            if (cfg.world > 1) exchange(nid_sum, (size_t)n_pad);
             nidx_init(t);
             nidx_eapply(1);
+            if (cfg.world > 1) exchange(nid_sum, (size_t)n_pad);
             nidx_step(1);
         }
         const int K = nidx_decide_read();
