@@ -77,6 +77,7 @@ __global__ __launch_bounds__(NT) void k_small_chain(
     uint32_t *err) {
     extern __shared__ double sX[];
     __shared__ double sU[kSmallMaxP][kSmallMaxP + 1];  // U, row-major (U[k][j])
+    __shared__ double s_row[2][kSmallMaxP];  // the next pivot row, unscaled (double-buffered)
     __shared__ double sG[kSmallMaxP][kSmallMaxP + 1];
     __shared__ double sb[kSmallMaxP], sl[kSmallMaxP], sc_[kSmallMaxP], sgd[kSmallMaxP];
     // Ga(shape, 1) variates of tau and sig2 and the beta normals of the next kSmallPre
@@ -207,38 +208,42 @@ __global__ __launch_bounds__(NT) void k_small_chain(
             }
         } else {
             // A = G + diag(lambda sig2 / tau^2), factored right-looking as A = U'U with one
-            // thread per upper-triangle entry (i, j) (two for the last 16 at p = 32): per
-            // pivot k the owner of (k, k) takes the square root, the owners of row k divide
-            // (row k of U goes to LDS), every trailing owner subtracts U(k, i) U(k, j) -- the
-            // reference's operations entry by entry (BridgeRegression.cpp:560), two barriers
-            // per pivot and no register arrays
+            // thread per upper-triangle entry (i, j) (two for the last 16 at p = 32), ONE
+            // barrier per pivot: the owners of row k publish its unscaled entries a_kj (all
+            // earlier updates applied) to an LDS row buffer at the end of step k - 1; at step
+            // k every trailing owner subtracts a_ki a_kj / a_kk -- U(k, i) U(k, j) of the
+            // reference's right-looking factor (BridgeRegression.cpp:560), the same value to
+            // rounding -- while the owners of row k form U(k, j) = a_kj / sqrt(a_kk) and those
+            // of row k + 1 publish theirs.  (Two barriers per pivot -- the square root, then
+            // the row division, then the update -- put three dependent steps on the path.)
             const double dl = tau * tau;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (own[h]) {
                     const int i = oi[h], j = oj[h];
                     av[h] = sG[i][j] + (i == j ? sl[i] * sig2 / dl : 0.0);
+                    if (i == 0) s_row[0][j] = av[h];
                 }
+            __syncthreads();
             for (int kk = 0; kk < p; ++kk) {
+                const double *r = s_row[kk & 1];
+                const double akk = r[kk];
+                const double rs = sqrt(akk);
+                const double dinv = 1.0 / akk;
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (own[h] && oi[h] == kk && oj[h] == kk) {
-                        if (!(av[h] > 0.0)) atomicOr(err, 8u);
-                        av[h] = sqrt(av[h]);
-                        sU[kk][kk] = av[h];
+                for (int h = 0; h < 2; ++h) {
+                    if (!own[h]) continue;
+                    const int i = oi[h], j = oj[h];
+                    if (i == kk) {
+                        if (j == kk && !(akk > 0.0)) atomicOr(err, 8u);
+                        av[h] = j == kk ? rs : av[h] / rs;
+                        sU[kk][j] = av[h];
+                    } else if (i > kk) {
+                        av[h] -= (r[i] * dinv) * r[j];
+                        if (i == kk + 1) s_row[(kk + 1) & 1][j] = av[h];
                     }
+                }
                 __syncthreads();
-                const double d = sU[kk][kk];
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (own[h] && oi[h] == kk && oj[h] > kk) {
-                        av[h] = av[h] / d;
-                        sU[kk][oj[h]] = av[h];
-                    }
-                __syncthreads();
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (own[h] && oi[h] > kk) av[h] -= sU[kk][oi[h]] * sU[kk][oj[h]];
             }
             if (wid == 0) {
                 // m: U'v = c (forward), U m = v (backward); x: U x = z; lane j holds entry j
