@@ -228,15 +228,19 @@ __global__ __launch_bounds__(NT) void k_small_chain(
             for (int kk = 0; kk < p; ++kk) {
                 const double *r = s_row[kk & 1];
                 const double akk = r[kk];
-                const double rs = sqrt(akk);
-                const double dinv = 1.0 / akk;
+                // 1 / sqrt(a_kk): the hardware estimate and two Newton steps (~1 ulp), one
+                // short sequence for both the row scale and the trailing 1 / a_kk
+                double rs = __builtin_amdgcn_rsq(akk);
+                rs = rs * __builtin_fma(-0.5 * akk * rs, rs, 1.5);
+                rs = rs * __builtin_fma(-0.5 * akk * rs, rs, 1.5);
+                const double dinv = rs * rs;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (!own[h]) continue;
                     const int i = oi[h], j = oj[h];
                     if (i == kk) {
                         if (j == kk && !(akk > 0.0)) atomicOr(err, 8u);
-                        av[h] = j == kk ? rs : av[h] / rs;
+                        av[h] = j == kk ? akk * rs : av[h] * rs;
                         sU[kk][j] = av[h];
                     } else if (i > kk) {
                         av[h] -= (r[i] * dinv) * r[j];
