@@ -67,11 +67,14 @@ void small_phase_ticks(unsigned long long out[4]) {
 // L lanes per coefficient in the lambda draw (stable_spec_draw<L, I>), the p x p system
 // dynamic LDS holds
 // X (n x p, column-major) when it fits, else X is read from HBM each sweep.
+// bb_set_tuning key 9: the p x p factor with one barrier per pivot (1) or in the reference's
+// order with two (0)
+int g_small_chol1 = 1;
 template <int NT, int L, int I>
 __global__ __launch_bounds__(NT) void k_small_chain(
     const double *__restrict__ X, int ldx, int n, int p, const double *__restrict__ y,
     const double *__restrict__ G, int ldg, const double *__restrict__ cvec,
-    const double *__restrict__ gdiag, int ortho, int x_lds, double *beta, double *lam,
+    const double *__restrict__ gdiag, int ortho, int chol1, int x_lds, double *beta, double *lam,
     DevScalars *sc, Hyper hy, Key key, uint64_t t0, int count, int first_slot, int slot_step,
     int cap, double *tr_beta, double *tr_lam, double *tr_sig2, double *tr_tau, double *tr_alpha,
     uint32_t *err) {
@@ -225,6 +228,7 @@ __global__ __launch_bounds__(NT) void k_small_chain(
                     if (i == 0) s_row[0][j] = av[h];
                 }
             __syncthreads();
+            if (chol1) {
             for (int kk = 0; kk < p; ++kk) {
                 const double *r = s_row[kk & 1];
                 const double akk = r[kk];
@@ -248,6 +252,33 @@ __global__ __launch_bounds__(NT) void k_small_chain(
                     }
                 }
                 __syncthreads();
+            }
+            } else {
+            // the reference's order entry by entry (chol1 = 0): per pivot k the owner of
+            // (k, k) takes the square root, the owners of row k divide (row k of U goes to
+            // LDS), every trailing owner subtracts U(k, i) U(k, j); two barriers per pivot
+            for (int kk = 0; kk < p; ++kk) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] == kk && oj[h] == kk) {
+                        if (!(av[h] > 0.0)) atomicOr(err, 8u);
+                        av[h] = sqrt(av[h]);
+                        sU[kk][kk] = av[h];
+                    }
+                __syncthreads();
+                const double d = sU[kk][kk];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] == kk && oj[h] > kk) {
+                        av[h] = av[h] / d;
+                        sU[kk][oj[h]] = av[h];
+                    }
+                __syncthreads();
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (own[h] && oi[h] > kk) av[h] -= sU[kk][oi[h]] * sU[kk][oj[h]];
+            }
+            __syncthreads();
             }
             if (wid == 0) {
                 // m: U'v = c (forward), U m = v (backward); x: U x = z; lane j holds entry j
@@ -313,7 +344,8 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
     small_chain_lds_optin<512, 32, 8>();
     small_chain_lds_optin<512, 16, 8>();
     auto go = [&](auto kern, int nt) {
-        kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, x_lds, beta, lam, sc,
+        kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, g_small_chol1, x_lds,
+                                beta, lam, sc,
                                 hy, Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta,
                                 tr_lam, tr_sig2, tr_tau, tr_alpha, err);
     };
