@@ -3384,11 +3384,6 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_lam_xu = value > 2 ? 2 : value;
             return old;
         }
-        case 9: {
-            const int old = g_small_chol1;
-            if (value >= 0) g_small_chol1 = value ? 1 : 0;
-            return old;
-        }
         case 8: {
             const int old = g_nid_sync;
             if (value >= 0) g_nid_sync = value > 2 ? 2 : value;

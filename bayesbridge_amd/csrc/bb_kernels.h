@@ -148,7 +148,6 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
                      int ldx, int n_pad, double *xu_part);
 extern int g_lam_xu;
-extern int g_small_chol1;  // bb_small.hip: the small chain's p x p factor variant (key 9)
 
 void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
                            uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,

@@ -67,20 +67,16 @@ void small_phase_ticks(unsigned long long out[4]) {
 // L lanes per coefficient in the lambda draw (stable_spec_draw<L, I>), the p x p system
 // dynamic LDS holds
 // X (n x p, column-major) when it fits, else X is read from HBM each sweep.
-// bb_set_tuning key 9: the p x p factor with one barrier per pivot (1) or in the reference's
-// order with two (0)
-int g_small_chol1 = 1;
 template <int NT, int L, int I>
 __global__ __launch_bounds__(NT) void k_small_chain(
     const double *__restrict__ X, int ldx, int n, int p, const double *__restrict__ y,
     const double *__restrict__ G, int ldg, const double *__restrict__ cvec,
-    const double *__restrict__ gdiag, int ortho, int chol1, int x_lds, double *beta, double *lam,
+    const double *__restrict__ gdiag, int ortho, int x_lds, double *beta, double *lam,
     DevScalars *sc, Hyper hy, Key key, uint64_t t0, int count, int first_slot, int slot_step,
     int cap, double *tr_beta, double *tr_lam, double *tr_sig2, double *tr_tau, double *tr_alpha,
     uint32_t *err) {
     extern __shared__ double sX[];
     __shared__ double sU[kSmallMaxP][kSmallMaxP + 1];  // U, row-major (U[k][j])
-    __shared__ double s_row[2][kSmallMaxP];  // the next pivot row, unscaled (double-buffered)
     __shared__ double sG[kSmallMaxP][kSmallMaxP + 1];
     __shared__ double sb[kSmallMaxP], sl[kSmallMaxP], sc_[kSmallMaxP], sgd[kSmallMaxP];
     // Ga(shape, 1) variates of tau and sig2 and the beta normals of the next kSmallPre
@@ -211,52 +207,22 @@ __global__ __launch_bounds__(NT) void k_small_chain(
             }
         } else {
             // A = G + diag(lambda sig2 / tau^2), factored right-looking as A = U'U with one
-            // thread per upper-triangle entry (i, j) (two for the last 16 at p = 32), ONE
-            // barrier per pivot: the owners of row k publish its unscaled entries a_kj (all
-            // earlier updates applied) to an LDS row buffer at the end of step k - 1; at step
-            // k every trailing owner subtracts a_ki a_kj / a_kk -- U(k, i) U(k, j) of the
-            // reference's right-looking factor (BridgeRegression.cpp:560), the same value to
-            // rounding -- while the owners of row k form U(k, j) = a_kj / sqrt(a_kk) and those
-            // of row k + 1 publish theirs.  (Two barriers per pivot -- the square root, then
-            // the row division, then the update -- put three dependent steps on the path.)
+            // thread per upper-triangle entry (i, j) (two for the last 16 at p = 32): per
+            // pivot k the owner of (k, k) takes the square root, the owners of row k divide
+            // (row k of U goes to LDS), every trailing owner subtracts U(k, i) U(k, j) -- the
+            // reference's operations entry by entry (BridgeRegression.cpp:560), two barriers
+            // per pivot and no register arrays.  (One barrier per pivot -- trailing owners
+            // subtracting a_ki a_kj / a_kk from a published unscaled row, one reciprocal square
+            // root per pivot -- measured the same at C1 in three alternations, 27 176-27 186
+            // against 27 152-27 188 sweeps/s, gpurun_out/r04q_*: the factor is not what bounds
+            // the chain.)
             const double dl = tau * tau;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (own[h]) {
                     const int i = oi[h], j = oj[h];
                     av[h] = sG[i][j] + (i == j ? sl[i] * sig2 / dl : 0.0);
-                    if (i == 0) s_row[0][j] = av[h];
                 }
-            __syncthreads();
-            if (chol1) {
-            for (int kk = 0; kk < p; ++kk) {
-                const double *r = s_row[kk & 1];
-                const double akk = r[kk];
-                // 1 / sqrt(a_kk): the hardware estimate and two Newton steps (~1 ulp), one
-                // short sequence for both the row scale and the trailing 1 / a_kk
-                double rs = __builtin_amdgcn_rsq(akk);
-                rs = rs * __builtin_fma(-0.5 * akk * rs, rs, 1.5);
-                rs = rs * __builtin_fma(-0.5 * akk * rs, rs, 1.5);
-                const double dinv = rs * rs;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (!own[h]) continue;
-                    const int i = oi[h], j = oj[h];
-                    if (i == kk) {
-                        if (j == kk && !(akk > 0.0)) atomicOr(err, 8u);
-                        av[h] = j == kk ? akk * rs : av[h] * rs;
-                        sU[kk][j] = av[h];
-                    } else if (i > kk) {
-                        av[h] -= (r[i] * dinv) * r[j];
-                        if (i == kk + 1) s_row[(kk + 1) & 1][j] = av[h];
-                    }
-                }
-                __syncthreads();
-            }
-            } else {
-            // the reference's order entry by entry (chol1 = 0): per pivot k the owner of
-            // (k, k) takes the square root, the owners of row k divide (row k of U goes to
-            // LDS), every trailing owner subtracts U(k, i) U(k, j); two barriers per pivot
             for (int kk = 0; kk < p; ++kk) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
@@ -277,8 +243,6 @@ __global__ __launch_bounds__(NT) void k_small_chain(
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                     if (own[h] && oi[h] > kk) av[h] -= sU[kk][oi[h]] * sU[kk][oj[h]];
-            }
-            __syncthreads();
             }
             if (wid == 0) {
                 // m: U'v = c (forward), U m = v (backward); x: U x = z; lane j holds entry j
@@ -344,8 +308,7 @@ void launch_small_chain(hipStream_t s, const double *X, int ldx, int n, int p, c
     small_chain_lds_optin<512, 32, 8>();
     small_chain_lds_optin<512, 16, 8>();
     auto go = [&](auto kern, int nt) {
-        kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, g_small_chol1, x_lds,
-                                beta, lam, sc,
+        kern<<<1, nt, shm, s>>>(X, ldx, n, p, y, G, ldg, cvec, gdiag, ortho, x_lds, beta, lam, sc,
                                 hy, Key{k0, k1}, t0, count, first_slot, slot_step, cap, tr_beta,
                                 tr_lam, tr_sig2, tr_tau, tr_alpha, err);
     };

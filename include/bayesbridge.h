@@ -347,10 +347,7 @@ void bb_set_trace_budget(long long bytes);
  * Chebyshev solve's first kernels enqueued before the wait and returning at once unless the
  * device decided so; 2: without them) or launches both
  * paths with the kernels of the one not taken returning at once (0); the draws are the same
- * except on sweeps where mode 0's launch hint fell short (it then takes the factor);
- * key 9: the small-p chain (p <= 32, one launch per block of sweeps) factors its p x p system
- * with one barrier per pivot (1, the default) or in the reference's order with two (0); the
- * same values to rounding.
+ * except on sweeps where mode 0's launch hint fell short (it then takes the factor).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
