@@ -355,6 +355,7 @@ struct bb_engine {
     hipEvent_t nid_sev = nullptr;
     bool nid_only = false;
     bool group_member = false;
+    int nid_last = -1;  // the previous sweep's decided K (-1: none since init_state)
     // communicator (own_comm false: lent by an RCCL shard group, which destroys it)
     ncclComm_t comm = nullptr;
     bool own_comm = true;
@@ -599,6 +600,7 @@ struct bb_engine {
         }
         const int K = nidx_decide_read();
         nid_only = K > 0;
+        nid_last = K;
         if (K > 0) {
             if (!spec) {
                 nidx_xu();
@@ -693,9 +695,12 @@ struct bb_engine {
             const bool sync = nid_sync();
             const int kl = (!sync && nid_enabled()) ? nid_launch_count() : 0;
             // a sweep that may take the Chebyshev path draws lambda and forms the X u partials
-            // in one launch (k_lambda_xu, dense)
+            // in one launch (k_lambda_xu, dense); under the synchronous protocol unless the
+            // previous sweep took the factor (then X u would be streamed for nothing: the
+            // residue pass forms it; a sweep that turns back to the Chebyshev path streams X u
+            // in its own pass)
             xu_fused = 0;
-            if (method == 2 && (sync || kl > 0))
+            if (method == 2 && (sync ? nid_last != 0 : kl > 0))
                 xu_fused = launch_lambda_xu(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc,
                                             cfg.seed, cfg.stream, t, lam, D, u, trl, err, X,
                                             n_pad, n_pad, nid_xu);
@@ -1345,6 +1350,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
 
 void engine_init_state_local(bb_engine *e) {
     const bb_config &c = e->cfg;
+    e->nid_seq = 0;  // the near-identity launch hint restarts with the chain
+    e->nid_last = -1;
     // least squares start (BridgeWrapper.cpp:242-244, BridgeRegression.cpp:79-91)
     bool ls_ok = false;
     if (e->G != nullptr) {
@@ -1397,7 +1404,6 @@ void engine_init_state_local(bb_engine *e) {
 }
 
 void engine_init_state(bb_engine *e) {
-    e->nid_seq = 0;  // the near-identity launch hint restarts with the chain
     engine_init_state_local(e);
     if (e->method == 4 && e->cfg.ortho) {
         // triangle ortho driver draws sig2 then tau before burn-in (BridgeWrapper.cpp:374-375)
@@ -2049,7 +2055,10 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
                     m->nidx_decide_launch();
                 }
                 const int K = m0->nidx_decide_read();
-                for (auto *m : g->members) m->nid_only = K > 0;
+                for (auto *m : g->members) {
+                    m->nid_only = K > 0;
+                    m->nid_last = K;
+                }
                 if (K > 0) {
                     for (auto *m : g->members) {
                         g->on(m);
