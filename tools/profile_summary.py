@@ -116,7 +116,7 @@ def main():
             algo[k] = 16.0 * n_oz * k_pad
     if sparse:  # the pair-list Gram's algorithmic bytes as bench.py counts them
         rf = bench["roofline"] if bench["roofline"].get("phase") == "gram" else \
-            bench.get("roofline_secondary", {})
+            (bench.get("roofline_secondary") or {})
         algo = {k: rf.get("algorithmic_bytes_per_launch") for k in out["kernels"]
                 if k.startswith("bb::k_sp_gram_col") or k.startswith("bb::k_sp_gram_flat")}
     out["workload"]["name"] = wl or None
