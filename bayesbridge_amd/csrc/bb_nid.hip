@@ -425,7 +425,7 @@ int eapply_parts(int p_loc, int n_pad) {
 bool eapply_supported(int n_pad) { return n_pad <= 16 * kEaThreads; }
 
 
-int nid_sum_groups(int p_loc) { return std::max(1, std::min(256, (p_loc + 1023) / 1024)); }
+int nid_sum_groups(int p_loc) { return std::max(1, std::min(256, (p_loc + 255) / 256)); }
 
 void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc,
                      const DevScalars *sc, NidState *nid, int k_launched, int allow, int decide,
