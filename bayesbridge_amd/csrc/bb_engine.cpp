@@ -3374,7 +3374,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 4: {
             const int old = g_lam_occ;
-            if (value >= 0) g_lam_occ = value & 7;
+            if (value >= 0) g_lam_occ = value & 15;
             return old;
         }
         case 5: {

@@ -598,12 +598,15 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     long threads = (long)p_pad * group;
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
-    if (p_loc <= kLamSpecMax) {
+    // bb_set_tuning key 4 bit 3: the continuous-batching launch also for p in
+    // (kLamSpecNarrow, kLamSpecMax], where the speculative launch is the default (A/B)
+    const bool force_cb = (g_lam_occ & 8) && p_loc > kLamSpecNarrow;
+    if (p_loc <= kLamSpecMax && !force_cb) {
         launch_spec(s, spec_lanes(p_loc), 0, beta, p_loc, p_pad, j0, sc, key, t,
                     mode, lam, D, u, lam_trace, err, PgTail{});
         return;
     }
-    if (ni && group == 8) {
+    if ((ni && group == 8) || force_cb) {
         // 4 workgroups of 4 waves per CU (the out-of-line sampler's occupancy; 3 inlined)
         const bool inl = (g_lam_occ & 4) != 0;
         const int nwg = std::max(1, std::min((inl ? 3 : 4) * device_cus_lam(), (p_pad + 31) / 32));
