@@ -13,7 +13,7 @@ from tests.conftest import synthetic_problem
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,p", [(200, 3000), (60, 60000)])
+@pytest.mark.parametrize("n,p", [(200, 3000), (50, 45000), (60, 60000)])
 def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
     bb = gpu_lib
     X, y, _ = synthetic_problem(n, p, seed=11, s=10)
@@ -21,7 +21,7 @@ def test_lambda_occupancy_variants_same_chain(gpu_lib, n, p):
     old = bb.set_tuning(4, -1)
     old6 = bb.set_tuning(6, 0)  # the separate lambda launch on every sweep (no fused X u)
     try:
-        for occ in (0, 3, 4, 5):
+        for occ in (0, 3, 4, 5, 12):
             bb.set_tuning(4, occ)
             e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=6,
                                           seed=77, stream=0), X, y)
