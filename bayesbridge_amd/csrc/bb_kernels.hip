@@ -242,8 +242,10 @@ k_lambda_spec_o4(BB_LAMBDA_SPEC_ARGS) {
 // sweeps/s against 1824-1831 out of line at 4 waves (lambda 0.334-0.341 against 0.351-0.356
 // ms); the fused k_lambda_xu and k_lambda_spec at 4 waves (bit 0, 128 VGPRs with 92-124 B of
 // spills) are slower: C3 1791-1794 against 1944-1948 sweeps/s, C2 6097-6114 against 6312-6423
-// (gpurun_out/r04n_*).  Default 4.
-int g_lam_occ = 4;
+// (gpurun_out/r04n_*).  Bit 3: the inlined continuous-batching launch also for
+// 40000 < p <= 50000 (the separate launch of C3's fitted-regime sweeps): lambda 0.157-0.161
+// against 0.169-0.174 ms for k_lambda_spec<8> (gpurun_out/r04s_*).  Default 12.
+int g_lam_occ = 12;
 
 // Large batches (p_loc >= 20000): continuous batching.  A launch of stable_group_draw is
 // as long as its slowest wave, and a wave is as long as the slowest of its G-lane groups'

@@ -334,8 +334,9 @@ void bb_set_trace_budget(long long bytes);
  * key 4: occupancy of the lambda launches, bit 0 = k_lambda_spec and bit 1 = k_lambda_cb
  * capped at 128 VGPRs for 4 waves per SIMD instead of their register-minimal 3 (default 2:
  * k_lambda_cb only: 4 % faster at C5 than 3 waves); bit 2: k_lambda_cb with the sampler
- * bodies inlined (3 waves per SIMD) instead -- the default (value 4), 6 % faster at C5 than
- * the out-of-line instance at 4 waves; the draws are the same;
+ * bodies inlined (3 waves per SIMD) instead, 6 % faster at C5 than the out-of-line instance at
+ * 4 waves; bit 3: that launch also for 40000 < p <= 50000 (7 % faster than the speculative
+ * launch there); default 12 (bits 2 and 3); the draws are the same;
  * key 5: lanes per coefficient of the speculative lambda launch (0 = the size-based default);
  * key 6: the most Chebyshev iterations a Woodbury sweep may take on the near-identity path
  * (default 16; 0 = every sweep forms the Gram and factors it);
