@@ -600,9 +600,10 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
     long threads = (long)p_pad * group;
     int blocks = (int)((threads + 255) / 256);
     const bool ni = stable_noinline_for(p_loc);
-    // bb_set_tuning key 4 bit 3: the continuous-batching launch also for p in
-    // (kLamSpecNarrow, kLamSpecMax], where the speculative launch is the default (A/B)
-    const bool force_cb = (g_lam_occ & 8) && p_loc > kLamSpecNarrow;
+    // bb_set_tuning key 4 bit 3 (default on): the continuous-batching launch also for p in
+    // (kLamSpecNarrow, kLamSpecMax]; a lane count forced through key 5 takes the speculative
+    // launch
+    const bool force_cb = (g_lam_occ & 8) && p_loc > kLamSpecNarrow && !g_lam_lanes;
     if (p_loc <= kLamSpecMax && !force_cb) {
         launch_spec(s, spec_lanes(p_loc), 0, beta, p_loc, p_pad, j0, sc, key, t,
                     mode, lam, D, u, lam_trace, err, PgTail{});
