@@ -66,7 +66,8 @@ EXPORTED_SYMBOLS = [
     "bb_bench_sparse_gram", "bb_engine_sparse_info", "bridge_reg_logit", "bb_engine_get_omega",
     "bb_pg_batch", "bb_group_create_rccl", "bb_group_sync", "bb_set_device_count",
     "bb_set_trace_budget", "bb_debug_interrupt_after", "bb_last_call_info",
-    "bb_engine_set_timed_phase", "bb_set_chol_version", "bb_set_tuning",
+    "bb_engine_set_timed_phase", "bb_engine_set_timing_stride", "bb_set_chol_version",
+    "bb_set_tuning",
 ]
 
 
@@ -112,6 +113,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_enable_timing.argtypes = [c.c_void_p, c.c_int]
     L.bb_engine_reset_timing.argtypes = [c.c_void_p]
     L.bb_engine_set_timed_phase.argtypes = [c.c_void_p, c.c_int]
+    L.bb_engine_set_timing_stride.argtypes = [c.c_void_p, c.c_int]
     L.bb_engine_kernel_times.argtypes = [c.c_void_p, _dp, _dp, _ip]
     L.bb_engine_error_flags.argtypes = [c.c_void_p, c.POINTER(c.c_uint32)]
     L.bb_retstable_batch.argtypes = [_dp, _dp, _dp, _dp, c.c_int, c.c_uint64, c.c_uint64,
@@ -1040,14 +1042,17 @@ class Engine:
         _check(library().bb_engine_set_state(self._h, _p(beta), tau, sig2, alpha),
                "bb_engine_set_state")
 
-    def enable_timing(self, on: bool = True, phases: bool = True, timed_phase: str = "gram"):
+    def enable_timing(self, on: bool = True, phases: bool = True, timed_phase: str = "gram",
+                      stride: int = 1):
         """HIP-event timing on the engine stream: every phase start (phases=True) or only
-        the bracket of `timed_phase` (a bb_phase_name, two events per sweep, used inside
-        timed loops; kernel_times()[0] is its average)."""
+        the bracket of `timed_phase` (a bb_phase_name, two events per bracketed sweep, used
+        inside timed loops; kernel_times()[0] is its average) in every `stride`-th sweep."""
         L = library()
         names = [L.bb_phase_name(i).decode() for i in range(L.bb_phase_count())]
         _check(L.bb_engine_set_timed_phase(self._h, names.index(timed_phase)),
                "bb_engine_set_timed_phase")
+        _check(L.bb_engine_set_timing_stride(self._h, int(stride)),
+               "bb_engine_set_timing_stride")
         L.bb_engine_enable_timing(self._h, (2 if phases else 1) if on else 0)
 
     def reset_timing(self):

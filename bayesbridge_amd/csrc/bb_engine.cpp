@@ -363,6 +363,7 @@ struct bb_engine {
     bool timing = false;
     int timing_level = 2;  // 1: one phase's bracket only (timed_phase), 2: every phase
     int timed_phase = PH_GRAM;
+    int timing_stride = 1;  // level 1: bracket every timing_stride-th sweep
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::vector<std::pair<int, int>>> sweep_marks;  // (phase, event)
     size_t ev_next = 0;
@@ -372,6 +373,7 @@ struct bb_engine {
         // level 1: only the timed phase's bracket (its start and the next mark), so a timed
         // run carries two events per sweep instead of one per phase
         if (timing_level == 1) {
+            if ((sweep_marks.size() - 1) % (size_t)timing_stride != 0) return;
             const bool open = !sweep_marks.back().empty() &&
                               sweep_marks.back().back().first == timed_phase;
             if (phase != timed_phase && !open) return;
@@ -1731,6 +1733,15 @@ int bb_engine_set_timed_phase(bb_engine *e, int phase) {
     return 0;
 }
 
+int bb_engine_set_timing_stride(bb_engine *e, int stride) {
+    if (stride < 1) {
+        set_error("bb_engine_set_timing_stride: stride %d < 1", stride);
+        return -1;
+    }
+    e->timing_stride = stride;
+    return 0;
+}
+
 int bb_engine_reset_timing(bb_engine *e) {
     (void)hipStreamSynchronize(e->stream);
     e->sweep_marks.clear();
@@ -1767,7 +1778,7 @@ int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_a
     try {
         HIPCHECK(hipStreamSynchronize(e->stream));
         double g = 0, s = 0;
-        int ng = 0;
+        int ng = 0, ns = 0;
         for (auto &marks : e->sweep_marks) {
             for (size_t i = 0; i + 1 < marks.size(); ++i)
                 if (marks[i].first == e->timed_phase) {
@@ -1782,11 +1793,12 @@ int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_a
                 HIPCHECK(hipEventElapsedTime(&v, e->ev_pool[marks.front().second],
                                              e->ev_pool[marks.back().second]));
                 s += v;
+                ++ns;
             }
         }
         if (gram_ms_avg) *gram_ms_avg = ng ? g / ng : 0.0;
-        if (sweep_ms_avg) *sweep_ms_avg = e->sweep_marks.empty() ? 0.0 : s / e->sweep_marks.size();
-        if (samples) *samples = (int)e->sweep_marks.size();
+        if (sweep_ms_avg) *sweep_ms_avg = ns ? s / ns : 0.0;
+        if (samples) *samples = ns;
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;

@@ -212,17 +212,65 @@ __device__ __forceinline__ double part_rowsum(const double *__restrict__ part, i
     return s;
 }
 
+// Row sums of the nparts partial n-vectors for the RW rows [row0, row0 + RW) of a 1024-thread
+// workgroup: thread (slot s, row r) adds partials s, s + S, ... (S = 1024 / RW slots, eight
+// independent accumulators), then the S slot sums are added in a fixed two-level order (eight
+// groups of S / 8 slots, then the eight groups): bitwise reproducible.  RW = 8 spreads the
+// sum of many partials over n_pad / 8 workgroups -- at C3 the 1568 X u partials of the fused
+// lambda launch (25.7 MB) took 15.7 us in 32 workgroups of 64 rows, each thread ~100 dependent
+// loads deep; 10.9-11.0 us now, and the 512 E-apply partials 6.0 -> 5.0 us (round 4,
+// gpurun_out/prof_v; non-temporal partial stores measured slower: 12.2 us).  Returns the row
+// sum on threads [0, RW).
+constexpr int kRsThreads = 1024;
+template <int RW>
+__device__ __forceinline__ double part_rowsum_rw(const double *__restrict__ part, int nparts,
+                                                 int n_pad, int row0) {
+    constexpr int S = kRsThreads / RW, G2 = S < 8 ? S : 8;
+    __shared__ double red[S][RW];
+    __shared__ double red2[G2][RW];
+    const int r = threadIdx.x % RW, sl = threadIdx.x / RW;
+    const int row = row0 + r;
+    double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (row < n_pad) {
+        int q = sl;
+        for (; q + 7 * S < nparts; q += 8 * S)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] += part[(size_t)(q + u * S) * n_pad + row];
+        for (; q < nparts; q += S) a[0] += part[(size_t)q * n_pad + row];
+    }
+    red[sl][r] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if ((int)threadIdx.x < G2 * RW) {
+        const int g = threadIdx.x / RW;
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < S / G2; ++k) v += red[g * (S / G2) + k][r];
+        red2[g][r] = v;
+    }
+    __syncthreads();
+    double v = 0.0;
+    if ((int)threadIdx.x < RW)
+#pragma unroll
+        for (int g = 0; g < G2; ++g) v += red2[g][r];
+    return v;
+}
+
+// rows per workgroup for nparts partials: 8 when there are many (more workgroups, fewer
+// dependent loads per thread), else 64
+static int rowsum_rw(int nparts) { return nparts >= 128 ? 8 : 64; }
+
 // r_0 = y / sig - (X u / sig + delta), x_1 = d_0 = r_0 / theta (x_0 = 0).  X u arrives as
-// nparts partial n-vectors (k_xu_pass, or the sparse row pass with nparts = 1).
-__global__ __launch_bounds__(64 * kRedWaves) void k_cheb_init(
+// nparts partial n-vectors (the fused lambda launch, k_eapply<XU>, or the sparse row pass
+// with nparts = 1).
+template <int RW>
+__global__ __launch_bounds__(kRsThreads) void k_cheb_init(
     const double *__restrict__ xu_part, int nparts, int n, int n_pad,
     const double *__restrict__ y, const DevScalars *sc, Key key, uint64_t t, const NidState *nid,
     double *x, double *r, double *d) {
     if (nid->mode == 0) return;
-    __shared__ double red[kRedWaves][64];
-    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double xu = part_rowsum(xu_part, nparts, n_pad, i, red);
-    if (threadIdx.x >= 64 || i >= n_pad) return;
+    const int i = blockIdx.x * RW + (int)threadIdx.x;
+    const double xu = part_rowsum_rw<RW>(xu_part, nparts, n_pad, blockIdx.x * RW);
+    if ((int)threadIdx.x >= RW || i >= n_pad) return;
     double rhs = 0.0;
     if (i < n) {
         const double sig = sqrt(sc->sig2);
@@ -237,14 +285,14 @@ __global__ __launch_bounds__(64 * kRedWaves) void k_cheb_init(
 
 // Chebyshev step j (1 <= j <= K - 1): q = d + (sum of the E-apply partials) / sig2,
 // r_j = r_{j-1} - q, d_j = rho_j rho_{j-1} d_{j-1} + (2 rho_j / delta) r_j, x_{j+1} = x_j + d_j.
-__global__ __launch_bounds__(64 * kRedWaves) void k_cheb_step(
+template <int RW>
+__global__ __launch_bounds__(kRsThreads) void k_cheb_step(
     const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
     const NidState *nid, int j, double *x, double *r, double *d) {
     if (nid->mode <= j) return;
-    __shared__ double red[kRedWaves][64];
-    const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double e = part_rowsum(part, nparts, n_pad, i, red);
-    if (threadIdx.x >= 64 || i >= n_pad) return;
+    const int i = blockIdx.x * RW + (int)threadIdx.x;
+    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, blockIdx.x * RW);
+    if ((int)threadIdx.x >= RW || i >= n_pad) return;
     const double dv = d[i];
     const double qv = dv + e / sc->sig2;
     const double rv = r[i] - qv;
@@ -474,15 +522,23 @@ void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int
 void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
                       const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
                       uint64_t t, const NidState *nid, double *x, double *r, double *d) {
-    k_cheb_init<<<(n_pad + 63) / 64, 64 * kRedWaves, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
-                                                             Key{k0, k1}, t, nid, x, r, d);
+    if (rowsum_rw(nparts) == 8)
+        k_cheb_init<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
+                                                              Key{k0, k1}, t, nid, x, r, d);
+    else
+        k_cheb_init<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y,
+                                                                 sc, Key{k0, k1}, t, nid, x, r, d);
 }
 
 void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
                       const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
                       double *d) {
-    k_cheb_step<<<(n_pad + 63) / 64, 64 * kRedWaves, 0, s>>>(part, nparts, n_pad, sc, nid, j, x,
-                                                             r, d);
+    if (rowsum_rw(nparts) == 8)
+        k_cheb_step<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j, x,
+                                                              r, d);
+    else
+        k_cheb_step<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j,
+                                                                 x, r, d);
 }
 
 void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,

@@ -457,6 +457,8 @@ def main():
                     help="drive --gpus N devices from ONE process through an RCCL shard group "
                          "(ncclCommInitAll) -- the path the .C entry points use under R; the "
                          "default for --gpus N > 1 without a torch.distributed launcher")
+    ap.add_argument("--timing-stride", type=int, default=4,
+                    help="bracket the dominant kernel with HIP events in every k-th timed sweep")
     ap.add_argument("--no-fitted", action="store_true",
                     help="skip the fitted-regime measurement that follows the timed run")
     ap.add_argument("--gram", choices=["fp64", "ozaki"], default=None,
@@ -621,7 +623,11 @@ def run_chain(args, n, p, alpha, kind, mode):
     _, sweep_ms_phases, _ = eng.kernel_times()
     dom = max((ph for ph in SINGLE_KERNEL_PHASES if ph in phases), key=lambda k: phases[k])
     barrier()
-    eng.enable_timing(True, phases=False, timed_phase=dom)
+    # every stride-th timed sweep brackets its dominant-phase launch (an event pair costs ~6 us
+    # of stream time per bracketed sweep: 1-2 % of a near-identity C3 sweep at stride 1); the
+    # E-apply's bytes per launch need every launch counted (pass_frac below)
+    stride = 1 if dom == "eapply" else max(1, args.timing_stride)
+    eng.enable_timing(True, phases=False, timed_phase=dom, stride=stride)
     eng.reset_timing()
     nid0 = eng.nid_stats()
     t0 = time.perf_counter()
@@ -678,7 +684,9 @@ def run_chain(args, n, p, alpha, kind, mode):
         t += 10000
     traffic_world = 1 if mode == "single" else world
     roof = roofline_for(dom, dom_ms, ctx, traffic_world)
-    roof["timing"] = "HIP events on rank 0's engine stream around every timed launch"
+    roof["timing"] = ("HIP events on rank 0's engine stream around "
+                      + ("every timed launch" if stride == 1 else
+                         f"the launch of every {stride}th timed sweep ({brackets} launches)"))
     secondary = None
     # the Gram's roofline beside the dominant kernel's: from this run's phase split when its
     # sweeps formed the Gram, else from the fitted-regime run (near-identity sweeps skip it)

@@ -399,6 +399,10 @@ int bb_engine_gram_mode(const bb_engine *e);
  * another (an index 0 .. bb_phase_count()-2 of bb_phase_name). */
 int bb_engine_enable_timing(bb_engine *e, int enable);
 int bb_engine_set_timed_phase(bb_engine *e, int phase);
+/* enable = 1: bracket the timed phase in every stride-th sweep only (default 1: every sweep);
+ * an event pair costs ~6 us of stream time per bracketed sweep (kernel boundaries the
+ * hardware cannot overlap), 1-2 % of a near-identity C3 sweep */
+int bb_engine_set_timing_stride(bb_engine *e, int stride);
 int bb_engine_kernel_times(bb_engine *e, double *gram_ms_avg, double *sweep_ms_avg,
                            int *samples);
 int bb_engine_reset_timing(bb_engine *e);

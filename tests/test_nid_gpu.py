@@ -243,3 +243,26 @@ def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
     assert rel_err(a["beta"], b["beta"]) < 1e-9, rel_err(a["beta"], b["beta"])
     assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-9
     assert abs(a["tau"] - b["tau"]) <= 1e-9 * b["tau"]
+
+
+@pytest.mark.parametrize("stride", [1, 3])
+def test_timed_phase_stride(gpu_lib, stride):
+    """bench.py's live roofline timing: the timed phase is bracketed by an event pair in every
+    stride-th sweep of a timed run (bb_engine_set_timing_stride), and its average is the
+    bracketed launches' mean; a stride < 1 is refused."""
+    bb = gpu_lib
+    n, p = 200, 2400
+    X, y, _ = synthetic_problem(n, p, seed=5)
+    e = _engine(bb, X, y, n, p)
+    e.init_state()
+    e.run(1, 2, first_slot=-1)
+    e.enable_timing(True, phases=False, timed_phase="lambda", stride=stride)
+    e.reset_timing()
+    e.run(3, 10, first_slot=-1)
+    e.sync()
+    ms, _, _ = e.kernel_times()
+    assert e.timed_brackets() == len(range(0, 10, stride))
+    assert 0.0 < ms < 50.0
+    e.enable_timing(False)
+    with pytest.raises(Exception):
+        e.enable_timing(True, phases=False, timed_phase="lambda", stride=0)
