@@ -81,6 +81,45 @@ def test_nid_sweep_equals_cholesky_sweep(gpu_lib, kind, gram_mode, scale):
     off.close()
 
 
+@pytest.mark.parametrize("n,p", [(96, 700), (128, 1500)])
+def test_nid_small_dense_partial_sums(gpu_lib, n, p):
+    """Narrow dense designs whose E-apply / X u passes write fewer than 128 partial n-vectors
+    (k_cheb_init / k_cheb_step then sum them in 64-row workgroups, the sparse engine's layout,
+    instead of 8-row ones): sweeps with the near-identity path on and off agree to 1e-12."""
+    bb = gpu_lib
+    X, y, btrue = synthetic_problem(n, p, seed=61)
+    rng = np.random.default_rng(9)
+    auto = _engine(bb, X, y, n, p)
+    old = bb.set_tuning(6, 0)
+    try:
+        off = _engine(bb, X, y, n, p)
+        off.init_state()
+    finally:
+        bb.set_tuning(6, old)
+    auto.init_state()
+    modes = []
+    for t, scale in ((3, 1e-6), (4, 1e-3)):
+        beta = btrue * scale + scale * rng.standard_normal(p)
+        auto.set_state(beta, scale, 1.0, 0.5)
+        off.set_state(beta, scale, 1.0, 0.5)
+        auto.run(t, 1)
+        old = bb.set_tuning(6, 0)
+        try:
+            off.run(t, 1)
+            off.sync()
+        finally:
+            bb.set_tuning(6, old)
+        a, o = auto.state(), off.state()
+        modes.append(auto.nid_stats()["mode"])
+        assert np.array_equal(a["lambda"], o["lambda"])
+        assert rel_err(a["beta"], o["beta"]) < 1e-12, (t, modes, rel_err(a["beta"], o["beta"]))
+    assert modes[0] >= 1, modes  # the near-null state takes the near-identity path
+    print(f"\n[dense n={n} p={p}] iterates per sweep {modes}")
+    assert auto.error_flags() == 0 and off.error_flags() == 0
+    auto.close()
+    off.close()
+
+
 @pytest.mark.parametrize("kind", ["dense", "sparse"])
 def test_nid_teacher_forced_from_reference_start(gpu_lib, kind, capsys):
     """A chain from the reference start (beta0 = 0, BridgeRegression.cpp:85-89) sits in the
