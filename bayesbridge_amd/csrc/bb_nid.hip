@@ -256,7 +256,8 @@ __device__ __forceinline__ double part_rowsum_rw(const double *__restrict__ part
 }
 
 // rows per workgroup for nparts partials: 8 when there are many (more workgroups, fewer
-// dependent loads per thread), else 64
+// dependent loads per thread), else 64.  (4 rows -- 32-byte row segments -- for the 1568
+// partials at C3 took 19.1 us against 11.0: gpurun_out/prof_ac.)
 static int rowsum_rw(int nparts) { return nparts >= 128 ? 8 : 64; }
 
 // r_0 = y / sig - (X u / sig + delta), x_1 = d_0 = r_0 / theta (x_0 = 0).  X u arrives as
