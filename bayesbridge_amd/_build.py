@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SO_PATH = os.path.join(HERE, "BayesBridge.so")
+OBJ_DIR = os.path.join(HERE, "build")  # per-source objects (kept: tests relink them)
 SOURCES = ["bb_kernels.hip", "bb_ozaki.hip", "bb_tri.hip", "bb_sparse.hip", "bb_logit.hip", "bb_nid.hip",
            "bb_small.hip", "bb_engine.cpp"]
 HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h", "bb_sparse.h", "bb_pg.h"]
@@ -37,33 +38,50 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > so_m for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return SO_PATH
-    objs = []
+LINK_LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-ldl", "-pthread"]
+
+
+def objects(force: bool = False, verbose: bool = False) -> list:
+    """Compile every translation unit of SOURCES into OBJ_DIR (in parallel; only the stale
+    ones unless force) and return the object paths in SOURCES order."""
+    os.makedirs(OBJ_DIR, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-result", "-pthread", f"-I{os.path.join(ROOT, 'include')}"]
-    procs = []
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS]
+    hdrs.append(os.path.join(ROOT, "include", "bayesbridge.h"))
+    newest_dep = max(os.path.getmtime(h) for h in hdrs + [os.path.abspath(__file__)])
+    objs, procs = [], []
     for src in SOURCES:  # translation units compile in parallel
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
-        cmd = [hipcc(), *flags, "-c", os.path.join(CSRC, src), "-o", obj]
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(OBJ_DIR, src.rsplit(".", 1)[0] + ".o")
+        objs.append(obj)
+        if (not force and os.path.exists(obj)
+                and os.path.getmtime(obj) >= max(newest_dep, os.path.getmtime(path))):
+            continue
+        cmd = [hipcc(), *flags, "-c", path, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((cmd, subprocess.Popen(cmd)))
-        objs.append(obj)
     failed = [cmd for cmd, pr in procs if pr.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    tmp = SO_PATH + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
-           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-ldl", "-pthread"]
+    return objs
+
+
+def link(objs: list, out: str, verbose: bool = False) -> str:
+    tmp = out + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, *LINK_LIBS]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(tmp, SO_PATH)
-    for o in objs:
-        os.remove(o)
-    return SO_PATH
+    os.replace(tmp, out)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return SO_PATH
+    return link(objects(force=force, verbose=verbose), SO_PATH, verbose=verbose)
 
 
 if __name__ == "__main__":

@@ -119,3 +119,35 @@ def test_dot_c_device_plan(setting, nvis, n, p, ortho, want):
         assert int(dev[0]) == want
     finally:
         bb.set_device_count(1)
+
+
+def _documented_makevars_objects():
+    """The OBJECTS line of INTEGRATION.md's package Makevars (Option B)."""
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"^OBJECTS\s*=\s*(.+)$", txt, flags=re.M)
+    assert m, "INTEGRATION.md has no Makevars OBJECTS line"
+    return m.group(1).split()
+
+
+def test_documented_makevars_objects_match_build_sources():
+    # Code/C/Makevars:1-6 is the reference's recipe; ours must name every translation unit
+    # the in-tree build compiles, or R's dyn.load fails on unresolved bb:: symbols
+    objs = _documented_makevars_objects()
+    want = [s.rsplit(".", 1)[0] + ".o" for s in bb._build.SOURCES]
+    assert sorted(objs) == sorted(want), (objs, want)
+    assert len(set(objs)) == len(objs)
+
+
+def test_documented_makevars_links_without_unresolved_engine_symbols(tmp_path):
+    """Link a .so from exactly the documented object list and check that nothing of the
+    engine (namespace bb, mangled _ZN2bb) is left undefined."""
+    built = {os.path.basename(o): o for o in bb._build.objects()}
+    objs = [built[o] for o in _documented_makevars_objects()]
+    so = bb._build.link(objs, str(tmp_path / "BayesBridge.so"))
+    out = subprocess.check_output(["nm", "-D", "--undefined-only", so], text=True)
+    bad = [ln.split()[-1] for ln in out.splitlines() if "_ZN2bb" in ln or " bb::" in ln]
+    assert not bad, bad[:10]
+    # and it exports the reference's .C symbols
+    exp = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True)
+    names = {ln.split()[-1] for ln in exp.splitlines()}
+    assert {"bridge_reg_stable", "retstable_LD", "bridge_EM"} <= names
