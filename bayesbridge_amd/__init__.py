@@ -138,6 +138,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_nid_stats.argtypes = [c.c_void_p, u64p, u64p, u64p, _dp, _ip]
     L.bb_engine_timed_brackets.argtypes = [c.c_void_p, _ip]
     L.bb_engine_nid_bound.argtypes = [c.c_void_p, _dp, _ip]
+    L.bb_engine_launch_counts.argtypes = [c.c_void_p, u64p, u64p]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -1094,6 +1095,13 @@ class Engine:
         library().bb_engine_nid_bound(self._h, ctypes.byref(lam), ctypes.byref(kmax))
         return dict(cheb_sweeps=a.value, products=b.value, chol_sweeps=c.value, eps=eps.value,
                     mode=mode.value, lambda_x=lam.value, kmax=kmax.value)
+
+    def launch_counts(self):
+        """Woodbury lambda launches since creation: dict(lambda_xu = fused with the X u stream
+        of the near-identity solve (k_lambda_xu), lambda_alone = a launch of their own)."""
+        a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        library().bb_engine_launch_counts(self._h, ctypes.byref(a), ctypes.byref(b))
+        return dict(lambda_xu=a.value, lambda_alone=b.value)
 
     def error_flags(self) -> int:
         f = ctypes.c_uint32()

@@ -279,6 +279,11 @@ int g_nid_kmax = 16;
 // gpurun_out/r04f_*): C3 1781 against 1746-1749 sweeps/s, C2 5840 against 5519, C5 1672
 // against 1636 -- the host's wake-up and first launch cost less than the gated no-ops.
 int g_nid_sync = 1;
+// bb_set_tuning key 9 (testing): an engine with world == 1 that owns a communicator (a 1-rank
+// RCCL comm) or belongs to an on-device shard group runs the world > 1 near-identity stage
+// sequence (bound-sum exchange, k_nid_decide_from, X u and per-product exchanges), so every
+// exchange call site of that protocol executes on a one-GPU box
+int g_shard_proto = 0;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -425,10 +430,16 @@ struct bb_engine {
         return nid != nullptr && (cfg.world == 1 || comm != nullptr || group_member) &&
                std::min(g_nid_kmax, nid_kmax) > 0;
     }
-    bool nid_sync() const { return (cfg.world > 1 || g_nid_sync) && nid_enabled(); }
+    // this engine runs the column-shard protocol of the near-identity solve (exchanged bound
+    // sums, the decision from them, exchanged X u and products): world > 1, or world == 1 with
+    // a communicator / in a group when forced for testing (g_shard_proto)
+    bool sharded() const {
+        return cfg.world > 1 || (g_shard_proto && (comm != nullptr || group_member));
+    }
+    bool nid_sync() const { return (sharded() || g_nid_sync) && nid_enabled(); }
     // the exchanged vectors are single n-vectors on a shard; an unsharded engine in the
     // synchronous mode reads the partials directly
-    bool nid_vec() const { return cfg.world > 1 || method == 5; }
+    bool nid_vec() const { return sharded() || method == 5; }
 
     // Cost model of the two exact solves, from the round-3/4 measured rates:
     // a Chebyshev solve of K iterates reads X K times (the X u pass and K - 1 products, ~6 TB/s
@@ -472,7 +483,7 @@ struct bb_engine {
         const int kmax = std::min(g_nid_kmax, nid_kmax);
         if (nid_seq < kNidLag) return kmax;
         const long q = nid_seq - kNidLag;
-        HIPCHECK(hipEventSynchronize(nid_ev[q % kNidRing]));
+        wait_event(nid_ev[q % kNidRing]);
         const double h = ((volatile double *)eps_host)[q % kNidRing];
         if (!(h >= 0.0)) return kmax;
         return cheb_iterations(8.0 * h, kmax, kNidTol);
@@ -521,7 +532,7 @@ struct bb_engine {
     // decides in the same launch (its sums need no exchange)
     void nidx_partials() {
         mark(PH_NID);
-        if (cfg.world > 1)
+        if (sharded())
             launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
         else
             launch_nid_sums_decide(stream, D, cn, p_loc, sc, nid, std::min(g_nid_kmax, nid_kmax),
@@ -529,15 +540,33 @@ struct bb_engine {
     }
     // the decision from the reduced sums (identical on every rank), then wait for it
     void nidx_decide_launch() {
-        if (cfg.world > 1)
+        if (sharded())
             launch_nid_decide_from(stream, nid_red, sc, std::min(g_nid_kmax, nid_kmax), nid,
                                    eps_dev + kNidRing);
         if (!nid_sev) HIPCHECK(hipEventCreateWithFlags(&nid_sev, hipEventDisableTiming));
         HIPCHECK(hipEventRecord(nid_sev, stream));
     }
     int nidx_decide_read() {
-        HIPCHECK(hipEventSynchronize(nid_sev));
+        wait_event(nid_sev);
         return (int)((volatile double *)eps_host)[kNidRing + 1];
+    }
+    // Block the host until ev completes.  A member of an RCCL group (stop != nullptr) polls
+    // instead, so that it gives up when another member failed: that member's all-reduces are
+    // never posted, so an event behind them never completes (the group then aborts the
+    // communicators once every member thread has returned, bb_group_run).
+    void wait_event(hipEvent_t ev) {
+        if (!stop) {
+            HIPCHECK(hipEventSynchronize(ev));
+            return;
+        }
+        for (long spin = 0;; ++spin) {
+            const hipError_t q = hipEventQuery(ev);
+            if (q == hipSuccess) return;
+            if (q != hipErrorNotReady) HIPCHECK(q);
+            if (stop->load(std::memory_order_relaxed))
+                throw HipError("stopped: another member of the shard group failed");
+            if (spin > 64) std::this_thread::yield();
+        }
     }
     // this shard's X u into nid_sum (exchanged: n_pad)
     void nidx_xu() {
@@ -594,10 +623,10 @@ struct bb_engine {
         const int spec = g_nid_sync != 2 ? 2 : 0;
         if (spec) {
             nidx_xu();
-            if (cfg.world > 1) exchange(nid_sum, (size_t)n_pad);
+            if (sharded()) exchange(nid_sum, (size_t)n_pad);
             nidx_init(t);
             nidx_eapply(1);
-            if (cfg.world > 1) exchange(nid_sum, (size_t)n_pad);
+            if (sharded()) exchange(nid_sum, (size_t)n_pad);
             nidx_step(1);
         }
         const int K = nidx_decide_read();
@@ -709,6 +738,7 @@ struct bb_engine {
             if (!xu_fused)
                 launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed,
                               cfg.stream, t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
+            ++(xu_fused ? n_lambda_xu : n_lambda_alone);
             nid_only = false;
             if (sync) {
                 // a shard: the bound sums now, the path after their exchange (shard_solve)
@@ -859,6 +889,7 @@ struct bb_engine {
     int fail_at = -1;
     int nid_kl = 0;  // Chebyshev iterations launched for the sweep being enqueued
     int xu_fused = 0;  // X u partials formed by this sweep's lambda launch (k_lambda_xu), or 0
+    unsigned long long n_lambda_xu = 0, n_lambda_alone = 0;  // Woodbury lambda launches by kind
 
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
     void run(uint64_t t0, int count, int first_slot, int slot_step, int mcmc_phase) {
@@ -1548,12 +1579,36 @@ int bb_comm_unique_id(void *id_bytes) {
     memcpy(id_bytes, &id, sizeof(id));
     return 0;
 }
+// Every shard must cap the Chebyshev iterations alike, or ranks deciding from the same reduced
+// sums would take different paths and post different collectives (a hang, or buffers mixed
+// between exchanges).  The cost model's inputs differ between shards (p_loc, p_pad, the sparse
+// non-zeros and pairs), so the ranks take the least of their caps: here through the
+// new communicator, for groups in group_create.
+static void agree_kmax_ranks(bb_engine *e) {
+    double *buf = nullptr;
+    HIPCHECK(hipMalloc(&buf, sizeof(double)));
+    const double mine = e->nid ? (double)e->nid_kmax : 0.0;
+    double got = mine;
+    try {
+        HIPCHECK(hipMemcpyAsync(buf, &mine, sizeof(double), hipMemcpyHostToDevice, e->stream));
+        NCCLCHECK(ncclAllReduce(buf, buf, 1, ncclFloat64, ncclMin, e->comm, e->stream));
+        HIPCHECK(hipMemcpyAsync(&got, buf, sizeof(double), hipMemcpyDeviceToHost, e->stream));
+        HIPCHECK(hipStreamSynchronize(e->stream));
+    } catch (...) {
+        (void)hipFree(buf);
+        throw;
+    }
+    (void)hipFree(buf);
+    if (e->nid) e->nid_kmax = (int)got;
+}
+
 int bb_engine_comm_init(bb_engine *e, const void *id_bytes) {
     try {
         HIPCHECK(hipSetDevice(e->cfg.device));
         ncclUniqueId id;
         memcpy(&id, id_bytes, sizeof(id));
         NCCLCHECK(ncclCommInitRank(&e->comm, e->cfg.world, id, e->cfg.rank));
+        agree_kmax_ranks(e);
     } catch (std::exception &ex) {
         set_error("%s", ex.what());
         return -1;
@@ -1842,6 +1897,13 @@ int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
     return 0;
 }
 
+int bb_engine_launch_counts(bb_engine *e, unsigned long long *lambda_xu,
+                            unsigned long long *lambda_alone) {
+    if (lambda_xu) *lambda_xu = e->n_lambda_xu;
+    if (lambda_alone) *lambda_alone = e->n_lambda_alone;
+    return 0;
+}
+
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags) {
     try {
         *flags = e->read_err();
@@ -1943,6 +2005,16 @@ bb_group *group_create(bb_engine **engines, int count, bool rccl) {
             if (m->woodbury()) c = std::max(c, m->red2_count());
         }
         g->tmp_count = c;
+        // one iteration cap for every member (see agree_kmax_ranks); members disagreeing on
+        // whether the near-identity path exists at all (n_pad decides it) cannot be grouped
+        int kmin = 1 << 30;
+        for (auto *m : g->members) {
+            if ((m->nid != nullptr) != (g->members[0]->nid != nullptr))
+                throw HipError("group members disagree on the near-identity solve (n differs?)");
+            if (m->nid) kmin = std::min(kmin, m->nid_kmax);
+        }
+        for (auto *m : g->members)
+            if (m->nid) m->nid_kmax = kmin;
         if (rccl) {
             g->rccl = true;
             std::vector<int> devs(count);
@@ -2068,6 +2140,11 @@ int bb_group_run(bb_group *g, uint64_t t0, int count, int first_slot, int slot_s
                 }
                 const int K = m0->nidx_decide_read();
                 for (auto *m : g->members) {
+                    // every member decided from the same reduced sums with the same cap: a
+                    // member whose device mode differed would skip both solves (stale w)
+                    if (m != m0 && m->nidx_decide_read() != K)
+                        throw HipError("shard group members decided different near-identity "
+                                       "paths");
                     m->nid_only = K > 0;
                     m->nid_last = K;
                 }
@@ -3342,9 +3419,22 @@ void bb_set_device_C(const int *device, int *status) {
 }
 void bb_set_verbose_C(const int *verbose) { bb_set_verbose(*verbose); }
 void bb_use_r_rng_C(const int *enable) { bb_use_r_rng(*enable); }
-void bb_set_seed_C(const double *seed) { bb_set_seed((uint64_t)*seed); }
+// R passes numbers as doubles; converting a negative, NaN or out-of-range double to an
+// integer type is undefined behaviour, so such a value is refused (the state is kept, the
+// reason goes to bb_last_error and stderr) instead of being cast
+static bool r_count_ok(const char *what, double v) {
+    if (std::isfinite(v) && v >= 0.0 && v <= 9007199254740992.0 && v == std::floor(v)) return true;
+    set_error("%s: %g is not an integer in [0, 2^53]; ignored", what, v);
+    fprintf(stderr, "BayesBridge: %s: %g is not an integer in [0, 2^53]; ignored\n", what, v);
+    return false;
+}
+void bb_set_seed_C(const double *seed) {
+    if (r_count_ok("bb_set_seed_C seed", *seed)) bb_set_seed((uint64_t)*seed);
+}
 void bb_set_rng_state_C(const double *seed, const double *stream) {
-    bb_set_rng_state((uint64_t)*seed, (uint64_t)*stream);
+    if (r_count_ok("bb_set_rng_state_C seed", *seed) &&
+        r_count_ok("bb_set_rng_state_C stream", *stream))
+        bb_set_rng_state((uint64_t)*seed, (uint64_t)*stream);
 }
 void bb_get_rng_state_C(double *seed, double *stream) {
     uint64_t s = 0, t = 0;
@@ -3352,7 +3442,9 @@ void bb_get_rng_state_C(double *seed, double *stream) {
     *seed = (double)s;
     *stream = (double)t;
 }
-void bb_set_trace_budget_C(const double *bytes) { bb_set_trace_budget((long long)*bytes); }
+void bb_set_trace_budget_C(const double *bytes) {
+    if (r_count_ok("bb_set_trace_budget_C bytes", *bytes)) bb_set_trace_budget((long long)*bytes);
+}
 void bb_last_call_info_C(int *devices, int *trace_capacity, int *interrupted) {
     (void)bb_last_call_info(devices, trace_capacity, interrupted);
 }
@@ -3408,6 +3500,11 @@ int bb_set_tuning(int key, int value) {
         case 8: {
             const int old = g_nid_sync;
             if (value >= 0) g_nid_sync = value > 2 ? 2 : value;
+            return old;
+        }
+        case 9: {
+            const int old = g_shard_proto;
+            if (value >= 0) g_shard_proto = value ? 1 : 0;
             return old;
         }
         default: return -1;

@@ -575,7 +575,12 @@ def run_chain(args, n, p, alpha, kind, mode):
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0])
     elif os.environ.get("BB_FORCE_RCCL", "0") == "1":
-        eng.comm_init(bb.Engine.comm_unique_id())  # 1-rank communicator (testing)
+        # per-rank proxy of an N-GPU job: a 1-rank RCCL communicator and
+        # the world > 1 near-identity protocol forced on it (bb_set_tuning key 9): the bound
+        # sums, X u and every product go through ncclAllReduce and the host waits for each
+        # sweep's decision, as every rank of the job does
+        bb.set_tuning(9, 1)
+        eng.comm_init(bb.Engine.comm_unique_id())
     runner = grp or eng
     runner.init_state()
     setup_s = time.perf_counter() - t_setup0
@@ -716,6 +721,9 @@ def run_chain(args, n, p, alpha, kind, mode):
                   "beta_step": ("p x p Cholesky of X'Omega X + diag(lambda/tau^2)" if logit
                                 else "woodbury (exact, p > n)")}
         config["gram"] = gram_name
+        if mode == "single" and os.environ.get("BB_FORCE_RCCL", "0") == "1":
+            config["proxy"] = ("one rank's share: a 1-rank RCCL communicator with the column-"
+                               "shard protocol forced (bb_set_tuning key 9)")
         if sparse:
             si = eng.sparse_info()
             config.update(density=SPARSE_DENSITY, nnz_local=si["nnz"], pairs_local=si["pairs"],

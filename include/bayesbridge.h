@@ -348,7 +348,11 @@ void bb_set_trace_budget(long long bytes);
  * Chebyshev solve's first kernels enqueued before the wait and returning at once unless the
  * device decided so; 2: without them) or launches both
  * paths with the kernels of the one not taken returning at once (0); the draws are the same
- * except on sweeps where mode 0's launch hint fell short (it then takes the factor).
+ * except on sweeps where mode 0's launch hint fell short (it then takes the factor);
+ * key 9 (testing): 1 makes an engine with world == 1 that owns a communicator (a 1-rank RCCL
+ * comm, bb_engine_comm_init) or belongs to an on-device shard group run the column-shard
+ * near-identity protocol of world > 1 (bound sums exchanged, the decision from them, X u and
+ * every product E d exchanged), so each of its exchanges executes on one GPU (default 0).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
@@ -425,6 +429,12 @@ int bb_engine_timed_brackets(bb_engine *e, int *count);
 int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
                         unsigned long long *products, unsigned long long *chol_sweeps,
                         double *eps, int *mode);
+
+/* Launch counts since the engine was created: sweeps whose lambda draws were launched together
+ * with the X u stream of the near-identity solve (k_lambda_xu), and sweeps whose
+ * lambda draws were a launch of their own. */
+int bb_engine_launch_counts(bb_engine *e, unsigned long long *lambda_xu,
+                            unsigned long long *lambda_alone);
 
 /* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags);

@@ -91,6 +91,13 @@ def test_dot_c_controls_take_pointers():
         bb.dot_c("bb_set_seed_C", 4242.0)
         s, t = bb.dot_c("bb_get_rng_state_C", 0.0, 0.0)
         assert (s[0], t[0]) == (4242.0, 0.0)
+        # a negative, NaN, fractional or > 2^53 double is refused, not cast (UB in C++)
+        for bad in (-1.0, float("nan"), float("inf"), 2.5, 2.0 ** 60):
+            bb.dot_c("bb_set_seed_C", bad)
+            assert bb.get_rng_state() == (4242, 0), bad
+            assert "ignored" in bb._err()
+            bb.dot_c("bb_set_rng_state_C", 5.0, bad)
+            assert bb.get_rng_state() == (4242, 0), bad
         bb.dot_c("bb_set_verbose_C", 0)
         d, c, i = bb.dot_c("bb_last_call_info_C", 0, 0, 0)
         assert d.dtype == np.int32 and c.dtype == np.int32 and i[0] in (0, 1)

@@ -107,10 +107,23 @@ def test_steady_state_teacher_forced(gpu_lib, name, free, capsys):
     beta, tau, sig2 = s["beta"], s["tau"], s["sig2"]
     assert np.all(np.isfinite(beta)) and tau > 0 and sig2 > 0
     worst = dict(beta=0.0, lam=0.0, tau=0.0, sig2=0.0)
+    # the path each teacher-forced sweep must take: C2 has reached the
+    # fitted regime (the Gram + Cholesky draw), C3 and C5 are near beta = 0 (the Chebyshev solve;
+    # at C3 with lambda and the X u stream in one launch, k_lambda_xu, as in the headline run)
+    want = {"c2": "chol", "c3": "cheb", "c5": "cheb"}[name]
+    paths = []
     for t in (1001, 1002, 1003):
         e.set_state(beta, tau, sig2, alpha)
+        s0, l0 = e.nid_stats(), e.launch_counts()
         e.run(t, 1, first_slot=-1)
         g = e.state()
+        s1, l1 = e.nid_stats(), e.launch_counts()
+        took = "cheb" if s1["cheb_sweeps"] == s0["cheb_sweeps"] + 1 else "chol"
+        assert s1["cheb_sweeps"] + s1["chol_sweeps"] == s0["cheb_sweeps"] + s0["chol_sweeps"] + 1
+        paths.append((took, s1["mode"], l1["lambda_xu"] - l0["lambda_xu"]))
+        assert took == want, (name, t, s1)
+        if name == "c3":
+            assert l1["lambda_xu"] == l0["lambda_xu"] + 1, (t, l0, l1)
         b, lam, tau, sig2 = oracle_sweep(X, y, beta, tau, sig2, alpha, t, SEED, 0)
         if t == 1001:
             cond, span, _ = m_condition(X, lam, tau, sig2)
@@ -125,7 +138,7 @@ def test_steady_state_teacher_forced(gpu_lib, name, free, capsys):
         worst["beta"] = max(worst["beta"], rel_err(g["beta"], b))
         beta = b
     with capsys.disabled():
-        print(f"[{name}] worst over 3 teacher-forced sweeps: {worst}")
+        print(f"[{name}] worst over 3 teacher-forced sweeps: {worst}; (path, K, fused) {paths}")
     assert worst["tau"] < 1e-11 and worst["sig2"] < 1e-11 and worst["lam"] < 1e-11, worst
     assert worst["beta"] < 1e-9, worst
     assert e.error_flags() == 0
