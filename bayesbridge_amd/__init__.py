@@ -139,6 +139,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_timed_brackets.argtypes = [c.c_void_p, _ip]
     L.bb_engine_nid_bound.argtypes = [c.c_void_p, _dp, _ip]
     L.bb_engine_launch_counts.argtypes = [c.c_void_p, u64p, u64p]
+    L.bb_kernel_instance.argtypes = [c.c_char_p, c.c_char_p, c.c_int]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -193,6 +194,15 @@ def device_count() -> int:
 def _require_gpu():
     if device_count() < 1:
         raise RuntimeError("bayesbridge_amd: no HIP device visible (the sampler has no CPU path)")
+
+
+def kernel_instance(phase: str):
+    """The kernel instance this process last launched for a roofline phase (exact name as in
+    the rocprofv3 summaries, e.g. "bb::k_eapply<8, false>"), or None."""
+    buf = ctypes.create_string_buffer(512)
+    if library().bb_kernel_instance(phase.encode(), buf, 512) != 0:
+        return None
+    return buf.value.decode()
 
 
 def _err() -> str:

@@ -28,6 +28,21 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
+def source_sha() -> str:
+    """sha256 (first 16 hex digits) of every source and header the library is built from: the
+    committed profiles record it, and bench.py uses a profile only if it matches the tree."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in sorted(SOURCES + HEADERS)]
+    files.append(os.path.join(ROOT, "include", "bayesbridge.h"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(SO_PATH):
         return True

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cxxabi.h>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1894,6 +1895,38 @@ int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
         set_error("%s", ex.what());
         return -1;
     }
+    return 0;
+}
+
+int bb_kernel_instance(const char *phase, char *buf, int len) {
+    static const char *kFam[KF_COUNT] = {"lambda", "gram", "reduce", "chol", "solve", "beta",
+                                         "eapply"};
+    if (!phase || !buf || len <= 0) return -1;
+    buf[0] = 0;
+    int f = -1;
+    for (int i = 0; i < KF_COUNT; ++i)
+        if (!strcmp(phase, kFam[i])) f = i;
+    const void *k = launched_instance(f);
+    if (!k) return -1;
+    const char *mangled = hipKernelNameRefByPtr(k, nullptr);
+    if (!mangled) return -1;
+    int st = 0;
+    char *dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+    std::string name = (st == 0 && dem) ? dem : mangled;
+    free(dem);
+    // "void bb::k_eapply<8, false>(double const*, ...)" -> "bb::k_eapply<8, false>" (the form
+    // tools/profile_summary.py gives rocprofv3's kernel names)
+    if (name.rfind("void ", 0) == 0) name = name.substr(5);
+    int depth = 0;
+    for (size_t i = 0; i < name.size(); ++i) {
+        if (name[i] == '<') ++depth;
+        if (name[i] == '>') --depth;
+        if (name[i] == '(' && depth == 0) {
+            name.resize(i);
+            break;
+        }
+    }
+    snprintf(buf, (size_t)len, "%s", name.c_str());
     return 0;
 }
 

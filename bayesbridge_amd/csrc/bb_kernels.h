@@ -83,6 +83,12 @@ __host__ __device__ inline int cheb_iterations(double eps, int kmax, double tol)
 // a kernel of the Gram + Cholesky path: skip it when the sweep took the Chebyshev path
 __device__ __forceinline__ bool gated(const int *gate) { return gate && *gate != 0; }
 
+// The kernel instance most recently launched (this process) per roofline family: bench.py
+// matches the committed PMC summaries by this exact instance (bb_kernel_instance)
+enum KernelFamily { KF_LAMBDA, KF_GRAM, KF_REDUCE, KF_CHOL, KF_SOLVE, KF_BETA, KF_EAPPLY, KF_COUNT };
+void note_launch(KernelFamily f, const void *kernel);
+const void *launched_instance(int f);
+
 int eapply_parts(int p_loc, int n_pad);  // E-apply partial n-vectors (one per workgroup)
 bool eapply_supported(int n_pad);        // dense E-apply register tiling covers n_pad
 // the decision's bound sums (bb_nid.hip): G = nid_sum_groups(p_loc) workgroup partials

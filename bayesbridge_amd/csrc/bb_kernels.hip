@@ -16,6 +16,8 @@
 // reference's chol(U, VInv, 'U') convention (A = U'U).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <mutex>
 #include <stdexcept>
 #include <unordered_map>
@@ -415,6 +417,7 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
     switch (L) {
 #define BB_SPEC_CASE(LL)                                                                      \
     case LL:                                                                                  \
+        note_launch(KF_LAMBDA, (const void *)(o4 ? k_lambda_spec_o4<LL> : k_lambda_spec<LL>)); \
         (o4 ? k_lambda_spec_o4<LL> : k_lambda_spec<LL>)<<<lb + pgb, 256, 0, s>>>(             \
             beta, p_loc, p_pad, j0, sc, key, t, mode, lam, D, u, lam_trace, err, lb, pgt);    \
         break;
@@ -566,9 +569,12 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     const int nr = (n_pad + 255) / 256;
     const bool o4 = (g_lam_occ & 1) != 0;
 #define BB_LXU(LL, NN)                                                                        \
-    (o4 ? k_lambda_xu_o4<LL, NN> : k_lambda_xu<LL, NN>)<<<G, 256, 0, s>>>(                   \
-        beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad, nchunk,  \
-        xu_part)
+    do {                                                                                      \
+        auto *kk = o4 ? k_lambda_xu_o4<LL, NN> : k_lambda_xu<LL, NN>;                         \
+        note_launch(KF_LAMBDA, (const void *)kk);                                             \
+        kk<<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, \
+                             ldx, n_pad, nchunk, xu_part);                                    \
+    } while (0)
     if (L == 8) {
         if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
     } else {
@@ -615,6 +621,7 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
         const int nwg = std::max(1, std::min((inl ? 3 : 4) * device_cus_lam(), (p_pad + 31) / 32));
         const int per = (p_pad + nwg - 1) / nwg;
         auto *kern = inl ? k_lambda_cb_in<8> : (g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>;
+        note_launch(KF_LAMBDA, (const void *)kern);
         kern<<<(p_pad + per - 1) / per, kLamCbWG, 0, s>>>(beta, p_loc, p_pad, per, j0, sc, key,
                                                           t, mode, lam, D, u, lam_trace, err);
         return;
@@ -779,6 +786,7 @@ void launch_gram(hipStream_t s, const double *Y, int ldy, const double *w, int n
                  int S, double *slabs, int ldo, size_t slab_stride, const int *gate) {
     const int nt = n_pad / kGramTile;
     const int tiles = nt * (nt + 1) / 2;
+    note_launch(KF_GRAM, (const void *)k_gram);
     k_gram<<<tiles * S, 256, 0, s>>>(Y, ldy, w, K, S, slabs, ldo, slab_stride, gate);
 }
 
@@ -2756,12 +2764,10 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
                  grid, resident);
         throw std::runtime_error(b);
     }
-    if (g_chol_version == 1)
-        k_chol_persistent<1><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
-    else if (g_chol_version == 2)
-        k_chol_persistent<2><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
-    else
-        k_chol_persistent<3><<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
+    auto *kern = g_chol_version == 1 ? k_chol_persistent<1>
+               : g_chol_version == 2 ? k_chol_persistent<2> : k_chol_persistent<3>;
+    note_launch(KF_CHOL, (const void *)kern);
+    kern<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
 }
 
 
@@ -2925,6 +2931,7 @@ void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const doubl
         // the solve's flags have their own epoch sequence (one per solve)
         unsigned int *bf = flags + bsolve_flag_offset(m_pad, 1);
         const unsigned int ep = flag_epoch(bf, (size_t)nblk, s, true);
+        note_launch(KF_SOLVE, (const void *)k_bsolve_persist);
         k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err, gate);
         return;
     }
@@ -3077,6 +3084,14 @@ int beta_xb_parts(int p_loc) {
     return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
+static std::atomic<const void *> g_kinst[KF_COUNT];
+void note_launch(KernelFamily f, const void *kernel) {
+    g_kinst[f].store(kernel, std::memory_order_relaxed);
+}
+const void *launched_instance(int f) {
+    return (f >= 0 && f < KF_COUNT) ? g_kinst[f].load(std::memory_order_relaxed) : nullptr;
+}
+
 bool beta_xb_supported(int n_pad) { return n_pad % 128 == 0 && n_pad <= 2048; }
 
 // non-temporal X loads in the fused beta pass (X is streamed once per sweep, larger than
@@ -3090,6 +3105,8 @@ void launch_beta_woodbury_xb(hipStream_t s, const double *X, int ldx, int n_pad,
     switch (n_pad / 128) {
 #define BXB(NR)                                                                             \
     case NR:                                                                                \
+        note_launch(KF_BETA, g_bxb_nt ? (const void *)k_beta_wb_xb<NR, true>                \
+                                      : (const void *)k_beta_wb_xb<NR, false>);             \
         if (g_bxb_nt)                                                                       \
             k_beta_wb_xb<NR, true><<<g, 64 * kBxbWaves, 0, s>>>(X, ldx, n_pad, w, u, D, sc,     \
                                                                p_loc, beta, beta_trace, part); \

@@ -503,16 +503,11 @@ static void launch_pass(hipStream_t s, const double *X, int ldx, int n_pad, int 
                         const double *D, const double *v, const NidState *nid, int j,
                         double *part) {
     const int g = eapply_parts(p_loc, n_pad);
-    switch ((n_pad + kEaThreads - 1) / kEaThreads) {
-        case 1: k_eapply<1, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 2: k_eapply<2, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 3: case 4:
-            k_eapply<4, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        case 5: case 6: case 7: case 8:
-            k_eapply<8, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-        default:
-            k_eapply<16, XU><<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part); break;
-    }
+    const int nr = (n_pad + kEaThreads - 1) / kEaThreads;
+    auto *kern = nr <= 1 ? k_eapply<1, XU> : nr <= 2 ? k_eapply<2, XU> : nr <= 4 ? k_eapply<4, XU>
+               : nr <= 8 ? k_eapply<8, XU> : k_eapply<16, XU>;
+    if (!XU) note_launch(KF_EAPPLY, (const void *)kern);
+    kern<<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part);
 }
 
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,

@@ -780,7 +780,9 @@ void launch_oz_gemm(hipStream_t s, const int8_t *R, int n_oz, int p_pad, int nsp
         case 4: k_oz_gemm16u<4><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
         case 7: k_oz_gemm16u<7><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
         case 16: k_oz_gemm16u<16><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate); break;
-        default: k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate);
+        default:
+            note_launch(KF_GRAM, (const void *)k_oz_gemm16u<0>);
+            k_oz_gemm16u<0><<<gu, 256, 0, s>>>(R, n_oz, nkc, nsplit, P, lead_pm, late_pm, C, gate);
     }
 }
 
@@ -942,10 +944,20 @@ void launch_oz_crt(hipStream_t s, const int8_t *P, int nsplit, int n_oz, int n_p
     const unsigned g = (unsigned)((nquad + 255) / 256 + (n_pad * 8 + 255) / 256);
     const OzConsts &C = oz_consts();
     switch (nsplit) {
-        case 1: k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
-        case 2: k_oz_crt<2><<<g, 256, 0, s>>>(P, 2, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
-        case 4: k_oz_crt<4><<<g, 256, 0, s>>>(P, 4, nt, n_pad, escale, xu_part, nxu, red2, C, gate); break;
+        case 1:
+            note_launch(KF_REDUCE, (const void *)k_oz_crt<1>);
+            k_oz_crt<1><<<g, 256, 0, s>>>(P, 1, nt, n_pad, escale, xu_part, nxu, red2, C, gate);
+            break;
+        case 2:
+            note_launch(KF_REDUCE, (const void *)k_oz_crt<2>);
+            k_oz_crt<2><<<g, 256, 0, s>>>(P, 2, nt, n_pad, escale, xu_part, nxu, red2, C, gate);
+            break;
+        case 4:
+            note_launch(KF_REDUCE, (const void *)k_oz_crt<4>);
+            k_oz_crt<4><<<g, 256, 0, s>>>(P, 4, nt, n_pad, escale, xu_part, nxu, red2, C, gate);
+            break;
         default:
+            note_launch(KF_REDUCE, (const void *)k_oz_crt<0>);
             k_oz_crt<0><<<g, 256, 0, s>>>(P, nsplit, nt, n_pad, escale, xu_part, nxu, red2, C, gate);
     }
 }

@@ -184,6 +184,7 @@ void launch_sp_gram(hipStream_t s, const unsigned *estart, const double *prod, c
                     const double *D, int n_pad, double *out, const int *gate) {
     const size_t nent = tri_count(n_pad);
     const size_t threads = nent * kSpLpe;
+    note_launch(KF_GRAM, (const void *)k_sp_gram);
     k_sp_gram<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(estart, prod, pj, D, nent, out, gate);
 }
 
@@ -398,6 +399,7 @@ void launch_sp_gram_col(hipStream_t s, const int *rowptr, const int *colidx, con
     const size_t lds = (size_t)(max_row > 0 ? max_row : 1) * sizeof(double);
     if (g_sp_nt >= 2) {
         auto kern = g_sp_nt == 2 ? k_sp_gram_flat<8> : k_sp_gram_flat<16>;
+        note_launch(KF_GRAM, (const void *)kern);
         kern<<<n_pad, 256, lds, s>>>(rowptr, colidx, rval, estart, prod, pidx, D, u, n_pad, tri,
                                      xu, gate);
     } else if (g_sp_nt)
@@ -476,6 +478,7 @@ void launch_sp_beta(hipStream_t s, const int *colptr, const int *rowidx, const d
                     int p_loc, const double *w, const double *u, const double *D,
                     const DevScalars *sc, double *beta, double *beta_trace) {
     const long threads = (long)p_loc * kSpBetaLanes;
+    note_launch(KF_BETA, (const void *)k_sp_beta);
     k_sp_beta<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(colptr, rowidx, cval, p_loc, w, u,
                                                                 D, sc, beta, beta_trace);
 }

@@ -198,80 +198,106 @@ def cpu_baseline(n, p, alpha, sweeps, threads=None, literal=False):
     return r["runtime"] / sweeps, threads
 
 
-def pmc_traffic(n, p, world, kernel):
-    """HBM bytes per launch of `kernel` (exact name or template prefix) from the newest
-    committed PMC summary of this workload (profiles/rNN_pmc.json, written by
-    tools/profile_round.sh + tools/profile_summary.py: separate FETCH_SIZE / WRITE_SIZE
-    passes, gfx950 x2 read correction).  None if absent or for another workload / world."""
+_SHA = None
+
+
+def tree_sha():
+    """source_sha of the library sources in this tree (bayesbridge_amd/_build.py)."""
+    global _SHA
+    if _SHA is None:
+        from bayesbridge_amd import _build
+        _SHA = _build.source_sha()
+    return _SHA
+
+
+def _profiles(pattern):
+    """Committed profile summaries (newest round last) with their path."""
     import glob
 
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
         try:
-            d = json.load(open(f))
+            yield json.load(open(f)), os.path.relpath(f, ROOT)
         except (OSError, ValueError):
             continue
+
+
+def _stale_note(d, f):
+    sha = d.get("source_sha")
+    if sha == tree_sha():
+        return None
+    return (f"{f} profiled source {sha or 'unrecorded'}, this tree is {tree_sha()}: "
+            "not used (re-profile: tools/profile_round.sh / pmc_valu.sh / pmc_mfma.sh)")
+
+
+def pmc_traffic(n, p, world, instance):
+    """HBM bytes per launch of the EXACT kernel instance (e.g. "bb::k_eapply<8, false>") from
+    the newest committed PMC summary of this workload (profiles/rNN_pmc.json:
+    tools/profile_round.sh + tools/profile_summary.py, separate FETCH_SIZE / WRITE_SIZE passes,
+    gfx950 x2 read correction) whose source_sha is this tree's.  Returns (bytes, source, note);
+    bytes None when there is no such profile (note says why)."""
+    best, note = None, "no committed PMC summary of this workload"
+    if instance is None or world != 1:
+        return None, None, "no kernel instance / multi-rank"
+    for d, f in _profiles("r*_pmc.json"):
         w = d.get("workload", {})
-        if w.get("n") != n or w.get("p") != p or world != 1:
+        if w.get("n") != n or w.get("p") != p:
             continue
-        for k, v in d.get("kernels", {}).items():
-            # exact name, a template instance, or (for the latency-bound phases, named by
-            # their family: bb::k_lambda, bb::k_bsolve, bb::k_beta) any kernel of the family
-            if k.startswith(kernel) and v.get("hbm_bytes") == v.get(
-                    "hbm_bytes"):  # skip NaN (kernel missing from one of the passes)
-                best = (v["hbm_bytes"], os.path.relpath(f, ROOT))
-    return best
+        v = d.get("kernels", {}).get(instance)
+        if not v or v.get("hbm_bytes") != v.get("hbm_bytes"):  # absent, or NaN (one pass lacks it)
+            note = f"{f} has no entry for {instance}"
+            continue
+        stale = _stale_note(d, f)
+        if stale:
+            best, note = None, stale
+            continue
+        best, note = (v["hbm_bytes"], f), None
+    return (best[0], best[1], None) if best else (None, None, note)
 
 
-def pmc_mfma(n, p, world, kernel, gram):
-    """MFMA-busy evidence for `kernel` at this workload from the newest committed
-    profiles/rNN_pmc_mfma.json (tools/pmc_mfma.sh: SQ_VALU_MFMA_BUSY_CYCLES and
-    GRBM_GUI_ACTIVE in separate rocprofv3 --pmc passes; tools/pmc_mfma_summary.py), or None."""
-    import glob
-
+def pmc_mfma(n, p, world, instance, gram):
+    """MFMA-busy evidence for the exact kernel instance at this workload from the newest
+    committed profiles/rNN_pmc_mfma.json of this tree (tools/pmc_mfma.sh:
+    SQ_VALU_MFMA_BUSY_CYCLES in its own rocprofv3 --pmc pass).  The busy fraction is taken
+    against the NOMINAL clock: busy cycles / (1024 SIMDs x 2.4 GHz x the dispatch duration)
+    (the GRBM_GUI_ACTIVE-derived clock read above 2.4 GHz on short dispatches)."""
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_mfma.json"))):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
+    for d, f in _profiles("r*_pmc_mfma.json"):
+        if _stale_note(d, f):
             continue
         for cfg in d.get("configs", {}).values():
             if cfg.get("n") != n or cfg.get("p") != p or world != 1 or cfg.get("gram") != gram:
                 continue
-            for k, v in cfg.get("kernels", {}).items():
-                if k.startswith(kernel) and "mfma_busy_frac" in v:
-                    best = {"mfma_busy_frac": v["mfma_busy_frac"],
-                            "mfma_busy_frac_nominal_clock": v.get("mfma_busy_frac_nominal_clock"),
-                            "effective_clock_GHz": v.get("effective_clock_GHz"),
-                            "source": os.path.relpath(f, ROOT),
-                            "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
-                                          "GRBM_GUI_ACTIVE / 8 XCDs); _nominal_clock: over "
-                                          "1024 x 2.4 GHz x the dispatch duration"}
+            v = cfg.get("kernels", {}).get(instance)
+            if v and "mfma_busy_frac_nominal_clock" in v:
+                best = {"mfma_busy_frac": v["mfma_busy_frac_nominal_clock"], "source": f,
+                        "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x the "
+                                      "dispatch duration)"}
     return best
 
 
-VALU_PEAK_GINST = 1024 * 2.4e9 / 4 / 1e9  # wave64 VALU instructions per second (1024 SIMDs)
+VALU_PEAK_GCYC = 1024 * 2.4  # SIMD issue cycles per ns: 1024 SIMDs at 2.4 GHz
 
 
-def pmc_valu(n, p, world, kernel):
-    """VALU evidence for `kernel` at this workload from the newest committed
-    profiles/rNN_pmc_valu.json (tools/pmc_valu.sh: SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU,
-    GRBM_GUI_ACTIVE in separate rocprofv3 --pmc passes; tools/pmc_valu_summary.py), or None."""
-    import glob
-
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json"))):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
+def pmc_valu(n, p, world, instance):
+    """VALU evidence for the exact kernel instance at this workload from the newest committed
+    profiles/rNN_pmc_valu.json of this tree (tools/pmc_valu.sh: SQ_INSTS_VALU and the per-class
+    SQ_INSTS_VALU_* counts, one counter per --pmc pass; tools/pmc_valu_summary.py prices them
+    in SIMD issue cycles).  Returns (entry, note)."""
+    best, note = None, "no committed VALU profile of this workload"
+    for d, f in _profiles("r*_pmc_valu.json"):
         for cfg in d.get("configs", {}).values():
             if cfg.get("n") != n or cfg.get("p") != p or world != 1:
                 continue
-            for k, v in cfg.get("kernels", {}).items():
-                if k.startswith(kernel) and "SQ_INSTS_VALU" in v:
-                    best = dict(v, kernel=k, source=os.path.relpath(f, ROOT))
-    return best
+            v = cfg.get("kernels", {}).get(instance)
+            if not v or "SQ_INSTS_VALU" not in v:
+                note = f"{f} has no entry for {instance}"
+                continue
+            stale = _stale_note(d, f)
+            if stale:
+                best, note = None, stale
+                continue
+            best, note = dict(v, kernel=instance, source=f), None
+    return best, note
 
 
 def rel_l2(a, b):
@@ -376,28 +402,33 @@ def roofline_for(phase, ms, ctx, traffic_world):
                    bytes_per_pass=byts, passes_per_launch=pf)
     elif phase == "lambda":
         # the tilted-stable draws: VALU-bound arithmetic with a rejection tail.
-        # achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, committed
-        # profile of this workload) / the live average launch time, against one wave64 VALU
-        # instruction per 4 cycles on each of the 1024 SIMDs at 2.4 GHz.  The fused launch
-        # (k_lambda_xu, dense near-identity sweeps) also streams X for X u: its HBM rate too.
-        fused = (not sparse and not logit and ctx.get("nid_cheb") and bb.set_tuning(7, -1) >= 1
-                 and n <= 4096)
-        if fused:
-            kfull = "bb::k_lambda_xu"
-        elif p_loc > 50000:
-            kfull = "bb::k_lambda_cb"
-        else:
-            kfull = "bb::k_lambda_spec"
-        v = pmc_valu(n, p, traffic_world, kfull)
-        ginst = (v["SQ_INSTS_VALU"] / sec / 1e9) if v else None
-        out.update(bound="valu", kernel=kfull, achieved=ginst, peak=VALU_PEAK_GINST,
-                   unit="G VALU wave-instructions/s", draws_per_launch=p_loc,
+        # achieved = SIMD issue cycles per launch -- the per-class VALU instruction counts of the
+        # committed profile of this workload and tree (rocprofv3 SQ_INSTS_VALU_*) priced at the
+        # measured cycles per wave64 instruction (f64 FMA/MUL/ADD 4, f64 rcp/sqrt 16, f32
+        # transcendental 8, 32-bit ops 2; profiles/r05_valu_costs.json) -- over the live average
+        # launch time, against every SIMD issuing every cycle (1024 SIMDs x 2.4 GHz).  The fused
+        # launch (k_lambda_xu, dense near-identity sweeps) also streams X for X u: its HBM rate.
+        kfull = ctx.get("instances", {}).get("lambda")
+        fused = bool(kfull) and kfull.startswith("bb::k_lambda_xu")
+        v, vnote = pmc_valu(n, p, traffic_world, kfull)
+        cyc = v.get("issue_cycles") if v else None
+        out.update(bound="valu", kernel=kfull,
+                   achieved=(cyc / sec / 1e9) if cyc else None, peak=VALU_PEAK_GCYC,
+                   unit="G SIMD issue-cycles/s (VALU)", draws_per_launch=p_loc,
                    draws_per_s=p_loc / sec,
+                   issue_cycles_per_launch=cyc,
+                   frac_bounds=([v["issue_cycles_low"] / sec / 1e9 / VALU_PEAK_GCYC,
+                                 v["issue_cycles_high"] / sec / 1e9 / VALU_PEAK_GCYC]
+                                if cyc else None),
                    valu_insts_per_launch=v["SQ_INSTS_VALU"] if v else None,
+                   valu_class_counts=v.get("class_counts") if v else None,
+                   valu_class_cycles=v.get("class_cycles") if v else None,
                    valu_busy_frac=v.get("valu_busy_frac") if v else None,
-                   valu_source=v["source"] if v else None)
+                   valu_source=v["source"] if v else None, valu_note=vnote,
+                   cost_model="INT32 / CVT / unclassified instructions at the average cost of "
+                              "their members in the kernel's ISA; frac_bounds price them at 2 "
+                              "and 4 cycles (tools/pmc_valu_summary.py)")
         if fused:
-            n_pad = -(-n // 128) * 128
             byts = 8.0 * n * p_loc + 32.0 * p_loc
             out["hbm"] = {"algorithmic_bytes_per_launch": byts, "achieved_GBps": byts / sec / 1e9,
                           "peak_GBps": 8000.0, "frac": byts / sec / 1e9 / 8000.0,
@@ -421,14 +452,20 @@ def roofline_for(phase, ms, ctx, traffic_world):
         out.update(bound="latency", kernel=kfull, achieved=None, peak=None, unit=None)
     out["frac"] = (out["achieved"] / out["peak"]) if (out.get("peak") and
                                                        out.get("achieved") is not None) else None
-    tr = pmc_traffic(n, p, traffic_world, kfull)
+    # the PMC evidence is matched on the exact kernel instance the timed run launched
+    # (bb_kernel_instance), never on a name prefix
+    inst = ctx.get("instances", {}).get(phase)
+    out["kernel_instance"] = inst
+    tb, tsrc, tnote = pmc_traffic(n, p, traffic_world, inst)
     if out.get("bound") == "mfma":
-        mf = pmc_mfma(n, p, traffic_world, kfull, ctx.get("gram_name"))
+        mf = pmc_mfma(n, p, traffic_world, inst, ctx.get("gram_name"))
         out["mfma_busy_frac"] = mf["mfma_busy_frac"] if mf else None
         out["mfma_busy"] = mf
-    out["traffic"] = tr[0] if tr else None
+    out["traffic"] = tb
     out["traffic_unit"] = "HBM bytes per launch (rocprofv3 PMC)"
-    out["traffic_source"] = tr[1] if tr else None
+    out["traffic_source"] = tsrc
+    if tnote:
+        out["traffic_note"] = tnote
     return out
 
 
@@ -649,6 +686,8 @@ def run_chain(args, n, p, alpha, kind, mode):
         elapsed = float(tt.item())
     dom_ms, _, _ = eng.kernel_times()
     brackets = eng.timed_brackets()
+    # the exact kernel instances the timed sweeps launched (the PMC evidence is matched on them)
+    instances = {ph: bb.kernel_instance(ph) for ph in SINGLE_KERNEL_PHASES}
     nid1 = eng.nid_stats()
     eng.enable_timing(False)
     nid = None
@@ -682,11 +721,15 @@ def run_chain(args, n, p, alpha, kind, mode):
                  ("ozaki-II int8 (fp64-accurate)" if eng.gram_mode() == bb.GRAM_OZAKI
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
-               gram_name=gram_name, pass_frac=ctx_pass_frac, nid_cheb=nid_phase_cheb)
+               gram_name=gram_name, pass_frac=ctx_pass_frac, nid_cheb=nid_phase_cheb,
+               instances=instances)
     fitted = None
     if mode == "single" and not logit and not args.no_fitted:
         fitted = fitted_regime(bb, eng, kind, n, p, alpha, t)
         t += 10000
+    # the Gram's instances as launched (by the fitted-regime run when the timed sweeps formed none)
+    ctx_gram = dict(ctx, instances=dict(instances, **{
+        ph: instances.get(ph) or bb.kernel_instance(ph) for ph in ("gram", "reduce", "chol")}))
     traffic_world = 1 if mode == "single" else world
     roof = roofline_for(dom, dom_ms, ctx, traffic_world)
     roof["timing"] = ("HIP events on rank 0's engine stream around "
@@ -699,7 +742,7 @@ def run_chain(args, n, p, alpha, kind, mode):
     if nid_phase_cheb and fitted:
         gram_src = (fitted["phases_ms"], "HIP events at phase starts, fitted-regime run")
     if dom != "gram" and "gram" in gram_src[0] and not (nid_phase_cheb and not fitted):
-        secondary = roofline_for("gram", gram_src[0]["gram"], ctx, traffic_world)
+        secondary = roofline_for("gram", gram_src[0]["gram"], ctx_gram, traffic_world)
         secondary["timing"] = gram_src[1]
     gram_total_ms = sum(phases.get(k, 0.0) for k in ("ozprep", "gram", "reduce"))
 

@@ -436,6 +436,11 @@ int bb_engine_nid_stats(bb_engine *e, unsigned long long *cheb_sweeps,
 int bb_engine_launch_counts(bb_engine *e, unsigned long long *lambda_xu,
                             unsigned long long *lambda_alone);
 
+/* The kernel instance this process most recently launched for a roofline phase ("lambda",
+ * "gram", "reduce", "chol", "solve", "beta", "eapply"), demangled without its parameter list
+ * ("bb::k_eapply<8, false>"), into buf.  Returns 0, or -1 if none was launched. */
+int bb_kernel_instance(const char *phase, char *buf, int len);
+
 /* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags);
 

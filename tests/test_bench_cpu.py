@@ -79,10 +79,10 @@ def test_dominant_phase_roofline_formulas():
 @pytest.mark.parametrize("world", [1, 2])
 @pytest.mark.parametrize("kind,n,p", [("dense", 2000, 50000), ("dense", 1000, 5000),
                                       ("sparse", 5000, 200000)])
-def test_lambda_and_beta_roofline_entries(world, kind, n, p):
-    """The lambda entry (bound "valu": VALU wave-instructions from a committed PMC profile
-    over the live time; no profile -- another shape, or a shard -- gives achieved = frac =
-    None, never an error) and the dense beta entry (one read of X)."""
+def test_lambda_and_beta_roofline_entries(world, kind, n, p, monkeypatch):
+    """The lambda entry (bound "valu": SIMD issue cycles per launch from a committed PMC
+    profile of THIS tree over the live time; no profile -- another shape, a shard, another
+    tree -- gives achieved = frac = None, never an error) and the dense beta entry."""
     sys.path.insert(0, ROOT)
     import bench
 
@@ -98,19 +98,47 @@ def test_lambda_and_beta_roofline_entries(world, kind, n, p):
         def sparse_info():
             return dict(nnz=n * p // 100, pairs=0, col_mode=1, max_row=0)
 
+    inst = "bb::k_lambda_xu<8, 8>"
+    prof = {"source_sha": bench.tree_sha(), "configs": {"c3": {"n": 2000, "p": 50000, "kernels": {
+        inst: {"SQ_INSTS_VALU": 5e7, "issue_cycles": 1.5e8, "issue_cycles_low": 1.2e8,
+               "issue_cycles_high": 2.0e8}}}}}
+    monkeypatch.setattr(bench, "_profiles", lambda pat: iter([(prof, "profiles/rXX_pmc_valu.json")]))
     p_loc = p // world
     ctx = dict(bb=FakeBB, eng=FakeEng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=1,
-               nid_cheb=True)
+               nid_cheb=True, instances={"lambda": inst})
     r = bench.roofline_for("lambda", 0.24, ctx, world)
-    assert r["bound"] == "valu" and r["peak"] == bench.VALU_PEAK_GINST
+    assert r["bound"] == "valu" and r["peak"] == bench.VALU_PEAK_GCYC
     assert abs(r["draws_per_s"] - p_loc / 0.24e-3) < 1e-6 * p_loc / 0.24e-3
-    if r["achieved"] is None:
-        assert r["frac"] is None
-    else:
-        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     if kind == "dense" and world == 1 and n == 2000:
-        assert r["kernel"] == "bb::k_lambda_xu"
-        assert r["valu_insts_per_launch"] > 0 and 0 < r["frac"] < 1  # profiles/r04_pmc_valu.json
+        assert r["kernel"] == inst
+        assert abs(r["achieved"] - 1.5e8 / 0.24e-3 / 1e9) < 1e-6
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+        assert r["frac_bounds"][0] < r["frac"] < r["frac_bounds"][1]
         assert abs(r["hbm"]["achieved_GBps"] - (8.0 * n * p + 32.0 * p) / 0.24e-3 / 1e9) < 1e-6
+    else:
+        assert r["achieved"] is None and r["frac"] is None
     b = bench.roofline_for("beta", 0.135, ctx, world)
     assert b["bound"] == "hbm" and b["frac"] is not None
+
+
+def test_pmc_lookup_matches_exact_instance_of_this_tree(monkeypatch):
+    """the traffic of the E-apply must come from the instance that ran
+    (k_eapply<8, false>), not from the no-op right-hand-side instance that shares its prefix,
+    and a profile of another tree (or one without a recorded source) is not used."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def prof(sha):
+        return {"source_sha": sha, "workload": {"n": 2000, "p": 50000}, "kernels": {
+            "bb::k_eapply<8, false>": {"hbm_bytes": 8.3e8},
+            "bb::k_eapply<8, true>": {"hbm_bytes": 2.1e4}}}
+
+    monkeypatch.setattr(bench, "_profiles", lambda pat: iter([(prof(bench.tree_sha()), "f")]))
+    assert bench.pmc_traffic(2000, 50000, 1, "bb::k_eapply<8, false>")[0] == 8.3e8
+    assert bench.pmc_traffic(2000, 50000, 1, "bb::k_eapply<8, true>")[0] == 2.1e4
+    assert bench.pmc_traffic(2000, 50000, 1, "bb::k_eapply")[0] is None  # no prefix match
+    assert bench.pmc_traffic(2000, 50000, 1, None)[0] is None
+    for sha in ("0123456789abcdef", None):
+        monkeypatch.setattr(bench, "_profiles", lambda pat, s=sha: iter([(prof(s), "f")]))
+        b, src, note = bench.pmc_traffic(2000, 50000, 1, "bb::k_eapply<8, false>")
+        assert b is None and "not used" in note

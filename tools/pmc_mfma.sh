@@ -8,9 +8,11 @@
 # Summary: python tools/pmc_mfma_summary.py <round>  ->  profiles/<round>_pmc_mfma.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 OUT=gpurun_out/pmc_mfma_$ROUND
 mkdir -p "$OUT"
+# the sources this profile measures (bench.py uses a profile only for the same tree)
+python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
 REGEX="k_oz_gemm16u|k_oz_residues|k_chol_persistent|k_gram"
 pass() {  # $1 = config name, $2 = counter, rest = bench args
     local cfg=$1 ctr=$2; shift 2

@@ -52,7 +52,9 @@ def bench_line(d):
 def main():
     rnd = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", f"pmc_mfma_{rnd}")
+    shaf = os.path.join(src, "source_sha.txt")
     out = {"round": rnd, "source": "tools/pmc_mfma.sh (one counter per rocprofv3 --pmc pass)",
+           "source_sha": open(shaf).read().strip() if os.path.exists(shaf) else None,
            "formula": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x GRBM_GUI_ACTIVE / 8)",
            "configs": {}}
     for cfg in sorted(os.listdir(src)):

@@ -5,9 +5,11 @@
 # near-identity pass k_eapply for reference.  Summary: python tools/pmc_valu_summary.py <round>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 OUT=gpurun_out/pmc_valu_$ROUND
 mkdir -p "$OUT"
+# the sources this profile measures (bench.py uses a profile only for the same tree)
+python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
 REGEX="k_lambda|k_eapply"
 pass() {  # $1 = config name, $2 = counter, rest = bench args
     local cfg=$1 ctr=$2; shift 2
@@ -23,7 +25,12 @@ for cfg in c3 c5; do
         c3) args="" ;;
         c5) args="--workload c5" ;;
     esac
-    for ctr in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES; do
+    # the totals, then the per-class counts that price the instructions in SIMD issue cycles
+    # (classes and costs: tools/valu_rate.hip, tools/pmc_valu_classes.sh)
+    for ctr in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 \
+        SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 \
+        SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 \
+        SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT; do
         pass $cfg $ctr $args
     done
 done

@@ -11,6 +11,8 @@ export TMPDIR=/tmp
 ROUND=${ROUND:-r01}
 OUT=gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
+# the sources this profile measures (bench.py uses a profile only for the same tree)
+python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
 ARGS="--no-cpu-baseline $*"
 set -o pipefail
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \

@@ -84,7 +84,9 @@ def main():
     n_pad = -(-n // 128) * 128
     p_pad = -(-p // 256) * 256
     x_bytes = 8.0 * n_pad * p_pad
-    out = {"round": rnd, "workload": {"n": n, "p": p, "n_pad": n_pad, "p_pad": p_pad},
+    shaf = os.path.join(src, "source_sha.txt")
+    out = {"round": rnd, "source_sha": open(shaf).read().strip() if os.path.exists(shaf) else None,
+           "workload": {"n": n, "p": p, "n_pad": n_pad, "p_pad": p_pad},
            "units": "bytes per dispatch (average over the profiled dispatches)",
            "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 1/2 reporting of wide "
                          "streaming reads); write_bytes = WRITE_SIZE x 1024",
@@ -96,7 +98,9 @@ def main():
                              "read_bytes": 2 * 1024 * f_kb, "write_bytes": 1024 * w_kb,
                              "hbm_bytes": 2 * 1024 * f_kb + 1024 * w_kb,
                              "avg_us": avg_us.get(k)}
-    for kname in ("bb::k_beta_wb_xb<16>", "bb::k_xv"):
+    # the fused beta pass (k_beta_wb_xb<NR, nt>: whatever instance ran) or the fp64 path's k_xv
+    cands = [k for k in out["kernels"] if k.startswith("bb::k_beta_wb_xb<")] + ["bb::k_xv"]
+    for kname in cands:
         if kname in out["kernels"]:
             kx = out["kernels"][kname]
             out["calibration"] = {"kernel": kname, "algorithmic_read_bytes": x_bytes,
