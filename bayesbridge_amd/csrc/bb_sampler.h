@@ -163,9 +163,14 @@ __device__ __forceinline__ double zolotarev_A_p(double x, double alpha, double i
 }
 
 // B(x) / B(0) = sinc(x) / (sinc(alpha x)^alpha sinc(ia x)^ia), the two powers as one exp:
-// sinc(x) exp(-(alpha log sinc(alpha x) + ia log sinc(ia x))) (the same value to rounding)
+// sinc(x) exp(-(alpha log sinc(alpha x) + ia log sinc(ia x))) (the same value to rounding).
+// At stable index alpha = 1/2 (the bridge exponent 1, the lasso: the chain draws lambda at
+// index alpha_bridge / 2) ia = alpha, so both sincs are one value s and alpha log s + ia log s
+// = log s exactly (halving and doubling are exact): one sine, one division and one log fewer
+// per inner attempt, the same bits.
 __device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia) {
-    const double l = alpha * log(sinc_mm(alpha * x)) + ia * log(sinc_mm(ia * x));
+    const double la = log(sinc_mm(alpha * x));
+    const double l = (alpha == ia) ? la : alpha * la + ia * log(sinc_mm(ia * x));
     return sinc_mm(x) * exp(-l);
 }
 

@@ -53,6 +53,28 @@ PUBLISHED = {
 }
 
 
+# Effective sampling rate, ESS / runtime (Notes/bbnotes.tex:913-925 general, :967-979
+# orthogonal): (min, med, max, sd) over coefficients
+PUBLISHED_ESR = {
+    ("DB", "tri"): (6412.15, 10979.52, 29850.64, 7212.68),
+    ("DB", "stable"): (6006.14, 11312.78, 20522.83, 5118.33),
+    ("DBI", "tri"): (5.06, 14.98, 35.10, 5.16),
+    ("DBI", "stable"): (261.86, 886.12, 1320.26, 276.42),
+    ("DB", "tri_orth"): (47343.30, 56407.57, 79058.63, 9447.09),
+    ("DB", "stable_orth"): (15842.58, 20500.59, 23991.48, 2581.22),
+    ("DBI", "tri_orth"): (2377.19, 7675.35, 11531.89, 2848.33),
+    ("DBI", "stable_orth"): (1267.65, 3029.24, 3965.43, 817.16),
+}
+
+
+def esr_stats(ess, rts):
+    """Per coefficient the median over simulations of ESS_s / runtime_s; min / median / max /
+    sd over coefficients (the published ESR rows, bbnotes.tex:1005-1012)."""
+    per = np.median(np.array(ess) / np.array(rts)[:, None], axis=0)
+    return {"min": float(per.min()), "median": float(np.median(per)), "max": float(per.max()),
+            "sd": float(np.std(per, ddof=1))}
+
+
 def unit_l2(Z):
     Z = Z - Z.mean(axis=0)
     return Z / np.linalg.norm(Z, axis=0)
@@ -94,6 +116,25 @@ def cpu_run(X, y, method, nsamp, burn):
     return nsamp / r["runtime"]
 
 
+def cpu_protocol(X, y, method, nsamp, burn, nsim):
+    """The compiled CPU chain (reference-literal, 1 core) under the full published protocol:
+    its ESS and ESR beside the GPU's (stable methods only)."""
+    import oracle
+    if method.startswith("tri"):
+        return None
+    ess, rts = [], []
+    for s in range(nsim):
+        r = oracle.cpu_chain(y, X, nsamp, burn=burn, method="ortho" if method.endswith("_orth")
+                             else "chol", seed=1000 + s, threads=1)
+        ess.append(effective_size(r["beta"].T))
+        rts.append(r["runtime"])
+    per = np.median(np.array(ess), axis=0)
+    return {"runtime_s": float(np.median(rts)), "threads": 1,
+            "ess": {"min": float(per.min()), "median": float(np.median(per)),
+                    "max": float(per.max()), "sd": float(np.std(per, ddof=1))},
+            "esr": esr_stats(ess, rts)}
+
+
 def main():
     nsamp = int(os.environ.get("NSAMP", "100000"))
     burn = int(os.environ.get("BURN", "10000"))
@@ -124,12 +165,18 @@ def main():
                    "runtime_s": rt, "sweeps_per_s": nsamp / rt,
                    "ess": {"min": float(per_coef.min()), "median": float(np.median(per_coef)),
                            "max": float(per_coef.max()), "sd": float(np.std(per_coef, ddof=1))},
-                   "esr_median": float(np.median(per_coef)) / rt}
+                   "esr": esr_stats(ess, rts)}
             pub = PUBLISHED.get((name, method))
             if pub:
                 rec["published"] = {"runtime_s": pub[0], "sweeps_per_s": 100000 / pub[0],
                                     "ess": dict(zip(("min", "median", "max", "sd"), pub[1:])),
+                                    "esr": dict(zip(("min", "median", "max", "sd"),
+                                                    PUBLISHED_ESR[(name, method)])),
                                     "source": "Notes/bbnotes.tex:901-978 (2011 laptop)"}
+                rec["esr_over_published_median"] = (rec["esr"]["median"]
+                                                    / PUBLISHED_ESR[(name, method)][1])
+            if os.environ.get("CPU_PROTOCOL", "0") == "1":
+                rec["cpu_compiled_protocol"] = cpu_protocol(X, y, method, nsamp, burn, nsim)
             cpu = cpu_run(X, y, method, cpu_samples, min(burn, cpu_samples // 10))
             if cpu:
                 rec["cpu_compiled_1core_sweeps_per_s"] = cpu
