@@ -140,6 +140,7 @@ def library(build: bool = True) -> ctypes.CDLL:
     L.bb_engine_nid_bound.argtypes = [c.c_void_p, _dp, _ip]
     L.bb_engine_launch_counts.argtypes = [c.c_void_p, u64p, u64p]
     L.bb_kernel_instance.argtypes = [c.c_char_p, c.c_char_p, c.c_int]
+    L.bb_engine_nid_mixed.argtypes = [c.c_void_p, u64p, u64p, _dp, _ip, _ip]
     L.bb_group_destroy.argtypes = [c.c_void_p]
     L.bb_group_init_state.argtypes = [c.c_void_p]
     L.bb_group_run.argtypes = [c.c_void_p, c.c_uint64, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -1105,6 +1106,17 @@ class Engine:
         library().bb_engine_nid_bound(self._h, ctypes.byref(lam), ctypes.byref(kmax))
         return dict(cheb_sweeps=a.value, products=b.value, chol_sweeps=c.value, eps=eps.value,
                     mode=mode.value, lambda_x=lam.value, kmax=kmax.value)
+
+    def nid_mixed(self):
+        """The mixed-precision plan: dict(mixed_sweeps, products32 (fp32
+        E-apply passes), eta and k2 of the latest sweep, holds_x32)."""
+        a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        eta, k2, hx = ctypes.c_double(), ctypes.c_int(), ctypes.c_int()
+        _check(library().bb_engine_nid_mixed(self._h, ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(eta), ctypes.byref(k2),
+                                             ctypes.byref(hx)), "bb_engine_nid_mixed")
+        return dict(mixed_sweeps=a.value, products32=b.value, eta=eta.value, k2=k2.value,
+                    holds_x32=bool(hx.value))
 
     def launch_counts(self):
         """Woodbury lambda launches since creation: dict(lambda_xu = fused with the X u stream

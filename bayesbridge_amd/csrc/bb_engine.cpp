@@ -285,6 +285,10 @@ int g_nid_sync = 1;
 // sequence (bound-sum exchange, k_nid_decide_from, X u and per-product exchanges), so every
 // exchange call site of that protocol executes on a one-GPU box
 int g_shard_proto = 0;
+// bb_set_tuning key 10: the mixed-precision near-identity plan of unsharded
+// dense engines: products over an fp32 copy of X with one fp64 residual pass (1, the default)
+// or fp64 products only (0)
+int g_nid_mixed = 1;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -346,6 +350,13 @@ struct bb_engine {
     double *ch_r = nullptr, *ch_d = nullptr, *ea_part = nullptr, *sp_s = nullptr,
            *nid_xu = nullptr;
     double *eps_host = nullptr;  // ring of kNidRing: eps of sweep q in slot q % kNidRing
+    // the mixed-precision plan (unsharded dense engines): X rounded to fp32 (n_pad x p_loc,
+    // ld n_pad; nullptr when not held), the right-hand side kept for the residual pass, and the
+    // correction iterates the latest sweep's decision asked for (0: the fp64 plan)
+    float *X32 = nullptr;
+    double *ch_b = nullptr;
+    int nid_k2 = 0;
+    double nid_cost[3] = {0.0, 0.0, 0.0};  // NidState c64, c32, cstep (s)
     int ea_parts = 1;
     int nid_kmax = 0;  // iterations beyond which the Gram + Cholesky path is cheaper (model)
     double lambda_x = 0.0;  // certified lambda_max(X X') bound (0: none)
@@ -438,6 +449,12 @@ struct bb_engine {
         return cfg.world > 1 || (g_shard_proto && (comm != nullptr || group_member));
     }
     bool nid_sync() const { return (sharded() || g_nid_sync) && nid_enabled(); }
+    // the mixed-precision plan may be chosen by this engine's decision: an unsharded dense
+    // engine that holds X32 (shards and shard-group members decide the fp64 plan only, so
+    // every rank runs the same collectives)
+    bool mixed_ok() const {
+        return X32 != nullptr && g_nid_mixed && !sharded() && !group_member && method == 2;
+    }
     // the exchanged vectors are single n-vectors on a shard; an unsharded engine in the
     // synchronous mode reads the partials directly
     bool nid_vec() const { return sharded() || method == 5; }
@@ -537,7 +554,7 @@ struct bb_engine {
             launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
         else
             launch_nid_sums_decide(stream, D, cn, p_loc, sc, nid, std::min(g_nid_kmax, nid_kmax),
-                                   nid_wg, nid_red, eps_dev + kNidRing);
+                                   nid_wg, nid_red, eps_dev + kNidRing, mixed_ok() ? 1 : 0);
     }
     // the decision from the reduced sums (identical on every rank), then wait for it
     void nidx_decide_launch() {
@@ -549,6 +566,7 @@ struct bb_engine {
     }
     int nidx_decide_read() {
         wait_event(nid_sev);
+        nid_k2 = mixed_ok() ? (int)((volatile double *)eps_host)[kNidRing + 2] : 0;
         return (int)((volatile double *)eps_host)[kNidRing + 1];
     }
     // Block the host until ev completes.  A member of an RCCL group (stop != nullptr) polls
@@ -586,7 +604,22 @@ struct bb_engine {
                              w, ch_r, ch_d);
         else
             launch_cheb_init(stream, nid_xu, xu_fused ? xu_fused : ea_parts, n, n_pad, y, sc,
-                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d);
+                             cfg.seed, cfg.stream, t, nid, w, ch_r, ch_d,
+                             mixed_ok() ? ch_b : nullptr);
+    }
+    // the mixed plan's residual pass, restart and correction solve (k2 iterates), after the
+    // first solve's products
+    void nidx_mixed_tail(int k2) {
+        mark(PH_EAPPLY);
+        launch_eapply(stream, X, n_pad, n_pad, p_loc, D, w, nid, 0, ea_part, X32, 2);
+        mark(PH_NID);
+        launch_cheb_restart(stream, ea_part, ea_parts, n_pad, sc, nid, ch_b, w, ch_r, ch_d);
+        for (int j = 1; j < k2; ++j) {
+            mark(PH_EAPPLY);
+            launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part, X32, 3);
+            mark(PH_NID);
+            launch_cheb_step(stream, ea_part, ea_parts, n_pad, sc, nid, j, w, ch_r, ch_d, 2);
+        }
     }
     // this shard's E d of step j into nid_sum (exchanged: n_pad)
     void nidx_eapply(int j) {
@@ -595,7 +628,8 @@ struct bb_engine {
             launch_sp_eapply(stream, spd.colptr, spd.rowidx, spd.cval, spd.rowptr, spd.colidx,
                              spd.rval, p_loc, n_pad, D, ch_d, nid, j, sp_s, nid_sum);
         } else {
-            launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part);
+            launch_eapply(stream, X, n_pad, n_pad, p_loc, D, ch_d, nid, j, ea_part,
+                          mixed_ok() ? X32 : nullptr);
             if (nid_vec()) launch_part_sum(stream, ea_part, ea_parts, n_pad, nid_sum);
         }
     }
@@ -644,6 +678,7 @@ struct bb_engine {
                 exchange(nid_sum, (size_t)n_pad);
                 nidx_step(j);
             }
+            if (nid_k2 > 0) nidx_mixed_tail(nid_k2);  // unsharded: exchange() is a no-op
         } else {
             wb_gram(nullptr);
             exchange(red2, red2_count());
@@ -1157,6 +1192,8 @@ void nid_certify_lambda(bb_engine *e) {
     }
     HIPCHECK(hipMemsetAsync(e->nid, 0, sizeof(NidState), s));
     HIPCHECK(hipMemcpyAsync(&e->nid->lambda_x, &lam, sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemcpyAsync(&e->nid->c64, e->nid_cost, sizeof(e->nid_cost), hipMemcpyHostToDevice,
+                            s));
     HIPCHECK(hipStreamSynchronize(s));
     e->lambda_x = lam;
     (void)hipFree(ones);
@@ -1283,17 +1320,39 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
                 e->nid_xu = dalloc<double>((size_t)xp * n_pad, o);
             }
             e->nid = dalloc<NidState>(1, o);
+            {
+                // the Chebyshev plans' cost model (bb_nid.hip nid_plan_mixed; copied into the
+                // NidState by nid_certify_lambda): a pass streams X at ~6.2 TB/s plus ~4 us of
+                // launch and partials; a step launch ~6 us
+                const double bytes = (double)n_pad * (double)c.p_local;
+                e->nid_cost[0] = 8.0 * bytes / 6.2e12 + 4e-6;
+                e->nid_cost[1] = 4.0 * bytes / 6.2e12 + 4e-6;
+                e->nid_cost[2] = 6e-6;
+            }
             e->ch_r = dalloc<double>(n_pad, o);
             e->ch_d = dalloc<double>(n_pad, o);
             e->nid_red = dalloc<double>(bb_engine::kNidRed, o);
             e->nid_wg = dalloc<double>((size_t)nid_sum_groups(c.p_local) * (kNidTS + 1), o);
             e->nid_sum = dalloc<double>(n_pad, o);
             // the hint ring, then a shard's [eps, mode] of the sweep being decided
-            const int nh = bb_engine::kNidRing + 2;
+            const int nh = bb_engine::kNidRing + 3;
             HIPCHECK(hipHostMalloc((void **)&e->eps_host, nh * sizeof(double), hipHostMallocMapped));
             for (int q = 0; q < nh; ++q) e->eps_host[q] = -1.0;  // no observation yet
             HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
             e->nid_kmax = e->nid_kmax_model();
+            // the mixed-precision plan's fp32 copy of X (unsharded dense engines; 4 B per
+            // element: 400 MB at C3), unless an entry is outside fp32's normal range
+            if (e->method == 2 && c.world == 1) {
+                e->X32 = dalloc<float>((size_t)n_pad * p_pad, o);
+                e->ch_b = dalloc<double>(n_pad, o);
+                int *bad = dalloc<int>(1, o);
+                HIPCHECK(hipMemsetAsync(bad, 0, sizeof(int), e->stream));
+                launch_cast_f32(e->stream, e->X, n_pad, n_pad, c.p_local, e->X32, bad);
+                int hb = 0;
+                HIPCHECK(hipMemcpyAsync(&hb, bad, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+                HIPCHECK(hipStreamSynchronize(e->stream));
+                if (hb) e->X32 = nullptr;  // (the buffer stays owned and is freed with the engine)
+            }
         }
     }
     // X'X / X'y when the chol or ortho path needs them, or for the least-squares start.
@@ -1868,6 +1927,26 @@ int bb_engine_timed_brackets(bb_engine *e, int *count) {
         for (size_t i = 0; i + 1 < marks.size(); ++i)
             if (marks[i].first == e->timed_phase) ++ng;
     *count = ng;
+    return 0;
+}
+
+int bb_engine_nid_mixed(bb_engine *e, unsigned long long *mixed_sweeps,
+                        unsigned long long *products32, double *eta, int *k2, int *holds_x32) {
+    try {
+        NidState h{};
+        if (e->nid) {
+            HIPCHECK(hipMemcpyAsync(&h, e->nid, sizeof(h), hipMemcpyDeviceToHost, e->stream));
+            HIPCHECK(hipStreamSynchronize(e->stream));
+        }
+        if (mixed_sweeps) *mixed_sweeps = h.n_mixed;
+        if (products32) *products32 = h.n_products32;
+        if (eta) *eta = h.eta;
+        if (k2) *k2 = h.k2;
+        if (holds_x32) *holds_x32 = e->X32 != nullptr;
+    } catch (std::exception &ex) {
+        set_error("%s", ex.what());
+        return -1;
+    }
     return 0;
 }
 
@@ -3533,6 +3612,11 @@ int bb_set_tuning(int key, int value) {
         case 8: {
             const int old = g_nid_sync;
             if (value >= 0) g_nid_sync = value > 2 ? 2 : value;
+            return old;
+        }
+        case 10: {
+            const int old = g_nid_mixed;
+            if (value >= 0) g_nid_mixed = value ? 1 : 0;
             return old;
         }
         case 9: {

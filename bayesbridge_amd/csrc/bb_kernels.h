@@ -44,11 +44,20 @@ enum LambdaMode { LAMBDA_ONLY = 0, LAMBDA_WOODBURY = 1 };
 // certified spectrum interval [1, 1 + eps].  Written on the device every sweep by
 // k_nid_reduce (k_nid_decide_from for shards); the kernels of the path not taken return at
 // once.
+// k2 > 0: the mixed-precision plan of an unsharded dense engine: mode = K1
+// iterates on M~ = I + X~ D X~' / sig2 (X~ = X rounded to fp32), one fp64 residual pass, then
+// k2 iterates on M~ from that residual; theta / delta / sigma1 are then those of [1, 1 + eps +
+// eta], eta >= |E - E~| certified.
 struct NidState {
     double eps, theta, delta, sigma1;
-    int mode, pad;
-    unsigned long long n_cheb, n_products, n_chol;  // sweeps per path, E-apply passes run
+    int mode, k2;
+    unsigned long long n_cheb, n_products, n_chol;  // sweeps per path, fp64 E-apply passes run
     double lambda_x;  // certified upper bound on lambda_max(X X') (0: none; setup)
+    double eta;       // the mixed plan's certified |E - E~| (0 on an fp64 sweep)
+    unsigned long long n_mixed, n_products32;  // mixed-plan sweeps, fp32 E-apply passes run
+    // the plans' cost model (s, set at setup from the shape): an fp64 / fp32 pass over X and
+    // the per-iterate step launch
+    double c64, c32, cstep;
 };
 constexpr double kNidTol = 1.3877787807814457e-17;  // 2^-56: bound on the relative error
 
@@ -101,21 +110,42 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
                      const DevScalars *sc, NidState *nid, int k_launched, int allow, int decide,
                      double *wg_part, double *red, double *eps_host);
 // unsharded, synchronous protocol: the sums and the decision, [eps, mode] into host2
+// allow_mixed: the engine holds an fp32 copy of X and may take the mixed-precision plan
+// (host2[2] = its k2, 0 for the fp64 plan)
 void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                             const DevScalars *sc, NidState *nid, int k_launched,
-                            double *wg_part, double *red, double *host2);
+                            double *wg_part, double *red, double *host2, int allow_mixed = 0);
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
                             int k_launched, NidState *nid, double *host2);
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
                    int n_pad, const NidState *nid, double *part);
+// b (optional): the right-hand side, kept for the mixed plan's residual pass
 void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
                       const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
-                      uint64_t t, const NidState *nid, double *x, double *r, double *d);
+                      uint64_t t, const NidState *nid, double *x, double *r, double *d,
+                      double *b = nullptr);
+// phase 1: step j of the first solve (runs if mode > j); phase 2: step j of the mixed plan's
+// correction solve (runs if k2 > j)
 void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
                       const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
-                      double *d);
+                      double *d, int phase = 1);
+// the mixed plan's restart: r = b - x - (E x) / sig2 from the fp64 residual pass's partials,
+// d = r / theta, x += d (runs if k2 > 0 and mode > 0)
+void launch_cheb_restart(hipStream_t s, const double *part, int nparts, int n_pad,
+                         const DevScalars *sc, const NidState *nid, const double *b, double *x,
+                         double *r, double *d);
+// One pass over X: part = X D X' v partials.  kind 0: product j of the first solve (runs if
+// mode > j; streams X32 when the sweep took the mixed plan and X32 is given); 2: the mixed
+// plan's fp64 residual pass (v = the iterate; runs if k2 > 0 and mode > 0); 3: product j of
+// the correction solve (X32; runs if k2 > j)
 void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
-                   const double *D, const double *v, const NidState *nid, int j, double *part);
+                   const double *D, const double *v, const NidState *nid, int j, double *part,
+                   const float *X32 = nullptr, int kind = 0);
+// X32 = X rounded to fp32 (n_pad x ncols, ld ldx); *bad = 1 if an entry is outside the range
+// where the rounding error is <= 2^-24 |x| (|x| > 2^126 or 0 < |x| < 2^-125)
+void launch_cast_f32(hipStream_t s, const double *X, int ldx, int n_pad, int ncols, float *X32,
+                     int *bad);
+constexpr double kU32 = 5.9604644775390625e-08;  // 2^-24: fp32 unit roundoff
 void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,
                       const int *rowptr, const int *colidx, const double *rval, int p_loc,
                       int n_pad, const double *D, const double *v, const NidState *nid, int j,

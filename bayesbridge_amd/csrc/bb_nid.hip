@@ -74,9 +74,75 @@ __device__ __forceinline__ double shard_threshold(double tau2, int k) {
     return ldexp(tau2, 40 - 2 * k);
 }
 
-// eps from the least bound, the iteration count K and the sweep's mode (thread 0)
+// ---------------------------------------------------------------------------------------
+// Mixed-precision plan (unsharded dense engines holding X32 = fl32(X)).
+// E~ = X32 D X32' / sig2 is exactly PSD, and with |X - X32| <= u32 |X| entrywise (u32 = 2^-24)
+//   |E - E~|_2 <= eta = 2 u32 sqrt(tr(E) eps) + u32^2 tr(E)
+// (|(X - X32) D^1/2|_F <= u32 sig sqrt(tr E), |X D^1/2|_2 <= sig sqrt(eps)).  So M~ = I + E~ has
+// its spectrum in [1, 1 + eps + eta] and |M^-1|, |M~^-1| <= 1.  The plan: x0 = K1 Chebyshev
+// iterates on M~ (each product one pass over the fp32 copy: half the bytes), r = b - M x0 in
+// fp64 (one pass over X), then K2 iterates on M~ from r, added to x0.  With t_K the Chebyshev
+// bound on [1, 1 + eps + eta]:
+//   |w - M^-1 b| / |M^-1 b| <= (eta + t_K2 (1 + eta)) (eta + t_K1 (1 + eta)),
+// (x0's error is eta + t_K1 (1 + eta) of the solution, the correction's relative error
+// eta + t_K2 (1 + eta)); the plan is taken when this is <= the tolerance and its cost -- in
+// fp64 passes: 0.55 per fp32 pass, 1 for the residual pass, 0.05 per launch of a step -- is
+// below the fp64 plan's and within the cap on the Chebyshev path's cost.
+// ---------------------------------------------------------------------------------------
+// The search runs on the 64 lanes of one wave: lane k - 1 holds t_k (T_k = cosh(k acosh
+// sigma1), overflow giving t_k = 0; a 1e-12 relative margin covers the closed form's rounding),
+// lane k1 - 1 finds its least k2 in one uniform scan (t_k2 by shuffle), then the cheapest
+// (cost, k1) by a wave minimum: ~1 us, against ~40 us for the same search on one thread.
+__device__ void nid_plan_mixed(double eps, double tr, int kcap, double cost_fp64,
+                               const NidState *nid, int &K1, int &K2, double &eta, double &e2) {
+    const int lane = threadIdx.x & 63;
+    K1 = K2 = 0;
+    eta = (2.0 * kU32 * sqrt(tr * eps) + kU32 * kU32 * tr) * (1.0 + 1e-6);
+    e2 = eps + eta;
+    if (!(e2 < 1e300) || kcap < 1) return;
+    const ChebConst c = cheb_const(e2);
+    const int kmax = kcap < 64 ? kcap : 64;
+    const double ac = acosh(c.sigma1);
+    const double tk = (lane + 1 <= kmax) ? sqrt(1.0 + e2) / cosh((lane + 1) * ac) * (1.0 + 1e-12)
+                                         : HUGE_VAL;
+    const double step32 = nid->c32 + nid->cstep, step64 = nid->c64 + nid->cstep;
+    const double cap = fmin(cost_fp64, (kcap - 1) * step64);
+    const int k1 = lane + 1;
+    const double err1 = eta + tk * (1.0 + eta);
+    const double need = kNidTol / err1;
+    int k2 = 0;
+    for (int k = 1; k <= kmax; ++k) {
+        const double t2 = __shfl(tk, k - 1, 64);
+        if (!k2 && eta + t2 * (1.0 + eta) <= need) k2 = k;
+    }
+    double cost = (k1 <= kmax && err1 < 1.0 && k2)
+                      ? (k1 - 1) * step32 + step64 + (k2 - 1) * step32
+                      : HUGE_VAL;
+    if (!(cost < cap * (1.0 - 1e-9))) cost = HUGE_VAL;
+    // wave minimum of (cost, k1): deterministic, ties to the smaller k1
+    double bc = cost;
+    int bk1 = k1, bk2 = k2;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double oc = __shfl_xor(bc, o, 64);
+        const int ok1 = __shfl_xor(bk1, o, 64), ok2 = __shfl_xor(bk2, o, 64);
+        if (oc < bc || (oc == bc && ok1 < bk1)) {
+            bc = oc;
+            bk1 = ok1;
+            bk2 = ok2;
+        }
+    }
+    if (bc < HUGE_VAL) {
+        K1 = bk1;
+        K2 = bk2;
+    }
+}
+
+// eps from the least bound, the iteration count K and the sweep's mode: called by the 64
+// lanes of one wave (every lane computes the same values; lane 0 writes them)
 __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launched, int allow,
-                           NidState *nid, double *eps_host, double *mode_host) {
+                           NidState *nid, double *eps_host, double *mode_host,
+                           int allow_mixed = 0, double *k2_host = nullptr) {
     const double tau2 = sc->tau * sc->tau;
     const double lam = red[kNidTS + 1];
     double best = red[kNidTS];
@@ -86,14 +152,37 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
     // rounding of the sums: a relative margin far above its worst case (p u)
     const double eps = best / sc->sig2 * (1.0 + 1e-6);
     const int K = cheb_iterations(eps, k_launched, kNidTol);
-    const int mode = (allow && K > 0) ? K : 0;
+    int mode = (allow && K > 0) ? K : 0, k2 = 0;
+    double ecb = eps, eta = 0.0;
+    if (allow && allow_mixed) {
+        const double tr = red[kNidTS] / sc->sig2 * (1.0 + 1e-6);
+        int k1m, k2m;
+        double e2;
+        nid_plan_mixed(eps, tr, k_launched, K > 0 ? (K - 1) * (nid->c64 + nid->cstep) : HUGE_VAL,
+                       nid, k1m, k2m, eta, e2);
+        if (k2m > 0) {
+            mode = k1m;
+            k2 = k2m;
+            ecb = e2;
+        } else {
+            eta = 0.0;
+        }
+    }
+    if ((threadIdx.x & 63) != 0) return;
     nid->eps = eps;
     nid->mode = mode;
-    const ChebConst c = cheb_const(eps);
+    nid->k2 = k2;
+    nid->eta = eta;
+    const ChebConst c = cheb_const(ecb);
     nid->theta = c.theta;
     nid->delta = c.delta;
     nid->sigma1 = c.sigma1;
-    if (mode) {
+    if (mode && k2) {
+        nid->n_cheb += 1;
+        nid->n_mixed += 1;
+        nid->n_products += 1ull;  // the fp64 residual pass
+        nid->n_products32 += (unsigned long long)(mode - 1 + k2 - 1);
+    } else if (mode) {
         nid->n_cheb += 1;
         nid->n_products += (unsigned long long)(mode - 1);
     } else {
@@ -101,6 +190,7 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
     }
     if (eps_host) *eps_host = eps;  // host-mapped: the launch hint / the shard's decision
     if (mode_host) *mode_host = (double)mode;
+    if (k2_host) *k2_host = (double)k2;
 }
 
 __global__ __launch_bounds__(kNidSumWG) void k_nid_sums(const double *__restrict__ D,
@@ -143,7 +233,7 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
                                                        const DevScalars *sc, int k_launched,
                                                        int allow, int decide, NidState *nid,
                                                        double *__restrict__ red,
-                                                       double *eps_host) {
+                                                       double *eps_host, int allow_mixed) {
     __shared__ double pq[kNidRedQ][kNidTS + 1];
     __shared__ double r[kNidTS + 2];
     const int t = threadIdx.x;
@@ -172,16 +262,16 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
         red[t] = v;
     }
     __syncthreads();
-    // decide 1: eps into eps_host (the launch hint); 2: [eps, mode] into eps_host[0..1]
-    if (decide && t == 0)
-        nid_finish(r, sc, k_launched, allow, nid, eps_host, decide == 2 ? eps_host + 1 : nullptr);
+    // decide 1: eps into eps_host (the launch hint); 2: [eps, mode, k2] into eps_host[0..2]
+    if (decide && t < 64)
+        nid_finish(r, sc, k_launched, allow, nid, eps_host, decide == 2 ? eps_host + 1 : nullptr,
+                   decide == 2 ? allow_mixed : 0, decide == 2 ? eps_host + 2 : nullptr);
 }
 
 __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
                                                         const DevScalars *sc, int k_launched,
                                                         NidState *nid, double *host2) {
-    if (threadIdx.x != 0) return;
-    nid_finish(red, sc, k_launched, 1, nid, host2, host2 + 1);
+    nid_finish(red, sc, k_launched, 1, nid, host2, host2 + 1, 0, host2 + 2);
 }
 
 // Row sums of the nparts partial n-vectors for rows [64 b, 64 b + 64): wave w adds partials
@@ -267,7 +357,7 @@ template <int RW>
 __global__ __launch_bounds__(kRsThreads) void k_cheb_init(
     const double *__restrict__ xu_part, int nparts, int n, int n_pad,
     const double *__restrict__ y, const DevScalars *sc, Key key, uint64_t t, const NidState *nid,
-    double *x, double *r, double *d) {
+    double *x, double *r, double *d, double *b) {
     if (nid->mode == 0) return;
     const int i = blockIdx.x * RW + (int)threadIdx.x;
     const double xu = part_rowsum_rw<RW>(xu_part, nparts, n_pad, blockIdx.x * RW);
@@ -282,6 +372,7 @@ __global__ __launch_bounds__(kRsThreads) void k_cheb_init(
     r[i] = rhs;
     d[i] = d0;
     x[i] = d0;
+    if (b) b[i] = rhs;
 }
 
 // Chebyshev step j (1 <= j <= K - 1): q = d + (sum of the E-apply partials) / sig2,
@@ -289,8 +380,8 @@ __global__ __launch_bounds__(kRsThreads) void k_cheb_init(
 template <int RW>
 __global__ __launch_bounds__(kRsThreads) void k_cheb_step(
     const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
-    const NidState *nid, int j, double *x, double *r, double *d) {
-    if (nid->mode <= j) return;
+    const NidState *nid, int j, double *x, double *r, double *d, int phase) {
+    if ((phase == 1 ? nid->mode : nid->k2) <= j) return;
     const int i = blockIdx.x * RW + (int)threadIdx.x;
     const double e = part_rowsum_rw<RW>(part, nparts, n_pad, blockIdx.x * RW);
     if ((int)threadIdx.x >= RW || i >= n_pad) return;
@@ -303,6 +394,24 @@ __global__ __launch_bounds__(kRsThreads) void k_cheb_step(
     r[i] = rv;
     d[i] = dn;
     x[i] += dn;
+}
+
+// The mixed plan's restart (k2 > 0): r = b - x - (the residual pass's E x partials) / sig2,
+// the correction's first iterate d = r / theta added to x (x then holds x0 + c_1).
+template <int RW>
+__global__ __launch_bounds__(kRsThreads) void k_cheb_restart(
+    const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
+    const NidState *nid, const double *__restrict__ b, double *x, double *r, double *d) {
+    if (nid->k2 == 0 || nid->mode == 0) return;
+    const int i = blockIdx.x * RW + (int)threadIdx.x;
+    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, blockIdx.x * RW);
+    if ((int)threadIdx.x >= RW || i >= n_pad) return;
+    const double xv = x[i];
+    const double rv = b[i] - (xv + e / sc->sig2);
+    const double dv = rv / nid->theta;
+    r[i] = rv;
+    d[i] = dv;
+    x[i] = xv + dv;
 }
 
 // out[i] = sum of the nparts partials of row i (setup: power iteration on X X')
@@ -339,38 +448,53 @@ constexpr int kEaCols = 8;
 constexpr int kEaThreads = 256;
 
 // XU: the same pass forming X u (part[wg][row] = sum_c X[row, c] D_c, with D = u), for the
-// right-hand side: no dot products, gated on mode != 0.
-template <int NR, bool XU>
-__global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict__ X, int ldx,
-                                                       int n_pad, int p_loc,
-                                                       const double *__restrict__ D,
-                                                       const double *__restrict__ v,
-                                                       const NidState *nid, int j,
-                                                       double *__restrict__ part) {
-    if (XU ? nid->mode == 0 : nid->mode <= j) return;
+// right-hand side: no dot products.  T: the element type streamed (double, or float for the
+// mixed plan's fp32 copy of X -- converted exactly to double, so the arithmetic is fp64).
+template <int NR, bool XU, typename T>
+__device__ __forceinline__ void eapply_body(const T *__restrict__ X, int ldx, int n_pad,
+                                            int p_loc, const double *__restrict__ D,
+                                            const double *__restrict__ v,
+                                            double *__restrict__ part) {
     __shared__ double ws[4][kEaCols];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     double vr[NR], acc[NR];
 #pragma unroll
     for (int m = 0; m < NR; ++m) {
         const int row = tid + kEaThreads * m;
-        vr[m] = row < n_pad ? v[row] : 0.0;
+        vr[m] = (!XU && row < n_pad) ? v[row] : 0.0;
         acc[m] = 0.0;
     }
     const int nchunk = (p_loc + kEaCols - 1) / kEaCols;
     for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
         const int c0 = ch * kEaCols;
-        double xv[kEaCols][NR];
+        // the chunk's elements in their stored type, every load in flight before the first use
+        // (a conversion inside a guarded load makes the compiler wait for each load in turn:
+        // the fp32 pass then ran at a third of the fp64 pass's rate)
+        T raw[kEaCols][NR];
+        if (c0 + kEaCols <= p_loc && NR * kEaThreads <= n_pad) {  // uniform: a full chunk
 #pragma unroll
-        for (int c = 0; c < kEaCols; ++c) {
-            const bool ok = c0 + c < p_loc;
-            const double *col = X + (size_t)(c0 + c) * ldx;
+            for (int c = 0; c < kEaCols; ++c)
 #pragma unroll
-            for (int m = 0; m < NR; ++m) {
-                const int row = tid + kEaThreads * m;
-                xv[c][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(col + row) : 0.0;
+                for (int m = 0; m < NR; ++m)
+                    raw[c][m] = __builtin_nontemporal_load(X + (size_t)(c0 + c) * ldx +
+                                                           tid + kEaThreads * m);
+        } else {
+#pragma unroll
+            for (int c = 0; c < kEaCols; ++c) {
+                const bool ok = c0 + c < p_loc;
+                const T *col = X + (size_t)(c0 + c) * ldx;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {
+                    const int row = tid + kEaThreads * m;
+                    raw[c][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(col + row) : T(0);
+                }
             }
         }
+        double xv[kEaCols][NR];
+#pragma unroll
+        for (int c = 0; c < kEaCols; ++c)
+#pragma unroll
+            for (int m = 0; m < NR; ++m) xv[c][m] = (double)raw[c][m];
         if constexpr (XU) {
 #pragma unroll
             for (int c = 0; c < kEaCols; ++c) {
@@ -406,6 +530,52 @@ __global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict_
         const int row = tid + kEaThreads * m;
         if (row < n_pad) part[(size_t)blockIdx.x * n_pad + row] = acc[m];
     }
+}
+
+// KIND (launch_eapply): 0 product j of the first solve (X32 when the mixed plan was taken),
+// 1 X u (XU), 2 the mixed plan's fp64 residual pass, 3 product j of its correction solve.
+// Each launch returns at once unless the device's decision needs it (the gate).
+template <int NR, int KIND>
+__global__ __launch_bounds__(kEaThreads) void k_eapply(const double *__restrict__ X,
+                                                       const float *__restrict__ X32, int ldx,
+                                                       int n_pad, int p_loc,
+                                                       const double *__restrict__ D,
+                                                       const double *__restrict__ v,
+                                                       const NidState *nid, int j,
+                                                       double *__restrict__ part) {
+    if constexpr (KIND == 1) {
+        if (nid->mode == 0) return;
+        eapply_body<NR, true, double>(X, ldx, n_pad, p_loc, D, v, part);
+    } else if constexpr (KIND == 0) {
+        if (nid->mode <= j) return;
+        if (X32 && nid->k2 > 0)
+            eapply_body<NR, false, float>(X32, ldx, n_pad, p_loc, D, v, part);
+        else
+            eapply_body<NR, false, double>(X, ldx, n_pad, p_loc, D, v, part);
+    } else if constexpr (KIND == 2) {
+        if (nid->k2 == 0 || nid->mode == 0) return;
+        eapply_body<NR, false, double>(X, ldx, n_pad, p_loc, D, v, part);
+    } else {
+        if (nid->k2 <= j) return;
+        eapply_body<NR, false, float>(X32, ldx, n_pad, p_loc, D, v, part);
+    }
+}
+
+// X32 = fl32(X); *bad = 1 for an entry whose fp32 rounding is not within 2^-24 relative
+// (beyond the normal range: the mixed plan is then not used)
+__global__ __launch_bounds__(256) void k_cast_f32(const double *__restrict__ X, int ldx,
+                                                  int n_pad, int ncols, float *__restrict__ X32,
+                                                  int *bad) {
+    const size_t tot = (size_t)n_pad * ncols;
+    bool b = false;
+    for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (size_t)gridDim.x * 256) {
+        const size_t c = e / n_pad, r = e % n_pad;
+        const double x = X[c * ldx + r];
+        const double ax = fabs(x);
+        b |= !(ax <= 0x1p126) || (ax != 0.0 && ax < 0x1p-125);
+        X32[c * ldx + r] = (float)x;
+    }
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -482,15 +652,16 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
     const int G = nid_sum_groups(p_loc);
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
     k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
-                                  eps_host);
+                                  eps_host, 0);
 }
 
 void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                             const DevScalars *sc, NidState *nid, int k_launched,
-                            double *wg_part, double *red, double *host2) {
+                            double *wg_part, double *red, double *host2, int allow_mixed) {
     const int G = nid_sum_groups(p_loc);
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
-    k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, 1, 2, nid, red, host2);
+    k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, 1, 2, nid, red, host2,
+                                      allow_mixed);
 }
 
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
@@ -498,48 +669,73 @@ void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *
     k_nid_decide_from<<<1, 64, 0, s>>>(red, sc, k_launched, nid, host2);
 }
 
-template <bool XU>
-static void launch_pass(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
-                        const double *D, const double *v, const NidState *nid, int j,
+template <int KIND>
+static void launch_pass(hipStream_t s, const double *X, const float *X32, int ldx, int n_pad,
+                        int p_loc, const double *D, const double *v, const NidState *nid, int j,
                         double *part) {
     const int g = eapply_parts(p_loc, n_pad);
     const int nr = (n_pad + kEaThreads - 1) / kEaThreads;
-    auto *kern = nr <= 1 ? k_eapply<1, XU> : nr <= 2 ? k_eapply<2, XU> : nr <= 4 ? k_eapply<4, XU>
-               : nr <= 8 ? k_eapply<8, XU> : k_eapply<16, XU>;
-    if (!XU) note_launch(KF_EAPPLY, (const void *)kern);
-    kern<<<g, kEaThreads, 0, s>>>(X, ldx, n_pad, p_loc, D, v, nid, j, part);
+    auto *kern = nr <= 1 ? k_eapply<1, KIND> : nr <= 2 ? k_eapply<2, KIND>
+               : nr <= 4 ? k_eapply<4, KIND> : nr <= 8 ? k_eapply<8, KIND> : k_eapply<16, KIND>;
+    if (KIND == 0) note_launch(KF_EAPPLY, (const void *)kern);
+    kern<<<g, kEaThreads, 0, s>>>(X, X32, ldx, n_pad, p_loc, D, v, nid, j, part);
 }
 
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
                    int n_pad, const NidState *nid, double *part) {
-    launch_pass<true>(s, X, ldx, n_pad, ncols, u, nullptr, nid, 0, part);
+    launch_pass<1>(s, X, nullptr, ldx, n_pad, ncols, u, nullptr, nid, 0, part);
 }
 
 void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, int n_pad,
                       const double *y, const DevScalars *sc, uint64_t k0, uint64_t k1,
-                      uint64_t t, const NidState *nid, double *x, double *r, double *d) {
+                      uint64_t t, const NidState *nid, double *x, double *r, double *d,
+                      double *b) {
     if (rowsum_rw(nparts) == 8)
         k_cheb_init<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
-                                                              Key{k0, k1}, t, nid, x, r, d);
+                                                              Key{k0, k1}, t, nid, x, r, d, b);
     else
         k_cheb_init<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y,
-                                                                 sc, Key{k0, k1}, t, nid, x, r, d);
+                                                                 sc, Key{k0, k1}, t, nid, x, r, d,
+                                                                 b);
 }
 
 void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
                       const DevScalars *sc, const NidState *nid, int j, double *x, double *r,
-                      double *d) {
+                      double *d, int phase) {
     if (rowsum_rw(nparts) == 8)
         k_cheb_step<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j, x,
-                                                              r, d);
+                                                              r, d, phase);
     else
         k_cheb_step<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j,
+                                                                 x, r, d, phase);
+}
+
+void launch_cheb_restart(hipStream_t s, const double *part, int nparts, int n_pad,
+                         const DevScalars *sc, const NidState *nid, const double *b, double *x,
+                         double *r, double *d) {
+    if (rowsum_rw(nparts) == 8)
+        k_cheb_restart<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, b,
                                                                  x, r, d);
+    else
+        k_cheb_restart<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid,
+                                                                    b, x, r, d);
 }
 
 void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,
-                   const double *D, const double *v, const NidState *nid, int j, double *part) {
-    launch_pass<false>(s, X, ldx, n_pad, p_loc, D, v, nid, j, part);
+                   const double *D, const double *v, const NidState *nid, int j, double *part,
+                   const float *X32, int kind) {
+    switch (kind) {
+        case 2: launch_pass<2>(s, X, X32, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        case 3: launch_pass<3>(s, X, X32, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+        default: launch_pass<0>(s, X, X32, ldx, n_pad, p_loc, D, v, nid, j, part); break;
+    }
+}
+
+void launch_cast_f32(hipStream_t s, const double *X, int ldx, int n_pad, int ncols, float *X32,
+                     int *bad) {
+    const size_t tot = (size_t)n_pad * ncols;
+    const unsigned g = (unsigned)std::min<size_t>((tot + 255) / 256, 4096);
+    k_cast_f32<<<g, 256, 0, s>>>(X, ldx, n_pad, ncols, X32, bad);
 }
 
 void launch_sp_eapply(hipStream_t s, const int *colptr, const int *rowidx, const double *cval,

@@ -397,9 +397,14 @@ def roofline_for(phase, ms, ctx, traffic_world):
             byts = 8.0 * n_pad * p_loc + 8.0 * p_loc + 8.0 * n_pad * (1 + ctx.get("ea_parts", 512))
             kname, kfull = "k_eapply (X D X' d, one pass over X)", "bb::k_eapply"
         pf = ctx.get("pass_frac", 1.0)
-        out.update(bound="hbm", kernel=kname, achieved=byts * pf / sec / 1e9, peak=8000.0,
-                   unit="GB/s", algorithmic_bytes_per_launch=byts * pf,
-                   bytes_per_pass=byts, passes_per_launch=pf)
+        # fp32 passes of the mixed plan: X at 4 B per element
+        pf32 = 0.0 if sparse else ctx.get("pass32_frac", 0.0)
+        byts32 = byts - 4.0 * n_pad * p_loc
+        algo = byts * pf + byts32 * pf32
+        out.update(bound="hbm", kernel=kname, achieved=algo / sec / 1e9, peak=8000.0,
+                   unit="GB/s", algorithmic_bytes_per_launch=algo,
+                   bytes_per_pass=byts, passes_per_launch=pf,
+                   bytes_per_fp32_pass=byts32, fp32_passes_per_launch=pf32)
     elif phase == "lambda":
         # the tilted-stable draws: VALU-bound arithmetic with a rejection tail.
         # achieved = SIMD issue cycles per launch -- the per-class VALU instruction counts of the
@@ -672,6 +677,7 @@ def run_chain(args, n, p, alpha, kind, mode):
     eng.enable_timing(True, phases=False, timed_phase=dom, stride=stride)
     eng.reset_timing()
     nid0 = eng.nid_stats()
+    mix0 = eng.nid_mixed()
     t0 = time.perf_counter()
     # the timed loop records every sweep's beta / lambda / sig2 / tau into the device trace
     # ring, as the reference's MCMC loop writes its output slots (BridgeWrapper.cpp:287-298)
@@ -689,15 +695,20 @@ def run_chain(args, n, p, alpha, kind, mode):
     # the exact kernel instances the timed sweeps launched (the PMC evidence is matched on them)
     instances = {ph: bb.kernel_instance(ph) for ph in SINGLE_KERNEL_PHASES}
     nid1 = eng.nid_stats()
+    mix1 = eng.nid_mixed()
     eng.enable_timing(False)
     nid = None
     ctx_pass_frac = 1.0
+    ctx_pass32 = 0.0
     if nid1["mode"] >= 0:
         dc = nid1["cheb_sweeps"] - nid0["cheb_sweeps"]
         dp = nid1["products"] - nid0["products"]
         nid = {"timed_sweeps": args.steps, "chebyshev_sweeps": dc,
                "cholesky_sweeps": nid1["chol_sweeps"] - nid0["chol_sweeps"],
                "eapply_passes_per_chebyshev_sweep": (dp / dc) if dc else None,
+               "mixed_plan_sweeps": mix1["mixed_sweeps"] - mix0["mixed_sweeps"],
+               "fp32_passes_per_chebyshev_sweep": ((mix1["products32"] - mix0["products32"]) / dc
+                                                   if dc else None),
                "eps_last": nid1["eps"],
                "rule": "per sweep on the device: Chebyshev iteration on the certified spectrum "
                        "interval [1, 1 + eps], eps >= lambda_max(X D X') / sig2 (the least of "
@@ -711,6 +722,9 @@ def run_chain(args, n, p, alpha, kind, mode):
         # bytes per launch are a pass's bytes x (passes run / launches), its time the average
         # over all launches (what a rocprofv3 kernel trace averages)
         ctx_pass_frac = (dp / brackets) if (dom == "eapply" and brackets) else 1.0
+        # the mixed plan's products stream the fp32 copy of X (4 B per element)
+        ctx_pass32 = ((mix1["products32"] - mix0["products32"]) / brackets
+                      if (dom == "eapply" and brackets) else 0.0)
     flags = eng.error_flags()
     st = eng.state()
     if not (math.isfinite(st["tau"]) and math.isfinite(st["sig2"])) or flags:
@@ -721,7 +735,8 @@ def run_chain(args, n, p, alpha, kind, mode):
                  ("ozaki-II int8 (fp64-accurate)" if eng.gram_mode() == bb.GRAM_OZAKI
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
-               gram_name=gram_name, pass_frac=ctx_pass_frac, nid_cheb=nid_phase_cheb,
+               gram_name=gram_name, pass_frac=ctx_pass_frac, pass32_frac=ctx_pass32,
+               nid_cheb=nid_phase_cheb,
                instances=instances)
     fitted = None
     if mode == "single" and not logit and not args.no_fitted:

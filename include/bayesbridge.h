@@ -353,6 +353,9 @@ void bb_set_trace_budget(long long bytes);
  * comm, bb_engine_comm_init) or belongs to an on-device shard group run the column-shard
  * near-identity protocol of world > 1 (bound sums exchanged, the decision from them, X u and
  * every product E d exchanged), so each of its exchanges executes on one GPU (default 0).
+ * key 10: the mixed-precision near-identity plan of unsharded dense Woodbury engines
+ * (products over an fp32 copy of X, one fp64 residual pass, the same certified bound; 1, the
+ * default) or fp64 products only (0).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
@@ -440,6 +443,13 @@ int bb_engine_launch_counts(bb_engine *e, unsigned long long *lambda_xu,
  * "gram", "reduce", "chol", "solve", "beta", "eapply"), demangled without its parameter list
  * ("bb::k_eapply<8, false>"), into buf.  Returns 0, or -1 if none was launched. */
 int bb_kernel_instance(const char *phase, char *buf, int len);
+
+/* The mixed-precision near-identity plan: sweeps that took it and the fp32
+ * E-apply passes they ran (counts since creation), the latest sweep's certified |E - E~| and
+ * correction iterates (0: that sweep took the fp64 plan or the factor), and whether the engine
+ * holds the fp32 copy of X at all. */
+int bb_engine_nid_mixed(bb_engine *e, unsigned long long *mixed_sweeps,
+                        unsigned long long *products32, double *eta, int *k2, int *holds_x32);
 
 /* Error flags raised on device (rejection-loop caps, non-SPD factorisations). */
 int bb_engine_error_flags(bb_engine *e, uint32_t *flags);

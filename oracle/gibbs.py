@@ -138,6 +138,68 @@ def beta_step_woodbury_nid(X, y, lam, sig2, tau, z, delta, kmax=16, lam_x=0.0):
     return u + D * (X.T @ w) / sig, K
 
 
+U32 = 2.0 ** -24  # bb_kernels.h kU32
+COST32, COST_STEP = 0.55, 0.05  # bb_nid.hip kCost32, kCostStep
+
+
+def cheb_bounds(eps, kmax):
+    """b[K] = sqrt(1 + eps) / T_K(sigma1), K = 1..kmax (b[0] unused): the relative error bound
+    of K Chebyshev iterates on [1, 1 + eps]."""
+    theta, delta = 1.0 + 0.5 * eps, 0.5 * eps
+    sigma1 = theta / delta
+    out = [np.inf]
+    tm1, tk = 1.0, sigma1
+    for _ in range(1, kmax + 1):
+        out.append(np.sqrt(1.0 + eps) / tk)
+        # T_K grows without bound: once it overflows every later bound is 0
+        tm1, tk = tk, (2.0 * sigma1 * tk - tm1 if tk < 1e300 else np.inf)
+    return out
+
+
+def nid_plan_mixed(eps, tr, kcap, cost_fp64, c64=1.0, c32=COST32, cstep=COST_STEP,
+                   tol=NID_TOL):
+    """Restates bb_nid.hip nid_plan_mixed: eta >= |E - E~|_2 for E~ built from
+    X rounded to fp32, and the cheapest (K1, K2) with
+    (eta + t_K2 (1 + eta)) (eta + t_K1 (1 + eta)) <= tol on [1, 1 + eps + eta], t_K =
+    sqrt(1 + e2) / cosh(K acosh sigma1) (1 + 1e-12); costs (K1 - 1 + K2 - 1)(c32 + cstep) +
+    c64 + cstep against the fp64 plan's cost_fp64 and the cap (kcap - 1)(c64 + cstep); (0, 0)
+    when neither is beaten.  Returns (K1, K2, eta, e2)."""
+    eta = (2.0 * U32 * np.sqrt(tr * eps) + U32 * U32 * tr) * (1.0 + 1e-6)
+    e2 = eps + eta
+    if not e2 < 1e300 or kcap < 1:
+        return 0, 0, eta, e2
+    kmax = min(kcap, 64)
+    sigma1 = (1.0 + 0.5 * e2) / (0.5 * e2)
+    ac = np.arccosh(sigma1)
+    with np.errstate(over="ignore"):
+        t = [np.inf] + [np.sqrt(1.0 + e2) / np.cosh(k * ac) * (1.0 + 1e-12)
+                        for k in range(1, kmax + 1)]
+    step32, step64 = c32 + cstep, c64 + cstep
+    cap = min(cost_fp64, (kcap - 1) * step64)
+    best, K1, K2 = np.inf, 0, 0
+    for k1 in range(1, kmax + 1):
+        err1 = eta + t[k1] * (1.0 + eta)
+        if not err1 < 1.0:
+            continue
+        need = tol / err1
+        k2 = next((k for k in range(1, kmax + 1) if eta + t[k] * (1.0 + eta) <= need), 0)
+        if not k2:
+            continue
+        cost = (k1 - 1) * step32 + step64 + (k2 - 1) * step32
+        if cost < cap * (1.0 - 1e-9) and cost < best:
+            best, K1, K2 = cost, k1, k2
+    return K1, K2, eta, e2
+
+
+def woodbury_solve_mixed(apply_E, apply_E32, rhs, e2, K1, K2):
+    """The mixed plan's solve (bb_engine nidx_mixed_tail): K1 Chebyshev iterates on M~ (apply_E32
+    = the product over X rounded to fp32), the fp64 residual r = rhs - M x0, then K2 iterates on
+    M~ from r added to x0; the interval [1, 1 + e2] for both."""
+    x0 = woodbury_solve_cheb(apply_E32, rhs, e2, K1)
+    r = rhs - (x0 + apply_E(x0))
+    return x0 + woodbury_solve_cheb(apply_E32, r, e2, K2)
+
+
 NID_TS = 32  # bb_kernels.h kNidTS
 
 

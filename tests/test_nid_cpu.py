@@ -97,3 +97,72 @@ def test_shard_bound_is_certified(world, log_tau):
     red[gibbs.NID_TS + 1] = np.inf
     eps_t, _ = gibbs.nid_decide_from(red, tau, sig2)
     assert abs(eps_t - trace * (1 + 1e-6)) <= 1e-12 * trace
+
+
+# ---------------------------------------------------------------------------------------
+# The mixed-precision plan (bb_nid.hip nid_plan_mixed, bb_engine
+# nidx_mixed_tail) restated in oracle/gibbs.py
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed,n,p,spread", [(1, 80, 400, 2.0), (2, 120, 900, 6.0),
+                                             (3, 60, 200, 0.5), (4, 100, 600, 10.0)])
+def test_mixed_eta_bounds_fp32_rounding_of_E(seed, n, p, spread):
+    """eta = 2 u32 sqrt(tr(E) eps) + u32^2 tr(E) bounds |E - E~|_2 for E~ = X32 D X32' / sig2
+    with X32 = fl32(X) and eps >= lambda_max(E) -- the certificate the mixed plan rests on --
+    on random designs with D over `spread` decades."""
+    from oracle import gibbs
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, p)) * 10.0 ** rng.uniform(-3, 3, size=p)
+    D = 10.0 ** rng.uniform(-spread, 0, size=p) * 1e-3
+    sig2 = 1.7
+    X32 = X.astype(np.float32).astype(np.float64)
+    E = (X * D) @ X.T / sig2
+    E32 = (X32 * D) @ X32.T / sig2
+    lmax = np.linalg.eigvalsh(E)[-1]
+    tr = np.trace(E)
+    for eps in (lmax, 3 * lmax, tr):
+        _, _, eta, _ = gibbs.nid_plan_mixed(eps, tr, 16, np.inf)
+        err = np.abs(np.linalg.eigvalsh(E - E32)).max()
+        assert err <= eta, (eps, err, eta)
+        assert eta < 64 * gibbs.U32 * np.sqrt(tr * eps) + 1e-300
+
+
+@pytest.mark.parametrize("eps_scale", [1e-12, 1e-8, 1e-5, 1e-3, 3e-2])
+def test_mixed_solve_meets_certified_bound(eps_scale):
+    """The mixed plan chosen for a state solves (I + E) w = b to the fp64 plan's accuracy: the
+    certified product (eta + t2)(eta + t1) <= 2^-56, and the computed w agrees with the exact
+    solve to rounding; it is chosen only when cheaper than the fp64 plan."""
+    from oracle import gibbs
+    rng = np.random.default_rng(7)
+    n, p = 150, 1200
+    X = rng.standard_normal((n, p))
+    lam_true = np.linalg.eigvalsh(X @ X.T)[-1]
+    D = rng.exponential(size=p) * eps_scale / lam_true * 3
+    sig2 = 1.0
+    X32 = X.astype(np.float32).astype(np.float64)
+    E = (X * D) @ X.T / sig2
+    tr = np.trace(E)
+    eps = 3.0 * np.linalg.eigvalsh(E)[-1]  # a certified bound (as the device's thresholded sums)
+    K64 = gibbs.cheb_iterations(eps, 16)
+    cost64 = (K64 - 1) * (1.0 + gibbs.COST_STEP) if K64 else np.inf
+    K1, K2, eta, e2 = gibbs.nid_plan_mixed(eps, tr, 16, cost64)
+    b = rng.standard_normal(n)
+    w_exact = np.linalg.solve(np.eye(n) + E, b)
+    if K2:
+        t = gibbs.cheb_bounds(e2, 64)  # the recurrence form: the closed form's margin holds
+        assert (eta + t[K2] * (1 + eta)) * (eta + t[K1] * (1 + eta)) <= gibbs.NID_TOL * (1 + 1e-9)
+        step32 = gibbs.COST32 + gibbs.COST_STEP
+        cost = (K1 + K2 - 2) * step32 + 1.0 + gibbs.COST_STEP
+        assert cost < cost64
+        w = gibbs.woodbury_solve_mixed(lambda v: (X @ (D * (X.T @ v))) / sig2,
+                                       lambda v: (X32 @ (D * (X32.T @ v))) / sig2, b, e2, K1, K2)
+    elif K64 == 0:
+        return  # neither Chebyshev plan within the cap: the sweep takes the factor
+    else:
+        w = gibbs.woodbury_solve_cheb(lambda v: (X @ (D * (X.T @ v))) / sig2, b, eps, K64)
+    err = np.linalg.norm(w - w_exact) / np.linalg.norm(w_exact)
+    print(f"\n[eps ~ {eps:.2e}] K64 {K64}, mixed ({K1}, {K2}), eta {eta:.2e}, rel err {err:.2e}")
+    assert err < 1e-14
+    if 1e-8 <= eps_scale <= 1e-5:
+        assert K2 > 0  # the plan is taken where the fp64 plan needs several products
+    if eta * eta > gibbs.NID_TOL:
+        assert K2 == 0  # beyond a single refinement's reach: the fp64 plan

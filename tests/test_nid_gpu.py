@@ -305,3 +305,101 @@ def test_timed_phase_stride(gpu_lib, stride):
     e.enable_timing(False)
     with pytest.raises(Exception):
         e.enable_timing(True, phases=False, timed_phase="lambda", stride=0)
+
+
+# ---------------------------------------------------------------------------------------
+# The mixed-precision plan: products over the fp32 copy of X, one fp64
+# residual pass; the same certified bound as the fp64 plan
+# ---------------------------------------------------------------------------------------
+def test_mixed_plan_sweep_equals_fp64_plan(gpu_lib, capsys):
+    """One sweep from the same state with the mixed plan allowed (bb_set_tuning key 10 = 1)
+    and with fp64 products only (0): the same lambda, tau, sig2 bits and beta to 1e-12
+    relative, over states from the near-null regime (2 iterates) to eps ~ 1e-2 (7, where the
+    certificate's eta^2 exceeds the tolerance and the fp64 plan is kept); the device takes the
+    mixed plan (nid_mixed counts it) in between.  C3's shape restricted to n = 2000,
+    p = 6250 (the E-apply's rows in registers, n_pad = 2048)."""
+    import bench
+    bb = gpu_lib
+    n, p = 2000, 6250
+    X = bench.make_columns(n, 0, p)
+    y, btrue = bench.make_problem_y(n, p)
+    rng = np.random.default_rng(11)
+    engs = {}
+    for mixed in (1, 0):
+        old = bb.set_tuning(10, mixed)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            engs[mixed] = e
+        finally:
+            bb.set_tuning(10, old)
+    assert engs[1].nid_mixed()["holds_x32"]
+    plans = []
+    for scale in (1e-5, 1e-4, 3e-4, 1e-3, 1e-2):
+        beta, tau = btrue * scale + scale * rng.standard_normal(p), scale
+        for t in (3, 4):
+            outs = {}
+            for mixed, e in engs.items():
+                old = bb.set_tuning(10, mixed)
+                try:
+                    e.set_state(beta, tau, 1.0, 0.5)
+                    e.run(t, 1)
+                    e.sync()
+                    outs[mixed] = (e.state(), e.nid_stats(), e.nid_mixed())
+                finally:
+                    bb.set_tuning(10, old)
+            (a, sa, ma), (o, so, _) = outs[1], outs[0]
+            plans.append((scale, sa["mode"], ma["k2"], so["mode"], f"{ma['eta']:.1e}"))
+            assert a["tau"] == o["tau"] and a["sig2"] == o["sig2"]
+            assert np.array_equal(a["lambda"], o["lambda"])
+            err = rel_err(a["beta"], o["beta"])
+            assert err < 1e-12, (plans[-1], err)
+            beta, tau = o["beta"], o["tau"]
+    m = engs[1].nid_mixed()
+    with capsys.disabled():
+        print(f"\n[mixed] (scale, K1, K2, K fp64, eta) per sweep {plans}; {m}")
+    assert engs[0].nid_mixed()["mixed_sweeps"] == 0
+    assert m["mixed_sweeps"] >= 2 and m["products32"] >= 1, (plans, m)
+    for e in engs.values():
+        assert e.error_flags() == 0
+        e.close()
+
+
+def test_mixed_plan_teacher_forced_against_oracle(gpu_lib, capsys):
+    """The C3 workload itself (bench.py's X, y, key) run free from the reference start for
+    600 sweeps -- eps ~ 2e-4, where the fp64 plan needs 4-5 products and the device takes the
+    mixed plan -- then 3 sweeps teacher-forced against the oracle's Cholesky-based Woodbury draw
+    (beta 1e-10 relative L2, lambda / tau / sig2 1e-11, no flips), asserting the plan each
+    sweep took."""
+    from tests.test_steady_state_gpu import oracle_sweep, workload
+    bb = gpu_lib
+    X, y, alpha = workload("c3")
+    n, p = X.shape
+    e = bb.Engine(bb.EngineConfig(n=n, p=p, seed=SEED, stream=0, true_alpha=alpha,
+                                  trace_capacity=1), X, y)
+    e.init_state()
+    e.run(1, 600, first_slot=-1)
+    e.sync()
+    s0 = e.state()
+    beta, tau, sig2 = s0["beta"], s0["tau"], s0["sig2"]
+    taken = []
+    for t in (1001, 1002, 1003):
+        m0 = e.nid_mixed()["mixed_sweeps"]
+        e.set_state(beta, tau, sig2, alpha)
+        e.run(t, 1, first_slot=-1)
+        g = e.state()
+        st, m = e.nid_stats(), e.nid_mixed()
+        b, lam, tau, sig2 = oracle_sweep(X, y, beta, tau, sig2, alpha, t, SEED, 0)
+        taken.append(m["mixed_sweeps"] - m0)
+        with capsys.disabled():
+            print(f"\n[mixed c3 t={t}] eps={st['eps']:.3g} K1={st['mode']} K2={m['k2']} "
+                  f"eta={m['eta']:.2e} beta rel {rel_err(g['beta'], b):.2e}")
+        assert (m["k2"] >= 1) == (taken[-1] == 1), (st, m)
+        assert abs(g["tau"] - tau) / tau < 1e-11 and abs(g["sig2"] - sig2) / sig2 < 1e-11
+        assert flips(g["lambda"], lam) == 0
+        assert np.max(np.abs(g["lambda"] - lam) / lam) < 1e-11
+        assert rel_err(g["beta"], b) < 1e-10
+        beta = b
+    assert sum(taken) >= 2, taken  # the mixed plan was exercised
+    assert e.error_flags() == 0
+    e.close()
