@@ -229,7 +229,7 @@ def _stale_note(d, f):
             "not used (re-profile: tools/profile_round.sh / pmc_valu.sh / pmc_mfma.sh)")
 
 
-def pmc_traffic(n, p, world, instance):
+def pmc_traffic(n, p, world, instance, window=None):
     """HBM bytes per launch of the EXACT kernel instance (e.g. "bb::k_eapply<8, false>") from
     the newest committed PMC summary of this workload (profiles/rNN_pmc.json:
     tools/profile_round.sh + tools/profile_summary.py, separate FETCH_SIZE / WRITE_SIZE passes,
@@ -242,6 +242,9 @@ def pmc_traffic(n, p, world, instance):
         w = d.get("workload", {})
         if w.get("n") != n or w.get("p") != p:
             continue
+        if window is not None and (d.get("window") or {}).get("steps") != window[0] or \
+                window is not None and (d.get("window") or {}).get("warmup") != window[1]:
+            continue  # a per-sweep kernel's average depends on the window's regime
         v = d.get("kernels", {}).get(instance)
         if not v or v.get("hbm_bytes") != v.get("hbm_bytes"):  # absent, or NaN (one pass lacks it)
             note = f"{f} has no entry for {instance}"
@@ -278,7 +281,7 @@ def pmc_mfma(n, p, world, instance, gram):
 VALU_PEAK_GCYC = 1024 * 2.4  # SIMD issue cycles per ns: 1024 SIMDs at 2.4 GHz
 
 
-def pmc_valu(n, p, world, instance):
+def pmc_valu(n, p, world, instance, window=None):
     """VALU evidence for the exact kernel instance at this workload from the newest committed
     profiles/rNN_pmc_valu.json of this tree (tools/pmc_valu.sh: SQ_INSTS_VALU and the per-class
     SQ_INSTS_VALU_* counts, one counter per --pmc pass; tools/pmc_valu_summary.py prices them
@@ -287,6 +290,9 @@ def pmc_valu(n, p, world, instance):
     for d, f in _profiles("r*_pmc_valu.json"):
         for cfg in d.get("configs", {}).values():
             if cfg.get("n") != n or cfg.get("p") != p or world != 1:
+                continue
+            cw = cfg.get("window") or {}
+            if window is not None and (cw.get("steps"), cw.get("warmup")) != tuple(window):
                 continue
             v = cfg.get("kernels", {}).get(instance)
             if not v or "SQ_INSTS_VALU" not in v:
@@ -415,7 +421,7 @@ def roofline_for(phase, ms, ctx, traffic_world):
         # launch (k_lambda_xu, dense near-identity sweeps) also streams X for X u: its HBM rate.
         kfull = ctx.get("instances", {}).get("lambda")
         fused = bool(kfull) and kfull.startswith("bb::k_lambda_xu")
-        v, vnote = pmc_valu(n, p, traffic_world, kfull)
+        v, vnote = pmc_valu(n, p, traffic_world, kfull, ctx.get("window"))
         cyc = v.get("issue_cycles") if v else None
         out.update(bound="valu", kernel=kfull,
                    achieved=(cyc / sec / 1e9) if cyc else None, peak=VALU_PEAK_GCYC,
@@ -461,7 +467,11 @@ def roofline_for(phase, ms, ctx, traffic_world):
     # (bb_kernel_instance), never on a name prefix
     inst = ctx.get("instances", {}).get(phase)
     out["kernel_instance"] = inst
-    tb, tsrc, tnote = pmc_traffic(n, p, traffic_world, inst)
+    # the per-sweep kernels' traffic from a profile of the same bench window; the Gram, CRT
+    # and factor run only on factor sweeps (the fitted-regime run at C3): any window
+    tb, tsrc, tnote = pmc_traffic(n, p, traffic_world, inst,
+                                  None if phase in ("gram", "reduce", "chol", "solve")
+                                  else ctx.get("window"))
     if out.get("bound") == "mfma":
         mf = pmc_mfma(n, p, traffic_world, inst, ctx.get("gram_name"))
         out["mfma_busy_frac"] = mf["mfma_busy_frac"] if mf else None
@@ -736,6 +746,7 @@ def run_chain(args, n, p, alpha, kind, mode):
                   else "fp64 mfma"))
     ctx = dict(bb=bb, eng=eng, kind=kind, n=n, p=p, p_loc=p_loc, gram_mode=eng.gram_mode(),
                gram_name=gram_name, pass_frac=ctx_pass_frac, pass32_frac=ctx_pass32,
+               window=(args.steps, args.warmup),
                nid_cheb=nid_phase_cheb,
                instances=instances)
     fitted = None

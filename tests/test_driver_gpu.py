@@ -90,7 +90,9 @@ def test_interrupt_during_burn_in(gpu_lib):
 @pytest.mark.parametrize("mode", ["rccl", "ondevice"])
 def test_one_member_group_equals_single_engine(gpu_lib, mode):
     """A one-member shard group (RCCL communicator from ncclCommInitAll, or the on-device
-    sums) reproduces the communicator-free engine bit for bit."""
+    sums) reproduces the communicator-free engine bit for bit.  Shard-group members decide the
+    fp64 near-identity plan only, so the on-device member is compared with
+    the engine run with the mixed-precision plan off (bb_set_tuning key 10 = 0)."""
     bb = gpu_lib
     n, p = 150, 2000
     X, y, _ = synthetic_problem(n, p, seed=31)
@@ -104,8 +106,13 @@ def test_one_member_group_equals_single_engine(gpu_lib, mode):
             g.run(1, 8, first_slot=0, slot_step=1)
             g.sync()
         else:
-            e.init_state()
-            e.run(1, 8, first_slot=0, slot_step=1)
+            old = bb.set_tuning(10, 1 if mode == "rccl" else 0)
+            try:
+                e.init_state()
+                e.run(1, 8, first_slot=0, slot_step=1)
+                e.sync()
+            finally:
+                bb.set_tuning(10, old)
         outs.append(e.trace(0, 8))
         if grouped:
             g.close()

@@ -15,7 +15,7 @@ pass() {  # $1 = config name, $2 = counter, rest = bench args
     local cfg=$1 ctr=$2; shift 2
     timeout -s KILL 240 rocprofv3 --pmc "$ctr" --kernel-include-regex "$REGEX" \
         -d "$OUT/$cfg/$ctr" -o run --output-format csv \
-        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fitted "$@" \
+        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fitted "$@" \
         > "$OUT/$cfg/$ctr.json" 2> "$OUT/$cfg/$ctr.err" || { echo "$cfg $ctr failed ($?)"; exit 1; }
     echo "$cfg $ctr ok"
 }

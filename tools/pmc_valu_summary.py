@@ -108,7 +108,8 @@ def main_counts(rnd, asm_path):
         bl = bench_line(d)
         steps = int(bl.get("steps", 0)) or None
         ent = {"workload": bl.get("config", {}).get("workload"), "n": bl.get("config", {}).get("n"),
-               "p": bl.get("config", {}).get("p"), "timed_dispatches": steps, "kernels": {}}
+               "p": bl.get("config", {}).get("p"), "timed_dispatches": steps,
+               "window": {"steps": bl.get("steps"), "warmup": bl.get("warmup")}, "kernels": {}}
         per = {}
         for cd in sorted(os.listdir(d)):
             if os.path.isdir(os.path.join(d, cd)):

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round profile of the bench workload (run on the GPU box):
-#   1. rocprofv3 --kernel-trace --stats       -> per-kernel average durations (the driver's
-#      --steps 20 --warmup 5)
+#   1. rocprofv3 --kernel-trace --stats       -> per-kernel average durations
+# every pass over the same bench window, STEPS timed sweeps after WARMUP (default the
+# driver's 20 after 5), recorded in the summary: bench.py matches the per-sweep kernels'
+# traffic on it (a kernel's average over its dispatches depends on the window's regime)
 #   2. rocprofv3 --pmc FETCH_SIZE  (own pass) -> HBM read KB per dispatch
 #   3. rocprofv3 --pmc WRITE_SIZE  (own pass) -> HBM write KB per dispatch
 # No --pmc pass is combined with any trace domain.  Each step has its own time limit and
@@ -14,16 +16,17 @@ mkdir -p "$OUT"
 # the sources this profile measures (bench.py uses a profile only for the same tree)
 python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
 ARGS="--no-cpu-baseline $*"
+WIN="--steps ${STEPS:-20} --warmup ${WARMUP:-5}"
 set -o pipefail
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
-    -- python3 bench.py --steps 20 --warmup 5 $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
+    -- python3 bench.py $WIN $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
     || { echo "kernel-trace pass failed ($?)"; exit 1; }
 echo "kernel-trace pass ok"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 $ARGS > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err" \
+    -- python3 bench.py $WIN $ARGS > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err" \
     || { echo "FETCH_SIZE pass failed ($?)"; exit 1; }
 echo "FETCH_SIZE pass ok"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 $ARGS > "$OUT/write_bench.json" 2> "$OUT/write_bench.err" \
+    -- python3 bench.py $WIN $ARGS > "$OUT/write_bench.json" 2> "$OUT/write_bench.err" \
     || { echo "WRITE_SIZE pass failed ($?)"; exit 1; }
 echo "WRITE_SIZE pass ok"

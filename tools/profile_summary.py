@@ -87,6 +87,10 @@ def main():
     shaf = os.path.join(src, "source_sha.txt")
     out = {"round": rnd, "source_sha": open(shaf).read().strip() if os.path.exists(shaf) else None,
            "workload": {"n": n, "p": p, "n_pad": n_pad, "p_pad": p_pad},
+           # the profiled bench window (every pass ran it): bench.py matches the per-sweep
+           # kernels' traffic on it; "fitted": the run included the fitted-regime sweeps
+           "window": {"steps": bench.get("steps"), "warmup": bench.get("warmup"),
+                      "fitted": bench.get("fitted_regime") is not None},
            "units": "bytes per dispatch (average over the profiled dispatches)",
            "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 1/2 reporting of wide "
                          "streaming reads); write_bytes = WRITE_SIZE x 1024",
