@@ -15,15 +15,16 @@ pass() {  # $1 = config name, $2 = counter, rest = bench args
     local cfg=$1 ctr=$2; shift 2
     timeout -s KILL 240 rocprofv3 --pmc "$ctr" --kernel-include-regex "$REGEX" \
         -d "$OUT/$cfg/$ctr" -o run --output-format csv \
-        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fitted "$@" \
+        -- python3 bench.py --no-cpu-baseline --no-fitted "$@" \
         > "$OUT/$cfg/$ctr.json" 2> "$OUT/$cfg/$ctr.err" || { echo "$cfg $ctr failed ($?)"; exit 1; }
     echo "$cfg $ctr ok"
 }
-for cfg in c3 c5; do
+for cfg in ${CONFIGS:-c3 c5}; do
     mkdir -p "$OUT/$cfg"
     case $cfg in
-        c3) args="" ;;
-        c5) args="--workload c5" ;;
+        # the windows of the committed bench lines: C3 the driver's 20 after 5, C5 200 after 20
+        c3) args="--steps 20 --warmup 5" ;;
+        c5) args="--workload c5 --steps 200 --warmup 20" ;;
     esac
     # the totals, then the per-class counts that price the instructions in SIMD issue cycles
     # (classes and costs: tools/valu_rate.hip, tools/pmc_valu_classes.sh)
