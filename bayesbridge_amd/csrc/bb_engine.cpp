@@ -289,6 +289,11 @@ int g_shard_proto = 0;
 // dense engines: products over an fp32 copy of X with one fp64 residual pass (1, the default)
 // or fp64 products only (0)
 int g_nid_mixed = 1;
+// bb_set_tuning key 11: the host learns a synchronous decision by polling its tag word in
+// coherent host memory (1, the default) or by an event recorded behind the decision kernel
+// (0).  The event's marker left the device idle ~4 us per sweep: C3 at the driver's settings
+// 2010 against 1995 sweeps/s, 1000 sweeps after 100 1370 against 1367 (gpurun_out/ab_*).
+int g_nid_poll = 1;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -554,21 +559,60 @@ struct bb_engine {
             launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
         else
             launch_nid_sums_decide(stream, D, cn, p_loc, sc, nid, std::min(g_nid_kmax, nid_kmax),
-                                   nid_wg, nid_red, eps_dev + kNidRing, mixed_ok() ? 1 : 0);
+                                   nid_wg, nid_red, eps_dev + kNidRing, mixed_ok() ? 1 : 0,
+                                   ++nid_dseq);
     }
     // the decision from the reduced sums (identical on every rank), then wait for it
     void nidx_decide_launch() {
         if (sharded())
             launch_nid_decide_from(stream, nid_red, sc, std::min(g_nid_kmax, nid_kmax), nid,
-                                   eps_dev + kNidRing);
+                                   eps_dev + kNidRing, ++nid_dseq);
+        if (g_nid_poll) return;
         if (!nid_sev) HIPCHECK(hipEventCreateWithFlags(&nid_sev, hipEventDisableTiming));
         HIPCHECK(hipEventRecord(nid_sev, stream));
     }
     int nidx_decide_read() {
-        wait_event(nid_sev);
-        nid_k2 = mixed_ok() ? (int)((volatile double *)eps_host)[kNidRing + 2] : 0;
-        return (int)((volatile double *)eps_host)[kNidRing + 1];
+        int mode, k2;
+        if (g_nid_poll) {
+            const unsigned long long tag = wait_tag(nid_dseq);
+            mode = (int)((tag >> 8) & 0xff);
+            k2 = (int)(tag & 0xff);
+        } else {
+            wait_event(nid_sev);
+            mode = (int)((volatile double *)eps_host)[kNidRing + 1];
+            k2 = (int)((volatile double *)eps_host)[kNidRing + 2];
+        }
+        nid_k2 = mixed_ok() ? k2 : 0;
+        return mode;
     }
+    // Poll the decision's tag word (host2[3]: seq << 16 | mode << 8 | k2, one 64-bit store by
+    // the decision kernel into coherent host memory) until it carries decision seq.  Every
+    // 1024 polls the stream is queried: a device error surfaces as the HIP error, and a drained
+    // stream without the tag is an error (never a silent wrong path); a shard-group member
+    // gives up when another member failed (wait_event).
+    unsigned long long wait_tag(unsigned long long seq) {
+        const unsigned long long *tp = (const unsigned long long *)(eps_host + kNidRing + 3);
+        const unsigned long long want = seq & 0xffffffffffffull;
+        for (long spin = 0;; ++spin) {
+            const unsigned long long v = __atomic_load_n(tp, __ATOMIC_ACQUIRE);
+            if ((v >> 16) == want) return v;
+            if ((spin & 1023) != 1023) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            if (stop && stop->load(std::memory_order_relaxed))
+                throw HipError("stopped: another member of the shard group failed");
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {
+                const unsigned long long w = __atomic_load_n(tp, __ATOMIC_ACQUIRE);
+                if ((w >> 16) == want) return w;
+                throw HipError("near-identity decision tag not written by the drained stream");
+            }
+            if (q != hipErrorNotReady) HIPCHECK(q);
+            if (spin > 65536) std::this_thread::yield();
+        }
+    }
+    unsigned long long nid_dseq = 0;  // decisions launched with a tag
     // Block the host until ev completes.  A member of an RCCL group (stop != nullptr) polls
     // instead, so that it gives up when another member failed: that member's all-reduces are
     // never posted, so an event behind them never completes (the group then aborts the
@@ -1334,10 +1378,13 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->nid_red = dalloc<double>(bb_engine::kNidRed, o);
             e->nid_wg = dalloc<double>((size_t)nid_sum_groups(c.p_local) * (kNidTS + 1), o);
             e->nid_sum = dalloc<double>(n_pad, o);
-            // the hint ring, then a shard's [eps, mode] of the sweep being decided
-            const int nh = bb_engine::kNidRing + 3;
-            HIPCHECK(hipHostMalloc((void **)&e->eps_host, nh * sizeof(double), hipHostMallocMapped));
+            // the hint ring, then [eps, mode, k2, tag] of the sweep being decided (coherent:
+            // the host polls the tag while the device runs on)
+            const int nh = bb_engine::kNidRing + 4;
+            HIPCHECK(hipHostMalloc((void **)&e->eps_host, nh * sizeof(double),
+                                   hipHostMallocMapped | hipHostMallocCoherent));
             for (int q = 0; q < nh; ++q) e->eps_host[q] = -1.0;  // no observation yet
+            *(unsigned long long *)(e->eps_host + bb_engine::kNidRing + 3) = 0ull;
             HIPCHECK(hipHostGetDevicePointer((void **)&e->eps_dev, e->eps_host, 0));
             e->nid_kmax = e->nid_kmax_model();
             // the mixed-precision plan's fp32 copy of X (unsharded dense engines; 4 B per
@@ -3622,6 +3669,16 @@ int bb_set_tuning(int key, int value) {
         case 9: {
             const int old = g_shard_proto;
             if (value >= 0) g_shard_proto = value ? 1 : 0;
+            return old;
+        }
+        case 11: {
+            const int old = g_nid_poll;
+            if (value >= 0) g_nid_poll = value ? 1 : 0;
+            return old;
+        }
+        case 12: {
+            const int old = g_rs_xcd;
+            if (value >= 0) g_rs_xcd = value ? 1 : 0;
             return old;
         }
         default: return -1;

@@ -103,7 +103,8 @@ bool eapply_supported(int n_pad);        // dense E-apply register tiling covers
 // the decision's bound sums (bb_nid.hip): G = nid_sum_groups(p_loc) workgroup partials
 // (wg_part, G x (kNidTS + 1)) reduced in order into red (kNidTS + 2: [S_k | trace | Lambda]);
 // decide != 0: the unsharded decision at once (eps into the host-mapped eps_host); a shard
-// exchanges red, then launch_nid_decide_from (host2 = host-mapped [eps, mode])
+// exchanges red, then launch_nid_decide_from (host2 = host-mapped [eps, mode, k2, tag]; tag_seq
+// != 0: the tag word (seq << 16 | mode << 8 | k2) the host polls for the decision)
 constexpr int kNidTS = 32;
 int nid_sum_groups(int p_loc);
 void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc,
@@ -114,9 +115,11 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
 // (host2[2] = its k2, 0 for the fp64 plan)
 void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                             const DevScalars *sc, NidState *nid, int k_launched,
-                            double *wg_part, double *red, double *host2, int allow_mixed = 0);
+                            double *wg_part, double *red, double *host2, int allow_mixed = 0,
+                            unsigned long long tag_seq = 0);
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
-                            int k_launched, NidState *nid, double *host2);
+                            int k_launched, NidState *nid, double *host2,
+                            unsigned long long tag_seq = 0);
 void launch_nid_xu(hipStream_t s, const double *X, int ldx, const double *u, int ncols,
                    int n_pad, const NidState *nid, double *part);
 // b (optional): the right-hand side, kept for the mixed plan's residual pass
@@ -259,6 +262,7 @@ size_t chol_flag_words(int m_pad, int nrhs_blocks);
 // doubles of the Wd buffer chol_factor needs (W_k blocks + scratch tiles)
 size_t chol_wd_words(int m_pad);
 extern int g_bxb_nt;  // non-temporal X loads in k_beta_wb_xb (bb_set_tuning key 2)
+extern int g_rs_xcd;  // XCD-aware row blocks of the partial row sums (key 12)
 extern int g_lam_occ;  // lambda launches at 4 waves per SIMD (bb_set_tuning key 4)
 extern int g_lam_lanes;  // lanes per coefficient of k_lambda_spec, 0 = default (key 5)
 // k_chol_persistent chain variant: 1 (default) or the pipelined 2 / 3, for A/B

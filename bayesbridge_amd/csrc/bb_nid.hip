@@ -91,7 +91,7 @@ __device__ __forceinline__ double shard_threshold(double tau2, int k) {
 // ---------------------------------------------------------------------------------------
 // The search runs on the 64 lanes of one wave: lane k - 1 holds t_k (T_k = cosh(k acosh
 // sigma1), overflow giving t_k = 0; a 1e-12 relative margin covers the closed form's rounding),
-// lane k1 - 1 finds its least k2 in one uniform scan (t_k2 by shuffle), then the cheapest
+// lane k1 - 1 finds its least k2 by a binary search (t_k2 by shuffle), then the cheapest
 // (cost, k1) by a wave minimum: ~1 us, against ~40 us for the same search on one thread.
 __device__ void nid_plan_mixed(double eps, double tr, int kcap, double cost_fp64,
                                const NidState *nid, int &K1, int &K2, double &eta, double &e2) {
@@ -110,11 +110,21 @@ __device__ void nid_plan_mixed(double eps, double tr, int kcap, double cost_fp64
     const int k1 = lane + 1;
     const double err1 = eta + tk * (1.0 + eta);
     const double need = kNidTol / err1;
-    int k2 = 0;
-    for (int k = 1; k <= kmax; ++k) {
-        const double t2 = __shfl(tk, k - 1, 64);
-        if (!k2 && eta + t2 * (1.0 + eta) <= need) k2 = k;
+    // least k2 in [1, kmax] with eta + t_k2 (1 + eta) <= need: t_k decreases in k, so the
+    // predicate holds on [k2, kmax] -- a binary search, every lane shuffling each round
+    int lo = 1, hi = kmax + 1;
+#pragma unroll
+    for (int it = 0; it < 7; ++it) {
+        const int mid = (lo + hi) >> 1;
+        const double t2 = __shfl(tk, (mid < kmax ? mid : kmax) - 1, 64);
+        if (lo < hi) {
+            if (eta + t2 * (1.0 + eta) <= need)
+                hi = mid;
+            else
+                lo = mid + 1;
+        }
     }
+    const int k2 = lo <= kmax ? lo : 0;
     double cost = (k1 <= kmax && err1 < 1.0 && k2)
                       ? (k1 - 1) * step32 + step64 + (k2 - 1) * step32
                       : HUGE_VAL;
@@ -142,7 +152,8 @@ __device__ void nid_plan_mixed(double eps, double tr, int kcap, double cost_fp64
 // lanes of one wave (every lane computes the same values; lane 0 writes them)
 __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launched, int allow,
                            NidState *nid, double *eps_host, double *mode_host,
-                           int allow_mixed = 0, double *k2_host = nullptr) {
+                           int allow_mixed = 0, double *k2_host = nullptr,
+                           unsigned long long tag_seq = 0) {
     const double tau2 = sc->tau * sc->tau;
     const double lam = red[kNidTS + 1];
     double best = red[kNidTS];
@@ -154,7 +165,8 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
     const int K = cheb_iterations(eps, k_launched, kNidTol);
     int mode = (allow && K > 0) ? K : 0, k2 = 0;
     double ecb = eps, eta = 0.0;
-    if (allow && allow_mixed) {
+    // a mixed plan costs at least one fp64 pass (k1 = k2 = 1): never below K <= 2's
+    if (allow && allow_mixed && (K == 0 || K > 2)) {
         const double tr = red[kNidTS] / sc->sig2 * (1.0 + 1e-6);
         int k1m, k2m;
         double e2;
@@ -191,6 +203,13 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
     if (eps_host) *eps_host = eps;  // host-mapped: the launch hint / the shard's decision
     if (mode_host) *mode_host = (double)mode;
     if (k2_host) *k2_host = (double)k2;
+    // the host's wake-up word (host2[3], coherent host memory): the decision's sequence number,
+    // mode and k2 in one 64-bit store, so the host polls it instead of waiting on an event
+    // (an event marker in the stream cost ~6 us of idle device per sweep)
+    if (tag_seq && mode_host)
+        __hip_atomic_store((unsigned long long *)(mode_host + 2),
+                           (tag_seq << 16) | ((unsigned long long)mode << 8) | (unsigned)k2,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kNidSumWG) void k_nid_sums(const double *__restrict__ D,
@@ -233,7 +252,8 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
                                                        const DevScalars *sc, int k_launched,
                                                        int allow, int decide, NidState *nid,
                                                        double *__restrict__ red,
-                                                       double *eps_host, int allow_mixed) {
+                                                       double *eps_host, int allow_mixed,
+                                                       unsigned long long tag_seq) {
     __shared__ double pq[kNidRedQ][kNidTS + 1];
     __shared__ double r[kNidTS + 2];
     const int t = threadIdx.x;
@@ -265,13 +285,15 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
     // decide 1: eps into eps_host (the launch hint); 2: [eps, mode, k2] into eps_host[0..2]
     if (decide && t < 64)
         nid_finish(r, sc, k_launched, allow, nid, eps_host, decide == 2 ? eps_host + 1 : nullptr,
-                   decide == 2 ? allow_mixed : 0, decide == 2 ? eps_host + 2 : nullptr);
+                   decide == 2 ? allow_mixed : 0, decide == 2 ? eps_host + 2 : nullptr,
+                   decide == 2 ? tag_seq : 0ull);
 }
 
 __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
                                                         const DevScalars *sc, int k_launched,
-                                                        NidState *nid, double *host2) {
-    nid_finish(red, sc, k_launched, 1, nid, host2, host2 + 1, 0, host2 + 2);
+                                                        NidState *nid, double *host2,
+                                                        unsigned long long tag_seq) {
+    nid_finish(red, sc, k_launched, 1, nid, host2, host2 + 1, 0, host2 + 2, tag_seq);
 }
 
 // Row sums of the nparts partial n-vectors for rows [64 b, 64 b + 64): wave w adds partials
@@ -345,9 +367,22 @@ __device__ __forceinline__ double part_rowsum_rw(const double *__restrict__ part
     return v;
 }
 
+// The row block of workgroup b: consecutive blocks on one XCD (dispatch deals workgroups to
+// the 8 XCDs round-robin), so the two 64-byte halves of a partial's 128-byte line, read by
+// blocks 2c and 2c + 1 at RW = 8, meet in the same L2.
+__device__ __forceinline__ int rs_block(int xcd) {
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    if (!xcd || (G & 7)) return b;
+    return (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // rows per workgroup for nparts partials: 8 when there are many (more workgroups, fewer
 // dependent loads per thread), else 64.  (4 rows -- 32-byte row segments -- for the 1568
 // partials at C3 took 19.1 us against 11.0: gpurun_out/prof_ac.)
+// bb_set_tuning key 12: the XCD-aware row blocks of the partial row sums (rs_block; 1, the
+// default) or blocks in dispatch order (0).  C3 at the driver's settings 2010 against 1993
+// sweeps/s (gpurun_out/ab_drv_p1_x*).
+int g_rs_xcd = 1;
 static int rowsum_rw(int nparts) { return nparts >= 128 ? 8 : 64; }
 
 // r_0 = y / sig - (X u / sig + delta), x_1 = d_0 = r_0 / theta (x_0 = 0).  X u arrives as
@@ -357,10 +392,10 @@ template <int RW>
 __global__ __launch_bounds__(kRsThreads) void k_cheb_init(
     const double *__restrict__ xu_part, int nparts, int n, int n_pad,
     const double *__restrict__ y, const DevScalars *sc, Key key, uint64_t t, const NidState *nid,
-    double *x, double *r, double *d, double *b) {
+    double *x, double *r, double *d, double *b, int xcd) {
     if (nid->mode == 0) return;
-    const int i = blockIdx.x * RW + (int)threadIdx.x;
-    const double xu = part_rowsum_rw<RW>(xu_part, nparts, n_pad, blockIdx.x * RW);
+    const int i = rs_block(xcd) * RW + (int)threadIdx.x;
+    const double xu = part_rowsum_rw<RW>(xu_part, nparts, n_pad, rs_block(xcd) * RW);
     if ((int)threadIdx.x >= RW || i >= n_pad) return;
     double rhs = 0.0;
     if (i < n) {
@@ -380,10 +415,10 @@ __global__ __launch_bounds__(kRsThreads) void k_cheb_init(
 template <int RW>
 __global__ __launch_bounds__(kRsThreads) void k_cheb_step(
     const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
-    const NidState *nid, int j, double *x, double *r, double *d, int phase) {
+    const NidState *nid, int j, double *x, double *r, double *d, int phase, int xcd) {
     if ((phase == 1 ? nid->mode : nid->k2) <= j) return;
-    const int i = blockIdx.x * RW + (int)threadIdx.x;
-    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, blockIdx.x * RW);
+    const int i = rs_block(xcd) * RW + (int)threadIdx.x;
+    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, rs_block(xcd) * RW);
     if ((int)threadIdx.x >= RW || i >= n_pad) return;
     const double dv = d[i];
     const double qv = dv + e / sc->sig2;
@@ -401,10 +436,10 @@ __global__ __launch_bounds__(kRsThreads) void k_cheb_step(
 template <int RW>
 __global__ __launch_bounds__(kRsThreads) void k_cheb_restart(
     const double *__restrict__ part, int nparts, int n_pad, const DevScalars *sc,
-    const NidState *nid, const double *__restrict__ b, double *x, double *r, double *d) {
+    const NidState *nid, const double *__restrict__ b, double *x, double *r, double *d, int xcd) {
     if (nid->k2 == 0 || nid->mode == 0) return;
-    const int i = blockIdx.x * RW + (int)threadIdx.x;
-    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, blockIdx.x * RW);
+    const int i = rs_block(xcd) * RW + (int)threadIdx.x;
+    const double e = part_rowsum_rw<RW>(part, nparts, n_pad, rs_block(xcd) * RW);
     if ((int)threadIdx.x >= RW || i >= n_pad) return;
     const double xv = x[i];
     const double rv = b[i] - (xv + e / sc->sig2);
@@ -652,21 +687,23 @@ void launch_nid_sums(hipStream_t s, const double *D, const double *cn, int p_loc
     const int G = nid_sum_groups(p_loc);
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
     k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, allow, decide, nid, red,
-                                  eps_host, 0);
+                                  eps_host, 0, 0ull);
 }
 
 void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, int p_loc,
                             const DevScalars *sc, NidState *nid, int k_launched,
-                            double *wg_part, double *red, double *host2, int allow_mixed) {
+                            double *wg_part, double *red, double *host2, int allow_mixed,
+                            unsigned long long tag_seq) {
     const int G = nid_sum_groups(p_loc);
     k_nid_sums<<<G, kNidSumWG, 0, s>>>(D, cn, p_loc, sc, wg_part);
     k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, 1, 2, nid, red, host2,
-                                      allow_mixed);
+                                      allow_mixed, tag_seq);
 }
 
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
-                            int k_launched, NidState *nid, double *host2) {
-    k_nid_decide_from<<<1, 64, 0, s>>>(red, sc, k_launched, nid, host2);
+                            int k_launched, NidState *nid, double *host2,
+                            unsigned long long tag_seq) {
+    k_nid_decide_from<<<1, 64, 0, s>>>(red, sc, k_launched, nid, host2, tag_seq);
 }
 
 template <int KIND>
@@ -692,11 +729,12 @@ void launch_cheb_init(hipStream_t s, const double *xu_part, int nparts, int n, i
                       double *b) {
     if (rowsum_rw(nparts) == 8)
         k_cheb_init<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y, sc,
-                                                              Key{k0, k1}, t, nid, x, r, d, b);
+                                                              Key{k0, k1}, t, nid, x, r, d, b,
+                                                              g_rs_xcd);
     else
         k_cheb_init<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(xu_part, nparts, n, n_pad, y,
                                                                  sc, Key{k0, k1}, t, nid, x, r, d,
-                                                                 b);
+                                                                 b, g_rs_xcd);
 }
 
 void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
@@ -704,10 +742,10 @@ void launch_cheb_step(hipStream_t s, const double *part, int nparts, int n_pad,
                       double *d, int phase) {
     if (rowsum_rw(nparts) == 8)
         k_cheb_step<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j, x,
-                                                              r, d, phase);
+                                                              r, d, phase, g_rs_xcd);
     else
         k_cheb_step<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, j,
-                                                                 x, r, d, phase);
+                                                                 x, r, d, phase, g_rs_xcd);
 }
 
 void launch_cheb_restart(hipStream_t s, const double *part, int nparts, int n_pad,
@@ -715,10 +753,10 @@ void launch_cheb_restart(hipStream_t s, const double *part, int nparts, int n_pa
                          double *r, double *d) {
     if (rowsum_rw(nparts) == 8)
         k_cheb_restart<8><<<(n_pad + 7) / 8, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid, b,
-                                                                 x, r, d);
+                                                                 x, r, d, g_rs_xcd);
     else
         k_cheb_restart<64><<<(n_pad + 63) / 64, kRsThreads, 0, s>>>(part, nparts, n_pad, sc, nid,
-                                                                    b, x, r, d);
+                                                                    b, x, r, d, g_rs_xcd);
 }
 
 void launch_eapply(hipStream_t s, const double *X, int ldx, int n_pad, int p_loc,

@@ -355,7 +355,13 @@ void bb_set_trace_budget(long long bytes);
  * every product E d exchanged), so each of its exchanges executes on one GPU (default 0).
  * key 10: the mixed-precision near-identity plan of unsharded dense Woodbury engines
  * (products over an fp32 copy of X, one fp64 residual pass, the same certified bound; 1, the
- * default) or fp64 products only (0).
+ * default) or fp64 products only (0);
+ * key 11: the host learns a synchronous near-identity decision by polling the tag word the
+ * decision kernel stores into coherent host memory (1, the default) or by waiting on an event
+ * recorded behind it (0);
+ * key 12: the partial row sums of the Chebyshev kernels read row blocks placed so that
+ * neighbouring blocks share an XCD (1, the default) or in dispatch order (0); under keys 11
+ * and 12 the draws are the same.
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

@@ -284,6 +284,35 @@ def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
     assert abs(a["tau"] - b["tau"]) <= 1e-9 * b["tau"]
 
 
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_decision_poll_and_row_blocks_same_bits(gpu_lib, kind):
+    """bb_set_tuning key 11 (the host polls the decision's tag word instead of waiting on an
+    event) and key 12 (XCD-aware row blocks of the partial row sums) change neither the path
+    nor a bit of the chain: 12 sweeps from the reference start, defaults against both off."""
+    bb = gpu_lib
+    n, p = 300, 4000
+    X, y, _ = _design(kind, n, p, 52)
+    out = []
+    for v in (1, 0):
+        o11, o12 = bb.set_tuning(11, v), bb.set_tuning(12, v)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            e.run(1, 12)
+            e.sync()
+            out.append((e.state(), e.nid_stats()))
+            assert e.error_flags() == 0
+            e.close()
+        finally:
+            bb.set_tuning(11, o11)
+            bb.set_tuning(12, o12)
+    (a, sa), (b, sb) = out
+    assert sa["cheb_sweeps"] == sb["cheb_sweeps"] >= 10 and sa["products"] == sb["products"]
+    for k in ("beta", "lambda"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["tau"] == b["tau"] and a["sig2"] == b["sig2"]
+
+
 @pytest.mark.parametrize("stride", [1, 3])
 def test_timed_phase_stride(gpu_lib, stride):
     """bench.py's live roofline timing: the timed phase is bracketed by an event pair in every
