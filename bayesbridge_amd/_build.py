@@ -28,14 +28,18 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
-def source_sha() -> str:
-    """sha256 (first 16 hex digits) of every source and header the library is built from: the
-    committed profiles record it, and bench.py uses a profile only if it matches the tree."""
+def source_sha(root: str | None = None) -> str:
+    """sha256 (first 16 hex digits) of every source and header the library is built from (of
+    this tree, or of the tree at root): the committed profiles record it; bench.py uses a
+    profile for a kernel whose code it recorded (bayesbridge_amd/_kernel_code.py) if that code
+    is unchanged, otherwise only if the tree matches."""
     import hashlib
 
+    root = root or ROOT
+    csrc = os.path.join(root, "bayesbridge_amd", "csrc")
     h = hashlib.sha256()
-    files = [os.path.join(CSRC, f) for f in sorted(SOURCES + HEADERS)]
-    files.append(os.path.join(ROOT, "include", "bayesbridge.h"))
+    files = [os.path.join(csrc, f) for f in sorted(SOURCES + HEADERS)]
+    files.append(os.path.join(root, "include", "bayesbridge.h"))
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:

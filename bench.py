@@ -221,7 +221,20 @@ def _profiles(pattern):
             continue
 
 
-def _stale_note(d, f):
+def _stale_note(d, f, entry=None, instance=None):
+    """None if the profile's entry for `instance` describes this build's kernel: the entry's
+    recorded code identity (gfx950 code bytes + kernel descriptor, bayesbridge_amd/_kernel_code.py)
+    equals this library's, or -- for an entry without one -- the profiled tree is this tree.
+    Otherwise the reason it is not used."""
+    cs = entry.get("code_sha") if isinstance(entry, dict) else None
+    if cs is not None and instance:
+        from bayesbridge_amd import _kernel_code
+
+        cur = _kernel_code.code_sha(instance)
+        if cur == cs:
+            return None
+        return (f"{f}: {instance} profiled as code {cs}, this build's is {cur}: not used "
+                "(re-profile: tools/profile_round.sh / pmc_valu.sh / pmc_mfma.sh)")
     sha = d.get("source_sha")
     if sha == tree_sha():
         return None
@@ -249,7 +262,7 @@ def pmc_traffic(n, p, world, instance, window=None):
         if not v or v.get("hbm_bytes") != v.get("hbm_bytes"):  # absent, or NaN (one pass lacks it)
             note = f"{f} has no entry for {instance}"
             continue
-        stale = _stale_note(d, f)
+        stale = _stale_note(d, f, v, instance)
         if stale:
             best, note = None, stale
             continue
@@ -265,13 +278,11 @@ def pmc_mfma(n, p, world, instance, gram):
     (the GRBM_GUI_ACTIVE-derived clock read above 2.4 GHz on short dispatches)."""
     best = None
     for d, f in _profiles("r*_pmc_mfma.json"):
-        if _stale_note(d, f):
-            continue
         for cfg in d.get("configs", {}).values():
             if cfg.get("n") != n or cfg.get("p") != p or world != 1 or cfg.get("gram") != gram:
                 continue
             v = cfg.get("kernels", {}).get(instance)
-            if v and "mfma_busy_frac_nominal_clock" in v:
+            if v and "mfma_busy_frac_nominal_clock" in v and not _stale_note(d, f, v, instance):
                 best = {"mfma_busy_frac": v["mfma_busy_frac_nominal_clock"], "source": f,
                         "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x the "
                                       "dispatch duration)"}
@@ -298,7 +309,7 @@ def pmc_valu(n, p, world, instance, window=None):
             if not v or "SQ_INSTS_VALU" not in v:
                 note = f"{f} has no entry for {instance}"
                 continue
-            stale = _stale_note(d, f)
+            stale = _stale_note(d, f, v, instance)
             if stale:
                 best, note = None, stale
                 continue

@@ -13,6 +13,8 @@ OUT=gpurun_out/pmc_mfma_$ROUND
 mkdir -p "$OUT"
 # the sources this profile measures (bench.py uses a profile only for the same tree)
 python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
+# and the code identity of every kernel in the library it runs (bayesbridge_amd/_kernel_code.py)
+python3 -m bayesbridge_amd._kernel_code > "$OUT/kernel_code.json" || exit 1
 REGEX="k_oz_gemm16u|k_oz_residues|k_chol_persistent|k_gram"
 pass() {  # $1 = config name, $2 = counter, rest = bench args
     local cfg=$1 ctr=$2; shift 2

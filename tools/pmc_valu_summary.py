@@ -147,6 +147,18 @@ def main_counts(rnd, asm_path):
                 e["valu_busy_frac"] = 4.0 * e["SQ_ACTIVE_INST_VALU"] / (SIMDS * e["GRBM_GUI_ACTIVE"] / 8)
             ent["kernels"][k] = e
         out["configs"][cfg] = ent
+    # the code identity of every profiled kernel (kernel_code.json, written on the GPU box
+    # from the library it ran): bench.py uses an entry while the kernel's code is unchanged
+    kcf = os.path.join(src, "kernel_code.json")
+    if os.path.exists(kcf):
+        sys.path.insert(0, ROOT)
+        from bayesbridge_amd import _kernel_code
+        shas = json.load(open(kcf))
+        maps = [out["kernels"]] if isinstance(out.get("kernels"), dict) else []
+        maps += [c["kernels"] for c in out.get("configs", {}).values() if "kernels" in c]
+        for m in maps:
+            _kernel_code.annotate(m, shas)
+        out["code_sha_from"] = "kernel_code.json written on the GPU box from the profiled library"
     dst = os.path.join(ROOT, "profiles", f"{rnd}_pmc_valu.json")
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))

@@ -15,18 +15,28 @@ OUT=gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
 # the sources this profile measures (bench.py uses a profile only for the same tree)
 python3 -c "from bayesbridge_amd._build import source_sha; print(source_sha())" > "$OUT/source_sha.txt"
+# and the code identity of every kernel in the library it runs (bayesbridge_amd/_kernel_code.py)
+python3 -m bayesbridge_amd._kernel_code > "$OUT/kernel_code.json" || exit 1
 ARGS="--no-cpu-baseline $*"
 WIN="--steps ${STEPS:-20} --warmup ${WARMUP:-5}"
 set -o pipefail
+# PASS=kt|fetch|write runs that one pass (one GPU step per call); unset: all three in turn
+PASS=${PASS:-all}
+if [ "$PASS" = all ] || [ "$PASS" = kt ]; then
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
     -- python3 bench.py $WIN $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" \
     || { echo "kernel-trace pass failed ($?)"; exit 1; }
 echo "kernel-trace pass ok"
+fi
+if [ "$PASS" = all ] || [ "$PASS" = fetch ]; then
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv \
     -- python3 bench.py $WIN $ARGS > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err" \
     || { echo "FETCH_SIZE pass failed ($?)"; exit 1; }
 echo "FETCH_SIZE pass ok"
+fi
+if [ "$PASS" = all ] || [ "$PASS" = write ]; then
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv \
     -- python3 bench.py $WIN $ARGS > "$OUT/write_bench.json" 2> "$OUT/write_bench.err" \
     || { echo "WRITE_SIZE pass failed ($?)"; exit 1; }
 echo "WRITE_SIZE pass ok"
+fi

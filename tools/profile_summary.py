@@ -134,6 +134,18 @@ def main():
             g = out["kernels"][k]
             out["gram_kernels"][k] = {"hbm_bytes_per_launch": g["hbm_bytes"],
                                       "algorithmic_bytes_per_launch": a, "avg_us": g["avg_us"]}
+    # the code identity of every profiled kernel (kernel_code.json, written on the GPU box
+    # from the library it ran): bench.py uses an entry while the kernel's code is unchanged
+    kcf = os.path.join(src, "kernel_code.json")
+    if os.path.exists(kcf):
+        sys.path.insert(0, ROOT)
+        from bayesbridge_amd import _kernel_code
+        shas = json.load(open(kcf))
+        maps = [out["kernels"]] if isinstance(out.get("kernels"), dict) else []
+        maps += [c["kernels"] for c in out.get("configs", {}).values() if "kernels" in c]
+        for m in maps:
+            _kernel_code.annotate(m, shas)
+        out["code_sha_from"] = "kernel_code.json written on the GPU box from the profiled library"
     json.dump(out, open(os.path.join(dst, f"{rnd}_pmc.json"), "w"), indent=1)
     print("\n".join(lines[:16]))
     print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
