@@ -3681,6 +3681,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_rs_xcd = value ? 1 : 0;
             return old;
         }
+        case 13: {
+            const int old = g_lam_wave;
+            if (value >= 0) g_lam_wave = value ? 1 : 0;
+            return old;
+        }
         default: return -1;
     }
 }

@@ -187,6 +187,7 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
                      int ldx, int n_pad, double *xu_part);
 extern int g_lam_xu;
+extern int g_lam_wave;  // wave-adaptive draw in the fused lambda + X u launch (key 13)
 
 void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
                            uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,

@@ -448,7 +448,10 @@ static void launch_spec(hipStream_t s, int L, int pgb, const double *beta, int p
 // continuous batching -- measured slower, C3 1895 against 1937-1948, C2 5532-5557 against
 // 6322-6372, gpurun_out/r04k_*, and was removed.)
 int g_lam_xu = 2;
-template <int L, int NR>
+// bb_set_tuning key 13: the fused launch at 8 lanes per coefficient draws with the
+// wave-adaptive sampler (stable_wave_draw; 1) or with fixed 8-lane groups (0); the same draws
+int g_lam_wave = 1;
+template <int L, int NR, bool WAVE = false>
 __device__ __forceinline__ void lambda_xu_body(const double *beta, int p_loc, int p_pad,
                                                    uint64_t j0, const DevScalars *sc, Key key,
                                                    uint64_t t, double *lam, double *D,
@@ -468,8 +471,15 @@ __device__ __forceinline__ void lambda_xu_body(const double *beta, int p_loc, in
         const int i = ch * C + tid / L;  // group-uniform
         const bool active = i < p_loc;
         const double b = active ? beta[i] : 0.0;
-        const double x = stable_spec_draw<L, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
-                                                key, t, j0 + (uint64_t)i, err);
+        double x;
+        if constexpr (WAVE) {
+            static_assert(L == 8, "the wave-adaptive draw deals 8-lane home groups");
+            x = stable_wave_draw(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0, key, t,
+                                 j0 + (uint64_t)i, err);
+        } else {
+            x = stable_spec_draw<L, 8>(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0, key, t,
+                                       j0 + (uint64_t)i, err);
+        }
         if ((tid % L) == 0) {
             double uv = 0.0;
             if (active) {
@@ -541,6 +551,13 @@ k_lambda_xu_o4(BB_LXU_ARGS) {
     lambda_xu_body<L, NR>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx,
                           n_pad, nchunk, xu_part);
 }
+// the wave-adaptive draw (stable_wave_draw, 8 lanes per coefficient): bb_set_tuning key 13
+template <int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void
+k_lambda_xw(BB_LXU_ARGS) {
+    lambda_xu_body<8, NR, true>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X,
+                                ldx, n_pad, nchunk, xu_part);
+}
 #undef BB_LXU_ARGS
 
 // (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
@@ -575,7 +592,12 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
         kk<<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, \
                              ldx, n_pad, nchunk, xu_part);                                    \
     } while (0)
-    if (L == 8) {
+    if (L == 8 && g_lam_wave && !o4) {
+        auto *kk = nr <= 4 ? k_lambda_xw<4> : nr <= 8 ? k_lambda_xw<8> : k_lambda_xw<16>;
+        note_launch(KF_LAMBDA, (const void *)kk);
+        kk<<<G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx,
+                             n_pad, nchunk, xu_part);
+    } else if (L == 8) {
         if (nr <= 4) BB_LXU(8, 4); else if (nr <= 8) BB_LXU(8, 8); else BB_LXU(8, 16);
     } else {
         if (nr <= 4) BB_LXU(16, 4); else if (nr <= 8) BB_LXU(16, 8); else BB_LXU(16, 16);

@@ -459,4 +459,135 @@ __device__ __forceinline__ double stable_spec_draw(bool active, double h, double
     return result;
 }
 
+// Wave-adaptive form of stable_spec_draw<8, 8> (the fused lambda + X u launch): a wave holds 8
+// coefficients on 8 "home" lanes each, and while more than 4 are unfinished each evaluates one
+// outer attempt of 8 inner attempts per round on its home lanes, as stable_spec_draw<8, 8>.
+// With a draw finishing in a round with probability ~0.66, a wave of 8 fixed groups runs the
+// maximum of 8 geometric round counts (~3 rounds against a mean of ~1.5) with the finished
+// groups' lanes idle.  Here, once m <= 4 coefficients are left, the wave's lanes are dealt to
+// them: G = 16, 32 or 64 lanes each (m = 3-4, 2, 1), i.e. O = G / 8 outer attempts of 8 inner
+// attempts per round, exactly the windows stable_spec_draw<G, 8> evaluates -- the same attempts
+// on the same counters, accepted by the same tests in the same order, so the same draws.  A
+// coefficient's per-draw constants and loop state move with it (shuffled from the group that
+// served it the round before); its result is shuffled back to its home lanes.  Returns the
+// draw of the home coefficient (every lane of its home group).  UA: alpha and V0 wave-uniform.
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    const unsigned lo = (unsigned)__shfl((int)(unsigned)v, src, 64);
+    const unsigned hi = (unsigned)__shfl((int)(unsigned)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+// lane of the group serving coefficient c in a round with unfinished set um and G lanes per
+// coefficient (G == 8: its home lanes)
+__device__ __forceinline__ int wave_group_base(int c, unsigned um, int G) {
+    return G == 8 ? 8 * c : __popc(um & ((1u << c) - 1u)) * G;
+}
+__device__ __forceinline__ int nth_set_bit(unsigned x, int k) {
+    for (int r = 0; r < k && x; ++r) x &= x - 1u;
+    return x ? __ffs(x) - 1 : -1;
+}
+__device__ __forceinline__ double stable_wave_draw(bool active, double h, double alpha, double V0,
+                                                   Key key, uint64_t t, uint64_t j,
+                                                   uint32_t *err) {
+    constexpr int I = 8;
+    const int lane = threadIdx.x & 63;
+    const int home = lane >> 3, ii = lane & 7;
+    if (active && alpha == 1.) active = false;  // retstable.cpp:104-110
+    if (active && (h < 0 || alpha < 0 || alpha > 1 || V0 < 0)) atomicOr(err, 4u);  // :112-115
+    // every lane forms constants (an inactive one from h = 1): the wave-uniform fields must be
+    // valid on every lane that may serve another coefficient
+    StableParams s = stable_params<true>(active ? h : 1.0, alpha, V0);
+    double result = V0;
+    uint64_t o0 = 0, ib = 0, jc = j;  // the served coefficient's loop state and index
+    unsigned um = 0;                  // unfinished coefficients (wave-uniform)
+    {
+        const unsigned long long a = __ballot(active && ii == 0);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) um |= (unsigned)((a >> (8 * c)) & 1ull) << c;
+    }
+    unsigned um_prev = um;
+    int G_prev = 8;
+    int c_cur = home;  // the coefficient this lane serves
+    int iter = 0;
+    for (; um && iter < BB_MAX_STABLE_ROUNDS; ++iter) {
+        const int m = __popc(um);
+        const int G = m > 4 ? 8 : m > 2 ? 16 : m > 1 ? 32 : 64;
+        if (G > 8) {
+            // deal the lanes: group `slot` serves the slot-th unfinished coefficient, whose
+            // constants and state come from the lanes that served it the round before
+            const int slot = lane / G;
+            const int cn = nth_set_bit(um, slot);
+            const int src = cn >= 0 ? wave_group_base(cn, um_prev, G_prev) : lane;
+            s.h = __shfl(s.h, src, 64);
+            s.lambda_alpha = __shfl(s.lambda_alpha, src, 64);
+            s.gamma = __shfl(s.gamma, src, 64);
+            s.sgamma = __shfl(s.sgamma, src, 64);
+            s.xi = __shfl(s.xi, src, 64);
+            s.psi = __shfl(s.psi, src, 64);
+            s.thr_w1 = __shfl(s.thr_w1, src, 64);
+            s.thr_w3 = __shfl(s.thr_w3, src, 64);
+            o0 = shfl_u64(o0, src);
+            ib = shfl_u64(ib, src);
+            jc = shfl_u64(jc, src);
+            c_cur = cn;
+        }
+        const bool serve = c_cur >= 0 && ((um >> c_cur) & 1u);
+        const int base = G == 8 ? (lane & ~7) : (lane / G) * G;
+        const int O = G / I, seg = (lane - base) >> 3;
+        const uint64_t o = o0 + (uint64_t)seg;
+        double U = 0.0, z = 0.0, Z = 0.0, B = 1.0;
+        bool acc = false;
+        if (serve)
+            acc = stable_inner<false>(s, key, t, jc, o, (seg == 0 ? ib : 0) + (uint64_t)ii, U, z, Z,
+                                      B);
+        const unsigned sb = (unsigned)((__ballot(acc) >> (base + 8 * seg)) & 0xffull);
+        const int wsrc = base + 8 * seg + (sb ? (__ffs(sb) - 1) : 0);
+        const double Uw = __shfl(U, wsrc, 64), zw = __shfl(z, wsrc, 64), Zw = __shfl(Z, wsrc, 64);
+        const double Bw = __shfl(B, wsrc, 64);
+        double X = 0.0;
+        bool oacc = false;
+        if (serve && sb) oacc = stable_outer<false>(s, key, t, jc, o, Uw, zw, Zw, Bw, X);
+        const unsigned long long hb = __ballot(ii == 0 && sb != 0) >> base;
+        const unsigned long long ab = __ballot(ii == 0 && oacc) >> base;
+        unsigned H = 0, A = 0;
+        for (int k = 0; k < O; ++k) {
+            H |= (unsigned)((hb >> (8 * k)) & 1ull) << k;
+            A |= (unsigned)((ab >> (8 * k)) & 1ull) << k;
+        }
+        const unsigned stop = (~H & ((1u << O) - 1u)) | A;
+        const int k = stop ? (__ffs(stop) - 1) : O;
+        const double Xk = __shfl(X, base + 8 * (k < O ? k : 0), 64);
+        bool fin = false;
+        double res = 0.0;
+        if (serve) {
+            if (k == O) {  // all O outer attempts rejected
+                o0 += (uint64_t)O;
+                ib = 0;
+            } else if ((A >> k) & 1u) {
+                res = stable_finish(s, Xk);
+                fin = true;
+            } else {  // outer attempt o0 + k needs more inner attempts
+                ib = (k == 0) ? ib + I : (uint64_t)I;
+                o0 += (uint64_t)k;
+            }
+        }
+        // the coefficients finished this round (wave-uniform), their results to the home lanes
+        const unsigned long long fb = __ballot(fin && lane == base);
+        unsigned fm = 0;
+        for (unsigned long long x = fb; x; x &= x - 1ull) {
+            const int b = __ffsll((unsigned long long)x) - 1;
+            fm |= 1u << (G == 8 ? b / 8 : nth_set_bit(um, b / G));
+        }
+        const double hr = __shfl(res, wave_group_base(home, um, G), 64);
+        if ((fm >> home) & 1u) result = hr;
+        um_prev = um;
+        G_prev = G;
+        um &= ~fm;
+    }
+    if (um) {
+        atomicOr(err, 2u);
+        if ((um >> home) & 1u) result = __builtin_nan("");
+    }
+    return result;
+}
+
 }  // namespace bb

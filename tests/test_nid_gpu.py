@@ -284,6 +284,46 @@ def test_nid_synchronous_decision_same_chain(gpu_lib, kind):
     assert abs(a["tau"] - b["tau"]) <= 1e-9 * b["tau"]
 
 
+@pytest.mark.parametrize("n,p,scale", [(200, 45000, 1e-6), (200, 45000, 1e-1),
+                                        (2000, 50000, 1e-6), (2000, 50000, 1e-2)])
+def test_lambda_wave_draw_same_bits(gpu_lib, n, p, scale):
+    """bb_set_tuning key 13: the fused lambda + X u launch at 8 lanes per coefficient with the
+    wave-adaptive sampler (stable_wave_draw: a wave's finished draws lend their lanes to the
+    unfinished ones, up to 8 outer attempts per round) against fixed 8-lane groups
+    (stable_spec_draw<8, 8>): the same attempts in the same order, so the same lambda bits and
+    the same chain, from a near-null state and from one with sizeable coefficients (where the
+    rejection loops run longer).  (2000, 50000) is C3's shape."""
+    import bench
+    bb = gpu_lib
+    if n == 2000:
+        X = bench.make_columns(n, 0, p)
+        y, _ = bench.make_problem_y(n, p)
+    else:
+        X, y, _ = synthetic_problem(n, p, seed=n)
+    rng = np.random.default_rng(17)
+    beta = scale * rng.standard_normal(p)
+    out = []
+    for wave in (1, 0):
+        old = bb.set_tuning(13, wave)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            e.set_state(beta, 1e-3, 1.0, 0.5)
+            e.run(5, 3)
+            e.sync()
+            out.append((e.state(), e.nid_stats()))
+            assert e.error_flags() == 0
+            e.close()
+        finally:
+            bb.set_tuning(13, old)
+    (a, sa), (b, sb) = out
+    assert sa == sb, (sa, sb)
+    for k in ("lambda", "beta"):
+        assert np.array_equal(a[k], b[k]), (k, np.max(np.abs(a[k] - b[k])))
+    assert a["tau"] == b["tau"] and a["sig2"] == b["sig2"]
+    assert np.all(np.isfinite(a["lambda"])) and np.all(a["lambda"] > 0)
+
+
 @pytest.mark.parametrize("kind", ["dense", "sparse"])
 def test_decision_poll_and_row_blocks_same_bits(gpu_lib, kind):
     """bb_set_tuning key 11 (the host polls the decision's tag word instead of waiting on an

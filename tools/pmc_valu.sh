@@ -30,10 +30,11 @@ for cfg in ${CONFIGS:-c3 c5}; do
     esac
     # the totals, then the per-class counts that price the instructions in SIMD issue cycles
     # (classes and costs: tools/valu_rate.hip, tools/pmc_valu_classes.sh)
-    for ctr in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 \
+    # (COUNTERS=<one counter> runs that pass alone: one GPU step per call)
+    for ctr in ${COUNTERS:-SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE SQ_INSTS_VALU_FMA_F64 \
         SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 \
         SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 \
-        SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT; do
+        SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT}; do
         pass $cfg $ctr $args
     done
 done
