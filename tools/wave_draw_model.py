@@ -105,20 +105,6 @@ def wave(seed, active, pin, pout, L0=8):
         um_prev, G_prev = um, G
         um &= ~fm
     return [res[c * L0] for c in range(NC)], rounds
-random.seed(1)
-tot = 0; rsum = 0
-for L0 in (8, 16):
-    for trial in range(3000):
-        seed = random.random(); pin = random.choice([0.05, 0.3, 0.6]); pout = random.choice([0.2, 0.7, 0.95])
-        NC = 64 // L0
-        active = [random.random() < 0.9 for _ in range(NC)]
-        got, rounds = wave(seed, active, pin, pout, L0)
-        for c in range(NC):
-            want = sequential(seed, c, pin, pout) if active[c] else None
-            assert got[c] == want, (L0, trial, c, got[c], want, pin, pout)
-        tot += 1; rsum += rounds
-print('ok', tot, 'avg rounds', rsum / tot)
-
 def fixed_rounds(seed, active, pin, pout, L0=8):
     # rounds of stable_spec_draw<L0, 8>: each coefficient's rounds with O = L0/8 outer attempts
     NC = 64 // L0; O = L0 // 8; mx = 0
@@ -140,11 +126,44 @@ def fixed_rounds(seed, active, pin, pout, L0=8):
             if done: break
         mx = max(mx, r)
     return mx
-import statistics
-for L0 in (8, 16):
-    fr, ar = [], []
-    for trial in range(2000):
-        seed = random.random()
-        active = [True] * (64 // L0)
-        fr.append(fixed_rounds(seed, active, 0.3, 0.7, L0)); ar.append(wave(seed, active, 0.3, 0.7, L0)[1])
-    print(L0, 'fixed', statistics.mean(fr), 'adaptive', statistics.mean(ar))
+
+
+def check(trials=3000, seed=1):
+    """Every coefficient's accepted (outer, inner) attempt under the schedule equals the
+    sequential loop's; returns the number of waves checked."""
+    rng = random.Random(seed)
+    n = 0
+    for L0 in (8, 16):
+        for _ in range(trials):
+            s = rng.random()
+            pin = rng.choice([0.05, 0.3, 0.6])
+            pout = rng.choice([0.2, 0.7, 0.95])
+            NC = 64 // L0
+            active = [rng.random() < 0.9 for _ in range(NC)]
+            got, _ = wave(s, active, pin, pout, L0)
+            for c in range(NC):
+                want = sequential(s, c, pin, pout) if active[c] else None
+                assert got[c] == want, (L0, c, got[c], want, pin, pout)
+            n += 1
+    return n
+
+
+def rounds(trials=2000, seed=2, pin=0.3, pout=0.7):
+    import statistics
+    rng = random.Random(seed)
+    out = {}
+    for L0 in (8, 16):
+        fr, ar = [], []
+        for _ in range(trials):
+            s = rng.random()
+            active = [True] * (64 // L0)
+            fr.append(fixed_rounds(s, active, pin, pout, L0))
+            ar.append(wave(s, active, pin, pout, L0)[1])
+        out[L0] = (statistics.mean(fr), statistics.mean(ar))
+    return out
+
+
+if __name__ == "__main__":
+    print("schedule == sequential loop on", check(), "waves")
+    for L0, (f, a) in rounds().items():
+        print(f"{L0} lanes per coefficient: fixed groups {f:.2f} rounds per wave, adaptive {a:.2f}")
