@@ -4,7 +4,8 @@ A committed profile (kernel durations, PMC traffic, VALU instruction counts) des
 kernel it measured; bench.py may use it for a later build only if that kernel's gfx950 code is
 the same.  `code_shas()` reads the clang offload bundles embedded in the library (one per HIP
 translation unit), parses each gfx950 ELF code object and hashes, per kernel, its code bytes
-together with its kernel descriptor (`<name>.kd`: register counts, LDS size, launch flags).
+together with its kernel descriptor (`<name>.kd`: register counts, LDS size, launch flags;
+its entry offset, which only locates the code, left out).
 Two builds whose hashes agree for a kernel run the same instructions with the same resources;
 any change of the kernel's source, of an inlined helper or of the compiler changes it.
 
@@ -85,6 +86,9 @@ def code_shas(so_path: str | None = None) -> dict:
             kd = syms.get(name + ".kd")
             if kd is None:
                 continue  # a device function, not a kernel
+            # the descriptor's kernel_code_entry_byte_offset (bytes 16-23) is the distance to
+            # the code, which moves with the layout of the code object: not part of identity
+            kd = kd[:16] + bytes(8) + kd[24:]
             out[name] = hashlib.sha256(code + b"|" + kd).hexdigest()[:16]
     _CACHE[key] = out
     return out

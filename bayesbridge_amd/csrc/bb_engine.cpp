@@ -3686,6 +3686,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_lam_wave = value ? 1 : 0;
             return old;
         }
+        case 15: {
+            const int old = g_lam_lend;
+            if (value >= 0) g_lam_lend = value ? 1 : 0;
+            return old;
+        }
         default: return -1;
     }
 }

@@ -188,6 +188,7 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
                      int ldx, int n_pad, double *xu_part);
 extern int g_lam_xu;
 extern int g_lam_wave;  // wave-adaptive draw in the fused lambda + X u launch (key 13)
+extern int g_lam_lend;  // the continuous-batching launch lends its tail lanes (key 15)
 
 void launch_lambda_variant(hipStream_t s, const double *beta, int p, const DevScalars *sc,
                            uint64_t k0, uint64_t k1, uint64_t t, int group, int noinline,

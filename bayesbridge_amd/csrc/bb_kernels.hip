@@ -274,7 +274,7 @@ static int device_cus_lam() {
 
 // chunk: the workgroup's range is [chunk per_wg, chunk per_wg + per_wg); us (LDS, or null):
 // u_j of the range, for the fused X u pass (k_lambda_xu); NI: the sampler bodies out of line
-template <int G, bool NI = true>
+template <int G, bool NI = true, bool LEND = false>
 __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, int p_pad,
                                                int per_wg, uint64_t j0, const DevScalars *sc,
                                                Key key, uint64_t t, int mode, double *lam,
@@ -369,6 +369,34 @@ __device__ __forceinline__ void lambda_cb_body(const double *beta, int p_loc, in
             if (have) start();
         }
         if (__all(!have)) break;
+        if constexpr (LEND) {
+            // A group without a coefficient means the range is used up: the wave's remaining
+            // draws continue from their state with the idle groups' lanes dealt to them
+            // (wave_draw_rounds, as the fused launch's stable_wave_draw) -- the same attempts
+            // in the same order, so the same draws.
+            static_assert(G == 8 && !NI, "lending deals 8-lane home groups, sampler inlined");
+            if (__any(!have)) {
+                if (have && !draw) {
+                    finish(1.0);  // V0
+                    have = false;
+                }
+                // the wave-uniform constants must be valid on every lane that may serve
+                if (!have) sp = stable_params<true>(1.0, a2, 1.0);
+                unsigned um = 0;
+                const unsigned long long hb = __ballot(have && g == 0);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) um |= (unsigned)((hb >> (8 * c)) & 1ull) << c;
+                uint64_t o0 = o, ibv = ib, jc = j0 + (uint64_t)j;
+                double res = 0.0;
+                const unsigned left = wave_draw_rounds(sp, o0, ibv, jc, um, res, key, t);
+                if (have) {
+                    if ((left >> (lane >> 3)) & 1u) atomicOr(err, 2u);
+                    else finish(res);
+                }
+                have = false;
+                break;
+            }
+        }
     }
     if (have) atomicOr(err, 2u);  // bounded: a draw that never finished is flagged
 }
@@ -397,6 +425,15 @@ __global__ __launch_bounds__(kLamCbWG) void k_lambda_cb_in(BB_LAMBDA_CB_ARGS) {
     lambda_cb_body<G, false>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u,
                              lam_trace, err, s_next, blockIdx.x);
 }
+// ... and the tail's lanes lent to the unfinished draws (bb_set_tuning key 15)
+template <int G>
+__global__ __launch_bounds__(kLamCbWG) __attribute__((amdgpu_waves_per_eu(3, 8))) void
+k_lambda_cl(BB_LAMBDA_CB_ARGS) {
+    __shared__ int s_next;
+    lambda_cb_body<G, false, true>(beta, p_loc, p_pad, per_wg, j0, sc, key, t, mode, lam, D, u,
+                                   lam_trace, err, s_next, blockIdx.x);
+}
+int g_lam_lend = 1;
 #undef BB_LAMBDA_CB_ARGS
 
 // One speculative lambda launch with L lanes per coefficient (the draws do not depend on L);
@@ -642,7 +679,8 @@ void launch_lambda(hipStream_t s, const double *beta, int p_loc, int p_pad, uint
         const bool inl = (g_lam_occ & 4) != 0;
         const int nwg = std::max(1, std::min((inl ? 3 : 4) * device_cus_lam(), (p_pad + 31) / 32));
         const int per = (p_pad + nwg - 1) / nwg;
-        auto *kern = inl ? k_lambda_cb_in<8> : (g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>;
+        auto *kern = inl ? (g_lam_lend ? k_lambda_cl<8> : k_lambda_cb_in<8>)
+                         : (g_lam_occ & 2) ? k_lambda_cb_o4<8> : k_lambda_cb<8>;
         note_launch(KF_LAMBDA, (const void *)kern);
         kern<<<(p_pad + per - 1) / per, kLamCbWG, 0, s>>>(beta, p_loc, p_pad, per, j0, sc, key,
                                                           t, mode, lam, D, u, lam_trace, err);

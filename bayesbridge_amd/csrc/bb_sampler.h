@@ -485,25 +485,18 @@ __device__ __forceinline__ int nth_set_bit(unsigned x, int k) {
     for (int r = 0; r < k && x; ++r) x &= x - 1u;
     return x ? __ffs(x) - 1 : -1;
 }
-__device__ __forceinline__ double stable_wave_draw(bool active, double h, double alpha, double V0,
-                                                   Key key, uint64_t t, uint64_t j,
-                                                   uint32_t *err) {
+// The rounds of the wave-adaptive draw from a given state: um = the wave's unfinished home
+// groups (bit c: lanes 8c..8c+7), and on every lane s / o0 / ib / jc = its home coefficient's
+// constants, loop state and counter index (the wave-uniform fields of s valid on every lane).
+// On return result holds, on the home lanes of every coefficient finished here, its draw; the
+// return value is the set still unfinished (nonempty only at the round cap).  s, o0, ib and jc
+// are overwritten (lanes serve other coefficients along the way).
+__device__ __forceinline__ unsigned wave_draw_rounds(StableParams &s, uint64_t &o0, uint64_t &ib,
+                                                     uint64_t &jc, unsigned um, double &result,
+                                                     Key key, uint64_t t) {
     constexpr int I = 8;
     const int lane = threadIdx.x & 63;
     const int home = lane >> 3, ii = lane & 7;
-    if (active && alpha == 1.) active = false;  // retstable.cpp:104-110
-    if (active && (h < 0 || alpha < 0 || alpha > 1 || V0 < 0)) atomicOr(err, 4u);  // :112-115
-    // every lane forms constants (an inactive one from h = 1): the wave-uniform fields must be
-    // valid on every lane that may serve another coefficient
-    StableParams s = stable_params<true>(active ? h : 1.0, alpha, V0);
-    double result = V0;
-    uint64_t o0 = 0, ib = 0, jc = j;  // the served coefficient's loop state and index
-    unsigned um = 0;                  // unfinished coefficients (wave-uniform)
-    {
-        const unsigned long long a = __ballot(active && ii == 0);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) um |= (unsigned)((a >> (8 * c)) & 1ull) << c;
-    }
     unsigned um_prev = um;
     int G_prev = 8;
     int c_cur = home;  // the coefficient this lane serves
@@ -583,6 +576,28 @@ __device__ __forceinline__ double stable_wave_draw(bool active, double h, double
         G_prev = G;
         um &= ~fm;
     }
+    return um;
+}
+
+__device__ __forceinline__ double stable_wave_draw(bool active, double h, double alpha, double V0,
+                                                   Key key, uint64_t t, uint64_t j,
+                                                   uint32_t *err) {
+    const int lane = threadIdx.x & 63;
+    const int home = lane >> 3, ii = lane & 7;
+    if (active && alpha == 1.) active = false;  // retstable.cpp:104-110
+    if (active && (h < 0 || alpha < 0 || alpha > 1 || V0 < 0)) atomicOr(err, 4u);  // :112-115
+    // every lane forms constants (an inactive one from h = 1): the wave-uniform fields must be
+    // valid on every lane that may serve another coefficient
+    StableParams s = stable_params<true>(active ? h : 1.0, alpha, V0);
+    double result = V0;
+    uint64_t o0 = 0, ib = 0, jc = j;  // the served coefficient's loop state and index
+    unsigned um = 0;                  // unfinished coefficients (wave-uniform)
+    {
+        const unsigned long long a = __ballot(active && ii == 0);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) um |= (unsigned)((a >> (8 * c)) & 1ull) << c;
+    }
+    um = wave_draw_rounds(s, o0, ib, jc, um, result, key, t);
     if (um) {
         atomicOr(err, 2u);
         if ((um >> home) & 1u) result = __builtin_nan("");

@@ -363,7 +363,10 @@ void bb_set_trace_budget(long long bytes);
  * neighbouring blocks share an XCD (1, the default) or in dispatch order (0);
  * key 13: the fused lambda + X u launch with 8 lanes per coefficient deals the lanes of a
  * wave's finished draws to its unfinished ones (1, the default) or keeps fixed 8-lane groups
- * (0); under keys 11-13 the draws are the same.
+ * (0);
+ * key 15: the continuous-batching lambda launch with its sampler inlined lends the lanes of a
+ * wave's idle groups to its unfinished draws once its range is used up (1, the default) or
+ * lets every group finish its own draw (0); under keys 11-15 the draws are the same.
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

@@ -66,3 +66,32 @@ def test_lambda_lane_counts_same_chain(gpu_lib):
     for tr in traces[1:]:
         for k in ("beta", "lambda", "tau", "sig2"):
             assert np.array_equal(traces[0][k], tr[k]), k
+
+
+@pytest.mark.parametrize("n,p", [(60, 60000), (200, 90000)])
+def test_lambda_tail_lending_same_chain(gpu_lib, n, p):
+    """bb_set_tuning key 15: the inlined continuous-batching launch (k_lambda_cl) lends the
+    lanes of a wave's idle groups to its unfinished draws once its range is used up
+    (wave_draw_rounds); with the key off (k_lambda_cb_in) every group finishes its own draw.
+    The same attempts in the same order: the chains are bit-identical."""
+    bb = gpu_lib
+    X, y, _ = synthetic_problem(n, p, seed=13, s=10)
+    traces = []
+    old = bb.set_tuning(15, -1)
+    old6 = bb.set_tuning(6, 0)  # the separate lambda launch on every sweep (no fused X u)
+    try:
+        for lend in (1, 0):
+            bb.set_tuning(15, lend)
+            e = bb.Engine(bb.EngineConfig(n=n, p=p, true_alpha=0.5, method=2, trace_capacity=6,
+                                          seed=79, stream=0), X, y)
+            e.init_state()
+            e.run(1, 6, first_slot=0)
+            e.sync()
+            assert e.error_flags() == 0
+            traces.append(e.trace(0, 6))
+            e.close()
+    finally:
+        bb.set_tuning(15, old)
+        bb.set_tuning(6, old6)
+    for k in ("beta", "lambda", "tau", "sig2"):
+        assert np.array_equal(traces[0][k], traces[1][k]), k
