@@ -27,6 +27,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -270,6 +271,45 @@ def pmc_traffic(n, p, world, instance, window=None):
     return (best[0], best[1], None) if best else (None, None, note)
 
 
+def pmc_traffic_family(n, p, world, instances, window=None):
+    """HBM bytes per launch averaged over several kernel instances that one timed phase
+    launches (the E-apply phase of the mixed plan: k_eapply<NR, 0> fp32 or fp64 products,
+    <NR, 2> the fp64 residual pass, <NR, 3> the fp32 correction products), weighted by their
+    dispatch counts in the newest committed profile of this workload and window that has them
+    all -- the same launches the live average over the phase's brackets covers.  Every
+    instance's entry must describe this build's code.  Returns (bytes, source, note,
+    {instance: {"dispatches", "hbm_bytes"}})."""
+    best, note = None, "no committed PMC summary of this workload"
+    if not instances or world != 1:
+        return None, None, "no kernel instance / multi-rank", None
+    for d, f in _profiles("r*_pmc.json"):
+        w = d.get("workload", {})
+        if w.get("n") != n or w.get("p") != p:
+            continue
+        if window is not None and ((d.get("window") or {}).get("steps"),
+                                   (d.get("window") or {}).get("warmup")) != tuple(window):
+            continue
+        ks = d.get("kernels", {})
+        ents = {i: ks.get(i) for i in instances if ks.get(i)}
+        if not ents:
+            note = f"{f} has none of {instances}"
+            continue
+        stale = [_stale_note(d, f, v, i) for i, v in ents.items()]
+        stale = [x for x in stale if x]
+        if stale:
+            best, note = None, stale[0]
+            continue
+        cnt = sum(v.get("dispatches", 0) for v in ents.values())
+        if not cnt or any(v.get("hbm_bytes") != v.get("hbm_bytes") for v in ents.values()):
+            note = f"{f}: no dispatch counts / traffic for {sorted(ents)}"
+            continue
+        tot = sum(v["dispatches"] * v["hbm_bytes"] for v in ents.values())
+        best = (tot / cnt, f, {i: {"dispatches": v["dispatches"], "hbm_bytes": v["hbm_bytes"]}
+                               for i, v in ents.items()})
+        note = None
+    return (best[0], best[1], None, best[2]) if best else (None, None, note, None)
+
+
 def pmc_mfma(n, p, world, instance, gram):
     """MFMA-busy evidence for the exact kernel instance at this workload from the newest
     committed profiles/rNN_pmc_mfma.json of this tree (tools/pmc_mfma.sh:
@@ -483,6 +523,16 @@ def roofline_for(phase, ms, ctx, traffic_world):
     tb, tsrc, tnote = pmc_traffic(n, p, traffic_world, inst,
                                   None if phase in ("gram", "reduce", "chol", "solve")
                                   else ctx.get("window"))
+    m = re.match(r"(bb::k_eapply<\d+), \d+>$", inst or "")
+    if phase == "eapply" and m and (out.get("fp32_passes_per_launch") or 0) > 0:
+        # the mixed plan's E-apply phase launches three instances (fp32 / fp64 products, the
+        # fp64 residual pass, the fp32 correction products): their dispatch-weighted traffic
+        fam = [f"{m.group(1)}, {k}>" for k in (0, 2, 3)]
+        tb, tsrc, tnote, per = pmc_traffic_family(n, p, traffic_world, fam, ctx.get("window"))
+        out["kernel_instances"] = per
+        out["traffic_definition"] = ("HBM bytes per E-apply launch, averaged over the phase's "
+                                     "instances weighted by their dispatches in the profiled "
+                                     "window (as the live time averages every launch)")
     if out.get("bound") == "mfma":
         mf = pmc_mfma(n, p, traffic_world, inst, ctx.get("gram_name"))
         out["mfma_busy_frac"] = mf["mfma_busy_frac"] if mf else None

@@ -81,3 +81,26 @@ def test_pmc_lookups_use_code_identity(tmp_path, monkeypatch):
     assert e and e["SQ_INSTS_VALU"] == 1.0
     e, note = bench.pmc_valu(7, 13, 1, inst, (20, 5))
     assert e is None and "not used" in note
+
+
+def test_eapply_family_traffic_is_dispatch_weighted(tmp_path, monkeypatch):
+    """The mixed plan's E-apply phase launches three instances; its traffic per launch is
+    their dispatch-weighted mean in the profile of the same window, and a changed kernel
+    retires the whole family's evidence."""
+    fam = ["bb::k_eapply<8, 0>", "bb::k_eapply<8, 2>", "bb::k_eapply<8, 3>"]
+    cs = {k: _kernel_code.code_sha(k) for k in fam}
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    ks = {fam[0]: {"hbm_bytes": 400.0, "dispatches": 3, "code_sha": cs[fam[0]]},
+          fam[1]: {"hbm_bytes": 800.0, "dispatches": 1, "code_sha": cs[fam[1]]},
+          fam[2]: {"hbm_bytes": 400.0, "dispatches": 4, "code_sha": cs[fam[2]]}}
+    d = {"source_sha": "0" * 16, "workload": {"n": 5, "p": 9}, "window": {"steps": 10, "warmup": 1},
+         "kernels": ks}
+    (prof / "r99a_pmc.json").write_text(json.dumps(d))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    b, src, note, per = bench.pmc_traffic_family(5, 9, 1, fam, (10, 1))
+    assert b == (3 * 400 + 800 + 4 * 400) / 8 and note is None and per[fam[1]]["dispatches"] == 1
+    ks[fam[1]]["code_sha"] = "f" * 16
+    (prof / "r99a_pmc.json").write_text(json.dumps(d))
+    b, src, note, per = bench.pmc_traffic_family(5, 9, 1, fam, (10, 1))
+    assert b is None and "not used" in note
