@@ -36,4 +36,8 @@ def gpu_lib():
     if bb.device_count() < 1:
         pytest.fail("GPU test selected but no HIP device is visible")
     bb.set_verbose(0)
+    # BB_TEST_TUNING="KEY=VALUE,...": bb_set_tuning before the GPU tests (A/B of a default)
+    for kv in filter(None, os.environ.get("BB_TEST_TUNING", "").split(",")):
+        k, v = kv.split("=")
+        bb.set_tuning(int(k), int(v))
     return bb

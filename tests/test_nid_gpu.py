@@ -324,14 +324,21 @@ def test_lambda_wave_draw_same_bits(gpu_lib, n, p, scale):
     assert np.all(np.isfinite(a["lambda"])) and np.all(a["lambda"] > 0)
 
 
-@pytest.mark.parametrize("kind", ["dense", "sparse"])
+@pytest.mark.parametrize("kind", ["dense", "sparse", "c3"])
 def test_decision_poll_and_row_blocks_same_bits(gpu_lib, kind):
     """bb_set_tuning key 11 (the host polls the decision's tag word instead of waiting on an
     event) and key 12 (XCD-aware row blocks of the partial row sums) change neither the path
-    nor a bit of the chain: 12 sweeps from the reference start, defaults against both off."""
+    nor a bit of the chain: 12 sweeps from the reference start, defaults against both off
+    (C3's shape included: the fused lambda launch and the mixed plan's decision)."""
     bb = gpu_lib
-    n, p = 300, 4000
-    X, y, _ = _design(kind, n, p, 52)
+    if kind == "c3":  # C3's shape: the fused lambda launch and the mixed plan's decision
+        import bench
+        n, p = 2000, 50000
+        X = bench.make_columns(n, 0, p)
+        y, _ = bench.make_problem_y(n, p)
+    else:
+        n, p = 300, 4000
+        X, y, _ = _design(kind, n, p, 52)
     out = []
     for v in (1, 0):
         o11, o12 = bb.set_tuning(11, v), bb.set_tuning(12, v)
