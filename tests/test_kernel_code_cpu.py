@@ -104,3 +104,39 @@ def test_eapply_family_traffic_is_dispatch_weighted(tmp_path, monkeypatch):
     (prof / "r99a_pmc.json").write_text(json.dumps(d))
     b, src, note, per = bench.pmc_traffic_family(5, 9, 1, fam, (10, 1))
     assert b is None and "not used" in note
+
+
+def _build_so(tmp_path, name, src):
+    import subprocess
+    f = tmp_path / f"{name}.hip"
+    f.write_text(src)
+    so = tmp_path / f"{name}.so"
+    subprocess.check_call([_build.hipcc(), "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                           "-o", str(so), str(f)])
+    return str(so)
+
+
+def test_identity_follows_code_not_layout(tmp_path):
+    """Two libraries built here: the second adds a kernel before `keep` (its code moves in
+    the code object) and changes `edit`.  `keep` keeps its identity (the descriptor's entry
+    offset is left out), `edit` gets a new one."""
+    base = """#include <hip/hip_runtime.h>
+namespace bb {
+__global__ void keep(double *x) { x[threadIdx.x] = x[threadIdx.x] * 2.0 + 1.0; }
+__global__ void edit(double *x) { x[threadIdx.x] += 3.0; }
+}
+"""
+    moved = """#include <hip/hip_runtime.h>
+namespace bb {
+__global__ void added(double *x, int n) { for (int i = 0; i < n; ++i) x[i] = x[i] * x[i] + 0.5; }
+__global__ void keep(double *x) { x[threadIdx.x] = x[threadIdx.x] * 2.0 + 1.0; }
+__global__ void edit(double *x) { x[threadIdx.x] += 4.0; }
+}
+"""
+    a = _kernel_code.code_shas(_build_so(tmp_path, "a", base))
+    b = _kernel_code.code_shas(_build_so(tmp_path, "b", moved))
+    k = [m for m in a if "4keep" in m][0]
+    e = [m for m in a if "4edit" in m][0]
+    assert a[k] == b[k]
+    assert a[e] != b[e]
+    assert any("5added" in m for m in b) and not any("5added" in m for m in a)
