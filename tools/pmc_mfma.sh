@@ -5,6 +5,8 @@
 #   c3      default C3 bench (Ozaki-II: k_oz_gemm16u, k_oz_residues; k_chol_persistent)
 #   c3fp64  C3 with the fp64 MFMA Gram (k_gram)
 #   c2      C2 (k_chol_persistent at n = 1000, k_oz_gemm16u)
+#   c4      C4, the logistic bridge (X'OmegaX on k_oz_gemm16u, k_chol_persistent at p = 1000)
+# CONFIGS / COUNTERS select configs and counters (one pass per GPU call: COUNTERS=<one>)
 # Summary: python tools/pmc_mfma_summary.py <round>  ->  profiles/<round>_pmc_mfma.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -24,14 +26,15 @@ pass() {  # $1 = config name, $2 = counter, rest = bench args
         > "$OUT/$cfg/$ctr.json" 2> "$OUT/$cfg/$ctr.err" || { echo "$cfg $ctr failed ($?)"; exit 1; }
     echo "$cfg $ctr ok"
 }
-for cfg in c3 c3fp64 c2; do
+for cfg in ${CONFIGS:-c3 c3fp64 c2 c4}; do
     mkdir -p "$OUT/$cfg"
     case $cfg in
         c3) args="" ;;
         c3fp64) args="--gram fp64" ;;
         c2) args="--workload c2" ;;
+        c4) args="--workload c4" ;;
     esac
-    pass $cfg SQ_VALU_MFMA_BUSY_CYCLES $args
-    pass $cfg GRBM_GUI_ACTIVE $args
-    pass $cfg SQ_BUSY_CU_CYCLES $args
+    for ctr in ${COUNTERS:-SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES}; do
+        pass $cfg $ctr $args
+    done
 done
