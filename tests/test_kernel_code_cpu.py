@@ -140,3 +140,22 @@ __global__ void edit(double *x) { x[threadIdx.x] += 4.0; }
     assert a[k] == b[k]
     assert a[e] != b[e]
     assert any("5added" in m for m in b) and not any("5added" in m for m in a)
+
+
+def test_round5_profiles_carry_code_identities():
+    """Every committed round-5 PMC / VALU / MFMA summary stamps its bb:: kernel entries with
+    the kernel's code identity (what bench.py matches a later build against)."""
+    import glob
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = glob.glob(os.path.join(root, "profiles", "r05*_pmc*.json"))
+    assert files
+    for f in files:
+        d = json.load(open(f))
+        maps = [d["kernels"]] if isinstance(d.get("kernels"), dict) else []
+        maps += [c["kernels"] for c in d.get("configs", {}).values() if "kernels" in c]
+        for m in maps:
+            for k, v in m.items():
+                if k.startswith("bb::") and isinstance(v, dict):
+                    assert v.get("code_sha"), (f, k)
