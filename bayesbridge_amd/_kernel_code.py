@@ -6,8 +6,10 @@ the same.  `code_shas()` reads the clang offload bundles embedded in the library
 translation unit), parses each gfx950 ELF code object and hashes, per kernel, its code bytes
 together with its kernel descriptor (`<name>.kd`: register counts, LDS size, launch flags;
 its entry offset, which only locates the code, left out).
-Two builds whose hashes agree for a kernel run the same instructions with the same resources;
-any change of the kernel's source, of an inlined helper or of the compiler changes it.
+A code object's out-of-line device functions (callees) are folded into the identity of each of
+its kernels.  Two builds whose hashes agree for a kernel run the same instructions with the same
+resources; any change of the kernel's source, of an inlined or called helper or of the
+compiler changes it.
 
 Pure host code (no GPU, no HIP calls): usable on the CPU container and on the GPU box.
 """
@@ -41,8 +43,9 @@ def _bundles(blob: bytes):
         pos = i + len(_BUNDLE_MAGIC)
 
 
-def _elf_symbols(elf: bytes):
-    """{name: (bytes of the symbol)} for the FUNC and OBJECT symbols of an ELF64 code object."""
+def _elf_symbols(elf: bytes, funcs: dict | None = None):
+    """{name: (bytes of the symbol)} for the FUNC and OBJECT symbols of an ELF64 code object;
+    `funcs`, if given, also receives the FUNC symbols alone."""
     if elf[:4] != b"\x7fELF" or elf[4] != 2:
         return {}
     shoff, = struct.unpack_from("<Q", elf, 0x28)
@@ -64,6 +67,8 @@ def _elf_symbols(elf: bytes):
             tsec = secs[shndx]
             start = tsec[4] + (value - tsec[3])
             out[name] = elf[start:start + ssize]
+            if funcs is not None and (st_info & 0xF) == 2:
+                funcs[name] = out[name]
     return out
 
 
@@ -79,7 +84,19 @@ def code_shas(so_path: str | None = None) -> dict:
     for triple, elf in _bundles(blob):
         if "gfx950" not in triple:
             continue
-        syms = _elf_symbols(elf)
+        funcs: dict = {}
+        syms = _elf_symbols(elf, funcs)
+        # out-of-line device functions of this code object (no .kd: not kernels), e.g. the
+        # __noinline__ sampler bodies the NI lambda variants call: their code is part of every
+        # kernel's identity in the code object (which kernel calls which is not resolved), so
+        # an edit of a callee retires the evidence of its callers
+        callees = sorted(n for n in funcs if not n.endswith(".kd") and n + ".kd" not in syms)
+        cdig = b""
+        if callees:
+            h = hashlib.sha256()
+            for n in callees:
+                h.update(n.encode() + b"\0" + funcs[n])
+            cdig = b"|" + h.digest()
         for name, code in syms.items():
             if name.endswith(".kd"):
                 continue
@@ -89,7 +106,7 @@ def code_shas(so_path: str | None = None) -> dict:
             # the descriptor's kernel_code_entry_byte_offset (bytes 16-23) is the distance to
             # the code, which moves with the layout of the code object: not part of identity
             kd = kd[:16] + bytes(8) + kd[24:]
-            out[name] = hashlib.sha256(code + b"|" + kd).hexdigest()[:16]
+            out[name] = hashlib.sha256(code + b"|" + kd + cdig).hexdigest()[:16]
     _CACHE[key] = out
     return out
 

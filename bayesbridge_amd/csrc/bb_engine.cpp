@@ -1389,16 +1389,29 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->nid_kmax = e->nid_kmax_model();
             // the mixed-precision plan's fp32 copy of X (unsharded dense engines; 4 B per
             // element: 400 MB at C3), unless an entry is outside fp32's normal range
-            if (e->method == 2 && c.world == 1) {
-                e->X32 = dalloc<float>((size_t)n_pad * p_pad, o);
-                e->ch_b = dalloc<double>(n_pad, o);
-                int *bad = dalloc<int>(1, o);
-                HIPCHECK(hipMemsetAsync(bad, 0, sizeof(int), e->stream));
-                launch_cast_f32(e->stream, e->X, n_pad, n_pad, c.p_local, e->X32, bad);
-                int hb = 0;
-                HIPCHECK(hipMemcpyAsync(&hb, bad, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-                HIPCHECK(hipStreamSynchronize(e->stream));
-                if (hb) e->X32 = nullptr;  // (the buffer stays owned and is freed with the engine)
+            // Only when the plan can be used (key 10 on, a Chebyshev path at all), and never
+            // at the price of the engine: a failed allocation keeps the fp64 plan.
+            if (e->method == 2 && c.world == 1 && g_nid_mixed && e->nid_kmax > 0) {
+                void *x32 = nullptr;
+                if (hipMalloc(&x32, (size_t)n_pad * p_pad * sizeof(float)) != hipSuccess) {
+                    (void)hipGetLastError();  // clear the sticky out-of-memory status
+                    x32 = nullptr;
+                }
+                if (x32) {
+                    e->ch_b = dalloc<double>(n_pad, o);
+                    int *bad = dalloc<int>(1, o);
+                    HIPCHECK(hipMemsetAsync(bad, 0, sizeof(int), e->stream));
+                    launch_cast_f32(e->stream, e->X, n_pad, n_pad, c.p_local, (float *)x32, bad);
+                    int hb = 0;
+                    HIPCHECK(hipMemcpyAsync(&hb, bad, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+                    HIPCHECK(hipStreamSynchronize(e->stream));
+                    if (hb) {
+                        (void)hipFree(x32);  // an entry outside fp32's normal range
+                    } else {
+                        o.push_back(x32);
+                        e->X32 = (float *)x32;
+                    }
+                }
             }
         }
     }

@@ -681,6 +681,7 @@ def run_chain(args, n, p, alpha, kind, mode):
     engines = [make_engine(r, devices[i], cap) for i, r in enumerate(my_ranks)]
     eng = engines[0]
     grp = None
+    forced_old = None  # key 9's value before BB_FORCE_RCCL forced it (restored at the end)
     if mode == "group":
         grp = bb.ShardGroup(engines, rccl=True)
     elif mode == "ranks":
@@ -692,7 +693,7 @@ def run_chain(args, n, p, alpha, kind, mode):
         # the world > 1 near-identity protocol forced on it (bb_set_tuning key 9): the bound
         # sums, X u and every product go through ncclAllReduce and the host waits for each
         # sweep's decision, as every rank of the job does
-        bb.set_tuning(9, 1)
+        forced_old = bb.set_tuning(9, 1)
         eng.comm_init(bb.Engine.comm_unique_id())
     runner = grp or eng
     runner.init_state()
@@ -891,6 +892,8 @@ def run_chain(args, n, p, alpha, kind, mode):
         grp.close()
     for e in engines:
         e.close()
+    if forced_old is not None:
+        bb.set_tuning(9, forced_old)  # the setting is process-global
     if dist:
         dist.destroy_process_group()
 

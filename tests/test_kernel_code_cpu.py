@@ -142,6 +142,21 @@ __global__ void edit(double *x) { x[threadIdx.x] += 4.0; }
     assert any("5added" in m for m in b) and not any("5added" in m for m in a)
 
 
+def test_identity_follows_out_of_line_callees(tmp_path):
+    """A kernel that calls a __noinline__ helper gets a new identity when only the helper
+    changes (the callee's code is part of the caller's identity)."""
+    src = """#include <hip/hip_runtime.h>
+namespace bb {
+__device__ __noinline__ double helper(double v) { return v * v + %s; }
+__global__ void caller(double *x) { x[threadIdx.x] = helper(x[threadIdx.x]); }
+}
+"""
+    a = _kernel_code.code_shas(_build_so(tmp_path, "ca", src % "0.25"))
+    b = _kernel_code.code_shas(_build_so(tmp_path, "cb", src % "0.75"))
+    k = [m for m in a if "6caller" in m][0]
+    assert a[k] != b[k]
+
+
 def test_round5_profiles_carry_code_identities():
     """Every committed round-5 PMC / VALU / MFMA summary stamps its bb:: kernel entries with
     the kernel's code identity (what bench.py matches a later build against)."""

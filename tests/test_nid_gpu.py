@@ -410,6 +410,8 @@ def test_mixed_plan_sweep_equals_fp64_plan(gpu_lib, capsys):
         finally:
             bb.set_tuning(10, old)
     assert engs[1].nid_mixed()["holds_x32"]
+    # created with the plan off: no fp32 copy (it could never be used)
+    assert not engs[0].nid_mixed()["holds_x32"]
     plans = []
     for scale in (1e-5, 1e-4, 3e-4, 1e-3, 1e-2):
         beta, tau = btrue * scale + scale * rng.standard_normal(p), scale
@@ -439,6 +441,36 @@ def test_mixed_plan_sweep_equals_fp64_plan(gpu_lib, capsys):
     for e in engs.values():
         assert e.error_flags() == 0
         e.close()
+
+
+def test_mixed_plan_refused_outside_fp32_range(gpu_lib):
+    """A design with one column scaled to ~1e-39 (below fp32's normal range) gets no fp32
+    copy: holds_x32 is false, no sweep takes the mixed plan, and the chain is bit-identical to
+    an engine created with the plan off."""
+    import bench
+    bb = gpu_lib
+    n, p = 2000, 6250
+    X = bench.make_columns(n, 0, p)
+    y, _ = bench.make_problem_y(n, p)
+    X[:, 17] *= 1e-39
+    outs = {}
+    for mixed in (1, 0):
+        old = bb.set_tuning(10, mixed)
+        try:
+            e = _engine(bb, X, y, n, p)
+            e.init_state()
+            e.run(1, 30, first_slot=-1)
+            e.sync()
+            outs[mixed] = (e.state(), e.nid_mixed())
+            assert e.error_flags() == 0
+            e.close()
+        finally:
+            bb.set_tuning(10, old)
+    (a, ma), (o, mo) = outs[1], outs[0]
+    assert not ma["holds_x32"] and not mo["holds_x32"]
+    assert ma["mixed_sweeps"] == 0
+    assert np.array_equal(a["beta"], o["beta"]) and np.array_equal(a["lambda"], o["lambda"])
+    assert a["tau"] == o["tau"] and a["sig2"] == o["sig2"]
 
 
 def test_mixed_plan_teacher_forced_against_oracle(gpu_lib, capsys):
