@@ -17,7 +17,7 @@ SO_PATH = os.path.join(HERE, "BayesBridge.so")
 OBJ_DIR = os.path.join(HERE, "build")  # per-source objects (kept: tests relink them)
 SOURCES = ["bb_kernels.hip", "bb_ozaki.hip", "bb_tri.hip", "bb_sparse.hip", "bb_logit.hip", "bb_nid.hip",
            "bb_small.hip", "bb_engine.cpp"]
-HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h", "bb_sparse.h", "bb_pg.h"]
+HEADERS = ["bb_kernels.h", "bb_sampler.h", "bb_ozaki.h", "bb_sparse.h", "bb_pg.h", "bb_chol4.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 
 

@@ -3627,7 +3627,7 @@ void bb_debug_fail_member(int member, int sweep) {
 
 int bb_set_chol_version(int version) {
     if (version == 0) return g_chol_version;  // query
-    if (version < 1 || version > 3) return -1;
+    if (version < 1 || version > 4) return -1;
     g_chol_version = version;
     return 0;
 }

@@ -2391,6 +2391,8 @@ __device__ void chol_chain_v2(double *A, int lda, int nblk, int ncb, double *Wd,
 #undef CHAIN2_TS
 }
 
+#include "bb_chol4.h"
+
 template <int V>
 __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int nblk, int ncb,
                                                          double *Wd, CholFlags F,
@@ -2401,8 +2403,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     // A_{k,k+1} -> U_{k,k+1}; Q: staging U_kj / W_i / the chain's next diagonal block.
     // During the v1 chain's elimination S and Q together hold the published pivot rows; the
     // v2 chain (chol_chain_v2) lays out U rows, S and the pivot rows side by side.
-    constexpr bool kV2 = V >= 2;  // the pipelined chains
-    __shared__ __attribute__((aligned(16))) double Lraw[kV2 ? 8320 + 64 * 130 : 3 * 64 * 65];
+    constexpr bool kV2 = V == 2 || V == 3;  // the pipelined chains
+    constexpr bool kV4 = V == 4;            // the 16-column leaf pipeline (bb_chol4.h)
+    __shared__ __attribute__((aligned(16))) double Lraw[kV4 ? 4 * 64 * kC4Ld
+                                                        : kV2 ? 8320 + 64 * 130 : 3 * 64 * 65];
     double(*Lb)[64][65] = (double(*)[64][65])Lraw;
     __shared__ double piv[64];
     __shared__ int cnt;
@@ -2414,7 +2418,10 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
     v4d acc[2];
     if (blockIdx.x == 0) {
         // ------------------------------ the chain ------------------------------
-        if constexpr (kV2) {
+        if constexpr (kV4) {
+            chol_chain_v4(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
+            return;
+        } else if constexpr (kV2) {
             chol_chain_v2<V>(A, lda, nblk, ncb, Wd, F, err, trace, Lraw);
             return;
         }
@@ -2787,16 +2794,18 @@ int g_chol_version = 1;
 // Workgroups of k_chol_persistent<V> the device can hold at once (occupancy query x CUs),
 // computed once per chain variant.
 static int chol_max_resident(int version) {
-    static int cache[4] = {-1, -1, -1, -1};
+    static int cache[5] = {-1, -1, -1, -1, -1};
     static std::mutex mu;
     std::lock_guard<std::mutex> lk(mu);
-    int &c = cache[version & 3];
+    int &c = cache[(version >= 1 && version <= 4) ? version : 1];
     if (c < 0) {
         int nb = 0;
         hipError_t e = version == 2
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<2>, 512, 0)
             : version == 3
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<3>, 512, 0)
+            : version == 4
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<4>, 512, 0)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_chol_persistent<1>, 512, 0);
         c = (e == hipSuccess ? nb : 0) * device_cus();
     }
@@ -2825,7 +2834,8 @@ void chol_factor(hipStream_t s, double *A, int lda, int m_pad, int nrhs_blocks, 
         throw std::runtime_error(b);
     }
     auto *kern = g_chol_version == 1 ? k_chol_persistent<1>
-               : g_chol_version == 2 ? k_chol_persistent<2> : k_chol_persistent<3>;
+               : g_chol_version == 2 ? k_chol_persistent<2>
+               : g_chol_version == 3 ? k_chol_persistent<3> : k_chol_persistent<4>;
     note_launch(KF_CHOL, (const void *)kern);
     kern<<<grid, 512, 0, s>>>(A, lda, nblk, ncb, Wd, F, err, trace, gate);
 }

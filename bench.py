@@ -563,6 +563,9 @@ def main():
     ap.add_argument("--alpha", type=float, default=None)
     ap.add_argument("--cpu-sweeps", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-literal", action="store_true",
+                    help="skip the reference-literal p x p CPU sweep for p > 8000 (C3: ~60 s, "
+                         "40 GB of host memory)")
     ap.add_argument("--no-parity-check", action="store_true",
                     help="skip the N > 1 pre-timing check of the sharded chain against one "
                          "device holding the whole problem")
@@ -815,6 +818,9 @@ def run_chain(args, n, p, alpha, kind, mode):
     if mode == "single" and not logit and not args.no_fitted:
         fitted = fitted_regime(bb, eng, kind, n, p, alpha, t)
         t += 10000
+    ref_proto = None
+    if mode == "single" and not args.no_fitted:
+        ref_proto = reference_protocol(runner, sync_all)
     # the Gram's instances as launched (by the fitted-regime run when the timed sweeps formed none)
     ctx_gram = dict(ctx, instances=dict(instances, **{
         ph: instances.get(ph) or bb.kernel_instance(ph) for ph in ("gram", "reduce", "chol")}))
@@ -884,6 +890,7 @@ def run_chain(args, n, p, alpha, kind, mode):
             "setup_s": setup_s,
             "near_identity": nid,
             "fitted_regime": fitted,
+            "reference_protocol": ref_proto,
         }
         if cpu_more:
             rec["cpu_baselines"] = cpu_more
@@ -896,6 +903,31 @@ def run_chain(args, n, p, alpha, kind, mode):
         bb.set_tuning(9, forced_old)  # the setting is process-global
     if dist:
         dist.destroy_process_group()
+
+
+def reference_protocol(runner, sync_all, burn=500, nsamp=1000):
+    """The reference's default call, timed on the same engine:
+    bridge.reg.stb(y, X, nsamp = 1000, burn = 500) (BridgeWrapper.R:194-201) from the
+    reference start (beta = 0 for p > n, BridgeWrapper.cpp:242-244): burn + 1 burn-in sweeps
+    then nsamp - 1 MCMC sweeps recorded into the trace (BridgeWrapper.cpp:266-298).  `value` is
+    the post-burn rate the reference's `runtime` out-parameter measures (BridgeWrapper.cpp:
+    284-311), `call_sweeps_per_s` the whole call's."""
+    runner.init_state()
+    sync_all()
+    t0 = time.perf_counter()
+    runner.run(1, burn + 1, first_slot=-1)
+    sync_all()
+    t1 = time.perf_counter()
+    runner.run(burn + 2, nsamp - 1, first_slot=0)
+    sync_all()
+    t2 = time.perf_counter()
+    return {"value": (nsamp - 1) / (t2 - t1), "unit": "sweeps/s",
+            "call_sweeps_per_s": (burn + nsamp) / (t2 - t0),
+            "burn": burn, "nsamp": nsamp, "burn_s": t1 - t0, "mcmc_s": t2 - t1,
+            "protocol": "bridge.reg.stb defaults (BridgeWrapper.R:194-201): burn-in 500 + 1 "
+                        "sweeps, then 999 MCMC sweeps recorded, from the reference start; value = "
+                        "MCMC sweeps / post-burn wall time (the reference's runtime is post-burn "
+                        "CPU time)"}
 
 
 def fitted_regime(bb, eng, kind, n, p, alpha, t, warm=20, steps=50):
@@ -999,6 +1031,16 @@ def shard_parity_check(bb, dist, rank, engines, my_ranks, runner, make_engine, d
                 against="one engine holding all p columns on rank 0's device", **errs)
 
 
+def literal_fits(p):
+    """Host memory for the reference-literal chain's two p x p matrices (X'X and the factor)
+    with a 2x margin."""
+    try:
+        import psutil
+        return psutil.virtual_memory().available > 4 * 8.0 * p * p
+    except Exception:
+        return False
+
+
 def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
     """The cpu_baseline leg (rank 0, N = 1 only), timed on this host."""
     sparse, logit = kind == "sparse", kind == "logit"
@@ -1035,6 +1077,10 @@ def cpu_baselines(args, n, p, alpha, kind, cpu_sweeps):
         variants = [(False, 1, max(1, min(cpu_sweeps, 3)))]
         if p <= 8000:
             variants += [(True, None, 3), (True, 1, 2)]
+        elif literal_fits(p) and not args.no_literal:
+            # the reference-literal p x p path in the same run (C3: X'X is
+            # 20 GB, one dpotrf of p = 50 000 per sweep, ~60 s with its setup on 16 threads)
+            variants += [(True, None, 1)]
         for lit, th, ns in variants:
             per_sweep, threads = cpu_baseline(n, p, alpha, ns, threads=th, literal=lit)
             cpu_more.append({

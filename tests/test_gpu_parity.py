@@ -160,12 +160,12 @@ def test_chol_solve_matches_numpy(gpu_lib, m, nrhs):
     assert rel_err(x, ref) < 1e-10 * np.linalg.cond(A) ** 0.5
 
 
-@pytest.mark.parametrize("version", [1, 2, 3])
+@pytest.mark.parametrize("version", [1, 2, 3, 4])
 @pytest.mark.parametrize("m", [40, 64, 128, 200, 1000, 2048, 5000])
 def test_chol_chain_versions_match_numpy(gpu_lib, m, version):
-    """Every chain variant of k_chol_persistent (1: the default; 2, 3: pipelined), from one
-    block (m <= 64) to 79 block steps, on an ill-conditioned SPD system.  The variant in use
-    before the test is restored afterwards."""
+    """Every chain variant of k_chol_persistent (1: the round-2 chain; 2, 3: pipelined; 4: the
+    16-column leaf pipeline), from one block (m <= 64) to 79 block steps, on an
+    ill-conditioned SPD system.  The variant in use before the test is restored afterwards."""
     bb = gpu_lib
     rng = np.random.default_rng(m + 7)
     B = rng.standard_normal((m, m)) * np.exp(rng.uniform(-6, 6, m))

@@ -65,3 +65,33 @@ for v in [v for v in VERSIONS if v == 1]:
           "last pivot", round(float(np.median((t[:, 1] - t[:, 0]) * 0.01)), 2),
           "step median", round(float(np.median(steps)), 2), flush=True)
 bb.set_chol_version(1)
+
+# v4 (16-column leaf pipeline, bb_chol4.h) per-step stamps, medians over the inner steps (us
+# after the step's leaf-0 start); slot names in bb_chol4.h
+V4_SLOTS = {1: "leaf3 done", 2: "W rel", 3: "S acq", 4: "U rel", 5: "D00 ready", 6: "leaf1 start",
+            7: "leaf2 start", 24: "d0 T3(012)", 25: "d1 T3(022)", 26: "d0 T3(123)",
+            27: "d1 T3(133)", 28: "s0 US0", 29: "s0 US3", 30: "s0 UU", 31: "w4 UU"}
+for t in range(4):
+    V4_SLOTS[8 + 4 * t] = f"L{t} piv"
+    V4_SLOTS[9 + 4 * t] = f"L{t} W"
+    if t < 3:
+        V4_SLOTS[10 + 4 * t] = f"X{t}"
+        V4_SLOTS[11 + 4 * t] = f"upd{t + 1}"
+for v in [v for v in VERSIONS if v == 4]:
+    bb.set_chol_version(v)
+    for m in (1024, 2048):
+        f, s, ts = bb.bench_chol(m, reps=3, trace=True)
+        nb = m // 64
+        t = ts[:nb].astype(np.int64)
+        steps = np.diff(t[:, 0]) * 0.01
+        print(f"v4 m={m} factor {f * 1e3:.1f} us; step median {np.median(steps[1:]):.2f} "
+              f"(min {steps[1:].min():.2f} max {steps[1:].max():.2f})", flush=True)
+        inner = t[1:-1]
+        rel = {}
+        for j, name in sorted(V4_SLOTS.items(), key=lambda kv: np.median(inner[:, kv[0]] - inner[:, 0])):
+            d = (inner[:, j] - inner[:, 0]) * 0.01
+            d = d[inner[:, j] > 0]
+            if len(d):
+                rel[name] = round(float(np.median(d)), 2)
+        print("  " + json.dumps(rel), flush=True)
+bb.set_chol_version(1)
