@@ -262,16 +262,22 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
                     for (int c = 0; c < 4; ++c) c4_wait(&sy.usr[t][c], k, err);
                 }
                 // W_tt = diag(1/sqrt p) E (U_tt itself is never needed: the later blocks use
-                // W_tt, and the backward solve W_k)
-                if (lane < 16) {
+                // W_tt, and the backward solve W_k).  Every 16-lane row holds the same E and
+                // pivots, so DPP row g scales rows 4q + g: four reciprocal square roots per
+                // lane instead of sixteen on one row.
+                {
+                    const int g = lane >> 4;
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const double pvi = pv[i];
+                    for (int q = 0; q < 4; ++q) {
+                        const double pvi = g == 0 ? pv[4 * q] : g == 1 ? pv[4 * q + 1]
+                                         : g == 2 ? pv[4 * q + 2] : pv[4 * q + 3];
+                        const double ei = g == 0 ? e[4 * q] : g == 1 ? e[4 * q + 1]
+                                        : g == 2 ? e[4 * q + 2] : e[4 * q + 3];
                         // 1/sqrt(p): v_rsq_f64 + two Newton steps
                         double r = __builtin_amdgcn_rsq(pvi);
                         r = r * __builtin_fma(-0.5 * pvi * r, r, 1.5);
                         r = r * __builtin_fma(-0.5 * pvi * r, r, 1.5);
-                        Wm[16 * t + i][16 * t + lane] = e[i] * r;
+                        Wm[16 * t + 4 * q + g][16 * t + j16] = ei * r;
                     }
                 }
                 if (lane == 0) {
@@ -422,9 +428,10 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
         const unsigned int *fS = &F.R[2 * k + 1], *fQ = &F.R[2 * (k + 1)];
         const int r0 = k * kNB, cs = (k + 1) * kNB;  // tile (k, k+1): rows r0.., cols cs..
         // D_{k+1} block (a, b) = Q_ab - acc (Q: the (k+1, k+1) hand-off; diagonal blocks
-        // mirrored from its upper triangle)
-        auto tq = [&](int a, int b, const v4d &acc) {
-            v4d d;
+        // mirrored from its upper triangle).  Q arrives early in the step: its blocks are
+        // loaded into registers before the last leaf (tq_ld) and only subtracted at the end.
+        auto tq_ld = [&](int a, int b) {
+            v4d q;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * r + (lane >> 4);
@@ -433,9 +440,12 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
                     y = 16 * a + j16;
                     x = 16 * a + i;
                 }
-                d[r] = ld_sc1(Aat(cs + y, cs + x)) - acc[r];
+                q[r] = ld_sc1(Aat(cs + y, cs + x));
             }
-            c4_st(Dn, a, b, d);
+            return q;
+        };
+        auto tq = [&](int a, int b, const v4d &q, const v4d &acc) {
+            c4_st(Dn, a, b, q - acc);
             c4_set(&sy.ver[a][b], nbase);
         };
         if (scol >= 0) {
@@ -453,8 +463,13 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
                 for (int q = 0; q < 16; ++q) Sm[16 * c + (lane & 15)][4 * q + (lane >> 4)] = v[q];
             }
             for (int b = 0; b < 4; ++b) c4_set(&sy.sver[c][b], base);
-            v4d accd = kC4Zero, acco = kC4Zero;
+            v4d accd = kC4Zero, acco = kC4Zero, qd = kC4Zero, qo = kC4Zero;
             for (int t = 0; t < 4; ++t) {
+                if (t == 3) {
+                    c4_gwait(fQ, F.ep, err);
+                    qd = tq_ld(c, c);
+                    if (c < 3) qo = tq_ld(c, c + 1);
+                }
                 // U_S,t column block c = W_tt S_tc (in place; also tile (k, k+1) of A)
                 c4_wait(&sy.leaf, 4 * k + t + 1, err);
                 c4_wait(&sy.sver[t][c], base + t, err);
@@ -484,7 +499,11 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
             if (c == 0) C4_TS(30);
             c4_add(&sy.t5done);
             if (c < 3) c4_add(&sy.t5done);
+            // the next diagonal block first (the next step's leaf 0 waits on it), then
             // U_{k,k+1} released once the four column waves' stores have drained
+            tq(c, c, qd, accd);
+            if (c == 0) C4_TS(5);
+            if (c < 3) tq(c, c + 1, qo, acco);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (c4_add(&sy.upub) == 4 * k + 3) {
                 if (lane == 0)
@@ -492,14 +511,16 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 C4_TS(4);
             }
-            c4_gwait(fQ, F.ep, err);
-            tq(c, c, accd);
-            if (c == 0) C4_TS(5);
-            if (c < 3) tq(c, c + 1, acco);
         } else {
             // wave 4: U'U blocks (0, 2), (0, 3), (1, 3) from the S buffer
-            v4d a02 = kC4Zero, a03 = kC4Zero, a13 = kC4Zero;
+            v4d a02 = kC4Zero, a03 = kC4Zero, a13 = kC4Zero, q02, q03, q13;
             for (int t = 0; t < 4; ++t) {
+                if (t == 3) {
+                    c4_gwait(fQ, F.ep, err);
+                    q02 = tq_ld(0, 2);
+                    q03 = tq_ld(0, 3);
+                    q13 = tq_ld(1, 3);
+                }
                 c4_wait(&sy.usr[t][0], kr, err);
                 c4_wait(&sy.usr[t][2], kr, err);
                 c4_mm<true, false>(a02, Sm, t, 0, Sm, t, 2);
@@ -512,10 +533,9 @@ __device__ void chol_chain_v4(double *A, int lda, int nblk, int ncb, double *Wd,
             c4_add(&sy.t5done);
             c4_add(&sy.t5done);
             c4_add(&sy.t5done);
-            c4_gwait(fQ, F.ep, err);
-            tq(0, 2, a02);
-            tq(0, 3, a03);
-            tq(1, 3, a13);
+            tq(0, 2, q02, a02);
+            tq(0, 3, q03, a03);
+            tq(1, 3, q13, a13);
         }
     }
 }

@@ -2648,18 +2648,14 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             const int k = merge ? i - 1 : i - 2;
             OWN_TS(0);
             flag_acquire2(&F.W[k], &F.H[k], F.ep, err);
-            // merge also reads the chain's U_{k,i} (i = k + 1): the v2 chain publishes W_k
-            // as soon as the elimination ends, before U_{k,k+1} (v1 released both together)
-            if (merge) flag_acquire2(&F.P[k * F.ncb + i], nullptr, F.ep, err);
             OWN_TS(1);
             const double *Wk = Wd + (size_t)k * kNB * kNB;
-            double vw[8], va[8], vu[8];
+            double vw[8], va[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int e = tid + q * 512, y = e & 63, x = e >> 6;
                 vw[q] = ld_sc1(&Wk[(size_t)x * kNB + y]);
                 va[q] = ld_sc1(&Hs[(size_t)k * kNB * kNB + (size_t)y + (size_t)x * kNB]);
-                vu[q] = merge ? ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(i * kNB + x) * lda]) : 0.0;
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -2674,6 +2670,16 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             __syncthreads();  // every wave has read W_k and A_{k,j}
             wl_put(Q, u2[0], u2[1]);
             if (merge) {
+                // merge also reads the chain's U_{k,i} (i = k + 1).  The v2 and v4 chains
+                // publish W_k before U_{k,k+1} (v1 releases both together), so U_{k,j} is
+                // formed above while the chain finishes U_{k,k+1}.
+                flag_acquire2(&F.P[k * F.ncb + i], nullptr, F.ep, err);
+                double vu[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int e = tid + q * 512, y = e & 63, x = e >> 6;
+                    vu[q] = ld_sc1(&A[(size_t)(k * kNB + y) + (size_t)(i * kNB + x) * lda]);
+                }
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int e = tid + q * 512, y = e & 63, x = e >> 6;
