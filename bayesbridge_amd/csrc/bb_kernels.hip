@@ -2670,9 +2670,13 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             __syncthreads();  // every wave has read W_k and A_{k,j}
             wl_put(Q, u2[0], u2[1]);
             if (merge) {
-                // merge also reads the chain's U_{k,i} (i = k + 1).  The v2 and v4 chains
-                // publish W_k before U_{k,k+1} (v1 releases both together), so U_{k,j} is
-                // formed above while the chain finishes U_{k,k+1}.
+                // U_{k,j} is stored now (released with the hand-off below), so the hand-off's
+                // drain waits only for T.  Merge also reads the chain's U_{k,i} (i = k + 1).
+                // The v2 and v4 chains publish W_k before U_{k,k+1} (v1 releases both
+                // together), so U_{k,j} is formed above while the chain finishes U_{k,k+1}.
+                __syncthreads();
+                tile_store(Q, A, lda, k, j);
+                pub = true;
                 flag_acquire2(&F.P[k * F.ncb + i], nullptr, F.ep, err);
                 double vu[8];
 #pragma unroll
@@ -2690,10 +2694,6 @@ __global__ __launch_bounds__(512) void k_chol_persistent(double *A, int lda, int
             if (merge) mm_tn<true>(S, Q, acc);
             else mm_tn<true>(Q, Q, acc);
             OWN_TS(3);
-            if (merge) {
-                tile_store(Q, A, lda, k, j);  // U_{k,j}, released with the hand-off below
-                pub = true;
-            }
         }
         if (nupd > 0) {
             MM_FOR(h, r, y, x) {
@@ -2793,9 +2793,10 @@ static int device_cus() {
     return n;
 }
 
-// chain variant of k_chol_persistent (1: the default; 2, 3: the pipelined chains, measured
-// slower -- DESIGN.md §5.2); bb_set_chol_version switches it for A/B measurements
-int g_chol_version = 1;
+// chain variant of k_chol_persistent (4: the default, the 16-column leaf pipeline of
+// bb_chol4.h; 1: the round-2 chain; 2, 3: its pipelined variants, measured slower -- DESIGN.md
+// §5.2); bb_set_chol_version switches it for A/B measurements
+int g_chol_version = 4;
 
 // Workgroups of k_chol_persistent<V> the device can hold at once (occupancy query x CUs),
 // computed once per chain variant.

@@ -140,6 +140,83 @@ __device__ inline double gamma1(double shape, Key key, uint64_t t, unsigned kind
 // ---------------------------------------------------------------------------
 // Tilted positive stable law, Code/C/retstable.cpp.
 // ---------------------------------------------------------------------------
+// The sampler's logarithms and sines, restricted to the arguments it produces, in straight-line
+// code whose constants the compiler keeps in scalar registers or instruction literals (the ocml
+// log and sin carry range reduction and special-case paths the sampler never takes: ~98 and
+// ~80 VALU instructions; these are ~35 and ~20).  BB_SAMPLER_OCML=1 builds the ocml versions
+// (A/B measurement; the draws then differ from these in the last bits only).
+#ifndef BB_SAMPLER_OCML
+#define BB_SAMPLER_OCML 0
+#endif
+
+// log x, x > 0 (also 0 -> -inf, +inf -> +inf, x < 0 or NaN -> NaN).  fdlibm's e_log.c method:
+// x = 2^e (1 + f), 1 + f in [sqrt(1/2), sqrt(2)), s = f / (2 + f),
+// log(1 + f) = f - hfsq + s (hfsq + R(s^2)), hfsq = f^2 / 2, R its degree-14 minimax polynomial
+// (coefficients Lg1..Lg7), e ln 2 in two parts; within 1 ulp (tests/test_sampler_math_cpu.py
+// checks this restatement against a 120-bit reference).
+__device__ __forceinline__ double bb_log(double x) {
+#if BB_SAMPLER_OCML
+    return log(x);
+#else
+    constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                     Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                     Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                     Lg7 = 1.479819860511658591e-01;
+    constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    double m = __builtin_amdgcn_frexp_mant(x) * 2.0;  // [1, 2)
+    int e = __builtin_amdgcn_frexp_exp(x) - 1;
+    if (m > kSqrt2) {
+        m *= 0.5;
+        e += 1;
+    }
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)e;
+    double r = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    if (!(x > 0.0 && x < __builtin_huge_val()))
+        r = x == 0.0 ? -__builtin_huge_val() : (x > 0.0 ? x : __builtin_nan(""));
+    return r;
+#endif
+}
+
+// sin x for x in [0, pi] (the sampler's sinc arguments alpha U, (1 - alpha) U and U, with U in
+// [0, pi) whenever the attempt can be accepted; other arguments return a finite value the
+// rejected attempt discards).  y = x on [0, pi/2], else pi - x in two parts (the difference
+// with the high part is exact, Sterbenz), then the Taylor polynomial of sin to degree 23 in
+// Horner form; within 2 ulp (tests/test_sampler_math_cpu.py).
+__device__ __forceinline__ double bb_sin_0pi(double x) {
+#if BB_SAMPLER_OCML
+    return sin(x);
+#else
+    constexpr double pi_hi = 3.141592653589793116, pi_lo = 1.2246467991473532e-16;
+    constexpr double c3 = -1.6666666666666666e-01, c5 = 8.3333333333333333e-03,
+                     c7 = -1.9841269841269841e-04, c9 = 2.7557319223985893e-06,
+                     c11 = -2.5052108385441720e-08, c13 = 1.6059043836821613e-10,
+                     c15 = -7.6471637318198164e-13, c17 = 2.8114572543455206e-15,
+                     c19 = -8.2206352466243297e-18, c21 = 1.9572941063391263e-20,
+                     c23 = -3.8681701706306835e-23;
+    const double y = x > kPi2 ? (pi_hi - x) + pi_lo : x;
+    const double z = y * y;
+    double p = c23;
+    p = p * z + c21;
+    p = p * z + c19;
+    p = p * z + c17;
+    p = p * z + c15;
+    p = p * z + c13;
+    p = p * z + c11;
+    p = p * z + c9;
+    p = p * z + c7;
+    p = p * z + c5;
+    p = p * z + c3;
+    return y + (y * z) * p;
+#endif
+}
+
 __device__ __forceinline__ double sinc_mm(double x) {  // retstable.cpp:18-29
     double ax = fabs(x);
     if (ax < 0.006) {
@@ -148,7 +225,7 @@ __device__ __forceinline__ double sinc_mm(double x) {  // retstable.cpp:18-29
         if (ax < 2e-4) return 1. - x2 / 6.;
         return 1. - x2 / 6. * (1 - x2 / 20.);
     }
-    return sin(x) / x;
+    return bb_sin_0pi(x) / x;
 }
 
 // x^y for x >= 0 as exp(y log x).  Every pow of retstable.cpp:94-271 has a non-negative
@@ -156,7 +233,7 @@ __device__ __forceinline__ double sinc_mm(double x) {  // retstable.cpp:18-29
 // exp(y log x) reproduces pow's special cases there (0^y, inf^-y, NaN for X < 0) at
 // ~|y log x| * 2^-53 relative error -- far below the GPU/oracle tolerance -- for roughly
 // half the instructions and registers of the correctly rounded ocml pow.
-__device__ __forceinline__ double powp(double x, double y) { return exp(y * log(x)); }
+__device__ __forceinline__ double powp(double x, double y) { return exp(y * bb_log(x)); }
 
 __device__ __forceinline__ double zolotarev_A_p(double x, double alpha, double ia) {
     return powp(ia * sinc_mm(ia * x), ia) * powp(alpha * sinc_mm(alpha * x), alpha) / sinc_mm(x);
@@ -169,8 +246,8 @@ __device__ __forceinline__ double zolotarev_A_p(double x, double alpha, double i
 // = log s exactly (halving and doubling are exact): one sine, one division and one log fewer
 // per inner attempt, the same bits.
 __device__ __forceinline__ double b_over_b0_p(double x, double alpha, double ia) {
-    const double la = log(sinc_mm(alpha * x));
-    const double l = (alpha == ia) ? la : alpha * la + ia * log(sinc_mm(ia * x));
+    const double la = bb_log(sinc_mm(alpha * x));
+    const double l = (alpha == ia) ? la : alpha * la + ia * bb_log(sinc_mm(ia * x));
     return sinc_mm(x) * exp(-l);
 }
 
@@ -287,11 +364,11 @@ __device__ __forceinline__ bool stable_outer_body(const StableParams &s, Key key
     } else {
         if (V_ < (a1 + a2) / ssum) Xc = m + delta * r.r[1];
         else {
-            E_ = -log(r.r[1]);
+            E_ = -bb_log(r.r[1]);
             Xc = m + delta + E_ * a3;
         }
     }
-    double E = -log(Z);
+    double E = -bb_log(Z);
     double c = a * (Xc - m);
     c += (m != 0) ? s.h * (powp(Xc, -1. * s.b) - powp(m, -1. * s.b)) : 0.0;
     if (Xc < m) c -= N_ * N_ / 2.;
@@ -330,7 +407,7 @@ __device__ __forceinline__ bool stable_outer(const StableParams &s, Key key, uin
 #endif
 
 __device__ __forceinline__ double stable_finish(const StableParams &s, double X) {
-    return exp(s.inv_alpha * log(s.V0) - s.b * log(X));  // :270
+    return exp(s.inv_alpha * bb_log(s.V0) - s.b * bb_log(X));  // :270
 }
 
 // Group sampler: the G lanes [gbase, gbase+G) of a wave cooperate on one coefficient by

@@ -69,8 +69,8 @@ bb.set_chol_version(1)
 # v4 (16-column leaf pipeline, bb_chol4.h) per-step stamps, medians over the inner steps (us
 # after the step's leaf-0 start); slot names in bb_chol4.h
 V4_SLOTS = {1: "leaf3 done", 2: "W rel", 3: "S acq", 4: "U rel", 5: "D00 ready", 6: "leaf1 start",
-            7: "leaf2 start", 24: "d0 T3(012)", 25: "d1 T3(022)", 26: "d0 T3(123)",
-            27: "d1 T3(133)", 28: "s0 US0", 29: "s0 US3", 30: "s0 UU", 31: "w4 UU"}
+            7: "leaf2 start", 24: "s3 UU", 25: "s2 UU", 26: "S free",
+            27: "s1 UU", 28: "s0 US0", 29: "s0 US3", 30: "s0 UU", 31: "w4 UU"}
 for t in range(4):
     V4_SLOTS[8 + 4 * t] = f"L{t} piv"
     V4_SLOTS[9 + 4 * t] = f"L{t} W"
