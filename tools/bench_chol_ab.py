@@ -94,4 +94,8 @@ for v in [v for v in VERSIONS if v == 4]:
             if len(d):
                 rel[name] = round(float(np.median(d)), 2)
         print("  " + json.dumps(rel), flush=True)
+        if m == 2048:  # the traced owner hop's step (owner stamps B / D above are for step 6)
+            row = t[6]
+            print("  step 6: " + json.dumps({name: round(float((row[j] - row[0]) * 0.01), 2)
+                                            for j, name in V4_SLOTS.items() if row[j] > 0}), flush=True)
 bb.set_chol_version(1)
