@@ -3689,6 +3689,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_nid_poll = value ? 1 : 0;
             return old;
         }
+        case 16: {  // forced Chebyshev iterate count (benchmarking only; bb_nid.hip)
+            const int old = g_nid_force_k;
+            if (value >= 0) nid_set_force_k(value > 64 ? 64 : value);
+            return old;
+        }
         case 12: {
             const int old = g_rs_xcd;
             if (value >= 0) g_rs_xcd = value ? 1 : 0;

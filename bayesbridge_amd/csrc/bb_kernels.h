@@ -265,6 +265,8 @@ size_t chol_flag_words(int m_pad, int nrhs_blocks);
 size_t chol_wd_words(int m_pad);
 extern int g_bxb_nt;  // non-temporal X loads in k_beta_wb_xb (bb_set_tuning key 2)
 extern int g_rs_xcd;  // XCD-aware row blocks of the partial row sums (key 12)
+extern int g_nid_force_k;  // forced Chebyshev iterate count, 0 = certified (key 16)
+void nid_set_force_k(int k);
 extern int g_lam_occ;  // lambda launches at 4 waves per SIMD (bb_set_tuning key 4)
 extern int g_lam_lanes;  // lanes per coefficient of k_lambda_spec, 0 = default (key 5)
 // k_chol_persistent chain variant: 1 (default) or the pipelined 2 / 3, for A/B

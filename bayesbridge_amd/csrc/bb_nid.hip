@@ -148,6 +148,16 @@ __device__ void nid_plan_mixed(double eps, double tr, int kcap, double cost_fp64
     }
 }
 
+// bb_set_tuning key 16 (benchmarking only): a forced iteration count K > 0 replaces the
+// certified one on the near-identity path (the solve is then no longer certified), so that the
+// per-rank proxy of an N-GPU C3 job runs a C3 rank's product count
+__device__ int g_dev_nid_force_k = 0;
+int g_nid_force_k = 0;
+void nid_set_force_k(int k) {
+    g_nid_force_k = k;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dev_nid_force_k), &k, sizeof(int));
+}
+
 // eps from the least bound, the iteration count K and the sweep's mode: called by the 64
 // lanes of one wave (every lane computes the same values; lane 0 writes them)
 __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launched, int allow,
@@ -162,11 +172,12 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
             best = fmin(best, red[k] + shard_threshold(tau2, k) * lam);
     // rounding of the sums: a relative margin far above its worst case (p u)
     const double eps = best / sc->sig2 * (1.0 + 1e-6);
-    const int K = cheb_iterations(eps, k_launched, kNidTol);
+    int K = cheb_iterations(eps, k_launched, kNidTol);
+    if (g_dev_nid_force_k > 0) K = g_dev_nid_force_k < k_launched ? g_dev_nid_force_k : k_launched;
     int mode = (allow && K > 0) ? K : 0, k2 = 0;
     double ecb = eps, eta = 0.0;
     // a mixed plan costs at least one fp64 pass (k1 = k2 = 1): never below K <= 2's
-    if (allow && allow_mixed && (K == 0 || K > 2)) {
+    if (allow && allow_mixed && g_dev_nid_force_k == 0 && (K == 0 || K > 2)) {
         const double tr = red[kNidTS] / sc->sig2 * (1.0 + 1e-6);
         int k1m, k2m;
         double e2;

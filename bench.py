@@ -861,6 +861,13 @@ def run_chain(args, n, p, alpha, kind, mode):
         if mode == "single" and os.environ.get("BB_FORCE_RCCL", "0") == "1":
             config["proxy"] = ("one rank's share: a 1-rank RCCL communicator with the column-"
                                "shard protocol forced (bb_set_tuning key 9)")
+        if args.tuning:
+            config["tuning"] = list(args.tuning)
+            if any(kv.split("=")[0] == "16" and kv.split("=")[1] != "0" for kv in args.tuning):
+                config["forced_iterates"] = ("bb_set_tuning key 16: the near-identity solve runs "
+                                             "this many Chebyshev iterates every sweep instead "
+                                             "of its certified count (a timing proxy, not a "
+                                             "certified chain)")
         if sparse:
             si = eng.sparse_info()
             config.update(density=SPARSE_DENSITY, nnz_local=si["nnz"], pairs_local=si["pairs"],

@@ -366,7 +366,10 @@ void bb_set_trace_budget(long long bytes);
  * (0);
  * key 15: the continuous-batching lambda launch with its sampler inlined lends the lanes of a
  * wave's idle groups to its unfinished draws once its range is used up (1, the default) or
- * lets every group finish its own draw (0); under keys 11-15 the draws are the same.
+ * lets every group finish its own draw (0); under keys 11-15 the draws are the same;
+ * key 16 (benchmarking only): K > 0 makes every near-identity sweep run K Chebyshev iterates
+ * (at most key 6's cap) instead of its certified count, for timing a C3 rank's product count
+ * on a narrower proxy; the solve is then not certified (default 0, the current device only).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
