@@ -814,7 +814,7 @@ struct bb_engine {
             if (method == 2 && (sync ? nid_last != 0 : kl > 0))
                 xu_fused = launch_lambda_xu(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc,
                                             cfg.seed, cfg.stream, t, lam, D, u, trl, err, X,
-                                            n_pad, n_pad, nid_xu);
+                                            n_pad, n_pad, nid_xu, lam_sync, ++lam_ep);
             if (!xu_fused)
                 launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed,
                               cfg.stream, t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
@@ -969,6 +969,8 @@ struct bb_engine {
     int fail_at = -1;
     int nid_kl = 0;  // Chebyshev iterations launched for the sweep being enqueued
     int xu_fused = 0;  // X u partials formed by this sweep's lambda launch (k_lambda_xu), or 0
+    unsigned int *lam_sync = nullptr;  // the split lambda launch's chunk flags and counter
+    unsigned int lam_ep = 0;           // its launch epoch (flags are never cleared)
     unsigned long long n_lambda_xu = 0, n_lambda_alone = 0;  // Woodbury lambda launches by kind
 
     // `count` sweeps from t0 into slots first_slot + k slot_step (mod cap)
@@ -1362,6 +1364,9 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
                 e->ea_part = dalloc<double>((size_t)e->ea_parts * n_pad, o);
                 const int xp = std::max(e->ea_parts, lambda_xu_parts(c.p_local, p_pad, n_pad));
                 e->nid_xu = dalloc<double>((size_t)xp * n_pad, o);
+                const int sw = lambda_xs_sync_words(p_pad);
+                e->lam_sync = dalloc<unsigned int>(sw, o);
+                HIPCHECK(hipMemsetAsync(e->lam_sync, 0, sizeof(unsigned int) * sw, e->stream));
             }
             e->nid = dalloc<NidState>(1, o);
             {
@@ -3666,7 +3671,7 @@ int bb_set_tuning(int key, int value) {
         }
         case 7: {
             const int old = g_lam_xu;
-            if (value >= 0) g_lam_xu = value > 2 ? 2 : value;
+            if (value >= 0) g_lam_xu = value > 3 ? 3 : value;
             return old;
         }
         case 8: {

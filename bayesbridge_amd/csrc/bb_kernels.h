@@ -185,7 +185,10 @@ int lambda_xu_parts(int p_loc, int p_pad, int n_pad);
 int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
-                     int ldx, int n_pad, double *xu_part);
+                     int ldx, int n_pad, double *xu_part, unsigned int *sync = nullptr,
+                     unsigned int ep = 0);
+// words of the split launch's (key 7 mode 3) synchronisation buffer, zeroed before first use
+int lambda_xs_sync_words(int p_pad);
 extern int g_lam_xu;
 extern int g_lam_wave;  // wave-adaptive draw in the fused lambda + X u launch (key 13)
 extern int g_lam_lend;  // the continuous-batching launch lends its tail lanes (key 15)

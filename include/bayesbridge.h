@@ -342,7 +342,9 @@ void bb_set_trace_budget(long long bytes);
  * (default 16; 0 = every sweep forms the Gram and factors it);
  * key 7: a dense Woodbury sweep that may take the near-identity path draws lambda and forms
  * the X u partials in one launch (1: up to 3 workgroups per CU looping over column chunks;
- * 2: one workgroup per chunk, the default) or in two (0); the draws are the same;
+ * 2: one workgroup per chunk, drawing then streaming; 3, the default: two drawing and one
+ * streaming workgroup per CU, the stream following per-chunk flags) or in two (0); the draws
+ * are the same;
  * key 8: an unsharded Woodbury engine decides each sweep's path as a column shard does (the
  * host waits for the decision, then launches that path only: 1, the default, with the
  * Chebyshev solve's first kernels enqueued before the wait and returning at once unless the

@@ -215,9 +215,10 @@ def test_nid_shard_certifies_its_columns(gpu_lib):
 
 @pytest.mark.parametrize("n,p", [(200, 2400), (700, 6000), (2000, 50000)])
 def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
-    """The fused lambda + X u launch (k_lambda_xu, bb_set_tuning key 7 = 1, the default, and
-    7 = 2, one workgroup per chunk) against separate lambda and X u launches (key 7 = 0) on
-    near-null states: the same
+    """The fused lambda + X u launch (k_lambda_xu, bb_set_tuning key 7 = 1, 7 = 2, one
+    workgroup per chunk, and 7 = 3, the default: drawing and streaming workgroups of one grid,
+    k_lambda_xs) against separate lambda and X u launches (key 7 = 0) on near-null states: the
+    same
     lambda bits (the same draws), beta to rounding (X u summed in another order), both on
     the Chebyshev path.  (2000, 50000) is C3's shape."""
     import bench
@@ -230,7 +231,7 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
     rng = np.random.default_rng(11)
     beta = 1e-6 * rng.standard_normal(p)
     out = []
-    for fused in (1, 2, 0):
+    for fused in (1, 2, 3, 0):
         old = bb.set_tuning(7, fused)
         try:
             e = _engine(bb, X, y, n, p)
@@ -245,7 +246,8 @@ def test_lambda_xu_fused_equals_separate(gpu_lib, n, p):
             bb.set_tuning(7, old)
     b, sb = out[-1]
     assert sb["cheb_sweeps"] == 2, sb
-    for a, sa in out[:-1]:  # modes 1 (loop over chunks) and 2 (one chunk each)
+    assert np.array_equal(out[1][0]["lambda"], out[2][0]["lambda"])  # modes 2 and 3: same draws
+    for a, sa in out[:-1]:  # modes 1 (loop over chunks), 2 (one chunk each), 3 (split roles)
         assert sa["cheb_sweeps"] == 2, (sa, sb)
         assert rel_err(a["beta"], b["beta"]) < 1e-12
         assert np.max(np.abs(a["lambda"] - b["lambda"]) / b["lambda"]) < 1e-12
