@@ -294,6 +294,11 @@ int g_nid_mixed = 1;
 // (0).  The event's marker left the device idle ~4 us per sweep: C3 at the driver's settings
 // 2010 against 1995 sweeps/s, 1000 sweeps after 100 1370 against 1367 (gpurun_out/ab_*).
 int g_nid_poll = 1;
+// bb_set_tuning key 17: under the synchronous protocol the split lambda launch (key 7 = 3)
+// forms the decision's bound sums in its stream role, k_nid_reduce adds them and decides
+// (1, the default); 2: unsharded, the launch's last stream workgroup reduces and decides too;
+// 0: k_nid_sums + k_nid_reduce after the launch
+int g_nid_fold = 1;
 static const char *kPhaseNames[PH_COUNT] = {"pre", "scalars", "lambda", "pg", "ozprep", "gram",
                                             "xu", "reduce", "form", "chol", "solve", "beta",
                                             "xb", "alpha", "nid", "eapply", "end"};
@@ -553,9 +558,18 @@ struct bb_engine {
     static constexpr int kNidRed = kNidTS + 2;
     // this shard's bound sums into nid_red (exchanged: kNidRed doubles); an unsharded engine
     // decides in the same launch (its sums need no exchange)
-    void nidx_partials() {
+    // folded: the split lambda launch formed the sums (1: its nstream partials in nid_wg, reduced
+    // here; 2: reduced and decided as well)
+    void nidx_partials(int folded = 0, int nstream = 0) {
         mark(PH_NID);
-        if (sharded())
+        if (folded == 2) return;
+        if (folded == 1 && sharded())
+            launch_nid_reduce(stream, nid_wg, nstream, sc, nid, nid_red);
+        else if (folded == 1)
+            launch_nid_reduce(stream, nid_wg, nstream, sc, nid, nid_red,
+                              std::min(g_nid_kmax, nid_kmax), eps_dev + kNidRing,
+                              mixed_ok() ? 1 : 0, ++nid_dseq);
+        else if (sharded())
             launch_nid_sums(stream, D, cn, p_loc, sc, nid, 0, 0, 0, nid_wg, nid_red, nullptr);
         else
             launch_nid_sums_decide(stream, D, cn, p_loc, sc, nid, std::min(g_nid_kmax, nid_kmax),
@@ -811,10 +825,29 @@ struct bb_engine {
             // residue pass forms it; a sweep that turns back to the Chebyshev path streams X u
             // in its own pass)
             xu_fused = 0;
-            if (method == 2 && (sync ? nid_last != 0 : kl > 0))
+            int folded = 0;
+            if (method == 2 && (sync ? nid_last != 0 : kl > 0)) {
+                // under the synchronous protocol the split launch also forms the bound sums
+                // (and, unsharded, decides): k_nid_sums / k_nid_reduce are not launched
+                NidFold fold;
+                if (sync && g_nid_fold) {
+                    fold.cn = cn;
+                    fold.wg_part = nid_wg;
+                    fold.cnt = lam_sync + lambda_xs_sync_words(p_pad);
+                    fold.decide = (!sharded() && g_nid_fold == 2) ? 1 : 0;
+                    fold.k_launched = std::min(g_nid_kmax, nid_kmax);
+                    fold.allow_mixed = mixed_ok() ? 1 : 0;
+                    fold.nid = nid;
+                    fold.red = nid_red;
+                    fold.host2 = eps_dev + kNidRing;
+                    fold.tag_seq = nid_dseq + 1;
+                }
                 xu_fused = launch_lambda_xu(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc,
                                             cfg.seed, cfg.stream, t, lam, D, u, trl, err, X,
-                                            n_pad, n_pad, nid_xu, lam_sync, ++lam_ep);
+                                            n_pad, n_pad, nid_xu, lam_sync, ++lam_ep, &fold,
+                                            &folded);
+                if (folded == 2) ++nid_dseq;
+            }
             if (!xu_fused)
                 launch_lambda(stream, beta, p_loc, p_pad, (uint64_t)cfg.j0, sc, cfg.seed,
                               cfg.stream, t, LAMBDA_WOODBURY, group, lam, D, u, trl, err);
@@ -823,7 +856,7 @@ struct bb_engine {
             if (sync) {
                 // a shard: the bound sums now, the path after their exchange (shard_solve)
                 nid_kl = 0;
-                nidx_partials();
+                nidx_partials(folded, xu_fused);
                 return;
             }
             nid_kl = nid_begin(kl);
@@ -1364,7 +1397,8 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
                 e->ea_part = dalloc<double>((size_t)e->ea_parts * n_pad, o);
                 const int xp = std::max(e->ea_parts, lambda_xu_parts(c.p_local, p_pad, n_pad));
                 e->nid_xu = dalloc<double>((size_t)xp * n_pad, o);
-                const int sw = lambda_xs_sync_words(p_pad);
+                // + the folded decision's count (the last word)
+                const int sw = lambda_xs_sync_words(p_pad) + 1;
                 e->lam_sync = dalloc<unsigned int>(sw, o);
                 HIPCHECK(hipMemsetAsync(e->lam_sync, 0, sizeof(unsigned int) * sw, e->stream));
             }
@@ -1381,7 +1415,9 @@ void engine_setup(bb_engine *e, const double *Xh, const double *yh, const Sparse
             e->ch_r = dalloc<double>(n_pad, o);
             e->ch_d = dalloc<double>(n_pad, o);
             e->nid_red = dalloc<double>(bb_engine::kNidRed, o);
-            e->nid_wg = dalloc<double>((size_t)nid_sum_groups(c.p_local) * (kNidTS + 1), o);
+            // k_nid_sums' partials, or the split lambda launch's (one per stream workgroup)
+            e->nid_wg = dalloc<double>(
+                (size_t)std::max(nid_sum_groups(c.p_local), 1024) * (kNidTS + 1), o);
             e->nid_sum = dalloc<double>(n_pad, o);
             // the hint ring, then [eps, mode, k2, tag] of the sweep being decided (coherent:
             // the host polls the tag while the device runs on)
@@ -3707,6 +3743,11 @@ int bb_set_tuning(int key, int value) {
         case 13: {
             const int old = g_lam_wave;
             if (value >= 0) g_lam_wave = value ? 1 : 0;
+            return old;
+        }
+        case 17: {
+            const int old = g_nid_fold;
+            if (value >= 0) g_nid_fold = value > 2 ? 2 : value;
             return old;
         }
         case 15: {

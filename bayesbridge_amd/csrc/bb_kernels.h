@@ -117,6 +117,23 @@ void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, in
                             const DevScalars *sc, NidState *nid, int k_launched,
                             double *wg_part, double *red, double *host2, int allow_mixed = 0,
                             unsigned long long tag_seq = 0);
+// the reduction of G partials the split lambda launch wrote (a shard: alone; host2 given:
+// and the unsharded decision, as launch_nid_sums_decide)
+void launch_nid_reduce(hipStream_t s, const double *wg_part, int G, const DevScalars *sc,
+                       NidState *nid, double *red, int k_launched = 0, double *host2 = nullptr,
+                       int allow_mixed = 0, unsigned long long tag_seq = 0);
+// The bound sums folded into the split lambda launch's stream role (wg_part: one kNidTS + 1
+// partial per stream workgroup); decide: the last stream workgroup (cnt, zeroed, re-armed by
+// it) reduces them into red and makes the unsharded decision (launch_nid_sums_decide's)
+struct NidFold {
+    const double *cn = nullptr;
+    double *wg_part = nullptr;
+    unsigned int *cnt = nullptr;
+    int decide = 0, k_launched = 0, allow_mixed = 0;
+    NidState *nid = nullptr;
+    double *red = nullptr, *host2 = nullptr;
+    unsigned long long tag_seq = 0;
+};
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
                             int k_launched, NidState *nid, double *host2,
                             unsigned long long tag_seq = 0);
@@ -186,7 +203,15 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
                      int ldx, int n_pad, double *xu_part, unsigned int *sync = nullptr,
-                     unsigned int ep = 0);
+                     unsigned int ep = 0, const NidFold *fold = nullptr, int *folded = nullptr);
+// the split launch (key 7 = 3; bb_nid.hip): ndraw drawing and nstream streaming workgroups;
+// returns 0, or 1 / 2 when the bound sums were folded in (2: and the unsharded decision made)
+int launch_lambda_xs(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                     const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
+                     double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
+                     int ldx, int n_pad, int nchunk, double *xu_part, unsigned int *sync,
+                     unsigned int ep, int ndraw, int nstream, const NidFold *fold);
+int lambda_xs_resident(int nr);  // k_lambda_xs workgroups resident per CU
 // words of the split launch's (key 7 mode 3) synchronisation buffer, zeroed before first use
 int lambda_xs_sync_words(int p_pad);
 extern int g_lam_xu;

@@ -596,137 +596,6 @@ k_lambda_xw(BB_LXU_ARGS) {
                                 ldx, n_pad, nchunk, xu_part);
 }
 
-// Mode 3: the draws and the X u stream as two roles of one grid.  Workgroups [0, ndraw) draw:
-// each claims 32-coefficient chunks from a counter (any resident draw workgroup takes the next
-// chunk, so the draws never wait on a workgroup that is not resident), draws them exactly as
-// k_lambda_xw does, and releases the chunk's u with a flag (write-through stores, drained,
-// then the flag, tagged with the launch's epoch: flags are never cleared).  Workgroups
-// [ndraw, grid) stream X: unit q = (chunk q / 4, its 8-column quarter q % 4) for q = s, s + S,
-// ... -- a fixed assignment, so each stream workgroup's partial n-vector (rows t + 256 m in
-// thread t's registers) sums the same columns in the same order every launch (bitwise
-// reproducible) -- waiting for a chunk's flag before its first unit.  With two draw and one
-// stream workgroup per CU the stream's loads run beside the draws' VALU work instead of
-// alternating with it inside each workgroup (mode 2).  Partials: S = the stream workgroups.
-template <int NR>
-__device__ __forceinline__ void lambda_xs_body(const double *beta, int p_loc, int p_pad,
-                                               uint64_t j0, const DevScalars *sc, Key key,
-                                               uint64_t t, double *lam, double *D, double *u,
-                                               double *lam_trace, uint32_t *err,
-                                               const double *__restrict__ X, int ldx, int n_pad,
-                                               int nchunk, double *__restrict__ xu_part,
-                                               unsigned int *sync, unsigned int ep, int ndraw) {
-    constexpr int C = 32;
-    const int tid = threadIdx.x;
-    unsigned int *ctr = sync + nchunk;
-    if ((int)blockIdx.x < ndraw) {
-        __shared__ int claim;
-        const double tau = sc->tau;
-        for (;;) {
-            if (tid == 0)
-                claim = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            const int ch = claim;
-            __syncthreads();  // claim is rewritten by the next round
-            if (ch >= nchunk) {
-                // the last of the nchunk + ndraw claims re-arms the counter for the next launch
-                if (tid == 0 && ch == nchunk + ndraw - 1)
-                    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return;
-            }
-            const int i = ch * C + tid / 8;
-            const bool active = i < p_loc;
-            const double b = active ? beta[i] : 0.0;
-            const double x = stable_wave_draw(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
-                                              key, t, j0 + (uint64_t)i, err);
-            if ((tid % 8) == 0) {
-                double uv = 0.0;
-                if (active) {
-                    const double l = 2 * x;
-                    lam[i] = l;
-                    if (lam_trace) lam_trace[i] = l;
-                    const double d = (tau * tau) / l;
-                    D[i] = d;
-                    uv = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
-                } else if (i < p_pad) {
-                    lam[i] = 1.0;
-                    D[i] = 0.0;
-                }
-                if (i < p_pad)
-                    __hip_atomic_store(&u[i], uv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(&sync[ch], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    // ---- stream role ----
-    const int sidx = (int)blockIdx.x - ndraw, S = (int)gridDim.x - ndraw;
-    __shared__ double us[8];
-    double a[NR];
-#pragma unroll
-    for (int m = 0; m < NR; ++m) a[m] = 0.0;
-    const int nunit = nchunk * 4;
-    int have = -1;  // the chunk whose flag this workgroup has seen
-    for (int q = sidx; q < nunit; q += S) {
-        const int ch = q >> 2, c0 = ch * C + (q & 3) * 8;
-        if (ch != have) {
-            if (tid == 0) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(&sync[ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                       ep) {
-                    __builtin_amdgcn_s_sleep(2);
-                    // bounded like every cross-workgroup wait (2 s): a launch that cannot make
-                    // progress ends with error bit 16 instead of hanging the device
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
-                        atomicOr(err, 16u);
-                        break;
-                    }
-                }
-            }
-            have = ch;
-        }
-        __syncthreads();  // the flag is seen; us of the previous unit is no longer read
-        if (tid < 8)
-            us[tid] = c0 + tid < p_pad ? __hip_atomic_load(&u[c0 + tid], __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0.0;
-        __syncthreads();
-        constexpr int CB = NR >= 16 ? 2 : 4;  // columns in flight (8 measured no faster)
-#pragma unroll
-        for (int cb = 0; cb < 8; cb += CB) {
-            double xv[CB][NR];
-#pragma unroll
-            for (int k = 0; k < CB; ++k) {
-                const int col = c0 + cb + k;
-                const bool ok = col < p_loc;
-                const double *xc = X + (size_t)col * ldx;
-#pragma unroll
-                for (int m = 0; m < NR; ++m) {
-                    const int row = tid + 256 * m;
-                    xv[k][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(xc + row) : 0.0;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < CB; ++k) {
-                const double f = us[cb + k];
-#pragma unroll
-                for (int m = 0; m < NR; ++m) a[m] = __builtin_fma(xv[k][m], f, a[m]);
-            }
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < NR; ++m) {
-        const int row = tid + 256 * m;
-        if (row < n_pad) xu_part[(size_t)sidx * n_pad + row] = a[m];
-    }
-}
-template <int NR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void
-k_lambda_xs(BB_LXU_ARGS, unsigned int *sync, unsigned int ep, int ndraw) {
-    lambda_xs_body<NR>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad,
-                       nchunk, xu_part, sync, ep, ndraw);
-}
 #undef BB_LXU_ARGS
 
 // (mode 1: G = min(chunks, 3 per CU), each workgroup loops over its chunks; mode 2: one
@@ -743,34 +612,17 @@ static int lambda_xu_groups(int p_loc, int p_pad, int n_pad, int mode) {
 int lambda_xu_parts(int p_loc, int p_pad, int n_pad) {
     return lambda_xu_groups(p_loc, p_pad, n_pad, 2);  // the most any mode writes
 }
-// words of the split launch's synchronisation buffer (mode 3): a flag per chunk + the counter
-int lambda_xs_sync_words(int p_pad) { return (p_pad + 31) / 32 + 1; }
-
-// the split launch needs its whole grid resident (three workgroups per CU)
-static int lambda_xs_resident(int nr) {
-    static int cache[3] = {-1, -1, -1};
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    const int idx = nr <= 4 ? 0 : nr <= 8 ? 1 : 2;
-    int &c = cache[idx];
-    if (c < 0) {
-        int nb = 0;
-        const hipError_t e = idx == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<4>, 256, 0)
-                           : idx == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<8>, 256, 0)
-                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<16>, 256, 0);
-        c = e == hipSuccess ? nb : 0;
-    }
-    return c;
-}
 
 int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
                      const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
                      double *D, double *u, double *lam_trace, uint32_t *err, const double *X,
-                     int ldx, int n_pad, double *xu_part, unsigned int *sync, unsigned int ep) {
+                     int ldx, int n_pad, double *xu_part, unsigned int *sync, unsigned int ep,
+                     const NidFold *fold, int *folded) {
     const int nr = (n_pad + 255) / 256;
     int mode = g_lam_xu;
     if (mode == 3 && (!sync || !g_lam_wave || (g_lam_occ & 1) || lambda_xs_resident(nr) < 3))
         mode = 2;
+    if (folded) *folded = 0;
     const int G = g_lam_lanes ? 0 : lambda_xu_groups(p_loc, p_pad, n_pad, mode);
     if (!G) {
         if (mode == 3) mode = 2;
@@ -781,11 +633,10 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     const int nchunk = (p_pad + 256 / L - 1) / (256 / L);
     const bool o4 = (g_lam_occ & 1) != 0;
     if (mode == 3 && G) {
-        const int ndraw = 2 * G;
-        auto *kk = nr <= 4 ? k_lambda_xs<4> : nr <= 8 ? k_lambda_xs<8> : k_lambda_xs<16>;
-        note_launch(KF_LAMBDA, (const void *)kk);
-        kk<<<ndraw + G, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err,
-                                     X, ldx, n_pad, nchunk, xu_part, sync, ep, ndraw);
+        const int f = launch_lambda_xs(s, beta, p_loc, p_pad, j0, sc, k0, k1, t, lam, D, u,
+                                       lam_trace, err, X, ldx, n_pad, nchunk, xu_part, sync, ep,
+                                       2 * G, G, fold);
+        if (folded) *folded = f;
         return G;
     }
     if (!G) return 0;

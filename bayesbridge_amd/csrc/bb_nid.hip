@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 
 #include "bb_kernels.h"
 #include "bb_sampler.h"
@@ -158,6 +159,19 @@ void nid_set_force_k(int k) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dev_nid_force_k), &k, sizeof(int));
 }
 
+// The bound and the trace are rounded UP to 12 significant bits (still bounds): the sums are
+// added in another order by the split lambda launch (by column units) than by k_nid_sums (by
+// strided threads), and the rounding makes the decision -- K, the Chebyshev interval, the mixed
+// plan -- the same bits either way unless the two sums straddle a grid point (relative gap
+// 2^-12 against a rounding difference ~1e-15: ~1e-12 of sweeps)
+__device__ __forceinline__ double round_up_12(double x) {
+    if (!(x > 0.0 && x < HUGE_VAL)) return x;
+    constexpr unsigned long long m = (1ull << 40) - 1;
+    unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    if (b & m) b = (b | m) + 1;
+    return __longlong_as_double((long long)b);
+}
+
 // eps from the least bound, the iteration count K and the sweep's mode: called by the 64
 // lanes of one wave (every lane computes the same values; lane 0 writes them)
 __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launched, int allow,
@@ -171,14 +185,14 @@ __device__ void nid_finish(const double *red, const DevScalars *sc, int k_launch
         for (int k = 0; k < kNidTS; ++k)
             best = fmin(best, red[k] + shard_threshold(tau2, k) * lam);
     // rounding of the sums: a relative margin far above its worst case (p u)
-    const double eps = best / sc->sig2 * (1.0 + 1e-6);
+    const double eps = round_up_12(best / sc->sig2 * (1.0 + 1e-6));
     int K = cheb_iterations(eps, k_launched, kNidTol);
     if (g_dev_nid_force_k > 0) K = g_dev_nid_force_k < k_launched ? g_dev_nid_force_k : k_launched;
     int mode = (allow && K > 0) ? K : 0, k2 = 0;
     double ecb = eps, eta = 0.0;
     // a mixed plan costs at least one fp64 pass (k1 = k2 = 1): never below K <= 2's
     if (allow && allow_mixed && g_dev_nid_force_k == 0 && (K == 0 || K > 2)) {
-        const double tr = red[kNidTS] / sc->sig2 * (1.0 + 1e-6);
+        const double tr = round_up_12(red[kNidTS] / sc->sig2 * (1.0 + 1e-6));
         int k1m, k2m;
         double e2;
         nid_plan_mixed(eps, tr, k_launched, K > 0 ? (K - 1) * (nid->c64 + nid->cstep) : HUGE_VAL,
@@ -259,23 +273,28 @@ __global__ __launch_bounds__(kNidSumWG) void k_nid_sums(const double *__restrict
 // red = the G workgroups' sums and Lambda (thread (k, q) adds workgroups q, q + 8, ... of
 // sum k, then the eight in order: a fixed order); decide: the unsharded decision at once
 constexpr int kNidRedQ = 8;
-__global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict__ wg_part, int G,
-                                                       const DevScalars *sc, int k_launched,
-                                                       int allow, int decide, NidState *nid,
-                                                       double *__restrict__ red,
-                                                       double *eps_host, int allow_mixed,
-                                                       unsigned long long tag_seq) {
+template <bool WT>
+__device__ __forceinline__ void nid_reduce_body(const double *__restrict__ wg_part, int G,
+                                                const DevScalars *sc, int k_launched, int allow,
+                                                int decide, NidState *nid,
+                                                double *__restrict__ red, double *eps_host,
+                                                int allow_mixed, unsigned long long tag_seq) {
     __shared__ double pq[kNidRedQ][kNidTS + 1];
     __shared__ double r[kNidTS + 2];
+    // WT: partials written through by other workgroups of the running launch
+    auto ld = [&](size_t i) {
+        return WT ? __hip_atomic_load(&wg_part[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : wg_part[i];
+    };
     const int t = threadIdx.x;
-    if (t < kNidRedQ * (kNidTS + 1)) {
-        const int k = t % (kNidTS + 1), q = t / (kNidTS + 1);
+    for (int tt = t; tt < kNidRedQ * (kNidTS + 1); tt += blockDim.x) {
+        const int k = tt % (kNidTS + 1), q = tt / (kNidTS + 1);
         double a[4] = {0.0, 0.0, 0.0, 0.0};
         int b = q;
         for (; b + 3 * kNidRedQ < G; b += 4 * kNidRedQ)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] += wg_part[(size_t)(b + u * kNidRedQ) * (kNidTS + 1) + k];
-        for (; b < G; b += kNidRedQ) a[0] += wg_part[(size_t)b * (kNidTS + 1) + k];
+            for (int u = 0; u < 4; ++u) a[u] += ld((size_t)(b + u * kNidRedQ) * (kNidTS + 1) + k);
+        for (; b < G; b += kNidRedQ) a[0] += ld((size_t)b * (kNidTS + 1) + k);
         pq[q][k] = (a[0] + a[1]) + (a[2] + a[3]);
     }
     __syncthreads();
@@ -298,6 +317,15 @@ __global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict_
         nid_finish(r, sc, k_launched, allow, nid, eps_host, decide == 2 ? eps_host + 1 : nullptr,
                    decide == 2 ? allow_mixed : 0, decide == 2 ? eps_host + 2 : nullptr,
                    decide == 2 ? tag_seq : 0ull);
+}
+__global__ __launch_bounds__(64 * 5) void k_nid_reduce(const double *__restrict__ wg_part, int G,
+                                                       const DevScalars *sc, int k_launched,
+                                                       int allow, int decide, NidState *nid,
+                                                       double *__restrict__ red,
+                                                       double *eps_host, int allow_mixed,
+                                                       unsigned long long tag_seq) {
+    nid_reduce_body<false>(wg_part, G, sc, k_launched, allow, decide, nid, red, eps_host,
+                           allow_mixed, tag_seq);
 }
 
 __global__ __launch_bounds__(64) void k_nid_decide_from(const double *__restrict__ red,
@@ -711,6 +739,16 @@ void launch_nid_sums_decide(hipStream_t s, const double *D, const double *cn, in
                                       allow_mixed, tag_seq);
 }
 
+void launch_nid_reduce(hipStream_t s, const double *wg_part, int G, const DevScalars *sc,
+                       NidState *nid, double *red, int k_launched, double *host2,
+                       int allow_mixed, unsigned long long tag_seq) {
+    if (host2)
+        k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, k_launched, 1, 2, nid, red, host2,
+                                          allow_mixed, tag_seq);
+    else
+        k_nid_reduce<<<1, 64 * 5, 0, s>>>(wg_part, G, sc, 0, 0, 0, nid, red, nullptr, 0, 0ull);
+}
+
 void launch_nid_decide_from(hipStream_t s, const double *red, const DevScalars *sc,
                             int k_launched, NidState *nid, double *host2,
                             unsigned long long tag_seq) {
@@ -813,6 +851,237 @@ void launch_sp_nid_xu(hipStream_t s, const int *rowptr, const int *colidx, const
                       int n_pad, const double *u, const NidState *nid, double *out) {
     k_sp_eapply_rows<<<(n_pad + 3) / 4, 256, 0, s>>>(rowptr, colidx, rval, n_pad, u, nid, 0, 1,
                                                      out);
+}
+
+// ---------------------------------------------------------------------------------------
+// The split lambda + X u launch (bb_set_tuning key 7 = 3, the default) with the decision's
+// bound sums folded into its stream role (they need D, which the launch writes)
+// ---------------------------------------------------------------------------------------
+// Mode 3: the draws and the X u stream as two roles of one grid.  Workgroups [0, ndraw) draw:
+// each claims 32-coefficient chunks from a counter (any resident draw workgroup takes the next
+// chunk, so the draws never wait on a workgroup that is not resident), draws them exactly as
+// k_lambda_xw does, and releases the chunk's u with a flag (write-through stores, drained,
+// then the flag, tagged with the launch's epoch: flags are never cleared).  Workgroups
+// [ndraw, grid) stream X: unit q = (chunk q / 4, its 8-column quarter q % 4) for q = s, s + S,
+// ... -- a fixed assignment, so each stream workgroup's partial n-vector (rows t + 256 m in
+// thread t's registers) sums the same columns in the same order every launch (bitwise
+// reproducible) -- waiting for a chunk's flag before its first unit.  With two draw and one
+// stream workgroup per CU the stream's loads run beside the draws' VALU work instead of
+// alternating with it inside each workgroup (mode 2).  Partials: S = the stream workgroups.
+// out of line: the decision's code stays out of the draw role's register allocation
+// (scalar arguments: a struct passed by reference would be copied to scratch memory)
+__device__ __noinline__ void nid_fold_decide(const double *wg_part, int S, const DevScalars *sc,
+                                             int k_launched, int allow_mixed, NidState *nid,
+                                             double *red, double *host2,
+                                             unsigned long long tag_seq) {
+    nid_reduce_body<true>(wg_part, S, sc, k_launched, 1, 2, nid, red, host2, allow_mixed,
+                          tag_seq);
+}
+
+template <int NR>
+__device__ __forceinline__ void lambda_xs_body(const double *beta, int p_loc, int p_pad,
+                                               uint64_t j0, const DevScalars *sc, Key key,
+                                               uint64_t t, double *lam, double *D, double *u,
+                                               double *lam_trace, uint32_t *err,
+                                               const double *__restrict__ X, int ldx, int n_pad,
+                                               int nchunk, double *__restrict__ xu_part,
+                                               unsigned int *sync, unsigned int ep, int ndraw,
+                                               NidFold fold) {
+    constexpr int C = 32;
+    const int tid = threadIdx.x;
+    unsigned int *ctr = sync + nchunk;
+    if ((int)blockIdx.x < ndraw) {
+        __shared__ int claim;
+        const double tau = sc->tau;
+        for (;;) {
+            if (tid == 0)
+                claim = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const int ch = claim;
+            __syncthreads();  // claim is rewritten by the next round
+            if (ch >= nchunk) {
+                // the last of the nchunk + ndraw claims re-arms the counter for the next launch
+                if (tid == 0 && ch == nchunk + ndraw - 1)
+                    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            const int i = ch * C + tid / 8;
+            const bool active = i < p_loc;
+            const double b = active ? beta[i] : 0.0;
+            const double x = stable_wave_draw(active, b * b / (tau * tau), 0.5 * sc->alpha, 1.0,
+                                              key, t, j0 + (uint64_t)i, err);
+            if ((tid % 8) == 0) {
+                double uv = 0.0;
+                if (active) {
+                    const double l = 2 * x;
+                    lam[i] = l;
+                    if (lam_trace) lam_trace[i] = l;
+                    const double d = (tau * tau) / l;
+                    __hip_atomic_store(&D[i], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    uv = sqrt(d) * normal_at(key, t, KIND_BETA_Z, j0 + (uint64_t)i);
+                } else if (i < p_pad) {
+                    lam[i] = 1.0;
+                    __hip_atomic_store(&D[i], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (i < p_pad)
+                    __hip_atomic_store(&u[i], uv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(&sync[ch], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // ---- stream role ----
+    const int sidx = (int)blockIdx.x - ndraw, S = (int)gridDim.x - ndraw;
+    __shared__ double us[8];
+    // the fold: the near-identity bound sums of this workgroup's columns (k_nid_sums' kNidTS + 1
+    // per column, D_j |x_j|^2 over D_j > T_k and the trace).  Thread (column slot tid / 32,
+    // threshold tid % 32) accumulates its slot's terms over the units in order -- a fixed order,
+    // so the partials are reproducible -- and slot threads k == 0 the trace.
+    const bool sums = fold.wg_part != nullptr;
+    const double nthr = sums ? shard_threshold(sc->tau * sc->tau, tid & 31) : 0.0;
+    double nacc = 0.0, ntr = 0.0;
+    double a[NR];
+#pragma unroll
+    for (int m = 0; m < NR; ++m) a[m] = 0.0;
+    const int nunit = nchunk * 4;
+    int have = -1;  // the chunk whose flag this workgroup has seen
+    for (int q = sidx; q < nunit; q += S) {
+        const int ch = q >> 2, c0 = ch * C + (q & 3) * 8;
+        if (ch != have) {
+            if (tid == 0) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(&sync[ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       ep) {
+                    __builtin_amdgcn_s_sleep(2);
+                    // bounded like every cross-workgroup wait (2 s): a launch that cannot make
+                    // progress ends with error bit 16 instead of hanging the device
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+                        atomicOr(err, 16u);
+                        break;
+                    }
+                }
+            }
+            have = ch;
+        }
+        __syncthreads();  // the flag is seen; us of the previous unit is no longer read
+        double ndv = 0.0, ncv = 0.0;
+        if (sums && c0 + (tid >> 5) < p_loc) {
+            ndv = __hip_atomic_load(&D[c0 + (tid >> 5)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ncv = fold.cn[c0 + (tid >> 5)];
+        }
+        if (tid < 8)
+            us[tid] = c0 + tid < p_pad ? __hip_atomic_load(&u[c0 + tid], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0.0;
+        __syncthreads();
+        if (sums) {
+            const double v = ndv * ncv;
+            if (ndv > nthr) nacc += v;
+            ntr += v;
+        }
+        constexpr int CB = NR >= 16 ? 2 : 4;  // columns in flight (8 measured no faster)
+#pragma unroll
+        for (int cb = 0; cb < 8; cb += CB) {
+            double xv[CB][NR];
+#pragma unroll
+            for (int k = 0; k < CB; ++k) {
+                const int col = c0 + cb + k;
+                const bool ok = col < p_loc;
+                const double *xc = X + (size_t)col * ldx;
+#pragma unroll
+                for (int m = 0; m < NR; ++m) {
+                    const int row = tid + 256 * m;
+                    xv[k][m] = (ok && row < n_pad) ? __builtin_nontemporal_load(xc + row) : 0.0;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CB; ++k) {
+                const double f = us[cb + k];
+#pragma unroll
+                for (int m = 0; m < NR; ++m) a[m] = __builtin_fma(xv[k][m], f, a[m]);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+        const int row = tid + 256 * m;
+        if (row < n_pad) xu_part[(size_t)sidx * n_pad + row] = a[m];
+    }
+    if (!sums) return;
+    __shared__ double nsum[8][kNidTS + 1];
+    nsum[tid >> 5][tid & 31] = nacc;
+    if ((tid & 31) == 0) nsum[tid >> 5][kNidTS] = ntr;
+    __syncthreads();
+    if (tid <= kNidTS) {
+        double sv = 0.0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) sv += nsum[c][tid];
+        __hip_atomic_store(&fold.wg_part[(size_t)sidx * (kNidTS + 1) + tid], sv, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!fold.decide) return;
+    // unsharded: the stream workgroup that finishes last adds the S partials (k_nid_reduce's
+    // body over the write-through partials) and decides, then re-arms the count
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(fold.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)S - 1;
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) __hip_atomic_store(fold.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nid_fold_decide(fold.wg_part, S, sc, fold.k_launched, fold.allow_mixed, fold.nid, fold.red,
+                    fold.host2, fold.tag_seq);
+}
+template <int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void
+k_lambda_xs(const double *beta, int p_loc, int p_pad, uint64_t j0, const DevScalars *sc, Key key,
+            uint64_t t, double *lam, double *D, double *u, double *lam_trace, uint32_t *err,
+            const double *__restrict__ X, int ldx, int n_pad, int nchunk,
+            double *__restrict__ xu_part, unsigned int *sync, unsigned int ep, int ndraw,
+            NidFold fold) {
+    lambda_xs_body<NR>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace, err, X, ldx, n_pad,
+                       nchunk, xu_part, sync, ep, ndraw, fold);
+}
+
+// the split launch needs its whole grid resident (three workgroups per CU)
+// a flag per 32-coefficient chunk + the claim counter
+int lambda_xs_sync_words(int p_pad) { return (p_pad + 31) / 32 + 1; }
+
+int lambda_xs_resident(int nr) {
+    static int cache[3] = {-1, -1, -1};
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    const int idx = nr <= 4 ? 0 : nr <= 8 ? 1 : 2;
+    int &c = cache[idx];
+    if (c < 0) {
+        int nb = 0;
+        const hipError_t e = idx == 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<4>, 256, 0)
+                           : idx == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<8>, 256, 0)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lambda_xs<16>, 256, 0);
+        c = e == hipSuccess ? nb : 0;
+    }
+    return c;
+}
+
+
+int launch_lambda_xs(hipStream_t s, const double *beta, int p_loc, int p_pad, uint64_t j0,
+                     const DevScalars *sc, uint64_t k0, uint64_t k1, uint64_t t, double *lam,
+                     double *D, double *u, double *lam_trace, uint32_t *err, const double *X, int ldx, int n_pad,
+                     int nchunk, double *xu_part, unsigned int *sync, unsigned int ep, int ndraw,
+                     int nstream, const NidFold *fold) {
+    const int nr = (n_pad + 255) / 256;
+    NidFold f{};
+    if (fold && fold->wg_part && (!fold->decide || fold->cnt)) f = *fold;
+    auto *kk = nr <= 4 ? k_lambda_xs<4> : nr <= 8 ? k_lambda_xs<8> : k_lambda_xs<16>;
+    note_launch(KF_LAMBDA, (const void *)kk);
+    const Key key{k0, k1};
+    kk<<<ndraw + nstream, 256, 0, s>>>(beta, p_loc, p_pad, j0, sc, key, t, lam, D, u, lam_trace,
+                                       err, X, ldx, n_pad, nchunk, xu_part, sync, ep, ndraw, f);
+    return f.wg_part ? (f.decide ? 2 : 1) : 0;
 }
 
 }  // namespace bb

@@ -371,7 +371,12 @@ void bb_set_trace_budget(long long bytes);
  * lets every group finish its own draw (0); under keys 11-15 the draws are the same;
  * key 16 (benchmarking only): K > 0 makes every near-identity sweep run K Chebyshev iterates
  * (at most key 6's cap) instead of its certified count, for timing a C3 rank's product count
- * on a narrower proxy; the solve is then not certified (default 0, the current device only).
+ * on a narrower proxy; the solve is then not certified (default 0, the current device only);
+ * key 17: the split lambda launch (key 7 = 3) also forms the near-identity decision's bound
+ * sums, reduced and decided on by one small launch after it (1, the default), or, unsharded,
+ * reduces them and decides in its last workgroup as well (2), or separate launches form them
+ * (0); the decision and the chain are the same bits in every mode (the bound is rounded up to
+ * 12 significant bits, so the sums' order does not reach it).
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */
