@@ -88,13 +88,19 @@ def static_costs(asm_text, kernel):
 def main_counts(rnd, asm_path):
     src = os.path.join(ROOT, "gpurun_out", f"pmc_valu_{rnd}")
     if asm_path is None:
-        asm_path = "/tmp/bb_kernels_isa.s"
-        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
-                               "-std=c++17", "-ffp-contract=off",
-                               f"-I{os.path.join(ROOT, 'include')}", "--cuda-device-only", "-S",
-                               "-o", asm_path,
-                               os.path.join(ROOT, "bayesbridge_amd", "csrc", "bb_kernels.hip")])
-    asm = open(asm_path).read()
+        # the kernels live in bb_kernels.hip and bb_nid.hip (the split lambda launch)
+        parts = []
+        for src_name in ("bb_kernels.hip", "bb_nid.hip"):
+            path = f"/tmp/{src_name}_isa.s"
+            subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3",
+                                   "-std=c++17", "-ffp-contract=off",
+                                   f"-I{os.path.join(ROOT, 'include')}", "--cuda-device-only",
+                                   "-S", "-o", path,
+                                   os.path.join(ROOT, "bayesbridge_amd", "csrc", src_name)])
+            parts.append(open(path).read())
+        asm = "\n".join(parts)
+    else:
+        asm = open(asm_path).read()
     out = {"round": rnd, "source": "tools/pmc_valu.sh (one counter per rocprofv3 --pmc pass)",
            "source_sha": read_sha(src), "cost_model": {
                "fixed_cycles": FIXED_COST,
