@@ -3745,6 +3745,11 @@ int bb_set_tuning(int key, int value) {
             if (value >= 0) g_lam_wave = value ? 1 : 0;
             return old;
         }
+        case 20: {
+            const int old = g_bsolve_ll;
+            if (value >= 0) g_bsolve_ll = value ? 1 : 0;
+            return old;
+        }
         case 17: {
             const int old = g_nid_fold;
             if (value >= 0) g_nid_fold = value > 2 ? 2 : value;

@@ -289,6 +289,7 @@ void launch_form_a(hipStream_t s, const double *G, int ldg, const double *lam,
 // flags tagged with a per-buffer epoch; zeroed only when first seen).  trace: optional
 // timestamps (bb_bench_chol).
 size_t chol_flag_words(int m_pad, int nrhs_blocks);
+extern int g_bsolve_ll;  // the persistent backward solve's tagged-word hand-off (key 20)
 // doubles of the Wd buffer chol_factor needs (W_k blocks + scratch tiles)
 size_t chol_wd_words(int m_pad);
 extern int g_bxb_nt;  // non-temporal X loads in k_beta_wb_xb (bb_set_tuning key 2)

@@ -2779,9 +2779,14 @@ static size_t bsolve_flag_offset(int m_pad, int nrhs_blocks) {
 // Wd: the nblk blocks W_k followed by nblk scratch tiles (chol_factor's Hs)
 size_t chol_wd_words(int m_pad) { return 2 * (size_t)kNB * m_pad; }
 
-// [... | backward-solve: nblk | H: nblk]
+// [... | backward-solve: nblk | H: nblk | pad to 8 bytes | the solve's LL hand-off words]
+static size_t bsolve_ll_offset(int m_pad, int nrhs_blocks) {
+    return (bsolve_flag_offset(m_pad, nrhs_blocks) + 2 * ((size_t)m_pad / kNB) + 1) & ~(size_t)1;
+}
+// per block: 2 right-hand sides x 64 elements x 2 tagged 64-bit words
+constexpr size_t kBsLLWords = 2 * 64 * 2 * 2;
 size_t chol_flag_words(int m_pad, int nrhs_blocks) {
-    return bsolve_flag_offset(m_pad, nrhs_blocks) + 2 * ((size_t)m_pad / kNB);
+    return bsolve_ll_offset(m_pad, nrhs_blocks) + kBsLLWords * ((size_t)m_pad / kNB);
 }
 
 // Host-side epoch per flag buffer: advance = true starts a new use (zeroing `words` flags
@@ -2960,11 +2965,17 @@ __global__ __launch_bounds__(256) void k_bsolve_multi(const double *A, int lda, 
 // forms w_i = W_i' y_i, stores it write-through (sc1) and sets its flag.  The critical path
 // is one hop + one 64 x 64 matvec per block instead of a launch per kBsNB blocks; every
 // workgroup waits only on higher blocks, all are co-resident (nblk <= CUs).
+//
+// ll (bb_set_tuning key 20 = 1, the default): w_i travels as 64-bit words each holding 32 bits
+// of it and the epoch in the other 32 (single-copy atomic stores), so the consumer polls the
+// data itself -- one write-through round trip per hop instead of the flag's and then the
+// data's -- and the producer needs no drain between data and flag.
 __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda, int nblk,
                                                         int m_pad, const double *__restrict__ Wd,
                                                         const double *Y, double *Wout, int nrhs,
                                                         unsigned int *fl, unsigned int ep,
-                                                        uint32_t *err, const int *gate) {
+                                                        uint32_t *err, const int *gate,
+                                                        unsigned long long *ll) {
     if (gated(gate)) return;
     __shared__ double yv[2][64];
     __shared__ double wv[2][64];
@@ -2986,8 +2997,26 @@ __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda
         const double *row = A + (size_t)(i * kNB + x) + (size_t)(j * kNB + g * 16) * lda;
 #pragma unroll
         for (int cc = 0; cc < 16; ++cc) ureg[cc] = row[(size_t)cc * lda];
-        flag_acquire2(&fl[j], nullptr, ep, err);
-        if (tid < 64 * nrhs) wv[tid >> 6][x] = ld_sc1(&Wout[(size_t)(tid >> 6) * m_pad + j * kNB + x]);
+        if (ll) {
+            if (tid < 64 * nrhs) {  // whole waves: the readiness test is wave-uniform
+                const unsigned long long *pw = ll + (((size_t)j * 2 + (tid >> 6)) * 64 + x) * 2;
+                unsigned long long lo, hi;
+                SpinGuard sg;
+                for (;;) {
+                    lo = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    hi = __hip_atomic_load(pw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const bool ok = (unsigned)(lo >> 32) == ep && (unsigned)(hi >> 32) == ep;
+                    if (__all(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if (sg.expired(err)) break;
+                }
+                wv[tid >> 6][x] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            }
+        } else {
+            flag_acquire2(&fl[j], nullptr, ep, err);
+            if (tid < 64 * nrhs)
+                wv[tid >> 6][x] = ld_sc1(&Wout[(size_t)(tid >> 6) * m_pad + j * kNB + x]);
+        }
         __syncthreads();
         for (int q = 0; q < nrhs; ++q) {
             double acc = 0.0;
@@ -3012,10 +3041,21 @@ __global__ __launch_bounds__(256) void k_bsolve_persist(const double *A, int lda
     if (tid < 64 * nrhs) {
         const int q = tid >> 6;
         const double w = ((part[0][q][x] + part[1][q][x]) + part[2][q][x]) + part[3][q][x];
-        st_sc1(&Wout[(size_t)q * m_pad + i * kNB + x], w);
+        if (ll) {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(w);
+            const unsigned long long tag = (unsigned long long)ep << 32;
+            unsigned long long *pw = ll + (((size_t)i * 2 + q) * 64 + x) * 2;
+            __hip_atomic_store(pw, (b & 0xffffffffull) | tag, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(pw + 1, (b >> 32) | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Wout[(size_t)q * m_pad + i * kNB + x] = w;  // the result (read after the launch)
+        } else {
+            st_sc1(&Wout[(size_t)q * m_pad + i * kNB + x], w);
+        }
     }
-    flag_release(&fl[i], ep);
+    if (!ll) flag_release(&fl[i], ep);
 }
+int g_bsolve_ll = 1;
 
 void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const double *Wd,
                  double *Y, double *W, int nrhs, unsigned int *flags, uint32_t *err, const int *gate) {
@@ -3025,9 +3065,15 @@ void chol_bsolve(hipStream_t s, const double *A, int lda, int m_pad, const doubl
     if (flags && err && nblk <= device_cus()) {
         // the solve's flags have their own epoch sequence (one per solve)
         unsigned int *bf = flags + bsolve_flag_offset(m_pad, 1);
-        const unsigned int ep = flag_epoch(bf, (size_t)nblk, s, true);
+        unsigned int *llw = flags + bsolve_ll_offset(m_pad, 1);
+        // (the LL words are zeroed with the flags on first use and on epoch wrap)
+        const unsigned int ep =
+            flag_epoch(bf, (size_t)(llw - bf) + kBsLLWords * (size_t)nblk, s, true);
         note_launch(KF_SOLVE, (const void *)k_bsolve_persist);
-        k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err, gate);
+        k_bsolve_persist<<<nblk, 256, 0, s>>>(A, lda, nblk, m_pad, Wd, Y, W, nrhs, bf, ep, err, gate,
+                                              (g_bsolve_ll && nrhs <= 2)
+                                                  ? (unsigned long long *)llw
+                                                  : nullptr);
         return;
     }
     for (int kb = nblk - 1; kb >= 0; kb -= kBsNB) {

@@ -376,7 +376,10 @@ void bb_set_trace_budget(long long bytes);
  * sums, reduced and decided on by one small launch after it (1, the default), or, unsharded,
  * reduces them and decides in its last workgroup as well (2), or separate launches form them
  * (0); the decision and the chain are the same bits in every mode (the bound is rounded up to
- * 12 significant bits, so the sums' order does not reach it).
+ * 12 significant bits, so the sums' order does not reach it);
+ * key 20: the persistent backward solve hands each solved block to the next as 64-bit words
+ * tagged with the solve's epoch, polled directly (1, the default), or behind a flag (0); the
+ * same bits.
  * A negative value changes nothing.  Returns the previous value, or -1 for an unknown key. */
 int bb_set_tuning(int key, int value);
 /* Test hook: the k-th interrupt poll from now reports an interrupt (k >= 0; -1 clears). */

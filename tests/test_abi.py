@@ -65,7 +65,7 @@ def test_tuning_keys_report_defaults_without_gpu():
     """bb_set_tuning with a negative value changes nothing and returns the setting; the keys
     include/bayesbridge.h documents (11: polled decision tag, 12: XCD-aware row blocks, 10: the
     mixed plan) answer with their defaults, an unknown key with -1."""
-    for key, want in ((10, 1), (11, 1), (12, 1), (13, 1), (15, 1), (9, 0), (8, 1), (16, 0), (17, 1)):
+    for key, want in ((10, 1), (11, 1), (12, 1), (13, 1), (15, 1), (9, 0), (8, 1), (16, 0), (17, 1), (20, 1)):
         assert bb.set_tuning(key, -1) == want, key
     assert bb.set_tuning(99, 1) == -1
     old = bb.set_tuning(12, 0)
