@@ -623,10 +623,12 @@ int launch_lambda_xu(hipStream_t s, const double *beta, int p_loc, int p_pad, ui
     if (mode == 3 && (!sync || !g_lam_wave || (g_lam_occ & 1) || lambda_xs_resident(nr) < 3))
         mode = 2;
     if (folded) *folded = 0;
-    const int G = g_lam_lanes ? 0 : lambda_xu_groups(p_loc, p_pad, n_pad, mode);
-    if (!G) {
-        if (mode == 3) mode = 2;
-        else return 0;
+    int G = g_lam_lanes ? 0 : lambda_xu_groups(p_loc, p_pad, n_pad, mode);
+    if (!G && mode == 3) {
+        // the split launch takes 8 lanes per coefficient only: 16-lane shapes (p_loc <= 40000,
+        // e.g. a C3 rank at N = 8) fall back to one chunk per workgroup (mode 2)
+        mode = 2;
+        G = g_lam_lanes ? 0 : lambda_xu_groups(p_loc, p_pad, n_pad, mode);
     }
     const Key key{k0, k1};
     const int L = spec_lanes(p_loc);
